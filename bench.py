@@ -1,0 +1,265 @@
+"""Benchmark: frames/sec embedded + ranked (BASELINE.json metric) on MI355X.
+
+One step = the reference's hot path over one batch of synthetic input, all on
+the GPU, inputs resident in HBM before the timed region:
+  encode_image of the rank's frame shard (ViT-B/32, bf16 MFMA)   -> corpus [N,512] f32 in HBM
+  encode_text of Q synthetic token rows (+L2 in the kernel)       -> queries [Q,512]
+  fused normalise + cosine + top-k over the corpus                -> [Q,k]
+  (N>1) RCCL all-gather of the per-shard top-k + merge kernel
+Workload at N=1 is BASELINE.json configs[1] (ViT-B/32 bf16, 10k frames x 32
+queries, top-10); with --gpus N each rank embeds its own 10k-frame shard
+(weak scaling, configs[3]'s design).
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; for N>1 under
+torch.distributed.run (RCCL backend "nccl").  Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "event-retrival-in-video-learning-transferable-visual-model-from-supervised-natural-language_amd")
+for _p in (PKG, ROOT):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md (spec)
+BF16_PEAK_TFLOPS = 2500.0      # dense bf16 MFMA (spec, no sparsity)
+F32_MFMA_PEAK_TFLOPS = 157.3
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--model", default="ViT-B/32")
+    ap.add_argument("--frames", type=int, default=10_000, help="frames per GPU (corpus shard)")
+    ap.add_argument("--queries", type=int, default=32)
+    ap.add_argument("--k", type=int, default=10)
+    ap.add_argument("--image-chunk", type=int, default=None)
+    ap.add_argument("--cpu-frames", type=int, default=64, help="CPU baseline sample (BASELINE configs[0])")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kernel-timing", action="store_true")
+    return ap.parse_args()
+
+
+def kernel_timing(model, cfg, chunk, reps=20):
+    """Average duration of each encoder kernel at the bench's chunk shape, timed
+    with HIP events on the stream the kernels are launched on."""
+    import torch
+    from miclip import _native as N
+
+    L = N.lib()
+    dev = model.device
+    W, S = cfg.vision_width, cfg.vision_tokens
+    M = chunk * S
+    g = torch.Generator(device=dev).manual_seed(0)
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
+    A = (torch.randn(M, 4 * W, device=dev, generator=g) * 0.5).bfloat16()
+    Wt = (torch.randn(4 * W, 4 * W, device=dev, generator=g) * 0.02).bfloat16()
+    bias = torch.zeros(4 * W, device=dev)
+    outb = torch.empty(M, 4 * W, dtype=torch.bfloat16, device=dev)
+    outf = torch.zeros(M, W, device=dev)
+    res = {}
+
+    def timed(name, fn, flops=None, nbytes=None):
+        fn()
+        torch.cuda.synchronize(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            fn()
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        us = e0.elapsed_time(e1) * 1e3 / reps
+        d = {"us": round(us, 2)}
+        if flops:
+            d["tflops"] = round(flops / us / 1e6, 1)
+        if nbytes:
+            d["gbs"] = round(nbytes / us / 1e3, 1)
+        res[name] = d
+
+    gemms = [("gemm_qkv", 3 * W, W, 0, outb), ("gemm_out", W, W, 2, outf), ("gemm_fc", 4 * W, W, 1, outb),
+             ("gemm_proj", W, 4 * W, 2, outf)]
+    for name, Nn, K, epi, out in gemms:
+        timed(name, lambda Nn=Nn, K=K, epi=epi, out=out: N.check(
+            L.mi_op_gemm(A.data_ptr(), Wt.data_ptr(), bias.data_ptr(), out.data_ptr(), M, Nn, K, epi, sp), "gemm"),
+            flops=2.0 * M * Nn * K)
+    qkv = torch.randn(M, 3 * W, device=dev, generator=g).bfloat16()
+    att = torch.empty(M, W, dtype=torch.bfloat16, device=dev)
+    timed("attention", lambda: N.check(L.mi_op_attention(qkv.data_ptr(), att.data_ptr(), chunk, S, W, 0, sp),
+                                       "attn"), flops=4.0 * chunk * S * S * W,
+          nbytes=M * 4 * W * 2)
+    x = torch.randn(M, W, device=dev, generator=g)
+    gam = torch.ones(W, device=dev)
+    timed("layernorm", lambda: N.check(L.mi_op_layernorm(x.data_ptr(), gam.data_ptr(), gam.data_ptr(),
+                                                         att.data_ptr(), M, W, sp), "ln"), nbytes=M * W * 6)
+    return res
+
+
+def rank_timing(corpus, txt, k, reps=50):
+    import torch
+    from miclip import retrieval
+    retrieval.rank_topk(corpus, txt, k)
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        retrieval.rank_topk(corpus, txt, k)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / reps
+    nbytes = corpus.numel() * corpus.element_size()
+    return {"us": round(us, 2), "gbs": round(nbytes / us / 1e3, 1),
+            "tflops_f32": round(2.0 * corpus.shape[0] * txt.shape[0] * corpus.shape[1] / us / 1e6, 2)}
+
+
+def cpu_baseline(cfg, n_frames_metric, Q, k, sample_frames):
+    """Oracle (numpy fp32 restatement of the reference CPU path) on a bounded
+    sample: `sample_frames` frames encoded at batch 64 (configs[0]) + 1 text
+    query + np.dot/np.argsort ranking over an N-row corpus
+    (embedding_service.py:314-320); extrapolated to the metric's workload."""
+    import numpy as np
+    from miclip import weights
+    from oracle import clip_ref, rank_ref
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max(i.get("num_threads", 1) for i in threadpool_info()) if threadpool_info() else os.cpu_count()
+    except Exception:
+        cores = os.cpu_count()
+    sd = weights.make_state_dict(cfg)
+    px = weights.synthetic_pixels(sample_frames, cfg.image_resolution)
+    tk = weights.synthetic_tokens(1, cfg.context_length, cfg.vocab_size)
+    t0 = time.perf_counter()
+    emb = np.concatenate([clip_ref.encode_image(px[i:i + 64], sd, cfg) for i in range(0, sample_frames, 64)])
+    t_img = (time.perf_counter() - t0) / sample_frames
+    t0 = time.perf_counter()
+    txt = clip_ref.encode_text(tk, sd, cfg)
+    t_txt = time.perf_counter() - t0
+    corpus = np.tile(emb, (n_frames_metric // sample_frames + 1, 1))[:n_frames_metric]
+    frames = list(range(n_frames_metric))
+    t0 = time.perf_counter()
+    rank_ref.search_top_frames_ref(corpus, txt, k, frames)
+    t_rank = time.perf_counter() - t0
+    total = n_frames_metric * t_img + Q * t_txt + Q * t_rank
+    return {"value": round(n_frames_metric / total, 2), "unit": "frames/s", "cores": int(cores), "kind": "port",
+            "sample": f"oracle numpy fp32 (reference CPU path restated): {sample_frames} frames at batch 64 "
+                      f"({t_img * 1e3:.1f} ms/frame) + 1 encode_text ({t_txt * 1e3:.1f} ms) + np.dot/argsort over "
+                      f"{n_frames_metric} rows ({t_rank * 1e3:.2f} ms/query); extrapolated to "
+                      f"{n_frames_metric} frames x {Q} queries"}
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from miclip import api, distributed, retrieval, weights
+
+    model, _ = api.load(args.model, device=dev, image_chunk=args.image_chunk)
+    cfg = model.cfg
+    chunk = model._chunks[0]
+    Nf, Q, k = args.frames, args.queries, args.k
+    R = cfg.image_resolution
+    g = torch.Generator(device=dev).manual_seed(1234 + rank)
+    pixels = torch.randn(Nf, 3, R, R, device=dev, generator=g, dtype=torch.float32).bfloat16()
+    tokens = torch.from_numpy(weights.synthetic_tokens(Q, cfg.context_length, cfg.vocab_size)).to(dev)
+    corpus = torch.empty(Nf, cfg.embed_dim, device=dev)
+    base = rank * Nf
+
+    def step():
+        emb = model.encode_image(pixels, out_dtype=torch.float32)
+        txt = model.encode_text(tokens, normalize=True, out_dtype=torch.float32)
+        if world > 1:
+            return emb, distributed.sharded_topk(emb, txt, k, base)
+        return emb, retrieval.rank_topk(emb, txt, k, index_base=base)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        emb, (top_s, top_i) = step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    assert torch.isfinite(top_s[:, 0]).all() and (top_i[:, 0] >= 0).all()
+    del corpus
+
+    ms = elapsed / args.steps * 1e3
+    total_frames = Nf * world * args.steps
+    value = total_frames / elapsed
+    result = None
+    if rank == 0:
+        kern = {} if args.no_kernel_timing else kernel_timing(model, cfg, chunk)
+        txt = model.encode_text(tokens, normalize=True, out_dtype=torch.float32)
+        kern["rank_topk"] = rank_timing(emb, txt, k)
+        F_frame, F_text = cfg.image_flops(), cfg.text_flops()
+        step_flops = Nf * F_frame + Q * F_text + 2.0 * Nf * Q * cfg.embed_dim
+        mfma_frac = step_flops / (ms / 1e3) / (BF16_PEAK_TFLOPS * 1e12)
+        dom = kern.get("gemm_fc")
+        M = chunk * cfg.vision_tokens
+        roof = None
+        if dom:
+            fl = 2.0 * M * 4 * cfg.vision_width * cfg.vision_width
+            ach = fl / (dom["us"] * 1e-6) / 1e12
+            roof = {"bound": "mfma", "kernel": "gemm_kernel<EPI_GELU_BF16> (mlp.c_fc + QuickGELU)",
+                    "achieved": round(ach, 1), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(ach / BF16_PEAK_TFLOPS, 4), "traffic": None,
+                    "flops_per_launch": fl, "launch_shape": [M, 4 * cfg.vision_width, cfg.vision_width],
+                    "avg_launch_us": dom["us"]}
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            cpu = cpu_baseline(cfg, Nf, Q, k, args.cpu_frames)
+        result = {
+            "metric": "frames/sec embedded+ranked, ViT-B/32 224², 1/2/4/8 MI355X; R@1/5/10 parity",
+            "value": round(value, 1), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "bf16", "data": "synthetic (random pixels/tokens, deterministic "
+                                                          "random-init weights of the real architecture)",
+            "config": {"workload": f"{cfg.name} bf16, {Nf} frames/GPU x {Q} text queries, top-{k}"
+                                   + (" (BASELINE configs[1])" if world == 1 and Nf == 10_000 else
+                                      f" ({world} shards, RCCL all-gather top-k)"),
+                       "model": cfg.name, "global_batch": Nf * world, "queries": Q, "k": k,
+                       "image_chunk": chunk, "parallelism": f"dp{world}"},
+            "roofline": roof,
+            "mfma_frac_end_to_end": round(mfma_frac, 4),
+            "kernels": kern,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return result
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,498 @@
+// C-ABI of libmiclip (include/miclip.h): model context, weight upload,
+// encode orchestration and the ranking entry points.
+//
+// encode_image follows openai/CLIP VisionTransformer.forward (restated in
+// oracle/clip_ref.py::encode_image): im2col + conv1 GEMM -> [CLS|patches]+pos
+// -> ln_pre -> L x {LN -> QKV GEMM -> attention -> out-proj GEMM (+residual)
+// -> LN -> c_fc GEMM (+QuickGELU) -> c_proj GEMM (+residual)} -> ln_post(CLS)
+// -> proj GEMM.  encode_text: token gather + pos -> L causal blocks ->
+// ln_final at argmax(tokens) -> text_projection GEMM.
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/miclip.h"
+#include "internal.hpp"
+
+using namespace miclip;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                           \
+  do {                                                                                          \
+    hipError_t e_ = (expr);                                                                     \
+    if (e_ != hipSuccess) return fail(MI_ERR_HIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                                      __FILE__, __LINE__);                                      \
+  } while (0)
+
+uint16_t f2bf_host(float f) {
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x007fffffu)) return (uint16_t)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+struct Layer {
+  const float *ln1_g, *ln1_b, *b_qkv, *b_out, *ln2_g, *ln2_b, *b_fc, *b_proj;
+  const uint16_t *w_qkv, *w_out, *w_fc, *w_proj;
+};
+
+// Device weight image: bf16 GEMM weights and f32 vectors in one allocation.
+// Built by walking the canonical host blob (DESIGN.md "Weight blob").
+struct Builder {
+  const float* src;   // host blob
+  int64_t pos = 0;    // elements consumed
+  int64_t numel;
+  std::vector<char> img;  // host copy of the device image
+  bool ok = true;
+
+  const float* take(int64_t n) {
+    if (pos + n > numel) { ok = false; return nullptr; }
+    const float* p = src + pos;
+    pos += n;
+    return p;
+  }
+  size_t align() {
+    size_t o = (img.size() + 255) & ~(size_t)255;
+    img.resize(o);
+    return o;
+  }
+  size_t f32(int64_t n) {  // copy n floats as-is
+    const float* p = take(n);
+    size_t o = align();
+    img.resize(o + n * 4);
+    if (p) memcpy(img.data() + o, p, n * 4);
+    return o;
+  }
+  // rows x cols fp32 matrix -> bf16 [rows][ldp] (zero padded columns)
+  size_t bf16(int64_t rows, int64_t cols, int64_t ldp) {
+    const float* p = take(rows * cols);
+    size_t o = align();
+    img.resize(o + rows * ldp * 2);
+    uint16_t* d = (uint16_t*)(img.data() + o);
+    for (int64_t r = 0; r < rows; ++r)
+      for (int64_t c = 0; c < ldp; ++c) d[r * ldp + c] = (p && c < cols) ? f2bf_host(p[r * cols + c]) : 0;
+    return o;
+  }
+  // [rows][cols] fp32 used as x @ P  ->  bf16 P^T [cols][rows]
+  size_t bf16_t(int64_t rows, int64_t cols) {
+    const float* p = take(rows * cols);
+    size_t o = align();
+    img.resize(o + rows * cols * 2);
+    uint16_t* d = (uint16_t*)(img.data() + o);
+    for (int64_t c = 0; c < cols; ++c)
+      for (int64_t r = 0; r < rows; ++r) d[c * rows + r] = p ? f2bf_host(p[r * cols + c]) : 0;
+    return o;
+  }
+};
+
+struct LayerOff {
+  size_t ln1_g, ln1_b, w_qkv, b_qkv, w_out, b_out, ln2_g, ln2_b, w_fc, b_fc, w_proj, b_proj;
+};
+
+void build_tower(Builder& b, int W, int L, std::vector<LayerOff>& out) {
+  out.resize(L);
+  for (int i = 0; i < L; ++i) {
+    LayerOff& l = out[i];
+    l.ln1_g = b.f32(W);
+    l.ln1_b = b.f32(W);
+    l.w_qkv = b.bf16(3 * W, W, W);
+    l.b_qkv = b.f32(3 * W);
+    l.w_out = b.bf16(W, W, W);
+    l.b_out = b.f32(W);
+    l.ln2_g = b.f32(W);
+    l.ln2_b = b.f32(W);
+    l.w_fc = b.bf16(4 * W, W, W);
+    l.b_fc = b.f32(4 * W);
+    l.w_proj = b.bf16(W, 4 * W, 4 * W);
+    l.b_proj = b.f32(W);
+  }
+}
+
+int64_t tower_numel(int64_t W, int64_t L) { return L * (W * 2 + 3 * W * W + 3 * W + W * W + W + 2 * W + 4 * W * W + 4 * W + 4 * W * W + W); }
+
+}  // namespace
+
+struct mi_clip {
+  mi_clip_arch a;
+  int device = 0;
+  int S_v = 0, G = 0, Kp = 0;
+  char* wdev = nullptr;
+  // vision
+  const uint16_t* conv_w = nullptr;
+  const float *cls = nullptr, *vpos = nullptr, *ln_pre_g = nullptr, *ln_pre_b = nullptr, *ln_post_g = nullptr,
+              *ln_post_b = nullptr;
+  const uint16_t* vproj_t = nullptr;
+  std::vector<Layer> vl, tl;
+  // text
+  const float *tok_emb = nullptr, *tpos = nullptr, *lnf_g = nullptr, *lnf_b = nullptr;
+  const uint16_t* tproj_t = nullptr;
+  // workspace
+  int64_t img_chunk = 0, txt_chunk = 0;
+  char* ws = nullptr;
+  float* x = nullptr;
+  uint16_t *h = nullptr, *qkv = nullptr, *att = nullptr, *mlp = nullptr, *patches = nullptr, *cls_ln = nullptr;
+  float* y = nullptr;
+  std::mutex mu;
+};
+
+extern "C" {
+
+int mi_abi_version(void) { return MICLIP_ABI_VERSION; }
+
+const char* mi_last_error(void) { return g_err.c_str(); }
+
+int64_t mi_clip_weights_numel(const mi_clip_arch* a) {
+  if (!a) return -1;
+  const int64_t W = a->vision_width, P = a->vision_patch_size, G = a->image_resolution / a->vision_patch_size;
+  const int64_t S = G * G + 1, E = a->embed_dim, TW = a->text_width;
+  int64_t n = W * 3 * P * P + W + S * W + 2 * W + tower_numel(W, a->vision_layers) + 2 * W + W * E;
+  n += (int64_t)a->vocab_size * TW + (int64_t)a->context_length * TW + tower_numel(TW, a->text_layers) + 2 * TW +
+       TW * E + 1;
+  return n;
+}
+
+int mi_clip_create(const mi_clip_arch* arch, const float* weights, int64_t numel, int device, int weight_dtype,
+                   mi_clip** out) {
+  if (!arch || !weights || !out) return fail(MI_ERR_ARG, "mi_clip_create: null argument");
+  *out = nullptr;
+  if (weight_dtype != MI_BF16) return fail(MI_ERR_UNSUPPORTED, "mi_clip_create: only MI_BF16 weights are supported");
+  const mi_clip_arch& a = *arch;
+  if (a.vision_width % 128 || a.text_width % 128 || a.vision_width > 1024 || a.text_width > 1024)
+    return fail(MI_ERR_UNSUPPORTED, "widths must be multiples of 128 and <= 1024 (got %d/%d)", a.vision_width,
+                a.text_width);
+  if (a.embed_dim % 128) return fail(MI_ERR_UNSUPPORTED, "embed_dim must be a multiple of 128");
+  if (a.image_resolution % a.vision_patch_size) return fail(MI_ERR_ARG, "resolution not divisible by patch");
+  if (a.text_heads * 64 != a.text_width) return fail(MI_ERR_UNSUPPORTED, "text head dim must be 64");
+  const int G = a.image_resolution / a.vision_patch_size;
+  if (G * G + 1 > 288 || a.context_length > 288)
+    return fail(MI_ERR_UNSUPPORTED, "sequence longer than 288 tokens not supported yet");
+  const int64_t expect = mi_clip_weights_numel(arch);
+  if (numel != expect) return fail(MI_ERR_ARG, "weight blob has %lld elements, expected %lld", (long long)numel,
+                                   (long long)expect);
+  HIP_TRY(hipSetDevice(device));
+
+  auto* c = new mi_clip();
+  c->a = a;
+  c->device = device;
+  c->G = G;
+  c->S_v = G * G + 1;
+  const int W = a.vision_width, TW = a.text_width, E = a.embed_dim;
+  const int K = 3 * a.vision_patch_size * a.vision_patch_size;
+  c->Kp = (K + 63) / 64 * 64;
+
+  Builder b;
+  b.src = weights;
+  b.numel = numel;
+  b.img.reserve((size_t)numel * 2 + (size_t)a.vocab_size * TW * 2 + (1 << 20));
+  const size_t o_conv = b.bf16(W, K, c->Kp);
+  const size_t o_cls = b.f32(W);
+  const size_t o_vpos = b.f32((int64_t)c->S_v * W);
+  const size_t o_lnpre_g = b.f32(W), o_lnpre_b = b.f32(W);
+  std::vector<LayerOff> vlo, tlo;
+  build_tower(b, W, a.vision_layers, vlo);
+  const size_t o_lnpost_g = b.f32(W), o_lnpost_b = b.f32(W);
+  const size_t o_vproj = b.bf16_t(W, E);
+  const size_t o_tok = b.f32((int64_t)a.vocab_size * TW);
+  const size_t o_tpos = b.f32((int64_t)a.context_length * TW);
+  build_tower(b, TW, a.text_layers, tlo);
+  const size_t o_lnf_g = b.f32(TW), o_lnf_b = b.f32(TW);
+  const size_t o_tproj = b.bf16_t(TW, E);
+  const float* ls = b.take(1);
+  if (!b.ok || b.pos != numel || !ls) {
+    delete c;
+    return fail(MI_ERR_ARG, "weight blob layout mismatch (consumed %lld of %lld)", (long long)b.pos,
+                (long long)numel);
+  }
+  hipError_t e = hipMalloc(&c->wdev, b.img.size());
+  if (e == hipSuccess) e = hipMemcpy(c->wdev, b.img.data(), b.img.size(), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    if (c->wdev) (void)hipFree(c->wdev);
+    delete c;
+    return fail(MI_ERR_HIP, "weight upload: %s", hipGetErrorString(e));
+  }
+  char* d = c->wdev;
+  auto F = [&](size_t o) { return (const float*)(d + o); };
+  auto H = [&](size_t o) { return (const uint16_t*)(d + o); };
+  c->conv_w = H(o_conv);
+  c->cls = F(o_cls);
+  c->vpos = F(o_vpos);
+  c->ln_pre_g = F(o_lnpre_g);
+  c->ln_pre_b = F(o_lnpre_b);
+  c->ln_post_g = F(o_lnpost_g);
+  c->ln_post_b = F(o_lnpost_b);
+  c->vproj_t = H(o_vproj);
+  c->tok_emb = F(o_tok);
+  c->tpos = F(o_tpos);
+  c->lnf_g = F(o_lnf_g);
+  c->lnf_b = F(o_lnf_b);
+  c->tproj_t = H(o_tproj);
+  auto conv_layers = [&](const std::vector<LayerOff>& lo, std::vector<Layer>& L) {
+    L.resize(lo.size());
+    for (size_t i = 0; i < lo.size(); ++i) {
+      const LayerOff& o = lo[i];
+      L[i] = Layer{F(o.ln1_g), F(o.ln1_b), F(o.b_qkv), F(o.b_out), F(o.ln2_g), F(o.ln2_b), F(o.b_fc), F(o.b_proj),
+                   H(o.w_qkv), H(o.w_out), H(o.w_fc), H(o.w_proj)};
+    }
+  };
+  conv_layers(vlo, c->vl);
+  conv_layers(tlo, c->tl);
+  *out = c;
+  return MI_OK;
+}
+
+int mi_clip_destroy(mi_clip* c) {
+  if (!c) return MI_OK;
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    (void)hipSetDevice(c->device);
+    if (c->ws) (void)hipFree(c->ws);
+    if (c->wdev) (void)hipFree(c->wdev);
+  }
+  delete c;
+  return MI_OK;
+}
+
+static int reserve_locked(mi_clip* c, int64_t ic, int64_t tc) {
+  if (ic <= c->img_chunk && tc <= c->txt_chunk && c->ws) return MI_OK;
+  ic = ic > c->img_chunk ? ic : c->img_chunk;
+  tc = tc > c->txt_chunk ? tc : c->txt_chunk;
+  const mi_clip_arch& a = c->a;
+  const int64_t Mv = ic * c->S_v, Mt = tc * a.context_length;
+  const int64_t Wv = a.vision_width, Wt = a.text_width;
+  auto mx = [](int64_t p, int64_t q) { return p > q ? p : q; };
+  const int64_t xw = mx(Mv * Wv, Mt * Wt);
+  const int64_t rows_max = mx(ic, tc);
+  size_t off = 0;
+  auto carve = [&](size_t bytes) { size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
+  const size_t o_x = carve(xw * 4);
+  const size_t o_h = carve(xw * 2);
+  const size_t o_qkv = carve(3 * xw * 2);
+  const size_t o_att = carve(xw * 2);
+  const size_t o_mlp = carve(4 * xw * 2);
+  const size_t o_pat = carve((size_t)ic * c->G * c->G * c->Kp * 2);
+  const size_t o_cls = carve((size_t)rows_max * mx(Wv, Wt) * 2);
+  const size_t o_y = carve((size_t)rows_max * a.embed_dim * 4);
+  HIP_TRY(hipSetDevice(c->device));
+  char* ws = nullptr;
+  HIP_TRY(hipMalloc(&ws, off));
+  if (c->ws) {
+    (void)hipDeviceSynchronize();
+    (void)hipFree(c->ws);
+  }
+  c->ws = ws;
+  c->x = (float*)(ws + o_x);
+  c->h = (uint16_t*)(ws + o_h);
+  c->qkv = (uint16_t*)(ws + o_qkv);
+  c->att = (uint16_t*)(ws + o_att);
+  c->mlp = (uint16_t*)(ws + o_mlp);
+  c->patches = (uint16_t*)(ws + o_pat);
+  c->cls_ln = (uint16_t*)(ws + o_cls);
+  c->y = (float*)(ws + o_y);
+  c->img_chunk = ic;
+  c->txt_chunk = tc;
+  return MI_OK;
+}
+
+int mi_clip_reserve(mi_clip* c, int64_t image_chunk, int64_t text_chunk) {
+  if (!c || image_chunk < 1 || text_chunk < 1) return fail(MI_ERR_ARG, "mi_clip_reserve: bad arguments");
+  std::lock_guard<std::mutex> g(c->mu);
+  return reserve_locked(c, image_chunk, text_chunk);
+}
+
+static GemmArgs gargs(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, const float* bias, void* out,
+                      int64_t ldo, int M, int N, int K) {
+  GemmArgs g;
+  g.A = A; g.lda = lda; g.W = W; g.ldw = ldw; g.bias = bias; g.out = out; g.ldo = ldo;
+  g.M = M; g.N = N; g.K = K; g.group = 0; g.gstride = 0; g.goffset = 0;
+  return g;
+}
+
+static int run_tower(mi_clip* c, const std::vector<Layer>& layers, int B, int S, int W, int causal, hipStream_t s) {
+  const int M = B * S;
+  for (const Layer& L : layers) {
+    HIP_TRY(layernorm_bf16(c->x, W, L.ln1_g, L.ln1_b, c->h, W, M, W, s));
+    HIP_TRY(gemm_bf16(gargs(c->h, W, L.w_qkv, W, L.b_qkv, c->qkv, 3 * W, M, 3 * W, W), EPI_BF16, s));
+    HIP_TRY(attention(c->qkv, c->att, B, S, W, causal, s));
+    HIP_TRY(gemm_bf16(gargs(c->att, W, L.w_out, W, L.b_out, c->x, W, M, W, W), EPI_RESID_F32, s));
+    HIP_TRY(layernorm_bf16(c->x, W, L.ln2_g, L.ln2_b, c->h, W, M, W, s));
+    HIP_TRY(gemm_bf16(gargs(c->h, W, L.w_fc, W, L.b_fc, c->mlp, 4 * W, M, 4 * W, W), EPI_GELU_BF16, s));
+    HIP_TRY(gemm_bf16(gargs(c->mlp, 4 * W, L.w_proj, 4 * W, L.b_proj, c->x, W, M, W, 4 * W), EPI_RESID_F32, s));
+  }
+  return MI_OK;
+}
+
+static size_t dtype_size(int dt) { return dt == MI_F32 ? 4 : 2; }
+
+int mi_clip_encode_image(mi_clip* c, const void* pixels, int64_t B, int in_dtype, void* out, int out_dtype,
+                         int l2_normalize, void* stream) {
+  if (!c || (!pixels && B > 0) || (!out && B > 0) || B < 0) return fail(MI_ERR_ARG, "encode_image: bad arguments");
+  if (in_dtype != MI_F32 && in_dtype != MI_BF16) return fail(MI_ERR_ARG, "encode_image: in_dtype must be f32/bf16");
+  if (out_dtype < MI_F32 || out_dtype > MI_F16) return fail(MI_ERR_ARG, "encode_image: bad out_dtype");
+  std::lock_guard<std::mutex> g(c->mu);
+  if (!c->ws) {
+    int r = reserve_locked(c, 256, 64);
+    if (r) return r;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  HIP_TRY(hipSetDevice(c->device));
+  const mi_clip_arch& a = c->a;
+  const int W = a.vision_width, E = a.embed_dim, S = c->S_v, R = a.image_resolution, P = a.vision_patch_size;
+  const int G2 = c->G * c->G;
+  const size_t in_img = (size_t)3 * R * R * dtype_size(in_dtype);
+  for (int64_t c0 = 0; c0 < B; c0 += c->img_chunk) {
+    const int nb = (int)((B - c0) < c->img_chunk ? (B - c0) : c->img_chunk);
+    HIP_TRY(im2col((const char*)pixels + c0 * in_img, in_dtype == MI_BF16, c->patches, nb, R, P, c->Kp, s));
+    GemmArgs pg = gargs(c->patches, c->Kp, c->conv_w, c->Kp, nullptr, c->x, W, nb * G2, W, c->Kp);
+    pg.group = G2;
+    pg.gstride = S;
+    pg.goffset = 1;
+    HIP_TRY(gemm_bf16(pg, EPI_F32, s));
+    HIP_TRY(vision_embed_ln(c->x, c->cls, c->vpos, c->ln_pre_g, c->ln_pre_b, nb, S, W, s));
+    int r = run_tower(c, c->vl, nb, S, W, 0, s);
+    if (r) return r;
+    HIP_TRY(layernorm_bf16(c->x, (int64_t)S * W, c->ln_post_g, c->ln_post_b, c->cls_ln, W, nb, W, s));
+    HIP_TRY(gemm_bf16(gargs(c->cls_ln, W, c->vproj_t, W, nullptr, c->y, E, nb, E, W), EPI_F32, s));
+    HIP_TRY(finalize_rows(c->y, (char*)out + c0 * E * dtype_size(out_dtype), out_dtype, nb, E, l2_normalize, s));
+  }
+  return MI_OK;
+}
+
+int mi_clip_encode_text(mi_clip* c, const int32_t* tokens, int64_t Q, void* out, int out_dtype, int l2_normalize,
+                        void* stream) {
+  if (!c || (!tokens && Q > 0) || (!out && Q > 0) || Q < 0) return fail(MI_ERR_ARG, "encode_text: bad arguments");
+  if (out_dtype < MI_F32 || out_dtype > MI_F16) return fail(MI_ERR_ARG, "encode_text: bad out_dtype");
+  std::lock_guard<std::mutex> g(c->mu);
+  if (!c->ws) {
+    int r = reserve_locked(c, 256, 64);
+    if (r) return r;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  HIP_TRY(hipSetDevice(c->device));
+  const mi_clip_arch& a = c->a;
+  const int W = a.text_width, E = a.embed_dim, S = a.context_length;
+  for (int64_t c0 = 0; c0 < Q; c0 += c->txt_chunk) {
+    const int nq = (int)((Q - c0) < c->txt_chunk ? (Q - c0) : c->txt_chunk);
+    const int32_t* tk = tokens + c0 * S;
+    HIP_TRY(text_embed(tk, c->tok_emb, c->tpos, c->x, nq, S, W, a.vocab_size, s));
+    int r = run_tower(c, c->tl, nq, S, W, 1, s);
+    if (r) return r;
+    HIP_TRY(eot_gather_ln(tk, c->x, c->lnf_g, c->lnf_b, c->cls_ln, nq, S, W, s));
+    HIP_TRY(gemm_bf16(gargs(c->cls_ln, W, c->tproj_t, W, nullptr, c->y, E, nq, E, W), EPI_F32, s));
+    HIP_TRY(finalize_rows(c->y, (char*)out + c0 * E * dtype_size(out_dtype), out_dtype, nq, E, l2_normalize, s));
+  }
+  return MI_OK;
+}
+
+size_t mi_rank_workspace_bytes(int64_t N, int64_t Q, int32_t k) {
+  if (N < 0 || Q < 0 || k < 1) return 0;
+  return rank_workspace_bytes(N, Q, k);
+}
+
+static int check_rank_args(int64_t N, int64_t D, int dt, int64_t Q, int32_t k, int norm_mode, int nan_policy) {
+  if (N < 0 || Q < 0) return fail(MI_ERR_ARG, "negative size");
+  if (k < 1 || k > 64) return fail(MI_ERR_UNSUPPORTED, "k must be in [1, 64] (got %d)", k);
+  if (D < 32 || D % 32 || D > 4096) return fail(MI_ERR_UNSUPPORTED, "D must be a multiple of 32 in [32, 4096]");
+  if (dt != MI_F32 && dt != MI_BF16 && dt != MI_F16) return fail(MI_ERR_ARG, "bad corpus dtype");
+  if (norm_mode < 0 || norm_mode > 2) return fail(MI_ERR_ARG, "bad norm_mode");
+  if (nan_policy != MI_NAN_FIRST && nan_policy != MI_NAN_LAST) return fail(MI_ERR_ARG, "bad nan_policy");
+  if (N >= (int64_t)1 << 31) return fail(MI_ERR_UNSUPPORTED, "N >= 2^31 per call: shard the corpus");
+  return MI_OK;
+}
+
+int mi_rank_topk(const void* corpus, int64_t N, int64_t D, int corpus_dtype, const float* queries, int64_t Q,
+                 int32_t k, int64_t index_base, int norm_mode, int nan_policy, float* out_scores, int64_t* out_index,
+                 void* workspace, size_t workspace_bytes, void* stream) {
+  int r = check_rank_args(N, D, corpus_dtype, Q, k, norm_mode, nan_policy);
+  if (r) return r;
+  if (Q == 0) return MI_OK;
+  if (!queries || !out_scores || !out_index || (N > 0 && !corpus))
+    return fail(MI_ERR_ARG, "mi_rank_topk: null pointer");
+  hipStream_t s = (hipStream_t)stream;
+  const int nf = nan_policy == MI_NAN_FIRST;
+  if (N == 0) {
+    HIP_TRY(rank_merge(nullptr, nullptr, Q, 0, k, nf, out_scores, out_index, s));
+    return MI_OK;
+  }
+  const size_t need = rank_workspace_bytes(N, Q, k);
+  if (!workspace || workspace_bytes < need)
+    return fail(MI_ERR_ARG, "mi_rank_topk: workspace too small (%zu < %zu)", workspace_bytes, need);
+  HIP_TRY(rank_topk(corpus, N, D, corpus_dtype, queries, Q, k, index_base, norm_mode, nf, out_scores, out_index,
+                    workspace, s));
+  return MI_OK;
+}
+
+int mi_rank_merge(const float* cs, const int64_t* ci, int64_t Q, int64_t C, int32_t k, int nan_policy, float* out_s,
+                  int64_t* out_i, void* stream) {
+  if (Q < 0 || C < 0) return fail(MI_ERR_ARG, "negative size");
+  if (k < 1 || k > 64) return fail(MI_ERR_UNSUPPORTED, "k must be in [1, 64] (got %d)", k);
+  if (nan_policy != MI_NAN_FIRST && nan_policy != MI_NAN_LAST) return fail(MI_ERR_ARG, "bad nan_policy");
+  if (Q == 0) return MI_OK;
+  if ((C > 0 && (!cs || !ci)) || !out_s || !out_i) return fail(MI_ERR_ARG, "mi_rank_merge: null pointer");
+  HIP_TRY(rank_merge(cs, ci, Q, C, k, nan_policy == MI_NAN_FIRST, out_s, out_i, (hipStream_t)stream));
+  return MI_OK;
+}
+
+int mi_score_matrix(const void* corpus, int64_t N, int64_t D, int corpus_dtype, const float* queries, int64_t Q,
+                    int norm_mode, float* out, void* stream) {
+  int r = check_rank_args(N, D, corpus_dtype, Q, 1, norm_mode, MI_NAN_FIRST);
+  if (r) return r;
+  if (N == 0 || Q == 0) return MI_OK;
+  if (!corpus || !queries || !out) return fail(MI_ERR_ARG, "mi_score_matrix: null pointer");
+  HIP_TRY(score_matrix(corpus, N, D, corpus_dtype, queries, Q, norm_mode, out, (hipStream_t)stream));
+  return MI_OK;
+}
+
+int mi_rank_of_targets(const float* scores, int64_t Q, int64_t N, const int64_t* pq, const int64_t* pt, int64_t T,
+                       int64_t* out, void* stream) {
+  if (Q < 0 || N < 0 || T < 0) return fail(MI_ERR_ARG, "negative size");
+  if (T == 0) return MI_OK;
+  if (!scores || !pq || !pt || !out) return fail(MI_ERR_ARG, "mi_rank_of_targets: null pointer");
+  HIP_TRY(rank_of_targets(scores, Q, N, pq, pt, T, out, (hipStream_t)stream));
+  return MI_OK;
+}
+
+int mi_op_gemm(const void* A, const void* W, const float* bias, void* out, int32_t M, int32_t N, int32_t K,
+               int32_t epi, void* stream) {
+  if (!A || !W || !out || M < 0) return fail(MI_ERR_ARG, "mi_op_gemm: bad arguments");
+  if (K % 64 || N % 128 || K <= 0) return fail(MI_ERR_UNSUPPORTED, "mi_op_gemm: needs K %% 64 == 0, N %% 128 == 0");
+  if (epi < 0 || epi > 3) return fail(MI_ERR_ARG, "mi_op_gemm: bad epilogue");
+  HIP_TRY(gemm_bf16(gargs((const uint16_t*)A, K, (const uint16_t*)W, K, bias, out, N, M, N, K), epi,
+                    (hipStream_t)stream));
+  return MI_OK;
+}
+
+int mi_op_layernorm(const float* x, const float* g, const float* b, void* out, int32_t rows, int32_t W,
+                    void* stream) {
+  if (!x || !g || !b || !out || rows < 0) return fail(MI_ERR_ARG, "mi_op_layernorm: bad arguments");
+  if (W % 4 || W > 1024) return fail(MI_ERR_UNSUPPORTED, "mi_op_layernorm: W must be a multiple of 4, <= 1024");
+  HIP_TRY(layernorm_bf16(x, W, g, b, (uint16_t*)out, W, rows, W, (hipStream_t)stream));
+  return MI_OK;
+}
+
+int mi_op_attention(const void* qkv, void* out, int32_t B, int32_t S, int32_t W, int32_t causal, void* stream) {
+  if (!qkv || !out || B < 0 || S < 1) return fail(MI_ERR_ARG, "mi_op_attention: bad arguments");
+  if (W % 64 || S > 288) return fail(MI_ERR_UNSUPPORTED, "mi_op_attention: W %% 64 == 0 and S <= 288");
+  HIP_TRY(attention((const uint16_t*)qkv, (uint16_t*)out, B, S, W, causal, (hipStream_t)stream));
+  return MI_OK;
+}
+
+}  // extern "C"

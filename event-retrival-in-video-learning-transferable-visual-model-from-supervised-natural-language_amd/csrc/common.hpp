@@ -1,0 +1,58 @@
+// Shared device helpers for libmiclip (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef uint16_t u16;
+
+#define LDS_AS __attribute__((address_space(3)))
+#define GLB_AS __attribute__((address_space(1)))
+
+// f32 -> bf16 round-to-nearest-even (NaN stays NaN: quiet bit forced).
+__device__ __host__ __forceinline__ u16 f2bf(float f) {
+  union { float f; uint32_t u; } v;
+  v.f = f;
+  uint32_t u = v.u;
+  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x007fffffu)) return (u16)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (u16)(u >> 16);
+}
+
+__device__ __host__ __forceinline__ float bf2f(u16 h) {
+  union { uint32_t u; float f; } v;
+  v.u = ((uint32_t)h) << 16;
+  return v.f;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// async 16-byte global -> LDS copy: LDS destination is lds_base + lane*16
+// (wave-uniform base), the global source is per lane.
+__device__ __forceinline__ void glds16(const void* gsrc, void* lds_base) {
+  __builtin_amdgcn_global_load_lds((const GLB_AS void*)gsrc, (LDS_AS void*)lds_base, 16, 0, 0);
+}
+
+__device__ __forceinline__ void vm_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// Bijective XCD-aware block remap (cdna_hip_programming.md §5 "XCD swizzle
+// must be bijective"): blocks that share an XCD (b % 8) get a contiguous run of
+// logical tile ids, so neighbouring tiles (which share operand panels) hit the
+// same L2.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int q = nwg / 8, r = nwg % 8;
+  const int xcd = bid % 8, idx = bid / 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}

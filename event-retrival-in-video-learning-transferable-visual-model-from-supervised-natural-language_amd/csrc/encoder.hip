@@ -1,0 +1,408 @@
+// CLIP tower support kernels (gfx950): LayerNorm, embeddings, im2col,
+// small-sequence multi-head attention, output finalisation.
+//
+// Reference semantics (openai/CLIP model.py, restated in oracle/clip_ref.py
+// and pinned to transformers/models/clip/modeling_clip.py):
+//   LayerNorm in fp32, eps 1e-5 (OpenAI LayerNorm casts to fp32)      V2/V3/V6/V8
+//   vision embeddings: [CLS | conv1 patches] + pos -> ln_pre            V1-V2 (:202-218)
+//   text embeddings: token_embedding[t] + positional_embedding          T1
+//   attention: softmax(q k^T / sqrt(64) [+ causal mask]) v per head     V4/T2 (:280-335)
+//   text pooling at argmax(tokens) then ln_final                        T3 (:559-571)
+// The residual stream stays f32 in HBM; GEMM operands are bf16.
+#include "common.hpp"
+#include "internal.hpp"
+
+namespace miclip {
+
+namespace {
+
+constexpr float LN_EPS = 1e-5f;
+
+// ---------------------------------------------------------------- LayerNorm
+// One wave per row, W <= 1024 (4 float4 per lane), two-pass mean/variance.
+struct RowVals {
+  float4 v[4];
+};
+
+__device__ __forceinline__ void ln_stats(RowVals& r, int n4, int lane, int W, float& mean, float& rstd) {
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (lane + 64 * i < n4) s += (r.v[i].x + r.v[i].y) + (r.v[i].z + r.v[i].w);
+  mean = wave_sum(s) / (float)W;
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (lane + 64 * i < n4) {
+      const float a = r.v[i].x - mean, b = r.v[i].y - mean, c = r.v[i].z - mean, d = r.v[i].w - mean;
+      ss += (a * a + b * b) + (c * c + d * d);
+    }
+  const float var = wave_sum(ss) / (float)W;
+  rstd = 1.0f / sqrtf(var + LN_EPS);
+}
+
+__global__ __launch_bounds__(256) void ln_bf16_kernel(const float* __restrict__ x, int64_t in_stride,
+                                                      const float* __restrict__ g, const float* __restrict__ b,
+                                                      uint16_t* __restrict__ out, int64_t out_stride, int rows, int W) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const int n4 = W >> 2;
+  const float4* xr = (const float4*)(x + (int64_t)row * in_stride);
+  RowVals r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) r.v[i] = (lane + 64 * i < n4) ? xr[lane + 64 * i] : make_float4(0.f, 0.f, 0.f, 0.f);
+  float mean, rstd;
+  ln_stats(r, n4, lane, W, mean, rstd);
+  const float4* g4 = (const float4*)g;
+  const float4* b4 = (const float4*)b;
+  uint2* o = (uint2*)(out + (int64_t)row * out_stride);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = lane + 64 * i;
+    if (idx < n4) {
+      const float4 gg = g4[idx], bb = b4[idx];
+      const float y0 = (r.v[i].x - mean) * rstd * gg.x + bb.x;
+      const float y1 = (r.v[i].y - mean) * rstd * gg.y + bb.y;
+      const float y2 = (r.v[i].z - mean) * rstd * gg.z + bb.z;
+      const float y3 = (r.v[i].w - mean) * rstd * gg.w + bb.w;
+      o[idx] = make_uint2((uint32_t)f2bf(y0) | ((uint32_t)f2bf(y1) << 16),
+                          (uint32_t)f2bf(y2) | ((uint32_t)f2bf(y3) << 16));
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void vision_embed_ln_kernel(float* __restrict__ x, const float* __restrict__ cls,
+                                                              const float* __restrict__ pos, const float* __restrict__ g,
+                                                              const float* __restrict__ b, int rows, int S, int W) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const int t = row % S, n4 = W >> 2;
+  float4* xr = (float4*)(x + (int64_t)row * W);
+  const float4* src = t == 0 ? (const float4*)cls : (const float4*)xr;
+  const float4* p4 = (const float4*)(pos + (int64_t)t * W);
+  RowVals r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = lane + 64 * i;
+    if (idx < n4) {
+      const float4 s = src[idx], p = p4[idx];
+      r.v[i] = make_float4(s.x + p.x, s.y + p.y, s.z + p.z, s.w + p.w);
+    } else {
+      r.v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  float mean, rstd;
+  ln_stats(r, n4, lane, W, mean, rstd);
+  const float4* g4 = (const float4*)g;
+  const float4* b4 = (const float4*)b;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = lane + 64 * i;
+    if (idx < n4) {
+      const float4 gg = g4[idx], bb = b4[idx];
+      xr[idx] = make_float4((r.v[i].x - mean) * rstd * gg.x + bb.x, (r.v[i].y - mean) * rstd * gg.y + bb.y,
+                            (r.v[i].z - mean) * rstd * gg.z + bb.z, (r.v[i].w - mean) * rstd * gg.w + bb.w);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void text_embed_kernel(const int32_t* __restrict__ tokens,
+                                                         const float* __restrict__ tok_emb,
+                                                         const float* __restrict__ pos, float* __restrict__ x,
+                                                         int64_t total4, int S, int W, int vocab) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total4) return;
+  const int n4 = W >> 2;
+  const int64_t row = i / n4;
+  const int c = (int)(i % n4);
+  const int t = (int)(row % S);
+  int tok = tokens[row];
+  tok = tok < 0 ? 0 : (tok >= vocab ? vocab - 1 : tok);
+  const float4 e = ((const float4*)(tok_emb + (int64_t)tok * W))[c];
+  const float4 p = ((const float4*)(pos + (int64_t)t * W))[c];
+  ((float4*)x)[i] = make_float4(e.x + p.x, e.y + p.y, e.z + p.z, e.w + p.w);
+}
+
+__global__ __launch_bounds__(256) void eot_gather_ln_kernel(const int32_t* __restrict__ tokens,
+                                                            const float* __restrict__ x, const float* __restrict__ g,
+                                                            const float* __restrict__ b, uint16_t* __restrict__ out,
+                                                            int Q, int S, int W) {
+  const int q = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (q >= Q) return;
+  // argmax with first-index tie break (torch.argmax)
+  int best = -2147483647 - 1, bi = 0x7fffffff;
+  for (int t = lane; t < S; t += 64) {
+    const int v = tokens[(int64_t)q * S + t];
+    if (v > best || (v == best && t < bi)) { best = v; bi = t; }
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const int ov = __shfl_xor(best, o, 64), oi = __shfl_xor(bi, o, 64);
+    if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
+  }
+  const int n4 = W >> 2;
+  const float4* xr = (const float4*)(x + ((int64_t)q * S + bi) * W);
+  RowVals r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) r.v[i] = (lane + 64 * i < n4) ? xr[lane + 64 * i] : make_float4(0.f, 0.f, 0.f, 0.f);
+  float mean, rstd;
+  ln_stats(r, n4, lane, W, mean, rstd);
+  const float4* g4 = (const float4*)g;
+  const float4* b4 = (const float4*)b;
+  uint2* o = (uint2*)(out + (int64_t)q * W);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = lane + 64 * i;
+    if (idx < n4) {
+      const float4 gg = g4[idx], bb = b4[idx];
+      o[idx] = make_uint2((uint32_t)f2bf((r.v[i].x - mean) * rstd * gg.x + bb.x) |
+                              ((uint32_t)f2bf((r.v[i].y - mean) * rstd * gg.y + bb.y) << 16),
+                          (uint32_t)f2bf((r.v[i].z - mean) * rstd * gg.z + bb.z) |
+                              ((uint32_t)f2bf((r.v[i].w - mean) * rstd * gg.w + bb.w) << 16));
+    }
+  }
+}
+
+// ------------------------------------------------------------------ im2col
+// One thread per 8 consecutive k of one patch row.
+template <bool IN_BF16>
+__global__ __launch_bounds__(256) void im2col_kernel(const void* __restrict__ pixels, uint16_t* __restrict__ out,
+                                                     int64_t total8, int R, int P, int G, int Kp) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total8) return;
+  const int k8 = Kp >> 3;
+  const int64_t prow = i / k8;
+  const int kb = (int)(i % k8) * 8;
+  const int64_t bimg = prow / (G * G);
+  const int p = (int)(prow % (G * G));
+  const int gy = p / G, gx = p % G;
+  const int PP = P * P, K = 3 * PP;
+  uint32_t packed[4];
+#pragma unroll
+  for (int e = 0; e < 8; e += 2) {
+    float v[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int k = kb + e + u;
+      if (k < K) {
+        const int c = k / PP, rem = k % PP, kh = rem / P, kw = rem % P;
+        const int64_t off = ((bimg * 3 + c) * R + (gy * P + kh)) * (int64_t)R + gx * P + kw;
+        v[u] = IN_BF16 ? bf2f(((const uint16_t*)pixels)[off]) : ((const float*)pixels)[off];
+      } else {
+        v[u] = 0.f;
+      }
+    }
+    packed[e >> 1] = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+  }
+  *(uint4*)(out + prow * Kp + kb) = make_uint4(packed[0], packed[1], packed[2], packed[3]);
+}
+
+// --------------------------------------------------------------- attention
+// One workgroup (4 waves) per (sequence, head); head dim 64; the whole padded
+// sequence (SP rows, multiple of 32) is resident in LDS: Q and K row-major,
+// V transposed (so P.V's B operand is a contiguous 16-byte read), P per wave.
+// Rows are padded to an odd number of 16-byte slots (bank-conflict free
+// ds_read_b128).  S = Q K^T and O = P V on mfma_f32_16x16x32_bf16; softmax in
+// fp32 registers, rows reduced across the 16 lanes that share them.
+template <int SP>
+__global__ __launch_bounds__(256) void attention_kernel(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ out,
+                                                        int S, int W, int H, int causal) {
+  constexpr int QK_STRIDE = 72;        // bf16 per Q/K row (144 B = 9 slots)
+  constexpr int VT_STRIDE = SP + 8;    // bf16 per V^T / P row
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * SP * QK_STRIDE + 64 * VT_STRIDE + 4 * 16 * VT_STRIDE];
+  uint16_t* Qs = lds;
+  uint16_t* Ks = Qs + SP * QK_STRIDE;
+  uint16_t* Vt = Ks + SP * QK_STRIDE;
+  uint16_t* Ps = Vt + 64 * VT_STRIDE;
+
+  const int bh = blockIdx.x;
+  const int bseq = bh / H, h = bh % H;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t ld = 3 * (int64_t)W;
+  const uint16_t* base = qkv + (int64_t)bseq * S * ld + h * 64;
+
+  // load Q, K (row-major) and V (transposed); zero the padding rows
+  for (int c = tid; c < SP * 8; c += 256) {
+    const int r = c >> 3, ch = c & 7;
+    uint4 q = make_uint4(0, 0, 0, 0), k = q, v = q;
+    if (r < S) {
+      const uint16_t* src = base + (int64_t)r * ld + ch * 8;
+      q = *(const uint4*)src;
+      k = *(const uint4*)(src + W);
+      v = *(const uint4*)(src + 2 * W);
+    }
+    *(uint4*)(Qs + r * QK_STRIDE + ch * 8) = q;
+    *(uint4*)(Ks + r * QK_STRIDE + ch * 8) = k;
+    const uint16_t* vv = (const uint16_t*)&v;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) Vt[(ch * 8 + e) * VT_STRIDE + r] = vv[e];
+  }
+  __syncthreads();
+
+  constexpr int NKT = SP / 16;
+  const float scale = 0.125f;  // 64 ** -0.5
+  uint16_t* Pw = Ps + wave * 16 * VT_STRIDE;
+  const int nqt = (S + 15) / 16;
+  for (int qt = wave; qt < nqt; qt += 4) {
+    f32x4 sc[NKT];
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+      f32x4 c = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 a = *(const bf16x8*)(Qs + (qt * 16 + (lane & 15)) * QK_STRIDE + 32 * s + 8 * (lane >> 4));
+        const bf16x8 bb = *(const bf16x8*)(Ks + (kt * 16 + (lane & 15)) * QK_STRIDE + 32 * s + 8 * (lane >> 4));
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bb, c, 0, 0, 0);
+      }
+      sc[kt] = c;
+    }
+    // row = qt*16 + 4*(lane>>4) + j, key = kt*16 + (lane&15)
+    float mx[4], sum[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = qt * 16 + 4 * (lane >> 4) + j;
+      float m = -INFINITY;
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt) {
+        const int key = kt * 16 + (lane & 15);
+        float v = sc[kt][j] * scale;
+        if (key >= S || (causal && key > row)) v = -INFINITY;
+        sc[kt][j] = v;
+        m = fmaxf(m, v);
+      }
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+      mx[j] = m;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float s = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt) {
+        const float p = __expf(sc[kt][j] - mx[j]);
+        sc[kt][j] = p;
+        s += p;
+      }
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) s += __shfl_xor(s, o, 64);
+      sum[j] = s;
+    }
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) Pw[(4 * (lane >> 4) + j) * VT_STRIDE + kt * 16 + (lane & 15)] = f2bf(sc[kt][j]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      f32x4 o = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < SP / 32; ++s) {
+        const bf16x8 a = *(const bf16x8*)(Pw + (lane & 15) * VT_STRIDE + 32 * s + 8 * (lane >> 4));
+        const bf16x8 bb = *(const bf16x8*)(Vt + (dt * 16 + (lane & 15)) * VT_STRIDE + 32 * s + 8 * (lane >> 4));
+        o = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bb, o, 0, 0, 0);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = qt * 16 + 4 * (lane >> 4) + j;
+        if (row < S)
+          out[((int64_t)bseq * S + row) * W + h * 64 + dt * 16 + (lane & 15)] = f2bf(o[j] / sum[j]);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// ---------------------------------------------------------------- finalize
+__global__ __launch_bounds__(256) void finalize_kernel(const float* __restrict__ y, void* __restrict__ out,
+                                                       int out_dtype, int rows, int D, int l2) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const float* yr = y + (int64_t)row * D;
+  float inv = 1.f;
+  if (l2) {
+    float ss = 0.f;
+    for (int c = lane; c < D; c += 64) ss += yr[c] * yr[c];
+    const float n = sqrtf(wave_sum(ss));
+    // l2 == 2: compare_models.py:1168-1171 guard (norm <= 1e-8 -> divide by 1)
+    inv = (l2 == 2 && !(n > 1e-8f)) ? 1.0f : 1.0f / n;
+  }
+  for (int c = lane; c < D; c += 64) {
+    const float v = l2 ? yr[c] * inv : yr[c];
+    if (out_dtype == 0) ((float*)out)[(int64_t)row * D + c] = v;
+    else if (out_dtype == 1) ((uint16_t*)out)[(int64_t)row * D + c] = f2bf(v);
+    else ((_Float16*)out)[(int64_t)row * D + c] = (_Float16)v;
+  }
+}
+
+}  // namespace
+
+hipError_t layernorm_bf16(const float* x, int64_t in_stride, const float* g, const float* b, uint16_t* out,
+                          int64_t out_stride, int rows, int W, hipStream_t s) {
+  if (rows <= 0) return hipSuccess;
+  if (W % 4 || W > 1024) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(ln_bf16_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, x, in_stride, g, b, out, out_stride,
+                     rows, W);
+  return hipGetLastError();
+}
+
+hipError_t vision_embed_ln(float* x, const float* cls, const float* pos, const float* g, const float* b, int B,
+                           int S, int W, hipStream_t s) {
+  const int rows = B * S;
+  if (rows <= 0) return hipSuccess;
+  if (W % 4 || W > 1024) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(vision_embed_ln_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, x, cls, pos, g, b, rows, S, W);
+  return hipGetLastError();
+}
+
+hipError_t text_embed(const int32_t* tokens, const float* tok_emb, const float* pos, float* x, int Q, int S, int W,
+                      int vocab, hipStream_t s) {
+  const int64_t total4 = (int64_t)Q * S * (W / 4);
+  if (total4 <= 0) return hipSuccess;
+  hipLaunchKernelGGL(text_embed_kernel, dim3((unsigned)((total4 + 255) / 256)), dim3(256), 0, s, tokens, tok_emb,
+                     pos, x, total4, S, W, vocab);
+  return hipGetLastError();
+}
+
+hipError_t eot_gather_ln(const int32_t* tokens, const float* x, const float* g, const float* b, uint16_t* out, int Q,
+                         int S, int W, hipStream_t s) {
+  if (Q <= 0) return hipSuccess;
+  hipLaunchKernelGGL(eot_gather_ln_kernel, dim3((Q + 3) / 4), dim3(256), 0, s, tokens, x, g, b, out, Q, S, W);
+  return hipGetLastError();
+}
+
+hipError_t im2col(const void* pixels, int in_bf16, uint16_t* out, int B, int R, int P, int Kp, hipStream_t s) {
+  const int G = R / P;
+  const int64_t total8 = (int64_t)B * G * G * (Kp / 8);
+  if (total8 <= 0) return hipSuccess;
+  const dim3 grid((unsigned)((total8 + 255) / 256));
+  if (in_bf16)
+    hipLaunchKernelGGL(im2col_kernel<true>, grid, dim3(256), 0, s, pixels, out, total8, R, P, G, Kp);
+  else
+    hipLaunchKernelGGL(im2col_kernel<false>, grid, dim3(256), 0, s, pixels, out, total8, R, P, G, Kp);
+  return hipGetLastError();
+}
+
+hipError_t attention(const uint16_t* qkv, uint16_t* out, int B, int S, int W, int causal, hipStream_t s) {
+  const int H = W / 64;
+  const dim3 grid(B * H), block(256);
+  if (B <= 0) return hipSuccess;
+  if (S <= 32) hipLaunchKernelGGL(attention_kernel<32>, grid, block, 0, s, qkv, out, S, W, H, causal);
+  else if (S <= 64) hipLaunchKernelGGL(attention_kernel<64>, grid, block, 0, s, qkv, out, S, W, H, causal);
+  else if (S <= 96) hipLaunchKernelGGL(attention_kernel<96>, grid, block, 0, s, qkv, out, S, W, H, causal);
+  else if (S <= 128) hipLaunchKernelGGL(attention_kernel<128>, grid, block, 0, s, qkv, out, S, W, H, causal);
+  else if (S <= 224) hipLaunchKernelGGL(attention_kernel<224>, grid, block, 0, s, qkv, out, S, W, H, causal);
+  else if (S <= 288) hipLaunchKernelGGL(attention_kernel<288>, grid, block, 0, s, qkv, out, S, W, H, causal);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+hipError_t finalize_rows(const float* y, void* out, int out_dtype, int rows, int D, int l2, hipStream_t s) {
+  if (rows <= 0) return hipSuccess;
+  hipLaunchKernelGGL(finalize_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, y, out, out_dtype, rows, D, l2);
+  return hipGetLastError();
+}
+
+}  // namespace miclip

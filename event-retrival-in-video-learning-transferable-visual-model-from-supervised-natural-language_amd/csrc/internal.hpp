@@ -1,0 +1,64 @@
+// Host-side launchers shared between the kernel translation units and api.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace miclip {
+
+enum GemmEpi {
+  EPI_BF16 = 0,        // out bf16 = acc + bias
+  EPI_GELU_BF16 = 1,   // out bf16 = quick_gelu(acc + bias)
+  EPI_RESID_F32 = 2,   // out f32 += acc + bias   (residual stream, in place)
+  EPI_F32 = 3          // out f32 = acc (+ bias)
+};
+
+struct GemmArgs {
+  const uint16_t* A;  // [M, K] bf16, row stride lda
+  const uint16_t* W;  // [N, K] bf16 (nn.Linear layout), row stride ldw
+  const float* bias;  // [N] or nullptr
+  void* out;          // see epilogue
+  int64_t lda, ldw, ldo;
+  int M, N, K;
+  // output row remap: r -> (r / group) * gstride + goffset + r % group (group == 0: identity)
+  int group, gstride, goffset;
+};
+
+// Requirements: K % 64 == 0, N % 128 == 0, A/W 16-byte aligned rows.
+hipError_t gemm_bf16(const GemmArgs& a, int epi, hipStream_t s);
+
+// out[r] = LN(x[r * in_stride]) over W features; out is bf16 (row stride out_stride).
+hipError_t layernorm_bf16(const float* x, int64_t in_stride, const float* g, const float* b,
+                          uint16_t* out, int64_t out_stride, int rows, int W, hipStream_t s);
+// x[b*S + t] = LN((t == 0 ? cls : x[b*S + t]) + pos[t]) in place (f32)
+hipError_t vision_embed_ln(float* x, const float* cls, const float* pos, const float* g,
+                           const float* b, int B, int S, int W, hipStream_t s);
+// x[q*S + t] = tok_emb[tokens[q*S + t]] + pos[t]
+hipError_t text_embed(const int32_t* tokens, const float* tok_emb, const float* pos, float* x,
+                      int Q, int S, int W, int vocab, hipStream_t s);
+// out[q] = LN(x[q*S + argmax_t tokens[q*S + t]]) bf16
+hipError_t eot_gather_ln(const int32_t* tokens, const float* x, const float* g, const float* b,
+                         uint16_t* out, int Q, int S, int W, hipStream_t s);
+// pixels [B,3,R,R] (f32 or bf16) -> patches [B*G*G, Kp] bf16, k = c*P*P + kh*P + kw, zero pad to Kp
+hipError_t im2col(const void* pixels, int in_bf16, uint16_t* out, int B, int R, int P, int Kp,
+                  hipStream_t s);
+// multi-head attention over qkv [B*S, 3W] bf16 -> out [B*S, W] bf16, head dim 64
+hipError_t attention(const uint16_t* qkv, uint16_t* out, int B, int S, int W, int causal,
+                     hipStream_t s);
+// y [rows, D] f32 -> out (f32/bf16/f16), optional L2 normalisation
+hipError_t finalize_rows(const float* y, void* out, int out_dtype, int rows, int D, int l2,
+                         hipStream_t s);
+
+}  // namespace miclip
+
+namespace miclip {
+size_t rank_workspace_bytes(int64_t N, int64_t Q, int k);
+hipError_t rank_topk(const void* corpus, int64_t N, int64_t D, int dt, const float* q, int64_t Q, int k,
+                     int64_t base, int norm_mode, int nan_first, float* out_s, int64_t* out_i, void* ws,
+                     hipStream_t s);
+hipError_t rank_merge(const float* cs, const int64_t* ci, int64_t Q, int64_t C, int k, int nan_first, float* out_s,
+                      int64_t* out_i, hipStream_t s);
+hipError_t score_matrix(const void* corpus, int64_t N, int64_t D, int dt, const float* q, int64_t Q, int norm_mode,
+                        float* out, hipStream_t s);
+hipError_t rank_of_targets(const float* S, int64_t Q, int64_t N, const int64_t* pq, const int64_t* pt, int64_t T,
+                           int64_t* out, hipStream_t s);
+}  // namespace miclip

@@ -1,0 +1,137 @@
+"""ctypes binding of ``libmiclip.so`` (C-ABI declared in ``include/miclip.h``).
+
+There is deliberately no CPU fallback: if the library is missing or cannot be
+loaded, every entry point raises.  ``torch`` is used only for device memory,
+streams and dtypes (plumbing); all compute runs in the HIP kernels.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from .config import CLIPConfig
+
+LIB_NAME = "libmiclip.so"
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+
+MI_F32, MI_BF16, MI_F16 = 0, 1, 2
+MI_NAN_FIRST, MI_NAN_LAST = 0, 1
+MI_NORM_L2, MI_NORM_L2_GUARD, MI_NORM_NONE = 0, 1, 2
+
+# every symbol include/miclip.h declares (checked by tests/test_abi.py)
+EXPORTS = (
+    "mi_abi_version", "mi_last_error", "mi_clip_weights_numel", "mi_clip_create", "mi_clip_destroy",
+    "mi_clip_reserve", "mi_clip_encode_image", "mi_clip_encode_text", "mi_rank_workspace_bytes",
+    "mi_rank_topk", "mi_rank_merge", "mi_score_matrix", "mi_rank_of_targets",
+    "mi_op_gemm", "mi_op_layernorm", "mi_op_attention",
+)
+
+
+class MiClipError(RuntimeError):
+    pass
+
+
+class Arch(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in (
+        "embed_dim", "image_resolution", "vision_layers", "vision_width", "vision_patch_size",
+        "context_length", "vocab_size", "text_width", "text_heads", "text_layers")]
+
+    @classmethod
+    def from_config(cls, cfg: CLIPConfig) -> "Arch":
+        return cls(cfg.embed_dim, cfg.image_resolution, cfg.vision_layers, cfg.vision_width,
+                   cfg.vision_patch_size, cfg.context_length, cfg.vocab_size, cfg.text_width,
+                   cfg.text_heads, cfg.text_layers)
+
+
+_lib = None
+
+
+def lib():
+    """Load libmiclip.so once; raise if it is absent (no silent fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.isfile(LIB_PATH):
+        raise MiClipError(f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+                          " or `make -C <pkg>/csrc`")
+    L = ctypes.CDLL(LIB_PATH)
+    P, I32, I64, SZ = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_size_t
+    sig = {
+        "mi_abi_version": (ctypes.c_int, []),
+        "mi_last_error": (ctypes.c_char_p, []),
+        "mi_clip_weights_numel": (I64, [ctypes.POINTER(Arch)]),
+        "mi_clip_create": (ctypes.c_int, [ctypes.POINTER(Arch), P, I64, ctypes.c_int, ctypes.c_int,
+                                          ctypes.POINTER(P)]),
+        "mi_clip_destroy": (ctypes.c_int, [P]),
+        "mi_clip_reserve": (ctypes.c_int, [P, I64, I64]),
+        "mi_clip_encode_image": (ctypes.c_int, [P, P, I64, ctypes.c_int, P, ctypes.c_int, ctypes.c_int, P]),
+        "mi_clip_encode_text": (ctypes.c_int, [P, P, I64, P, ctypes.c_int, ctypes.c_int, P]),
+        "mi_rank_workspace_bytes": (SZ, [I64, I64, I32]),
+        "mi_rank_topk": (ctypes.c_int, [P, I64, I64, ctypes.c_int, P, I64, I32, I64, ctypes.c_int, ctypes.c_int,
+                                        P, P, P, SZ, P]),
+        "mi_rank_merge": (ctypes.c_int, [P, P, I64, I64, I32, ctypes.c_int, P, P, P]),
+        "mi_score_matrix": (ctypes.c_int, [P, I64, I64, ctypes.c_int, P, I64, ctypes.c_int, P, P]),
+        "mi_rank_of_targets": (ctypes.c_int, [P, I64, I64, P, P, I64, P, P]),
+        "mi_op_gemm": (ctypes.c_int, [P, P, P, P, I32, I32, I32, I32, P]),
+        "mi_op_layernorm": (ctypes.c_int, [P, P, P, P, I32, I32, P]),
+        "mi_op_attention": (ctypes.c_int, [P, P, I32, I32, I32, I32, P]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    if L.mi_abi_version() != 1:
+        raise MiClipError("libmiclip ABI version mismatch")
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = lib().mi_last_error().decode(errors="replace")
+        raise MiClipError(f"{what} failed ({rc}): {msg}")
+
+
+def weight_order(cfg: CLIPConfig):
+    """Canonical blob order (DESIGN.md "Weight blob"): OpenAI state-dict keys."""
+    def tower(prefix, layers):
+        keys = []
+        for i in range(layers):
+            p = f"{prefix}resblocks.{i}."
+            keys += [p + k for k in ("ln_1.weight", "ln_1.bias", "attn.in_proj_weight", "attn.in_proj_bias",
+                                     "attn.out_proj.weight", "attn.out_proj.bias", "ln_2.weight", "ln_2.bias",
+                                     "mlp.c_fc.weight", "mlp.c_fc.bias", "mlp.c_proj.weight", "mlp.c_proj.bias")]
+        return keys
+    return (["visual.conv1.weight", "visual.class_embedding", "visual.positional_embedding",
+             "visual.ln_pre.weight", "visual.ln_pre.bias"] + tower("visual.transformer.", cfg.vision_layers)
+            + ["visual.ln_post.weight", "visual.ln_post.bias", "visual.proj",
+               "token_embedding.weight", "positional_embedding"] + tower("transformer.", cfg.text_layers)
+            + ["ln_final.weight", "ln_final.bias", "text_projection", "logit_scale"])
+
+
+def pack_weights(sd, cfg: CLIPConfig) -> np.ndarray:
+    parts = []
+    for k in weight_order(cfg):
+        if k not in sd:
+            raise MiClipError(f"state dict is missing {k}")
+        parts.append(np.ascontiguousarray(np.asarray(sd[k], dtype=np.float32)).reshape(-1))
+    blob = np.concatenate(parts)
+    expect = lib().mi_clip_weights_numel(ctypes.byref(Arch.from_config(cfg)))
+    if blob.size != expect:
+        raise MiClipError(f"packed {blob.size} weights, the library expects {expect}")
+    return blob
+
+
+def stream_ptr(device=None) -> int:
+    import torch
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def dtype_code(t) -> int:
+    import torch
+    m = {torch.float32: MI_F32, torch.bfloat16: MI_BF16, torch.float16: MI_F16}
+    if t not in m:
+        raise MiClipError(f"unsupported dtype {t}")
+    return m[t]

@@ -1,0 +1,43 @@
+"""Standalone folder -> ``.npy`` embedder: mirror of
+``Backend/embedding.py:9-59`` ``extract_and_save_embeddings_from_folder``.
+
+Same walk order (``os.walk``), same extensions, same UN-normalised rows
+(``embedding.py:48-56``), same ``{video_name}_embeddings.npy`` naming.  The
+reference encodes one image per call and hard-codes a Windows output
+directory; here frames are encoded in batches on the GPU (results are
+per-frame, so batching does not change them) and ``output_dir`` is a
+parameter (default ``./embedding``).
+"""
+from __future__ import annotations
+
+import os
+from pathlib import Path
+
+import numpy as np
+
+from . import api
+
+
+def extract_and_save_embeddings_from_folder(folder_path, model_name, video_name=None, output_dir="embedding",
+                                            batch_size=256, model=None, preprocess=None):
+    import torch
+    from PIL import Image
+
+    if model is None:
+        model, preprocess = api.load(model_name, device="cuda")
+    os.makedirs(output_dir, exist_ok=True)
+    if not video_name:
+        video_name = Path(folder_path).name
+    output_file = os.path.join(output_dir, f"{video_name}_embeddings.npy")
+    paths = []
+    for root, _, files in os.walk(folder_path):
+        for file in files:
+            if file.lower().endswith((".jpg", ".jpeg", ".png")):
+                paths.append(os.path.join(root, file))
+    rows = []
+    for i in range(0, len(paths), batch_size):
+        batch = torch.stack([preprocess(Image.open(p).convert("RGB")) for p in paths[i:i + batch_size]])
+        rows.append(model.encode_image(batch, out_dtype=torch.float32).cpu().numpy())
+    all_embeddings = np.vstack(rows) if rows else np.zeros((0, model.visual.output_dim), np.float32)
+    np.save(output_file, all_embeddings)
+    return output_file

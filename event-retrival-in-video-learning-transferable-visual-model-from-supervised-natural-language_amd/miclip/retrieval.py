@@ -1,0 +1,121 @@
+"""Device-side ranking: the fused normalise + cosine + top-k kernel and the
+R@K helpers, behind torch tensors.
+
+Reference call sites this replaces:
+  ``np.dot(embeddings, text_features.T)`` + ``np.argsort(s)[::-1][:top_k]``
+      Backend/services/embedding_service.py:314-320 (text) and :365-372 (image query)
+  ``image_features @ text_features.T`` + per-query ``np.argsort(-s)`` rank of GT
+      Backend/content/Test_compare_model/compare_models.py:999-1016, 1045-1062
+
+Order rule (documented in include/miclip.h): score descending, then index
+ascending; NaN (a zero-norm row divided by its norm) first for the
+``search_top_frames`` semantics (``argsort(s)[::-1]``), last for the
+``compare_models`` semantics (``argsort(-s)``).
+"""
+from __future__ import annotations
+
+import threading
+
+from . import _native as N
+
+_NORMS = {"l2": N.MI_NORM_L2, "l2_guard": N.MI_NORM_L2_GUARD, "none": N.MI_NORM_NONE}
+_NANS = {"first": N.MI_NAN_FIRST, "last": N.MI_NAN_LAST}
+MAX_K = 64
+
+_ws_lock = threading.Lock()
+_ws = {}
+
+
+def _workspace(device, nbytes):
+    import torch
+    with _ws_lock:
+        buf = _ws.get(device)
+        if buf is None or buf.numel() < nbytes:
+            buf = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
+            _ws[device] = buf
+        return buf
+
+
+def _corpus(corpus):
+    import torch
+    if corpus.dim() != 2:
+        raise N.MiClipError("corpus must be [N, D]")
+    if corpus.dtype not in (torch.float32, torch.bfloat16, torch.float16):
+        corpus = corpus.float()
+    return corpus.contiguous()
+
+
+def _queries(queries, device):
+    import torch
+    q = queries if queries.dim() == 2 else queries.reshape(1, -1)
+    return q.to(device=device, dtype=torch.float32).contiguous()
+
+
+def rank_topk(corpus, queries, k, index_base=0, norm="l2", nan_policy="first"):
+    """Top-k rows of ``corpus`` [N,D] (device) for each query [Q,D].
+
+    Returns (scores f32 [Q, min(k,N)], index int64 [Q, min(k,N)]) on the device.
+    """
+    import torch
+    if not corpus.is_cuda:
+        raise N.MiClipError("rank_topk runs on the GPU: move the corpus to the device first")
+    c = _corpus(corpus)
+    q = _queries(queries, c.device)
+    if q.shape[1] != c.shape[1]:
+        raise N.MiClipError(f"dimension mismatch: corpus D={c.shape[1]}, queries D={q.shape[1]}")
+    Nrows, D = c.shape
+    Q = q.shape[0]
+    if not 1 <= k <= MAX_K:
+        raise N.MiClipError(f"k must be in [1, {MAX_K}]")
+    out_s = torch.empty((Q, k), dtype=torch.float32, device=c.device)
+    out_i = torch.empty((Q, k), dtype=torch.int64, device=c.device)
+    L = N.lib()
+    nbytes = L.mi_rank_workspace_bytes(Nrows, Q, k)
+    with torch.cuda.device(c.device):
+        ws = _workspace(c.device, nbytes)
+        N.check(L.mi_rank_topk(c.data_ptr(), Nrows, D, N.dtype_code(c.dtype), q.data_ptr(), Q, k, int(index_base),
+                               _NORMS[norm], _NANS[nan_policy], out_s.data_ptr(), out_i.data_ptr(), ws.data_ptr(),
+                               ws.numel(), N.stream_ptr(c.device)), "mi_rank_topk")
+    kk = min(k, Nrows)
+    return out_s[:, :kk], out_i[:, :kk]
+
+
+def merge_topk(cand_scores, cand_index, k, nan_policy="first"):
+    """Merge [Q, C] candidate lists (index -1 = empty) into the top-k (device)."""
+    import torch
+    s = cand_scores.to(torch.float32).contiguous()
+    i = cand_index.to(torch.int64).contiguous()
+    Q, C = s.shape
+    out_s = torch.empty((Q, k), dtype=torch.float32, device=s.device)
+    out_i = torch.empty((Q, k), dtype=torch.int64, device=s.device)
+    with torch.cuda.device(s.device):
+        N.check(N.lib().mi_rank_merge(s.data_ptr(), i.data_ptr(), Q, C, k, _NANS[nan_policy], out_s.data_ptr(),
+                                      out_i.data_ptr(), N.stream_ptr(s.device)), "mi_rank_merge")
+    return out_s, out_i
+
+
+def score_matrix(corpus, queries, norm="none"):
+    """[Q, N] f32 scores <q, c/|c|> with fp32-exact products (device)."""
+    import torch
+    c = _corpus(corpus)
+    q = _queries(queries, c.device)
+    out = torch.empty((q.shape[0], c.shape[0]), dtype=torch.float32, device=c.device)
+    with torch.cuda.device(c.device):
+        N.check(N.lib().mi_score_matrix(c.data_ptr(), c.shape[0], c.shape[1], N.dtype_code(c.dtype), q.data_ptr(),
+                                        q.shape[0], _NORMS[norm], out.data_ptr(), N.stream_ptr(c.device)),
+                "mi_score_matrix")
+    return out
+
+
+def rank_of_targets(scores, pair_query, pair_target):
+    """1-based rank of scores[q, g] in argsort(-scores[q]) for each (q, g) pair."""
+    import torch
+    s = scores.to(torch.float32).contiguous()
+    pq = torch.as_tensor(pair_query, dtype=torch.int64).to(s.device).contiguous()
+    pt = torch.as_tensor(pair_target, dtype=torch.int64).to(s.device).contiguous()
+    out = torch.empty(pq.shape[0], dtype=torch.int64, device=s.device)
+    with torch.cuda.device(s.device):
+        N.check(N.lib().mi_rank_of_targets(s.data_ptr(), s.shape[0], s.shape[1], pq.data_ptr(), pt.data_ptr(),
+                                           pq.shape[0], out.data_ptr(), N.stream_ptr(s.device)),
+                "mi_rank_of_targets")
+    return out

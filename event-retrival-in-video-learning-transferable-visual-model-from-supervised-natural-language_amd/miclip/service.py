@@ -1,0 +1,291 @@
+"""``EmbeddingService`` with the reference's interface, ranking on the GPU.
+
+Mirror of ``Backend/services/embedding_service.py:69-536`` — same constructor
+(injected cache/path/data services), same method names, arguments, return
+types and swallow-to-``[]``/``0.0`` error semantics (:280-282, :342-344), so
+``Backend/app.py`` and ``Backend/query_strategies.py`` (which receive
+``search_top_frames`` / ``extract_query_confidence`` as callables,
+app.py:157-174) work unchanged.  What moves to the device:
+
+  get_text_features      clip.tokenize -> encode_text (+L2 in the kernel)      :151-184
+  search_top_frames      np.dot + np.argsort(s)[::-1][:k] -> one fused kernel  :284-344
+                         over the HBM-resident corpus (file rows, normalised
+                         in-kernel, as get_embeddings does at load :209-210)
+  search_top_frames_by_image                                                    :346-392
+  extract_and_save_embeddings_from_folder  batches -> encode_image (+L2)      :425-536
+
+The frame list (row order) still comes from ``data_service.load_frames_from_json``
+(data_service.py:48), and ``get_embeddings`` keeps returning the normalised
+numpy array other callers (visualization_service) expect.
+"""
+from __future__ import annotations
+
+import json
+import os
+
+import numpy as np
+
+from . import api
+from .retrieval import MAX_K, rank_topk, score_matrix
+from .weights import load_state_dict
+
+
+class FinetunedCLIP:
+    """Inference side of ``CLIPWithClassifier`` (embedding_service.py:16-67):
+    ``model(images)`` = L2-normalised image features; the 3-class head is only
+    used for training and is not evaluated here."""
+
+    def __init__(self, clip_model):
+        self.clip_model = clip_model.float()
+        self.logit_scale = clip_model.logit_scale
+
+    def __call__(self, images, texts=None, get_embeddings=False):
+        if texts is not None:
+            raise NotImplementedError("classification head forward is training-only (out of scope)")
+        return self.clip_model.encode_image(images, normalize=True)
+
+    def eval(self):
+        return self
+
+    def to(self, device):
+        self.clip_model.to(device)
+        return self
+
+
+class EmbeddingService:
+    def __init__(self, cache_service, path_service, data_service, device="cuda", model_name="ViT-B/32",
+                 checkpoint_path=None):
+        self.cache_service = cache_service
+        self.path_service = path_service
+        self.data_service = data_service
+        self.device = device
+        self.model_name = model_name
+        self.original_model, self.preprocess = api.load(model_name, device=device)
+        self.finetuned_model = None
+        self.active_model = "original"
+        self.checkpoint_path = checkpoint_path or os.environ.get("CLIP_FINETUNED_CHECKPOINT", "")
+        self._device_corpus = {}
+        self._lookup = {}
+        if self.checkpoint_path and os.path.exists(self.checkpoint_path):
+            try:
+                self._load_finetuned_model(self.checkpoint_path)
+            except Exception as e:  # reference: print and continue (:98-99)
+                print(f"Error loading finetuned model: {e}")
+
+    # ----------------------------------------------------------- model state
+    def _load_finetuned_model(self, checkpoint_path):
+        sd = load_state_dict(checkpoint_path)       # unwraps model_state_dict / clip_model.*
+        model, _ = api.load(self.model_name, device=self.device)
+        model.load_state_dict(sd)
+        self.finetuned_model = FinetunedCLIP(model)
+
+    def set_active_model(self, model_name):
+        if model_name == "original":
+            self.active_model = "original"
+            return True
+        if model_name == "finetuned":
+            if self.finetuned_model is not None:
+                self.active_model = "finetuned"
+                return True
+            return False
+        return False
+
+    def get_active_model_name(self):
+        return self.active_model
+
+    def _clip(self):
+        if self.active_model == "finetuned" and self.finetuned_model is not None:
+            return self.finetuned_model.clip_model
+        return self.original_model
+
+    # ------------------------------------------------------------- features
+    def get_text_features(self, query, video_name=None):
+        cache_key = f"{self.active_model}_{query}_{video_name or 'default'}"
+        features = self.cache_service.get_text_features(cache_key, video_name)
+        if features is not None:
+            return features
+        tokens = api.tokenize([query])
+        feats = self._clip().encode_text(tokens, normalize=True, out_dtype=__import__("torch").float32)
+        features = feats.cpu().numpy()
+        self.cache_service.set_text_features(cache_key, video_name, features)
+        return features
+
+    def get_embeddings(self, video_name=None):
+        embeddings_path = self.path_service.get_embeddings_path(video_name)
+        embeddings = self.cache_service.get_embeddings(embeddings_path)
+        if embeddings is not None:
+            return embeddings
+        if not os.path.exists(embeddings_path):
+            print(f"Warning: Embeddings file not found: {embeddings_path}")
+            return None
+        try:
+            embeddings = np.load(embeddings_path)
+            embeddings = embeddings / np.linalg.norm(embeddings, axis=-1, keepdims=True)
+            self.cache_service.set_embeddings(embeddings_path, embeddings)
+            return embeddings
+        except Exception as e:
+            print(f"Error loading embeddings: {e}")
+            return None
+
+    def _corpus_on_device(self, video_name):
+        """Raw file rows resident in HBM (fp32 or fp16 as stored); the rank
+        kernel normalises each row in the same pass."""
+        import torch
+        path = self.path_service.get_embeddings_path(video_name)
+        if not os.path.exists(path):
+            return None
+        mtime = os.path.getmtime(path)
+        hit = self._device_corpus.get(path)
+        if hit is not None and hit[0] == mtime:
+            return hit[1]
+        raw = np.load(path)
+        if raw.dtype not in (np.float32, np.float16):
+            raw = raw.astype(np.float32)
+        t = torch.from_numpy(np.ascontiguousarray(raw)).to(self.original_model.device)
+        self._device_corpus[path] = (mtime, t)
+        return t
+
+    def _frames(self, video_name):
+        json_path = self.path_service.get_metadata_path(video_name)
+        frames = self.cache_service.get_frames_list(json_path)
+        if frames is None:
+            frames = self.data_service.load_frames_from_json(video_name)
+            self.cache_service.set_frames_list(json_path, frames)
+        return frames
+
+    def _rank(self, corpus, query_vec, top_k):
+        """Top-k (score desc, index asc; NaN first as argsort(s)[::-1])."""
+        import torch
+        k = min(int(top_k), corpus.shape[0])
+        if k <= 0:
+            return np.zeros(0, np.float32), np.zeros(0, np.int64)
+        q = torch.as_tensor(np.asarray(query_vec, dtype=np.float32).reshape(1, -1), device=corpus.device)
+        if k <= MAX_K:
+            s, i = rank_topk(corpus, q, k, norm="l2", nan_policy="first")
+            return s[0].cpu().numpy(), i[0].cpu().numpy()
+        # large k: fused score kernel, then a stable device sort (descending,
+        # ties by index; torch sorts NaN as largest -> first)
+        s = score_matrix(corpus, q, norm="l2")[0]
+        order = torch.sort(s, descending=True, stable=True).indices[:k]
+        return s[order].cpu().numpy(), order.cpu().numpy()
+
+    # --------------------------------------------------------------- search
+    def extract_query_confidence(self, frame_path, query, video_name=None):
+        try:
+            text_features = self.get_text_features(query, video_name)
+            embeddings = self.get_embeddings(video_name)
+            if embeddings is None:
+                return 0.0
+            frames = self._frames(video_name)
+            cached = self._lookup.get(id(frames))
+            if cached is None or cached[0] is not frames:
+                # first occurrence wins, as list.index (embedding_service.py:264-271)
+                by_path = {f: i for i, f in reversed(list(enumerate(frames)))}
+                by_name = {os.path.basename(f): i for i, f in reversed(list(enumerate(frames)))}
+                cached = (frames, by_path, by_name)
+                self._lookup[id(frames)] = cached
+            index = cached[1].get(frame_path)
+            if index is None:
+                index = cached[2].get(os.path.basename(frame_path))
+                if index is None:
+                    return 0.0
+            return float(np.dot(embeddings[index:index + 1], text_features.T)[0][0])
+        except Exception as e:
+            print(f"Error extracting query confidence: {e}")
+            return 0.0
+
+    def search_top_frames(self, query, top_k, video_name=None):
+        try:
+            cache_key = f"search_{self.active_model}_{query}_{top_k}"
+            cached = self.cache_service.get_search_results(cache_key, video_name)
+            if cached is not None:
+                return cached
+            text_features = self.get_text_features(query, video_name)
+            corpus = self._corpus_on_device(video_name)
+            if corpus is None:
+                return []
+            _, idx = self._rank(corpus, text_features, top_k)
+            frames = self._frames(video_name)
+            top_frames = [frames[i] for i in idx]
+            self.cache_service.set_search_results(cache_key, video_name, top_frames)
+            return top_frames
+        except Exception as e:
+            print(f"Error in search_top_frames: {e}")
+            return []
+
+    def search_top_frames_by_image(self, image_features, top_k, video_name=None):
+        try:
+            corpus = self._corpus_on_device(video_name)
+            if corpus is None:
+                return []
+            _, idx = self._rank(corpus, np.asarray(image_features, dtype=np.float32).reshape(-1), top_k)
+            frames = self._frames(video_name)
+            return [frames[i] for i in idx]
+        except Exception as e:
+            print(f"Error in search_top_frames_by_image: {e}")
+            return []
+
+    # --------------------------------------------------------------- ingest
+    def extract_image_embedding(self, image_path):
+        try:
+            from PIL import Image
+            import torch
+            image = self.preprocess(Image.open(image_path)).unsqueeze(0)
+            if self.active_model == "finetuned" and self.finetuned_model is not None:
+                feats = self.finetuned_model(image)
+            else:
+                feats = self.original_model.encode_image(image, normalize=True, out_dtype=torch.float32)
+            return feats.float().cpu().numpy()
+        except Exception as e:
+            print(f"Error extracting embedding from {image_path}: {e}")
+            return None
+
+    def extract_and_save_embeddings_from_folder(self, folder_path, model_name=None, video_name=None,
+                                                batch_size=256):
+        import torch
+        from PIL import Image
+
+        current = self.active_model
+        if model_name:
+            if model_name == "finetuned" and self.finetuned_model is None:
+                model_name = "original"
+            self.set_active_model(model_name)
+        embeddings_path = self.path_service.get_embeddings_path(video_name)
+        os.makedirs(os.path.dirname(embeddings_path) or ".", exist_ok=True)
+        frame_files = sorted(f for f in os.listdir(folder_path) if f.endswith((".jpg", ".jpeg", ".png")))
+        if not frame_files:
+            self.set_active_model(current)
+            return None
+        model = self._clip()
+        R = model.cfg.image_resolution
+        out = []
+        last = None
+        for i in range(0, len(frame_files), batch_size):
+            imgs = []
+            for f in frame_files[i:i + batch_size]:
+                try:
+                    last = self.preprocess(Image.open(os.path.join(folder_path, f)).convert("RGB"))
+                    imgs.append(last)
+                except Exception as e:
+                    print(f"Error preprocessing image {f}: {e}")
+                    imgs.append(torch.zeros(3, R, R))
+            batch = torch.stack(imgs)
+            out.append(model.encode_image(batch, normalize=True, out_dtype=torch.float32).cpu().numpy())
+        embeddings = np.vstack(out)
+        np.save(embeddings_path, embeddings)
+        metadata_path = self.path_service.get_metadata_path(video_name)
+        if os.path.exists(metadata_path):
+            try:
+                with open(metadata_path, "r", encoding="utf-8") as f:
+                    metadata = json.load(f)
+                if isinstance(metadata, list):
+                    for item in metadata:
+                        item["embedding_model"] = self.active_model
+                elif isinstance(metadata, dict):
+                    metadata["embedding_model"] = self.active_model
+                with open(metadata_path, "w", encoding="utf-8") as f:
+                    json.dump(metadata, f, ensure_ascii=False, indent=2)
+            except Exception as e:
+                print(f"Error updating metadata with model info: {e}")
+        self.set_active_model(current)
+        return embeddings_path

@@ -1,0 +1,135 @@
+"""``clip.tokenize`` — CLIP's byte-level BPE (openai/CLIP ``simple_tokenizer``
+algorithm, restated) over a LOCAL vocabulary file.
+
+Call sites: ``embedding_service.py:169`` (``clip.tokenize([q])``) and
+``compare_models.py:1202`` (``truncate=True``).  The BPE merges file
+(``bpe_simple_vocab_16e6.txt.gz``) is not in the container, so
+it is read from ``$CLIP_BPE_PATH`` or an explicit path; without it tokenize
+raises and callers pass token ids directly (the bench and the parity tests do).
+Tokenizer parity against openai/CLIP is therefore **unpinned** here.
+"""
+from __future__ import annotations
+
+import functools
+import gzip
+import html
+import os
+
+import regex as re
+
+SOT = "<|startoftext|>"
+EOT = "<|endoftext|>"
+
+
+@functools.lru_cache()
+def bytes_to_unicode():
+    bs = list(range(ord("!"), ord("~") + 1)) + list(range(ord("¡"), ord("¬") + 1)) + list(range(ord("®"), ord("ÿ") + 1))
+    cs = bs[:]
+    n = 0
+    for b in range(256):
+        if b not in bs:
+            bs.append(b)
+            cs.append(256 + n)
+            n += 1
+    return dict(zip(bs, [chr(c) for c in cs]))
+
+
+def _pairs(word):
+    return {(a, b) for a, b in zip(word[:-1], word[1:])}
+
+
+def _clean(text):
+    text = html.unescape(html.unescape(text))
+    return re.sub(r"\s+", " ", text.strip()).strip()
+
+
+class SimpleTokenizer:
+    def __init__(self, bpe_path: str, n_merges: int = 49152 - 256 - 2):
+        opener = gzip.open if bpe_path.endswith(".gz") else open
+        with opener(bpe_path, "rb") as f:
+            lines = f.read().decode("utf-8").split("\n")
+        merges = [tuple(m.split()) for m in lines[1:n_merges + 1] if m.strip()]
+        self.byte_encoder = bytes_to_unicode()
+        vocab = list(self.byte_encoder.values())
+        vocab = vocab + [v + "</w>" for v in vocab]
+        vocab += ["".join(m) for m in merges]
+        vocab += [SOT, EOT]
+        self.encoder = {v: i for i, v in enumerate(vocab)}
+        self.decoder = {i: v for v, i in self.encoder.items()}
+        self.bpe_ranks = {m: i for i, m in enumerate(merges)}
+        self.cache = {SOT: SOT, EOT: EOT}
+        self.pat = re.compile(r"""<\|startoftext\|>|<\|endoftext\|>|'s|'t|'re|'ve|'m|'ll|'d|[\p{L}]+|[\p{N}]|[^\s\p{L}\p{N}]+""",
+                              re.IGNORECASE)
+
+    def bpe(self, token):
+        if token in self.cache:
+            return self.cache[token]
+        word = tuple(token[:-1]) + (token[-1] + "</w>",)
+        pairs = _pairs(word)
+        if not pairs:
+            return token + "</w>"
+        while True:
+            bigram = min(pairs, key=lambda p: self.bpe_ranks.get(p, float("inf")))
+            if bigram not in self.bpe_ranks:
+                break
+            first, second = bigram
+            new_word = []
+            i = 0
+            while i < len(word):
+                try:
+                    j = word.index(first, i)
+                except ValueError:
+                    new_word.extend(word[i:])
+                    break
+                new_word.extend(word[i:j])
+                i = j
+                if word[i] == first and i < len(word) - 1 and word[i + 1] == second:
+                    new_word.append(first + second)
+                    i += 2
+                else:
+                    new_word.append(word[i])
+                    i += 1
+            word = tuple(new_word)
+            if len(word) == 1:
+                break
+            pairs = _pairs(word)
+        out = " ".join(word)
+        self.cache[token] = out
+        return out
+
+    def encode(self, text):
+        ids = []
+        text = _clean(text).lower()
+        for tok in re.findall(self.pat, text):
+            tok = "".join(self.byte_encoder[b] for b in tok.encode("utf-8"))
+            ids.extend(self.encoder[t] for t in self.bpe(tok).split(" "))
+        return ids
+
+
+@functools.lru_cache(maxsize=4)
+def _tokenizer(path):
+    return SimpleTokenizer(path)
+
+
+def tokenize(texts, context_length: int = 77, truncate: bool = False, bpe_path: str | None = None):
+    """Same contract as openai/CLIP ``clip.tokenize``: IntTensor [len(texts), context_length]."""
+    import torch
+    path = bpe_path or os.environ.get("CLIP_BPE_PATH")
+    if not path or not os.path.isfile(path):
+        raise RuntimeError("clip.tokenize needs the CLIP BPE vocabulary (bpe_simple_vocab_16e6.txt.gz); set "
+                           "CLIP_BPE_PATH to a local copy or pass token ids to encode_text directly")
+    tok = _tokenizer(path)
+    if isinstance(texts, str):
+        texts = [texts]
+    sot, eot = tok.encoder[SOT], tok.encoder[EOT]
+    result = torch.zeros(len(texts), context_length, dtype=torch.int)
+    for i, t in enumerate(texts):
+        ids = [sot] + tok.encode(t) + [eot]
+        if len(ids) > context_length:
+            if truncate:
+                ids = ids[:context_length]
+                ids[-1] = eot
+            else:
+                raise RuntimeError(f"Input {t} is too long for context length {context_length}")
+        result[i, :len(ids)] = torch.tensor(ids, dtype=torch.int)
+    return result

@@ -1,0 +1,214 @@
+"""Portable deterministic weights and synthetic inputs.
+
+There are no CLIP checkpoints offline, so parity and
+benchmarks run on random-init weights of the real architecture, produced by a
+counter-based generator that gives bit-identical float32 tensors on any host:
+splitmix64 of (seed, crc32(name), element index) -> four 16-bit uniforms ->
+Irwin-Hall(4) approximate normal.  Every step is exact integer arithmetic or a
+single correctly-rounded IEEE operation, so the GPU box regenerates exactly the
+tensors the golden fixtures were computed from.
+
+The parameter layout is the OpenAI state dict consumed by ``clip.load``
+(openai/CLIP ``model.py``; call sites ``Backend/embedding.py:22``,
+``Backend/services/embedding_service.py:86``), and the standard deviations
+follow openai/CLIP ``CLIP.initialize_parameters`` (text tower) and the PyTorch
+defaults it leaves in place (vision tower).  LayerNorm gains/biases and linear
+biases are perturbed away from 1/0 so that a swapped or dropped parameter
+shows up in the parity tests.
+"""
+from __future__ import annotations
+
+import os
+import zlib
+
+import numpy as np
+
+from .config import CLIPConfig, from_state_dict
+
+_M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+_SQRT3 = float(np.sqrt(np.float64(3.0)))
+
+WEIGHT_SEED = 2
+PIXEL_SEED = 0
+TOKEN_SEED = 1
+CORPUS_SEED = 3
+
+SOT_TOKEN = 49406
+EOT_TOKEN = 49407
+
+
+def _splitmix64(x: np.ndarray) -> np.ndarray:
+    x = x + np.uint64(0x9E3779B97F4A7C15)
+    z = x
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def _stream_key(seed: int, name: str) -> np.uint64:
+    return np.uint64(((seed & 0xFFFFFFFF) << 32) | (zlib.crc32(name.encode()) & 0xFFFFFFFF))
+
+
+def hash_u64(seed: int, name: str, n: int, offset: int = 0) -> np.ndarray:
+    key = _splitmix64(np.array([_stream_key(seed, name)], dtype=np.uint64))[0]
+    idx = np.arange(offset, offset + n, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        return _splitmix64(idx * np.uint64(0xD1B54A32D192ED03) ^ key)
+
+
+def normal(seed: int, name: str, shape, std: float = 1.0, mean: float = 0.0,
+           chunk: int = 1 << 22) -> np.ndarray:
+    """Deterministic approximately-N(mean, std^2) float32 tensor."""
+    n = int(np.prod(shape)) if len(shape) else 1
+    out = np.empty(n, dtype=np.float32)
+    with np.errstate(over="ignore"):
+        for s in range(0, n, chunk):
+            e = min(n, s + chunk)
+            h = hash_u64(seed, name, e - s, s)
+            acc = np.zeros(e - s, dtype=np.float64)
+            for j in range(4):
+                u = ((h >> np.uint64(16 * j)) & np.uint64(0xFFFF)).astype(np.float64)
+                acc += u
+            # each u/65536 + 0.5/65536 ~ U(0,1): sum of four has mean 2, var 1/3
+            z = (acc + 2.0) / 65536.0 - 2.0
+            out[s:e] = (z * (_SQRT3 * std) + mean).astype(np.float32)
+    return out.reshape(shape)
+
+
+def uniform_int(seed: int, name: str, shape, lo: int, hi: int) -> np.ndarray:
+    """Deterministic integers in [lo, hi)."""
+    n = int(np.prod(shape))
+    h = hash_u64(seed, name, n)
+    return (lo + (h % np.uint64(hi - lo)).astype(np.int64)).reshape(shape)
+
+
+def make_state_dict(cfg: CLIPConfig, seed: int = WEIGHT_SEED) -> dict:
+    """OpenAI-layout float32 state dict (numpy arrays) for ``cfg``."""
+    sd = {}
+    g = lambda name, shape, std, mean=0.0: normal(seed, name, shape, std, mean)  # noqa: E731
+
+    def tower(prefix, width, layers):
+        attn_std = width ** -0.5
+        proj_std = (width ** -0.5) * ((2 * layers) ** -0.5)
+        fc_std = (2 * width) ** -0.5
+        for i in range(layers):
+            p = f"{prefix}resblocks.{i}."
+            sd[p + "attn.in_proj_weight"] = g(p + "attn.in_proj_weight", (3 * width, width), attn_std)
+            sd[p + "attn.in_proj_bias"] = g(p + "attn.in_proj_bias", (3 * width,), 0.02)
+            sd[p + "attn.out_proj.weight"] = g(p + "attn.out_proj.weight", (width, width), proj_std)
+            sd[p + "attn.out_proj.bias"] = g(p + "attn.out_proj.bias", (width,), 0.02)
+            sd[p + "ln_1.weight"] = g(p + "ln_1.weight", (width,), 0.1, 1.0)
+            sd[p + "ln_1.bias"] = g(p + "ln_1.bias", (width,), 0.02)
+            sd[p + "mlp.c_fc.weight"] = g(p + "mlp.c_fc.weight", (4 * width, width), fc_std)
+            sd[p + "mlp.c_fc.bias"] = g(p + "mlp.c_fc.bias", (4 * width,), 0.02)
+            sd[p + "mlp.c_proj.weight"] = g(p + "mlp.c_proj.weight", (width, 4 * width), proj_std)
+            sd[p + "mlp.c_proj.bias"] = g(p + "mlp.c_proj.bias", (width,), 0.02)
+            sd[p + "ln_2.weight"] = g(p + "ln_2.weight", (width,), 0.1, 1.0)
+            sd[p + "ln_2.bias"] = g(p + "ln_2.bias", (width,), 0.02)
+
+    W = cfg.vision_width
+    scale = W ** -0.5
+    P = cfg.vision_patch_size
+    fan_in = 3 * P * P
+    sd["visual.class_embedding"] = g("visual.class_embedding", (W,), scale)
+    sd["visual.positional_embedding"] = g("visual.positional_embedding", (cfg.vision_tokens, W), scale)
+    sd["visual.proj"] = g("visual.proj", (W, cfg.embed_dim), scale)
+    sd["visual.conv1.weight"] = g("visual.conv1.weight", (W, 3, P, P), (1.0 / fan_in) ** 0.5)
+    sd["visual.ln_pre.weight"] = g("visual.ln_pre.weight", (W,), 0.1, 1.0)
+    sd["visual.ln_pre.bias"] = g("visual.ln_pre.bias", (W,), 0.02)
+    sd["visual.ln_post.weight"] = g("visual.ln_post.weight", (W,), 0.1, 1.0)
+    sd["visual.ln_post.bias"] = g("visual.ln_post.bias", (W,), 0.02)
+    tower("visual.transformer.", W, cfg.vision_layers)
+
+    TW = cfg.text_width
+    sd["token_embedding.weight"] = g("token_embedding.weight", (cfg.vocab_size, TW), 0.02)
+    sd["positional_embedding"] = g("positional_embedding", (cfg.context_length, TW), 0.01)
+    sd["ln_final.weight"] = g("ln_final.weight", (TW,), 0.1, 1.0)
+    sd["ln_final.bias"] = g("ln_final.bias", (TW,), 0.02)
+    sd["text_projection"] = g("text_projection", (TW, cfg.embed_dim), TW ** -0.5)
+    sd["logit_scale"] = np.array(np.log(1 / 0.07), dtype=np.float32)
+    tower("transformer.", TW, cfg.text_layers)
+    return sd
+
+
+def synthetic_pixels(n: int, resolution: int, seed: int = PIXEL_SEED, offset: int = 0) -> np.ndarray:
+    """[n,3,R,R] float32 frames already in the normalised domain."""
+    per = 3 * resolution * resolution
+    out = np.empty((n, per), dtype=np.float32)
+    for i in range(n):
+        out[i] = normal(seed, f"pixels.{offset + i}", (per,))
+    return out.reshape(n, 3, resolution, resolution)
+
+
+def synthetic_tokens(q: int, context_length: int = 77, vocab_size: int = 49408,
+                     seed: int = TOKEN_SEED, offset: int = 0) -> np.ndarray:
+    """[q,77] int32 rows ``[SOT] + L ids in [256, EOT) + [EOT]`` zero padded, L in [5,30]
+    (SURVEY.md §8(d)).  For a vocab smaller than CLIP's, SOT/EOT are the two
+    largest ids so that EOT stays the row argmax (the pooling rule)."""
+    sot, eot = (SOT_TOKEN, EOT_TOKEN) if vocab_size == 49408 else (vocab_size - 2, vocab_size - 1)
+    lo = 256 if vocab_size == 49408 else 1
+    out = np.zeros((q, context_length), dtype=np.int32)
+    for r in range(q):
+        L = int(uniform_int(seed, f"toklen.{offset + r}", (1,), 5, 31)[0])
+        L = min(L, context_length - 2)
+        ids = uniform_int(seed, f"tokids.{offset + r}", (L,), lo, sot)
+        out[r, 0] = sot
+        out[r, 1:1 + L] = ids
+        out[r, 1 + L] = eot
+    return out
+
+
+def synthetic_corpus(n: int, d: int, seed: int = CORPUS_SEED) -> np.ndarray:
+    """[n,d] float32 L2-normalised rows (ranking microbench corpus)."""
+    x = normal(seed, "corpus", (n, d))
+    return x / np.linalg.norm(x, axis=-1, keepdims=True)
+
+
+def load_state_dict(path: str) -> dict:
+    """Load an OpenAI-layout state dict from a LOCAL file (``$CLIP_WEIGHTS``).
+
+    Accepted: ``.safetensors``, a plain ``torch.save`` state dict
+    (``weights_only=True``), or an OpenAI TorchScript archive (its
+    ``state_dict()`` is read, as openai/CLIP ``clip.load(jit=False)`` does).
+    A fine-tuned ``CLIPWithClassifier`` checkpoint
+    (``{'model_state_dict': {'clip_model.*', 'classifier.*'}}``,
+    ``Backend/services/embedding_service.py:112-113``) is unwrapped to its
+    ``clip_model.*`` part."""
+    import torch
+
+    if path.endswith(".safetensors"):
+        from safetensors.numpy import load_file
+        sd = load_file(path)
+    else:
+        try:
+            obj = torch.load(path, map_location="cpu", weights_only=True)
+        except Exception:
+            obj = torch.jit.load(path, map_location="cpu").state_dict()
+        if isinstance(obj, dict) and "model_state_dict" in obj:
+            obj = obj["model_state_dict"]
+        sd = {k: (v.float().numpy() if hasattr(v, "numpy") else np.asarray(v)) for k, v in obj.items()}
+    if any(k.startswith("clip_model.") for k in sd):
+        sd = {k[len("clip_model."):]: v for k, v in sd.items() if k.startswith("clip_model.")}
+    for k in ("input_resolution", "context_length", "vocab_size"):
+        sd.pop(k, None)
+    return {k: np.ascontiguousarray(v, dtype=np.float32) for k, v in sd.items()}
+
+
+def resolve(name_or_path: str):
+    """(cfg, state_dict) for a model name or a local checkpoint path.
+
+    ``$CLIP_WEIGHTS`` (a local file) supplies real weights for a named model;
+    otherwise the deterministic generator is used (no network)."""
+    from .config import get_config
+
+    if os.path.isfile(name_or_path):
+        sd = load_state_dict(name_or_path)
+        return from_state_dict(sd), sd
+    cfg = get_config(name_or_path)
+    env = os.environ.get("CLIP_WEIGHTS")
+    if env and os.path.isfile(env):
+        sd = load_state_dict(env)
+        real = from_state_dict(sd)
+        if real.name == cfg.name:
+            return real, sd
+    return cfg, make_state_dict(cfg)

@@ -1,0 +1,154 @@
+/*
+ * miclip.h — C-ABI of the MI355X-native CLIP frame-embedding + text->frame
+ * retrieval path (gfx950 HIP kernels in libmiclip.so).
+ *
+ * The reference has no native code: its GPU work is the
+ * third-party openai/CLIP package driven from Python, and its ranking is host
+ * NumPy.  Each entry point below replaces one reference interface; the
+ * replaced interface is cited next to it.  Plain pointers and sizes only: the
+ * Python host (`miclip/_native.py`, ctypes) passes torch tensors' data_ptr()
+ * and the current HIP stream.
+ *
+ * Conventions
+ *   - Return 0 (MI_OK) on success, a negative MI_ERR_* code on error; the
+ *     message is in mi_last_error() (thread-local).  The Python shim raises.
+ *   - Callers own every input/output buffer (device pointers unless noted);
+ *     an mi_clip context owns weights and activation workspace.
+ *   - `stream` is a hipStream_t (NULL = legacy default stream).  No entry point
+ *     allocates or synchronises after mi_clip_reserve(), so encode/rank calls
+ *     can be captured in a hipGraph.
+ *   - Context entry points are serialised by a per-context mutex (the Flask
+ *     dev server shares one EmbeddingService across request threads,
+ *     Backend/app.py:969).
+ *   - Ranking order: score descending, then global index ascending.  NaN
+ *     scores (zero-norm rows) sort first under MI_NAN_FIRST
+ *     (np.argsort(s)[::-1], embedding_service.py:317-320) or last under
+ *     MI_NAN_LAST (np.argsort(-s), compare_models.py:1014).
+ */
+#ifndef MICLIP_H
+#define MICLIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MICLIP_ABI_VERSION 1
+
+enum mi_dtype { MI_F32 = 0, MI_BF16 = 1, MI_F16 = 2 };
+enum mi_status { MI_OK = 0, MI_ERR_ARG = -1, MI_ERR_HIP = -2, MI_ERR_UNSUPPORTED = -3, MI_ERR_STATE = -4 };
+enum mi_nan_policy { MI_NAN_FIRST = 0, MI_NAN_LAST = 1 };
+/* corpus row normalisation inside the rank/score kernels */
+enum mi_norm_mode {
+  MI_NORM_L2 = 0,       /* e/||e|| ; zero row -> NaN   (embedding_service.py:210)           */
+  MI_NORM_L2_GUARD = 1, /* e/||e|| if ||e||>1e-8 else e (compare_models.py:1168-1171)       */
+  MI_NORM_NONE = 2      /* raw dot products (features already normalised, compare_models:999) */
+};
+
+/* Architecture of a ViT CLIP (openai/CLIP build_model inference; miclip/config.py). */
+typedef struct mi_clip_arch {
+  int32_t embed_dim;         /* D: 512 (B/32), 768 (L/14)      */
+  int32_t image_resolution;  /* 224 / 336                      */
+  int32_t vision_layers;
+  int32_t vision_width;      /* multiple of 64; heads = width/64 */
+  int32_t vision_patch_size;
+  int32_t context_length;    /* 77                             */
+  int32_t vocab_size;        /* 49408                          */
+  int32_t text_width;        /* multiple of 64                 */
+  int32_t text_heads;        /* text_width / 64                */
+  int32_t text_layers;
+} mi_clip_arch;
+
+typedef struct mi_clip mi_clip;
+
+int mi_abi_version(void);
+const char* mi_last_error(void);
+
+/* Number of float32 elements of the canonical weight blob for `arch`
+ * (OpenAI state-dict tensors concatenated in the order documented in
+ * DESIGN.md "Weight blob"; packer: miclip/_native.py pack_weights). */
+int64_t mi_clip_weights_numel(const mi_clip_arch* arch);
+
+/* Replaces openai/CLIP `clip.load(name, device, jit=False)` model construction
+ * (call sites Backend/embedding.py:22, Backend/services/embedding_service.py:86,106,
+ * compare_models.py:316).  `weights` is a HOST float32 blob of
+ * mi_clip_weights_numel(arch) elements; weights are converted to `weight_dtype`
+ * (MI_BF16; MI_F32 is rejected until the fp32 parity GEMM lands) and uploaded to
+ * `device`. */
+int mi_clip_create(const mi_clip_arch* arch, const float* weights, int64_t numel,
+                   int device, int weight_dtype, mi_clip** out);
+int mi_clip_destroy(mi_clip* ctx);
+
+/* Allocate activation workspace for up to `image_chunk` frames / `text_chunk`
+ * queries per internal pass (larger batches are processed chunk by chunk).
+ * The only allocating call besides create. */
+int mi_clip_reserve(mi_clip* ctx, int64_t image_chunk, int64_t text_chunk);
+
+/* Replaces `model.encode_image(x)` (VisionTransformer.forward; call sites
+ * Backend/embedding.py:49, embedding_service.py:490, compare_models.py:1118)
+ * and, with l2_normalize=1, the normalisation that follows it
+ * (embedding_service.py:502, CLIPWithClassifier.forward :45).
+ * pixels: device [B,3,R,R] in `in_dtype` (MI_F32 / MI_BF16);
+ * out: device [B,embed_dim] in `out_dtype` (MI_F32 / MI_BF16 / MI_F16). */
+int mi_clip_encode_image(mi_clip* ctx, const void* pixels, int64_t B, int in_dtype,
+                         void* out, int out_dtype, int l2_normalize, void* stream);
+
+/* Replaces `model.encode_text(tokens)` (embedding_service.py:174,177;
+ * compare_models.py:1204).  tokens: device int32 [Q,context_length] in
+ * clip.tokenize format; pooling at the row argmax (EOT). */
+int mi_clip_encode_text(mi_clip* ctx, const int32_t* tokens, int64_t Q,
+                        void* out, int out_dtype, int l2_normalize, void* stream);
+
+/* Workspace bytes mi_rank_topk needs for (N, Q, k). */
+size_t mi_rank_workspace_bytes(int64_t N, int64_t Q, int32_t k);
+
+/* Replaces the ranking of EmbeddingService.search_top_frames
+ * (embedding_service.py:314-320: np.dot(E_normalised, t.T) + np.argsort(s)[::-1][:k])
+ * and search_top_frames_by_image (:365-372).  One fused pass: per corpus row
+ * L2 norm (norm_mode) + fp32-exact dot with every query + top-k.
+ * corpus: device [N,D] (MI_F32/MI_BF16/MI_F16, row stride D); queries: device
+ * f32 [Q,D]; out_scores f32 [Q,k], out_index int64 [Q,k] (global index =
+ * index_base + row; slots past N are index -1, score -inf).  1 <= k <= 64. */
+int mi_rank_topk(const void* corpus, int64_t N, int64_t D, int corpus_dtype,
+                 const float* queries, int64_t Q, int32_t k, int64_t index_base,
+                 int norm_mode, int nan_policy, float* out_scores, int64_t* out_index,
+                 void* workspace, size_t workspace_bytes, void* stream);
+
+/* Merge per-query candidate lists (e.g. the RCCL all-gather of per-shard
+ * top-k) into the global top-k with the same order rule.
+ * cand_scores f32 [Q,C], cand_index int64 [Q,C] (index -1 = empty slot). */
+int mi_rank_merge(const float* cand_scores, const int64_t* cand_index, int64_t Q, int64_t C,
+                  int32_t k, int nan_policy, float* out_scores, int64_t* out_index, void* stream);
+
+/* Full similarity matrix for the R@K evaluation flow
+ * (compare_models.py:999 `image_features @ text_features.T`):
+ * out[q][n] = <queries[q], corpus[n]/norm(n)>  (f32, fp32-exact products). */
+int mi_score_matrix(const void* corpus, int64_t N, int64_t D, int corpus_dtype,
+                    const float* queries, int64_t Q, int norm_mode, float* out, void* stream);
+
+/* Rank of a target column per query row (compare_models.py:1013-1015,
+ * 1057-1061: position of the ground truth in argsort(-s), 1-based):
+ * rank[t] = 1 + #{n : s[q][n] > s[q][g]} + #{n < g : s[q][n] == s[q][g]},
+ * q = pair_query[t], g = pair_target[t]; NaN sorts last (argsort(-s)). */
+int mi_rank_of_targets(const float* scores, int64_t Q, int64_t N, const int64_t* pair_query,
+                       const int64_t* pair_target, int64_t T, int64_t* out_rank, void* stream);
+
+/* ---- operator-level entry points (per-kernel parity tests) ----
+ * mi_op_gemm: out = A[M,K] . W[N,K]^T (+bias) with epilogue
+ *   0: bf16 out; 1: bf16 QuickGELU out; 2: f32 out += (residual); 3: f32 out.
+ *   (nn.Linear of attn.in_proj / out_proj / mlp.c_fc / c_proj, conv1 as GEMM)
+ * mi_op_layernorm: bf16 out = LN(x f32 [rows,W]) (openai/CLIP LayerNorm, fp32)
+ * mi_op_attention: bf16 [B*S, W] = MHA core over packed qkv bf16 [B*S, 3W]
+ *   (nn.MultiheadAttention softmax(qk^T/8)v per 64-wide head; causal for text) */
+int mi_op_gemm(const void* A, const void* W, const float* bias, void* out, int32_t M, int32_t N, int32_t K,
+               int32_t epilogue, void* stream);
+int mi_op_layernorm(const float* x, const float* gamma, const float* beta, void* out, int32_t rows, int32_t W,
+                    void* stream);
+int mi_op_attention(const void* qkv, void* out, int32_t B, int32_t S, int32_t W, int32_t causal, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MICLIP_H */

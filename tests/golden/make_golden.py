@@ -1,0 +1,129 @@
+"""Generate the committed golden fixtures (run in the build container, which has
+``/root/reference`` and HF ``transformers``; the GPU box only reads the .npz).
+
+  python tests/golden/make_golden.py
+
+Encoder goldens (``<model>.npz``): HF ``transformers`` 5.15.0 ``CLIPModel`` —
+the architecture-equivalent stand-in for the absent openai/CLIP — loaded with
+the deterministic weights of ``miclip.weights.make_state_dict`` (seed 2) and run
+in fp32 on deterministic synthetic frames/tokens (regenerated bit-exactly from
+their seeds, so only outputs are stored).
+
+Ranking goldens: the reference's own committed corpus
+``Backend/embedding/video_test_4_embeddings.npy`` ([387,512] fp32 encode_image
+rows) ranked by the literal restatement of ``search_top_frames``
+(embedding_service.py:209-210, 314-336), and the R@K flow of
+``compare_models.py:994-1090`` on those rows.  Seeds are advanced until no
+score comparison that decides an output is closer than 1e-6 (so the pinned
+answer does not depend on fp32 summation order).
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "event-retrival-in-video-learning-transferable-visual-model-from-supervised-natural-language_amd"))
+sys.path.insert(0, ROOT)
+
+from miclip import config, weights  # noqa: E402
+from oracle import hf_map, rank_ref  # noqa: E402
+
+REF_CORPUS = "/root/reference/Backend/embedding/video_test_4_embeddings.npy"
+
+
+def encoder_golden(name, n_img, n_txt):
+    cfg = config.get_config(name)
+    sd = weights.make_state_dict(cfg)
+    px = weights.synthetic_pixels(n_img, cfg.image_resolution)
+    tk = weights.synthetic_tokens(n_txt, cfg.context_length, cfg.vocab_size)
+    m = hf_map.build_hf(sd, cfg)
+    r = hf_map.hf_encode(m, px, tk)
+    out = os.path.join(HERE, name.replace("/", "").replace("@", "_").replace("-", "_").lower() + ".npz")
+    np.savez_compressed(out, n_images=n_img, tokens=tk, image=r["image"].astype(np.float32),
+                        text=r["text"].astype(np.float32))
+    print("wrote", out)
+
+
+def min_decisive_gap(S, k):
+    """Smallest gap between consecutive scores within the top k+1 of each row."""
+    g = np.inf
+    for s in S:
+        t = np.sort(s)[::-1][:k + 1]
+        g = min(g, np.min(t[:-1] - t[1:]))
+    return g
+
+
+def rank_golden():
+    corpus = np.load(REF_CORPUS).astype(np.float32)
+    frames = [f"{i}.jpg" for i in range(corpus.shape[0])]
+    k = 60                                      # top_k * 3 for the UI's default 20 (query_strategies.py:55)
+    E = rank_ref.normalize_rows(corpus.astype(np.float64))
+    for seed in range(100):
+        rng = np.random.default_rng(seed)
+        Q = 8
+        picks = rng.integers(0, corpus.shape[0], size=(Q, 3))
+        q = E[picks].mean(1) + 0.05 * rng.standard_normal((Q, corpus.shape[1]))
+        q = (q / np.linalg.norm(q, axis=1, keepdims=True)).astype(np.float32)
+        S = q.astype(np.float64) @ E.T
+        if min_decisive_gap(S, k) > 1e-6:
+            break
+    top_i, top_s = [], []
+    for r in range(Q):
+        _, idx = rank_ref.search_top_frames_ref(corpus, q[r:r + 1], k, frames)
+        top_i.append(np.asarray(idx[:k]))
+        top_s.append(S[r][idx[:k]])
+    out = os.path.join(HERE, "rank_video_test_4.npz")
+    np.savez_compressed(out, corpus=corpus, queries=q, k=k, top_index=np.array(top_i), top_score=np.array(top_s),
+                        seed=seed)
+    print("wrote", out, "seed", seed)
+
+
+def rk_golden():
+    corpus = np.load(REF_CORPUS).astype(np.float32)
+    n_img = 100
+    img = rank_ref.normalize_rows_guarded(corpus[:n_img])
+    for seed in range(200):
+        rng = np.random.default_rng(1000 + seed)
+        caps = np.repeat(img, 5, axis=0) + 0.12 * rng.standard_normal((5 * n_img, img.shape[1]))
+        txt = rank_ref.normalize_rows_guarded(caps).astype(np.float32)
+        S = img.astype(np.float64) @ txt.T.astype(np.float64)
+        cap_ids = np.repeat(np.arange(n_img), 5)
+        # decisive comparisons: every score against each ground-truth score
+        ok = True
+        for i in range(txt.shape[0]):
+            col = S[:, i]
+            if np.min(np.abs(np.delete(col, cap_ids[i]) - col[cap_ids[i]])) < 1e-6:
+                ok = False
+                break
+        if ok:
+            for j in range(n_img):
+                row = S[j]
+                for c in range(5 * j, 5 * j + 5):
+                    if np.min(np.abs(np.delete(row, c) - row[c])) < 1e-6:
+                        ok = False
+                        break
+                if not ok:
+                    break
+        if ok:
+            break
+    ref = rank_ref.retrieval_metrics_ref(img.astype(np.float32), txt, list(cap_ids), list(range(n_img)))
+    out = os.path.join(HERE, "rk_flow.npz")
+    np.savez_compressed(out, image_features=img.astype(np.float32), text_features=txt, caption_image_ids=cap_ids,
+                        image_ids=np.arange(n_img), t2i_ranks=ref["t2i_ranks"], i2t_ranks=ref["i2t_ranks"],
+                        t2i_r=np.array([ref["t2i"]["R@1"], ref["t2i"]["R@5"], ref["t2i"]["R@10"]]),
+                        i2t_r=np.array([ref["i2t"]["R@1"], ref["i2t"]["R@5"], ref["i2t"]["R@10"]]), seed=seed)
+    print("wrote", out, "seed", seed, ref["t2i"], ref["i2t"])
+
+
+if __name__ == "__main__":
+    encoder_golden("test-tiny", 3, 4)
+    encoder_golden("test-small", 3, 4)
+    encoder_golden("ViT-B/32", 4, 4)
+    if "--large" in sys.argv:
+        encoder_golden("ViT-L/14", 2, 2)
+    rank_golden()
+    rk_golden()

@@ -1,0 +1,78 @@
+"""CPU: libmiclip.so loads, exports every symbol include/miclip.h declares, and
+validates arguments before touching a GPU (no compute calls here)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, state_dict
+
+
+def _declared():
+    hdr = open(os.path.join(ROOT, "include", "miclip.h")).read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(mi_[a-z_0-9]+)\s*\(", hdr, re.M)))
+
+
+def test_header_and_binding_agree():
+    from miclip import _native
+    assert _declared() == sorted(_native.EXPORTS)
+
+
+def test_library_exports_every_symbol():
+    from miclip import _native
+    L = _native.lib()
+    for name in _declared():
+        assert hasattr(L, name), name
+    out = os.popen(f"nm -D --defined-only {_native.LIB_PATH}").read()
+    for name in _declared():
+        assert re.search(rf"\bT {name}$", out, re.M), f"{name} not exported"
+    assert L.mi_abi_version() == 1
+
+
+def test_weights_numel_matches_packer():
+    from miclip import _native, config
+    for name in ("test-tiny", "test-small", "ViT-B/32"):
+        cfg = config.get_config(name)
+        n = _native.lib().mi_clip_weights_numel(ctypes.byref(_native.Arch.from_config(cfg)))
+        if name == "ViT-B/32":
+            assert n == 151277313  # openai ViT-B/32 parameter count
+        assert n == sum(np.asarray(v).size for v in state_dict(name).values())
+
+
+def test_argument_errors_without_gpu():
+    from miclip import _native
+    L = _native.lib()
+    rc = L.mi_rank_topk(None, 10, 512, 0, None, 1, 100, 0, 0, 0, None, None, None, 0, None)
+    assert rc == -3 and b"k must be" in L.mi_last_error()
+    rc = L.mi_rank_topk(None, 10, 500, 0, None, 1, 10, 0, 0, 0, None, None, None, 0, None)
+    assert rc == -3 and b"multiple of 32" in L.mi_last_error()
+    rc = L.mi_rank_merge(None, None, 1, 4, 0, 0, None, None, None)
+    assert rc == -3
+    arch = _native.Arch(512, 224, 12, 768, 32, 77, 49408, 512, 8, 12)
+    ctx = ctypes.c_void_p()
+    blob = np.zeros(10, np.float32)
+    rc = L.mi_clip_create(ctypes.byref(arch), blob.ctypes.data, 10, 0, 1, ctypes.byref(ctx))
+    assert rc == -1 and b"expected" in L.mi_last_error()
+    rc = L.mi_clip_create(ctypes.byref(arch), blob.ctypes.data, 10, 0, 0, ctypes.byref(ctx))
+    assert rc == -3
+    assert L.mi_rank_workspace_bytes(1_000_000, 32, 10) > 0
+
+
+def test_missing_library_fails_loudly(monkeypatch):
+    from miclip import _native
+    monkeypatch.setattr(_native, "_lib", None)
+    monkeypatch.setattr(_native, "LIB_PATH", "/nonexistent/libmiclip.so")
+    with pytest.raises(_native.MiClipError):
+        _native.lib()
+
+
+def test_no_cpu_execution_path():
+    from miclip import api, _native
+    with pytest.raises(RuntimeError):
+        api.load("test-tiny", device="cpu")
+    import miclip.model as M
+    from miclip import config
+    with pytest.raises(_native.MiClipError):
+        M.CLIP(config.get_config("test-tiny"), state_dict("test-tiny"), device="cpu")

@@ -1,0 +1,113 @@
+"""encode_image / encode_text through the C-ABI vs the oracle (float64 truth)
+and the committed HF-pinned golden vectors.  North-star tolerance: cosine
+similarity to the reference >= 1 - 1e-3 (we also bound the error on the
+frame-to-frame deviations, which the near-constant CLS part would hide)."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, golden, state_dict
+
+pytestmark = pytest.mark.gpu
+
+COS_TOL = 1e-3
+
+
+def _model(name, gpu, **kw):
+    from miclip import model as M, config
+    return M.CLIP(config.get_config(name), state_dict(name), device=gpu, **kw)
+
+
+def _check(got, ref, what):
+    from oracle.clip_ref import cosine
+    cos = cosine(got, ref)
+    assert np.all(cos > 1 - COS_TOL), f"{what}: min cosine {cos.min()}"
+    if got.shape[0] > 1:
+        dg, dr = got - got.mean(0), ref - ref.mean(0)
+        dcos = cosine(dg, dr)
+        assert np.all(dcos > 0.99), f"{what}: deviation cosine {dcos.min()}"
+    return cos.min()
+
+
+@pytest.mark.parametrize("name", ["test-tiny", "test-small"])
+def test_encode_small_configs(gpu, name):
+    import torch
+    from miclip import config, weights
+    from oracle import clip_ref
+    cfg = config.get_config(name)
+    m = _model(name, gpu)
+    px = weights.synthetic_pixels(5, cfg.image_resolution)
+    tk = weights.synthetic_tokens(6, cfg.context_length, cfg.vocab_size)
+    sd = state_dict(name)
+    img = m.encode_image(torch.from_numpy(px)).cpu().numpy()
+    txt = m.encode_text(torch.from_numpy(tk)).cpu().numpy()
+    _check(img, clip_ref.encode_image(px, sd, cfg, np.float64), f"{name} image")
+    _check(txt, clip_ref.encode_text(tk, sd, cfg, np.float64), f"{name} text")
+
+
+def test_encode_b32_golden(gpu):
+    """ViT-B/32 against the HF-transformers-pinned fixture."""
+    import torch
+    from miclip import config, weights
+    cfg = config.get_config("ViT-B/32")
+    g = golden("vit_b32.npz")
+    m = _model("ViT-B/32", gpu)
+    px = weights.synthetic_pixels(int(g["n_images"]), cfg.image_resolution)
+    tk = g["tokens"]
+    img = m.encode_image(torch.from_numpy(px)).cpu().numpy()
+    txt = m.encode_text(torch.from_numpy(tk)).cpu().numpy()
+    _check(img, g["image"], "B/32 image")
+    _check(txt, g["text"], "B/32 text")
+
+
+def test_encode_chunking_and_dtypes(gpu):
+    """Batches larger than the internal chunk, bf16 input, fp16/bf16 output,
+    in-kernel L2 normalisation: all consistent with the fp32 single-chunk run."""
+    import torch
+    from miclip import config, weights
+    cfg = config.get_config("test-tiny")
+    m = _model("test-tiny", gpu, image_chunk=3, text_chunk=2)
+    px = torch.from_numpy(weights.synthetic_pixels(8, cfg.image_resolution)).to(gpu)
+    base = m.encode_image(px).cpu().numpy()
+    m2 = _model("test-tiny", gpu, image_chunk=64)
+    one = m2.encode_image(px).cpu().numpy()
+    assert np.allclose(base, one, atol=1e-5)
+    n = m.encode_image(px, normalize=True).cpu().numpy()
+    assert np.allclose(n, base / np.linalg.norm(base, axis=1, keepdims=True), atol=1e-5)
+    h = m.encode_image(px, out_dtype=torch.float16).float().cpu().numpy()
+    assert np.allclose(h, base, rtol=2e-3, atol=2e-3)
+    b = m.encode_image(px.bfloat16()).cpu().numpy()
+    from oracle.clip_ref import cosine
+    assert cosine(b, base).min() > 0.999
+    tk = torch.from_numpy(weights.synthetic_tokens(5, cfg.context_length, cfg.vocab_size))
+    t1 = m.encode_text(tk).cpu().numpy()
+    t2 = m2.encode_text(tk).cpu().numpy()
+    assert np.allclose(t1, t2, atol=1e-5)
+
+
+def test_encode_empty_and_shape_errors(gpu):
+    import torch
+    from miclip import _native
+    m = _model("test-tiny", gpu)
+    assert m.encode_image(torch.zeros(0, 3, 64, 64)).shape == (0, 128)
+    with pytest.raises(_native.MiClipError):
+        m.encode_image(torch.zeros(2, 3, 32, 32))
+    with pytest.raises(_native.MiClipError):
+        m.encode_text(torch.zeros(2, 10, dtype=torch.int32))
+
+
+def test_clip_dropin_surface(gpu):
+    """The reference's call pattern (Backend/embedding.py:22,46-50)."""
+    import torch
+    import clip
+    from PIL import Image
+    model, preprocess = clip.load("test-tiny", device="cuda")
+    assert model.visual.output_dim == 128
+    img = Image.fromarray((np.arange(80 * 100 * 3) % 255).astype(np.uint8).reshape(80, 100, 3))
+    x = preprocess(img).unsqueeze(0).to("cuda")
+    with torch.no_grad():
+        e = model.encode_image(x).cpu().numpy().flatten()
+    assert e.shape == (128,) and np.isfinite(e).all()
+    li, lt = model(x, torch.from_numpy(np.zeros((1, 77), np.int32)))
+    assert li.shape == (1, 1) and lt.shape == (1, 1)

@@ -1,0 +1,106 @@
+"""Per-kernel parity: HIP GEMM / LayerNorm / attention vs a
+plain torch fp32 reference on the same bf16 operands."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _lib():
+    from miclip import _native
+    return _native
+
+
+def _stream():
+    import torch
+    return torch.cuda.current_stream().cuda_stream
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 128, 64), (100, 128, 64), (513, 384, 768), (3200, 2304, 768),
+                                   (777, 768, 3072)])
+@pytest.mark.parametrize("epi", [0, 1, 2, 3])
+def test_gemm(gpu, M, N, K, epi):
+    import torch
+    N_ = _lib()
+    g = torch.Generator(device="cpu").manual_seed(M * 7 + N + K + epi)
+    A = (torch.randn(M, K, generator=g) * 0.5).bfloat16().to(gpu)
+    W = (torch.randn(N, K, generator=g) * K ** -0.5).bfloat16().to(gpu)
+    bias = torch.randn(N, generator=g).float().to(gpu)
+    ref = A.float() @ W.float().t() + bias
+    if epi in (0, 1):
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=gpu)
+    else:
+        out = torch.randn(M, N, generator=g).float().to(gpu) if epi == 2 else torch.empty(M, N, device=gpu)
+        base = out.clone()
+    N_.check(N_.lib().mi_op_gemm(A.data_ptr(), W.data_ptr(), bias.data_ptr(), out.data_ptr(), M, N, K, epi,
+                                 _stream()), "gemm")
+    torch.cuda.synchronize()
+    if epi == 1:
+        ref = ref * torch.sigmoid(1.702 * ref)
+    if epi == 2:
+        ref = ref + base
+    got = out.float()
+    err = (got - ref).abs().max().item()
+    tol = (2e-2 if epi in (0, 1) else 2e-4) * max(1.0, ref.abs().max().item())
+    assert err < tol, f"max err {err} (tol {tol})"
+
+
+def test_gemm_asymmetric_identity(gpu):
+    """A = I with an asymmetric W catches a transposed C write (guide §3)."""
+    import torch
+    N_ = _lib()
+    M, N, K = 128, 128, 128
+    A = torch.eye(M, K, dtype=torch.bfloat16, device=gpu)
+    W = (torch.arange(N * K, device=gpu).reshape(N, K) % 251).bfloat16()
+    out = torch.empty(M, N, device=gpu)
+    N_.check(N_.lib().mi_op_gemm(A.data_ptr(), W.data_ptr(), None, out.data_ptr(), M, N, K, 3, _stream()), "gemm")
+    torch.cuda.synchronize()
+    assert torch.equal(out, W.float().t().contiguous())
+
+
+@pytest.mark.parametrize("rows,W", [(1, 128), (77, 512), (1000, 768), (50, 1024)])
+def test_layernorm(gpu, rows, W):
+    import torch
+    N_ = _lib()
+    g = torch.Generator(device="cpu").manual_seed(rows + W)
+    x = (torch.randn(rows, W, generator=g) * 3 + 1).to(gpu)
+    gamma = (1 + 0.1 * torch.randn(W, generator=g)).to(gpu)
+    beta = (0.1 * torch.randn(W, generator=g)).to(gpu)
+    out = torch.empty(rows, W, dtype=torch.bfloat16, device=gpu)
+    N_.check(N_.lib().mi_op_layernorm(x.data_ptr(), gamma.data_ptr(), beta.data_ptr(), out.data_ptr(), rows, W,
+                                      _stream()), "layernorm")
+    torch.cuda.synchronize()
+    ref = torch.nn.functional.layer_norm(x.double(), (W,), gamma.double(), beta.double(), 1e-5)
+    err = (out.double() - ref).abs().max().item()
+    assert err < 2e-2, err
+
+
+@pytest.mark.parametrize("B,S,W,causal", [(1, 50, 768, 0), (7, 50, 768, 0), (3, 77, 512, 1), (2, 17, 128, 0),
+                                          (2, 10, 256, 1), (1, 257, 1024, 0), (4, 197, 768, 0)])
+def test_attention(gpu, B, S, W, causal):
+    import torch
+    N_ = _lib()
+    g = torch.Generator(device="cpu").manual_seed(B * S + W + causal)
+    qkv = (torch.randn(B * S, 3 * W, generator=g) * 1.5).bfloat16().to(gpu)
+    out = torch.empty(B * S, W, dtype=torch.bfloat16, device=gpu)
+    N_.check(N_.lib().mi_op_attention(qkv.data_ptr(), out.data_ptr(), B, S, W, causal, _stream()), "attention")
+    torch.cuda.synchronize()
+    H = W // 64
+    x = qkv.double().reshape(B, S, 3, H, 64)
+    q, k, v = (x[:, :, i].transpose(1, 2) for i in range(3))
+    s = q @ k.transpose(-1, -2) * 0.125
+    if causal:
+        s = s.masked_fill(torch.triu(torch.ones(S, S, dtype=torch.bool, device=gpu), 1), float("-inf"))
+    ref = (torch.softmax(s, -1) @ v).transpose(1, 2).reshape(B * S, W)
+    err = (out.double() - ref).abs().max().item()
+    assert err < 3e-2 * max(1.0, ref.abs().max().item()), err
+
+
+def test_errors_are_raised(gpu):
+    import torch
+    N_ = _lib()
+    A = torch.zeros(8, 64, dtype=torch.bfloat16, device=gpu)
+    rc = N_.lib().mi_op_gemm(A.data_ptr(), A.data_ptr(), None, A.data_ptr(), 8, 100, 64, 0, _stream())
+    assert rc != 0 and b"N" in N_.lib().mi_last_error()
+    with pytest.raises(N_.MiClipError):
+        N_.check(rc, "gemm")

@@ -1,0 +1,137 @@
+"""Fused normalise + cosine + top-k kernel, merge, score matrix and
+rank-of-target vs the NumPy restatement of the reference ranking
+(embedding_service.py:314-320, compare_models.py:994-1090)."""
+import numpy as np
+import pytest
+
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+
+def _t(a, gpu):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a)).to(gpu)
+
+
+@pytest.mark.parametrize("N,D,Q,k", [(1, 512, 1, 10), (9, 512, 3, 10), (49, 512, 1, 60), (1000, 512, 32, 10),
+                                     (10000, 512, 32, 10), (4097, 768, 33, 16), (20000, 128, 5, 64),
+                                     (300, 1024, 70, 1)])
+def test_topk_matches_oracle(gpu, N, D, Q, k):
+    from miclip import retrieval, weights
+    from oracle import rank_ref
+    corpus = weights.normal(11, f"c{N}", (N, D))          # un-normalised rows
+    q = weights.synthetic_corpus(Q, D, seed=12)
+    s, i = retrieval.rank_topk(_t(corpus, gpu), _t(q, gpu), k)
+    S = rank_ref.scores_ref(corpus, q)
+    assert s.shape == (Q, min(k, N))
+    for r in range(Q):
+        rank_ref.assert_topk_equivalent(s[r].cpu().numpy(), i[r].cpu().numpy(), S[r], k)
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f16"])
+def test_topk_half_corpus(gpu, dtype):
+    """bf16/fp16 corpus rows are ranked on their exact f32 values."""
+    import torch
+    from miclip import retrieval, weights
+    from oracle import rank_ref
+    corpus = weights.normal(13, "half", (3000, 512))
+    tdt = torch.bfloat16 if dtype == "bf16" else torch.float16
+    c = torch.from_numpy(corpus).to(tdt)
+    q = weights.synthetic_corpus(8, 512, seed=14)
+    s, i = retrieval.rank_topk(c.to(gpu), _t(q, gpu), 10)
+    S = rank_ref.scores_ref(c.float().numpy(), q)
+    for r in range(8):
+        rank_ref.assert_topk_equivalent(s[r].cpu().numpy(), i[r].cpu().numpy(), S[r], 10)
+
+
+def test_topk_nan_rows_and_ties(gpu):
+    from miclip import retrieval
+    from oracle import rank_ref
+    rng = np.random.default_rng(0)
+    corpus = rng.standard_normal((500, 512)).astype(np.float32)
+    corpus[[3, 77, 400]] = 0.0                 # zero rows -> NaN scores
+    corpus[10] = corpus[20]                    # exact duplicate rows -> exact tie
+    q = rng.standard_normal((2, 512)).astype(np.float32)
+    q[1] = corpus[20] / np.linalg.norm(corpus[20])
+    for pol in ("first", "last"):
+        s, i = retrieval.rank_topk(_t(corpus, gpu), _t(q, gpu), 12, nan_policy=pol)
+        rs, ri = rank_ref.topk_ref(corpus, q, 12, nan_policy=pol)
+        s, i = s.cpu().numpy(), i.cpu().numpy()
+        if pol == "first":
+            assert list(i[0, :3]) == [3, 77, 400] and np.isnan(s[0, :3]).all()
+        assert list(i[1, :2] if pol == "last" else i[1, 3:5]) == [10, 20]   # tie -> index asc
+        for r in range(2):
+            rank_ref.assert_topk_equivalent(s[r], i[r], rank_ref.scores_ref(corpus, q)[r], 12, nan_policy=pol)
+
+
+def test_topk_index_base_and_empty(gpu):
+    import torch
+    from miclip import retrieval, weights
+    corpus = weights.synthetic_corpus(100, 512)
+    q = corpus[5:7]
+    s, i = retrieval.rank_topk(_t(corpus, gpu), _t(q, gpu), 3, index_base=1_000_000)
+    assert i[0, 0].item() == 1_000_005 and i[1, 0].item() == 1_000_006
+    e = torch.zeros(0, 512, device=gpu)
+    s, i = retrieval.rank_topk(e, _t(q, gpu), 5)
+    assert s.shape == (2, 0)
+
+
+def test_merge_matches_oracle(gpu):
+    from miclip import retrieval
+    from oracle import rank_ref
+    rng = np.random.default_rng(1)
+    Q, C, k = 7, 8 * 10, 10
+    cs = rng.standard_normal((Q, C)).astype(np.float32)
+    ci = rng.permutation(10_000)[:Q * C].reshape(Q, C).astype(np.int64)
+    ci[0, :5] = -1
+    cs[1, 3] = np.nan
+    for pol in ("first", "last"):
+        s, i = retrieval.merge_topk(_t(cs, gpu), _t(ci, gpu), k, nan_policy=pol)
+        rs, ri = rank_ref.merge_ref(cs, ci, k, nan_policy=pol)
+        assert np.array_equal(i.cpu().numpy(), ri)
+        assert np.allclose(s.cpu().numpy(), rs, equal_nan=True)
+
+
+def test_score_matrix_and_ranks(gpu):
+    from miclip import evaluate, retrieval, weights
+    from oracle import rank_ref
+    img = weights.synthetic_corpus(200, 512, seed=21)
+    txt = weights.synthetic_corpus(1000, 512, seed=22)
+    S = retrieval.score_matrix(_t(img, gpu), _t(txt, gpu)).cpu().numpy()     # [T, I]
+    assert np.allclose(S, (txt.astype(np.float64) @ img.T.astype(np.float64)), atol=2e-6)
+    cap_ids = [j // 5 for j in range(1000)]
+    res = evaluate.retrieval_metrics(_t(img, gpu), _t(txt, gpu), cap_ids, list(range(200)))
+    ref = rank_ref.retrieval_metrics_ref(img, txt, cap_ids, list(range(200)))
+    assert np.array_equal(res["t2i_ranks"], ref["t2i_ranks"])
+    assert np.array_equal(res["i2t_ranks"], ref["i2t_ranks"])
+    for d in ("t2i", "i2t", "mean"):
+        for m, v in ref[d].items():
+            assert res[d][m] == pytest.approx(v, abs=0), (d, m)
+
+
+def test_reference_corpus_fixture(gpu):
+    """The reference's own committed encode_image outputs
+    (Backend/embedding/video_test_4_embeddings.npy, fp32 un-normalised) ranked
+    for synthetic text vectors: identical frame lists to the literal
+    search_top_frames restatement (fixture generated by make_golden.py)."""
+    from miclip import retrieval
+    g = golden("rank_video_test_4.npz")
+    corpus, queries = g["corpus"], g["queries"]
+    s, i = retrieval.rank_topk(_t(corpus, gpu), _t(queries, gpu), int(g["k"]))
+    assert np.array_equal(i.cpu().numpy(), g["top_index"])
+    assert np.allclose(s.cpu().numpy(), g["top_score"], atol=2e-6)
+
+
+def test_reference_flow_rk_fixture(gpu):
+    """R@K flow on the reference's committed embeddings (frames as 'images',
+    noisy copies as 'captions'): ranks and R@1/5/10 identical to the literal
+    compare_models.py restatement."""
+    from miclip import evaluate
+    g = golden("rk_flow.npz")
+    res = evaluate.retrieval_metrics(_t(g["image_features"], gpu), _t(g["text_features"], gpu),
+                                     list(g["caption_image_ids"]), list(g["image_ids"]))
+    assert np.array_equal(res["t2i_ranks"], g["t2i_ranks"])
+    assert np.array_equal(res["i2t_ranks"], g["i2t_ranks"])
+    for d, arr in (("t2i", g["t2i_r"]), ("i2t", g["i2t_r"])):
+        assert [res[d]["R@1"], res[d]["R@5"], res[d]["R@10"]] == list(arr)

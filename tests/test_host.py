@@ -1,0 +1,99 @@
+"""CPU: host-side logic around the kernels (config inference, weight packing,
+tokenizer, preprocessing, sharding, service/ranking glue with fakes)."""
+import gzip
+import os
+
+import numpy as np
+import pytest
+
+from conftest import state_dict
+
+
+def test_config_inference_from_state_dict():
+    from miclip import config
+    for name in ("test-tiny", "test-small", "ViT-B/32"):
+        cfg = config.from_state_dict(state_dict(name))
+        assert cfg == config.get_config(name)
+    assert "ViT-B/32" in config.available_models() and "test-tiny" not in config.available_models()
+
+
+def test_flops_match_survey():
+    from miclip import config
+    b32 = config.get_config("ViT-B/32")
+    assert abs(b32.image_flops() / 1e9 - 8.818) < 0.01
+    assert abs(config.get_config("ViT-L/14").image_flops() / 1e9 - 162.03) < 0.1
+    assert abs(config.get_config("ViT-L/14@336px").image_flops() / 1e9 - 381.92) < 0.1
+
+
+def test_pack_order_covers_state_dict():
+    from miclip import _native, config
+    cfg = config.get_config("test-small")
+    sd = state_dict("test-small")
+    order = _native.weight_order(cfg)
+    assert sorted(order) == sorted(sd)
+    blob = _native.pack_weights(sd, cfg)
+    assert blob[0] == sd["visual.conv1.weight"].reshape(-1)[0] and blob[-1] == sd["logit_scale"]
+
+
+def _toy_bpe(tmp_path):
+    lines = ["#version: 0.2", "h e", "l l", "he ll", "hell o</w>", "w o", "r l", "wo rl", "worl d</w>"]
+    p = tmp_path / "toy_bpe.txt.gz"
+    with gzip.open(p, "wb") as f:
+        f.write("\n".join(lines).encode())
+    return str(p)
+
+
+def test_tokenizer_contract(tmp_path):
+    from miclip.tokenizer import tokenize, _tokenizer
+    path = _toy_bpe(tmp_path)
+    tok = _tokenizer(path)
+    t = tokenize(["Hello   world", "hello"], bpe_path=path)
+    assert t.shape == (2, 77) and str(t.dtype) == "torch.int32"
+    sot, eot = tok.encoder["<|startoftext|>"], tok.encoder["<|endoftext|>"]
+    assert t[0, 0] == sot and t[0, 3] == eot and (t[0, 4:] == 0).all()
+    assert tok.decoder[int(t[0, 1])] == "hello</w>" and tok.decoder[int(t[0, 2])] == "world</w>"
+    assert int(t[1].argmax()) == 2            # EOT is the row argmax (pooling rule)
+    long = " ".join(["hello"] * 100)
+    with pytest.raises(RuntimeError):
+        tokenize([long], bpe_path=path)
+    tt = tokenize([long], truncate=True, bpe_path=path)
+    assert tt[0, -1] == eot
+
+
+def test_tokenize_without_vocab_raises(monkeypatch):
+    from miclip.tokenizer import tokenize
+    monkeypatch.delenv("CLIP_BPE_PATH", raising=False)
+    with pytest.raises(RuntimeError, match="CLIP_BPE_PATH"):
+        tokenize(["a photo"])
+
+
+def test_preprocess_matches_torchvision_semantics():
+    from PIL import Image
+    from miclip.preprocess import Transform, MEAN, STD
+    img = Image.fromarray((np.arange(720 * 1280 * 3) % 251).astype(np.uint8).reshape(720, 1280, 3))
+    x = Transform(224)(img)
+    assert tuple(x.shape) == (3, 224, 224)
+    # resize short side 720 -> 224: long side int(224*1280/720) = 398, crop left round(87.0)
+    r = img.resize((398, 224), Image.BICUBIC).crop((87, 0, 311, 224))
+    ref = (np.asarray(r, np.float32) / 255 - MEAN) / STD
+    np.testing.assert_allclose(x.numpy().transpose(1, 2, 0), ref, atol=1e-6)
+    y = Transform(224, squash=True)(img)
+    assert tuple(y.shape) == (3, 224, 224)
+
+
+def test_shard_range_partitions():
+    from miclip.distributed import shard_range
+    for n, w in ((10, 3), (1_000_000, 8), (5, 8), (0, 2)):
+        spans = [shard_range(n, w, r) for r in range(w)]
+        assert spans[0][0] == 0 and spans[-1][1] == n
+        assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+        assert max(e - s for s, e in spans) - min(e - s for s, e in spans) <= 1
+
+
+def test_synthetic_tokens_format():
+    from miclip import weights
+    t = weights.synthetic_tokens(50)
+    for row in t:
+        L = int(np.argmax(row))
+        assert row[0] == 49406 and row[L] == 49407 and 6 <= L <= 31 and (row[L + 1:] == 0).all()
+        assert (row[1:L] >= 256).all() and (row[1:L] < 49406).all()
