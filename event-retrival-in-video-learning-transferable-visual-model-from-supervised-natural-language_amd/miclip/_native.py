@@ -56,6 +56,12 @@ def lib():
     if not os.path.isfile(LIB_PATH):
         raise MiClipError(f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
                           " or `make -C <pkg>/csrc`")
+    # torch ships its own libamdhip64 with the same SONAME (libamdhip64.so.7)
+    # as /opt/rocm's.  Loading torch first makes the dynamic linker bind
+    # libmiclip to torch's HIP runtime, so tensors, streams and our kernels
+    # live in ONE runtime; the other order makes torch bind to /opt/rocm's
+    # runtime and fail ("No HIP GPUs are available").
+    import torch  # noqa: F401
     L = ctypes.CDLL(LIB_PATH)
     P, I32, I64, SZ = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_size_t
     sig = {

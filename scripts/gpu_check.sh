@@ -1,0 +1,14 @@
+# GPU-box check: parity tests, smoke, short bench.  Each GPU step has its own
+# time limit; a crash/timeout (not a plain test failure) stops the script.
+mkdir -p gpurun_out
+timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1
+rc=$?
+echo "pytest rc=$rc"
+tail -5 gpurun_out/pytest_gpu.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.build(); g.smoke()" > gpurun_out/smoke.log 2>&1 || exit $?
+tail -2 gpurun_out/smoke.log
+timeout -k 10 600 python bench.py ${BENCH_ARGS:---steps 3 --warmup 1} > gpurun_out/bench.log 2>&1
+rc=$?
+tail -c 3000 gpurun_out/bench.log
+exit $rc
