@@ -85,8 +85,8 @@ def kernel_timing(model, cfg, chunk, reps=20):
             d["gbs"] = round(nbytes / us / 1e3, 1)
         res[name] = d
 
-    gemms = [("gemm_qkv", 3 * W, W, 0, outb), ("gemm_out", W, W, 2, outf), ("gemm_fc", 4 * W, W, 1, outb),
-             ("gemm_proj", W, 4 * W, 2, outf)]
+    gemms = [("gemm_qkv", 3 * W, W, 0, outb), ("gemm_out", W, W, 0, outb), ("gemm_fc", 4 * W, W, 1, outb),
+             ("gemm_proj", W, 4 * W, 0, outb)]
     for name, Nn, K, epi, out in gemms:
         timed(name, lambda Nn=Nn, K=K, epi=epi, out=out: N.check(
             L.mi_op_gemm(A.data_ptr(), Wt.data_ptr(), bias.data_ptr(), out.data_ptr(), M, Nn, K, epi, sp), "gemm"),

@@ -150,6 +150,7 @@ struct mi_clip {
   char* ws = nullptr;
   float* x = nullptr;
   uint16_t *h = nullptr, *qkv = nullptr, *att = nullptr, *mlp = nullptr, *patches = nullptr, *cls_ln = nullptr;
+  uint16_t* delta = nullptr;  // bf16 GEMM output added to x by the next residual_ln
   float* y = nullptr;
   std::mutex mu;
 };
@@ -287,6 +288,7 @@ static int reserve_locked(mi_clip* c, int64_t ic, int64_t tc) {
   const size_t o_h = carve(xw * 2);
   const size_t o_qkv = carve(3 * xw * 2);
   const size_t o_att = carve(xw * 2);
+  const size_t o_delta = carve(xw * 2);
   const size_t o_mlp = carve(4 * xw * 2);
   const size_t o_pat = carve((size_t)ic * c->G * c->G * c->Kp * 2);
   const size_t o_cls = carve((size_t)rows_max * mx(Wv, Wt) * 2);
@@ -303,6 +305,7 @@ static int reserve_locked(mi_clip* c, int64_t ic, int64_t tc) {
   c->h = (uint16_t*)(ws + o_h);
   c->qkv = (uint16_t*)(ws + o_qkv);
   c->att = (uint16_t*)(ws + o_att);
+  c->delta = (uint16_t*)(ws + o_delta);
   c->mlp = (uint16_t*)(ws + o_mlp);
   c->patches = (uint16_t*)(ws + o_pat);
   c->cls_ln = (uint16_t*)(ws + o_cls);
@@ -326,16 +329,26 @@ static GemmArgs gargs(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t
   return g;
 }
 
+// One tower.  On return x + delta is the final residual stream (the last
+// c_proj output is left in delta; the caller's final LayerNorm adds it).
+// Per block (openai/CLIP ResidualAttentionBlock):
+//   qkv = h W_qkv^T + b ; att = MHA(qkv) ; delta = att W_o^T + b_o
+//   x += delta ; h = ln_2(x)                      (residual_ln)
+//   m = QuickGELU(h W_fc^T + b_fc) ; delta = m W_pr^T + b_pr
+//   x += delta ; h = ln_1'(x)  (next block)       (residual_ln)
 static int run_tower(mi_clip* c, const std::vector<Layer>& layers, int B, int S, int W, int causal, hipStream_t s) {
   const int M = B * S;
-  for (const Layer& L : layers) {
-    HIP_TRY(layernorm_bf16(c->x, W, L.ln1_g, L.ln1_b, c->h, W, M, W, s));
+  HIP_TRY(layernorm_bf16(c->x, W, layers[0].ln1_g, layers[0].ln1_b, c->h, W, M, W, s));
+  for (size_t l = 0; l < layers.size(); ++l) {
+    const Layer& L = layers[l];
     HIP_TRY(gemm_bf16(gargs(c->h, W, L.w_qkv, W, L.b_qkv, c->qkv, 3 * W, M, 3 * W, W), EPI_BF16, s));
     HIP_TRY(attention(c->qkv, c->att, B, S, W, causal, s));
-    HIP_TRY(gemm_bf16(gargs(c->att, W, L.w_out, W, L.b_out, c->x, W, M, W, W), EPI_RESID_F32, s));
-    HIP_TRY(layernorm_bf16(c->x, W, L.ln2_g, L.ln2_b, c->h, W, M, W, s));
+    HIP_TRY(gemm_bf16(gargs(c->att, W, L.w_out, W, L.b_out, c->delta, W, M, W, W), EPI_BF16, s));
+    HIP_TRY(residual_ln(c->x, c->delta, W, 1, L.ln2_g, L.ln2_b, c->h, M, W, s));
     HIP_TRY(gemm_bf16(gargs(c->h, W, L.w_fc, W, L.b_fc, c->mlp, 4 * W, M, 4 * W, W), EPI_GELU_BF16, s));
-    HIP_TRY(gemm_bf16(gargs(c->mlp, 4 * W, L.w_proj, 4 * W, L.b_proj, c->x, W, M, W, 4 * W), EPI_RESID_F32, s));
+    HIP_TRY(gemm_bf16(gargs(c->mlp, 4 * W, L.w_proj, 4 * W, L.b_proj, c->delta, W, M, W, 4 * W), EPI_BF16, s));
+    if (l + 1 < layers.size())
+      HIP_TRY(residual_ln(c->x, c->delta, W, 1, layers[l + 1].ln1_g, layers[l + 1].ln1_b, c->h, M, W, s));
   }
   return MI_OK;
 }
@@ -369,7 +382,8 @@ int mi_clip_encode_image(mi_clip* c, const void* pixels, int64_t B, int in_dtype
     HIP_TRY(vision_embed_ln(c->x, c->cls, c->vpos, c->ln_pre_g, c->ln_pre_b, nb, S, W, s));
     int r = run_tower(c, c->vl, nb, S, W, 0, s);
     if (r) return r;
-    HIP_TRY(layernorm_bf16(c->x, (int64_t)S * W, c->ln_post_g, c->ln_post_b, c->cls_ln, W, nb, W, s));
+    // ln_post(x[:, 0] + last c_proj delta) over the CLS rows only
+    HIP_TRY(residual_ln(c->x, c->delta, (int64_t)S * W, 0, c->ln_post_g, c->ln_post_b, c->cls_ln, nb, W, s));
     HIP_TRY(gemm_bf16(gargs(c->cls_ln, W, c->vproj_t, W, nullptr, c->y, E, nb, E, W), EPI_F32, s));
     HIP_TRY(finalize_rows(c->y, (char*)out + c0 * E * dtype_size(out_dtype), out_dtype, nb, E, l2_normalize, s));
   }
@@ -395,7 +409,7 @@ int mi_clip_encode_text(mi_clip* c, const int32_t* tokens, int64_t Q, void* out,
     HIP_TRY(text_embed(tk, c->tok_emb, c->tpos, c->x, nq, S, W, a.vocab_size, s));
     int r = run_tower(c, c->tl, nq, S, W, 1, s);
     if (r) return r;
-    HIP_TRY(eot_gather_ln(tk, c->x, c->lnf_g, c->lnf_b, c->cls_ln, nq, S, W, s));
+    HIP_TRY(eot_gather_ln(tk, c->x, c->delta, c->lnf_g, c->lnf_b, c->cls_ln, nq, S, W, s));
     HIP_TRY(gemm_bf16(gargs(c->cls_ln, W, c->tproj_t, W, nullptr, c->y, E, nq, E, W), EPI_F32, s));
     HIP_TRY(finalize_rows(c->y, (char*)out + c0 * E * dtype_size(out_dtype), out_dtype, nq, E, l2_normalize, s));
   }

@@ -21,6 +21,12 @@ __device__ __host__ __forceinline__ u16 f2bf(float f) {
   return (u16)(u >> 16);
 }
 
+// Hardware RNE conversion (v_cvt_pk_bf16_f32; keeps NaN a NaN).
+__device__ __forceinline__ u16 f2bf_hw(float f) { return __builtin_bit_cast(u16, (__bf16)f); }
+__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
+  return (uint32_t)f2bf_hw(lo) | ((uint32_t)f2bf_hw(hi) << 16);
+}
+
 __device__ __host__ __forceinline__ float bf2f(u16 h) {
   union { uint32_t u; float f; } v;
   v.u = ((uint32_t)h) << 16;

@@ -71,6 +71,50 @@ __global__ __launch_bounds__(256) void ln_bf16_kernel(const float* __restrict__ 
   }
 }
 
+// Residual add + LayerNorm: xr = x[r*stride] + delta[r*stride] (delta = the
+// bf16 out_proj / c_proj GEMM output, bias included); optionally x is
+// written back (f32 residual stream), and out[r] = LN(xr) in bf16.
+// This is `x = x + attn(ln_1(x)); h = ln_2(x)` (and `x = x + mlp(..);
+// h = ln_1'(x)` / `ln_post(x[:, 0])`) of openai/CLIP ResidualAttentionBlock.
+__global__ __launch_bounds__(256) void residual_ln_kernel(float* __restrict__ x, const uint16_t* __restrict__ delta,
+                                                          int64_t stride, int write_x, const float* __restrict__ g,
+                                                          const float* __restrict__ b, uint16_t* __restrict__ out,
+                                                          int rows, int W) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const int n4 = W >> 2;
+  float4* xr = (float4*)(x + (int64_t)row * stride);
+  const uint2* dr = (const uint2*)(delta + (int64_t)row * stride);
+  RowVals r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = lane + 64 * i;
+    if (idx < n4) {
+      const float4 v = xr[idx];
+      const uint2 d = dr[idx];
+      r.v[i] = make_float4(v.x + bf2f((uint16_t)(d.x & 0xffff)), v.y + bf2f((uint16_t)(d.x >> 16)),
+                           v.z + bf2f((uint16_t)(d.y & 0xffff)), v.w + bf2f((uint16_t)(d.y >> 16)));
+      if (write_x) xr[idx] = r.v[i];
+    } else {
+      r.v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  float mean, rstd;
+  ln_stats(r, n4, lane, W, mean, rstd);
+  const float4* g4 = (const float4*)g;
+  const float4* b4 = (const float4*)b;
+  uint2* o = (uint2*)(out + (int64_t)row * W);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = lane + 64 * i;
+    if (idx < n4) {
+      const float4 gg = g4[idx], bb = b4[idx];
+      o[idx] = make_uint2(pack_bf16x2((r.v[i].x - mean) * rstd * gg.x + bb.x, (r.v[i].y - mean) * rstd * gg.y + bb.y),
+                          pack_bf16x2((r.v[i].z - mean) * rstd * gg.z + bb.z, (r.v[i].w - mean) * rstd * gg.w + bb.w));
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void vision_embed_ln_kernel(float* __restrict__ x, const float* __restrict__ cls,
                                                               const float* __restrict__ pos, const float* __restrict__ g,
                                                               const float* __restrict__ b, int rows, int S, int W) {
@@ -124,7 +168,9 @@ __global__ __launch_bounds__(256) void text_embed_kernel(const int32_t* __restri
 }
 
 __global__ __launch_bounds__(256) void eot_gather_ln_kernel(const int32_t* __restrict__ tokens,
-                                                            const float* __restrict__ x, const float* __restrict__ g,
+                                                            const float* __restrict__ x,
+                                                            const uint16_t* __restrict__ delta,
+                                                            const float* __restrict__ g,
                                                             const float* __restrict__ b, uint16_t* __restrict__ out,
                                                             int Q, int S, int W) {
   const int q = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -142,9 +188,19 @@ __global__ __launch_bounds__(256) void eot_gather_ln_kernel(const int32_t* __res
   }
   const int n4 = W >> 2;
   const float4* xr = (const float4*)(x + ((int64_t)q * S + bi) * W);
+  const uint2* dr = delta ? (const uint2*)(delta + ((int64_t)q * S + bi) * W) : nullptr;
   RowVals r;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) r.v[i] = (lane + 64 * i < n4) ? xr[lane + 64 * i] : make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int i = 0; i < 4; ++i) {
+    r.v[i] = (lane + 64 * i < n4) ? xr[lane + 64 * i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    if (dr && lane + 64 * i < n4) {
+      const uint2 d = dr[lane + 64 * i];
+      r.v[i].x += bf2f((uint16_t)(d.x & 0xffff));
+      r.v[i].y += bf2f((uint16_t)(d.x >> 16));
+      r.v[i].z += bf2f((uint16_t)(d.y & 0xffff));
+      r.v[i].w += bf2f((uint16_t)(d.y >> 16));
+    }
+  }
   float mean, rstd;
   ln_stats(r, n4, lane, W, mean, rstd);
   const float4* g4 = (const float4*)g;
@@ -366,10 +422,20 @@ hipError_t text_embed(const int32_t* tokens, const float* tok_emb, const float* 
   return hipGetLastError();
 }
 
-hipError_t eot_gather_ln(const int32_t* tokens, const float* x, const float* g, const float* b, uint16_t* out, int Q,
-                         int S, int W, hipStream_t s) {
+hipError_t eot_gather_ln(const int32_t* tokens, const float* x, const uint16_t* delta, const float* g,
+                         const float* b, uint16_t* out, int Q, int S, int W, hipStream_t s) {
   if (Q <= 0) return hipSuccess;
-  hipLaunchKernelGGL(eot_gather_ln_kernel, dim3((Q + 3) / 4), dim3(256), 0, s, tokens, x, g, b, out, Q, S, W);
+  hipLaunchKernelGGL(eot_gather_ln_kernel, dim3((Q + 3) / 4), dim3(256), 0, s, tokens, x, delta, g, b, out, Q, S,
+                     W);
+  return hipGetLastError();
+}
+
+hipError_t residual_ln(float* x, const uint16_t* delta, int64_t stride, int write_x, const float* g, const float* b,
+                       uint16_t* out, int rows, int W, hipStream_t s) {
+  if (rows <= 0) return hipSuccess;
+  if (W % 4 || W > 1024) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(residual_ln_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, x, delta, stride, write_x, g, b, out,
+                     rows, W);
   return hipGetLastError();
 }
 

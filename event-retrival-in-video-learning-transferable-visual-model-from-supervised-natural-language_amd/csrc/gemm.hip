@@ -1,20 +1,43 @@
 // bf16 MFMA GEMM with fused CLIP epilogues (gfx950).
 //
-//   C[M,N] = A[M,K] . W[N,K]^T  (+ bias, QuickGELU, residual add)
+//   C[M,N] = A[M,K] . W[N,K]^T  (+ bias, QuickGELU)
 //
 // Replaces the nn.Linear / conv1 GEMMs that openai/CLIP's encode_image /
 // encode_text run inside PyTorch:
-// attn.in_proj (+bias), attn.out_proj (+bias +residual), mlp.c_fc (+bias
-// +QuickGELU, transformers/activations.py:117-123), mlp.c_proj (+bias
-// +residual), conv1 as an im2col GEMM, and the bias-free CLS projections.
+// attn.in_proj (+bias), attn.out_proj (+bias), mlp.c_fc (+bias +QuickGELU,
+// transformers/activations.py:117-123), mlp.c_proj (+bias), conv1 as an
+// im2col GEMM, and the bias-free CLS projections.  The residual additions
+// x += out_proj(..) / c_proj(..) are done by the following LayerNorm kernel
+// (encoder.hip residual_ln), so every GEMM epilogue is a pure store.
 //
-// Tile: 128x128x64, 256 threads = 4 waves in 2x2, each wave 64x64 =
-// 4x4 x mfma_f32_16x16x32_bf16.  Operands are staged global->LDS with
-// 16-byte LDS-DMA (global_load_lds_dwordx4) into two buffers; the LDS image
-// is lane-linear, so the bank-conflict XOR swizzle (slot ^= row & 7 on the
-// 16-byte chunk of a 128-byte row) is applied to the per-lane SOURCE address
-// and again on the ds_read (cdna_hip_programming.md §5.4 rule 21).  Block ids
-// are remapped XCD-aware so tiles sharing an A row-panel share an L2.
+// Tiles (mfma_f32_16x16x32_bf16):
+//   256x256, 512 threads = 8 waves (2 M x 4 N), 128x64 per wave — the tower
+//     GEMMs: 128 FLOP per staged byte keeps the operand stream at ~half the
+//     L2 bandwidth at full MFMA rate (a 128^2 tile would need more than L2 has);
+//   128x128, 256 threads = 4 waves (2 x 2), 64x64 per wave — small / ragged N.
+//
+// Persistent grid, one continuous staging pipeline per workgroup: K is
+// consumed in BK = 32 stages held in a 4-deep LDS ring, each loaded by
+// 16-byte LDS-DMA (global_load_lds_dwordx4) THREE stages ahead of its use —
+// across tile boundaries, so the next tile's first stages are in flight while
+// the current tile finishes and stores.  One raw s_barrier per stage, preceded
+// by a COUNTED vmcnt that retires only the stage about to be read (a
+// __syncthreads() would drain every in-flight load, cdna_hip_programming.md §5
+// "Pipelining across barriers").  The epilogue's global stores are younger
+// than the next tile's first three stages, so they drain under its first
+// three stages of MFMA work (the counts below include them).  Bias lives in
+// LDS, so the epilogue issues no vector-memory load.
+//
+// LDS image: rows of 64 bytes (32 bf16) = four 16-byte chunks; chunk c of row
+// r is stored in slot c ^ g[(r >> 2) & 3], g = {0,2,3,1}, which makes the
+// 16-lane groups of every ds_read_b128 fragment read hit 16 distinct bank
+// slots.  The DMA destination is lane-linear, so the permutation is applied to
+// each lane's SOURCE address and again on the read (guide §5.4 rule 21).
+//
+// The MFMA computes the transposed tile (A operand = W fragment, B operand =
+// activation fragment) so each lane holds 4 consecutive output columns of one
+// row: 8-byte (bf16) / 16-byte (f32) stores, a wave writing whole 128/256-byte
+// row segments over its 4 column fragments.
 #include "common.hpp"
 #include "internal.hpp"
 
@@ -22,125 +45,217 @@ namespace miclip {
 
 namespace {
 
-constexpr int BM = 128, BN = 128, BK = 64;
-constexpr int STAGE_BYTES = (BM + BN) * BK * 2;  // 32 KiB: A tile then W tile
+constexpr int BK = 32;       // k per stage
+constexpr int RING = 4;      // LDS stages
+constexpr int LEAD = 3;      // stages in flight ahead of the one being read
+constexpr int MAX_N = 4096;  // bias staged in LDS
 
-__device__ __forceinline__ float quick_gelu(float v) { return v / (1.0f + __expf(-1.702f * v)); }
+// QuickGELU x * sigmoid(1.702 x) with the hardware exp/rcp (~1 ulp; output is bf16)
+__device__ __forceinline__ float quick_gelu(float v) {
+  return v * __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * v));
+}
 
-template <int EPI>
-__global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
+__device__ __forceinline__ int swz(int x) { return (0x1320 >> (4 * x)) & 0xF; }  // g = {0,2,3,1}
+
+// LDS read the compiler does not see: a plain ds_read of the bias would make
+// hipcc wait vmcnt(0) (it cannot prove the read misses the in-flight LDS-DMA
+// of the next tile's stages), draining the prefetch at every epilogue.
+__device__ __forceinline__ float4 lds_read_f4(const float* p) {
+  float4 v;
+  const uint32_t addr = (uint32_t)(uintptr_t)(const LDS_AS float*)p;
+  asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(addr) : "memory");
+  return v;
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm_barrier() {
+  // retire all but the N youngest vector-memory ops of this wave, then a raw
+  // workgroup barrier; "memory" keeps the compiler from moving LDS accesses across
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"i"(N) : "memory");
+}
+
+template <int EPI, int BM, int BN, int WAVES_M, int WAVES_N>
+__global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_kernel(GemmArgs a) {
+  constexpr int NT = 64 * WAVES_M * WAVES_N;
+  constexpr int NWAVES = WAVES_M * WAVES_N;
+  constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;  // per-wave tile
+  constexpr int MI = WTM / 16, NI = WTN / 16;
+  constexpr int A_BYTES = BM * BK * 2, STAGE_BYTES = (BM + BN) * BK * 2;
+  constexpr int GA = BM / 16 / NWAVES;     // A DMA instructions per wave per stage (16 rows each)
+  constexpr int GB = BN / 16 / NWAVES;
+  constexpr int PS = GA + GB;              // vmcnt units per stage
+  constexpr int S = MI * NI;               // epilogue stores per lane
+  static_assert(2 * PS + S <= 63, "vmcnt field is 6 bits");
+  __shared__ __attribute__((aligned(16))) char smem[RING * STAGE_BYTES + MAX_N * 4];
+  float* sbias = (float*)(smem + RING * STAGE_BYTES);
+
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int tiles_n = a.N / BN;
   const int tiles_m = (a.M + BM - 1) / BM;
-  const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
-  const int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
+  const int ntiles = tiles_m * tiles_n;
+  const int G = gridDim.x;
+  const int slot = xcd_remap(blockIdx.x, G);  // XCD-contiguous runs of tiles per round
+  if (slot >= ntiles) return;
+  const int my_tiles = (ntiles - 1 - slot) / G + 1;
+  const int nk = a.K / BK;
+  const int T = my_tiles * nk;                 // stages this workgroup consumes
 
-  // --- LDS-DMA source addresses: instruction j of wave w fills LDS bytes
-  // [(w*4+j)*1024, +1024) = rows (w*4+j)*8 .. +7 of the tile; lane i -> row
-  // +(i>>3), LDS slot (i&7) which holds global chunk (i&7) ^ (row&7).
-  const uint16_t* asrc[4];
-  const uint16_t* wsrc[4];
+  for (int i = tid; i < a.N; i += NT) sbias[i] = a.bias ? a.bias[i] : 0.f;
+  __syncthreads();
+
+  // ---- issuer: DMA geometry — instruction j of wave w fills LDS bytes
+  // [(w*G+j)*1024, +1024) = tile rows (w*G+j)*16 .. +15; lane i -> row +(i>>2),
+  // slot (i&3) holding global chunk (i&3) ^ g[i>>4]  ((row>>2)&3 == i>>4).
+  const int lrow = lane >> 2;
+  const int lchunk = ((lane & 3) ^ swz(lane >> 4)) * 8;
+  const uint16_t* asrc[GA];
+  const uint16_t* wsrc[GB];
+  int is_g = 0, is_kt = 0, is_tile = 0;
+  auto set_src = [&](int t) {
+    const int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int row = (wave * 4 + j) * 8 + (lane >> 3);
-    const int chunk = (lane & 7) ^ (row & 7);
-    const int ra = min(m0 + row, a.M - 1);
-    asrc[j] = a.A + (int64_t)ra * a.lda + chunk * 8;
-    wsrc[j] = a.W + (int64_t)(n0 + row) * a.ldw + chunk * 8;
-  }
-  auto stage = [&](int kt, int buf) {
-    char* base = smem + buf * STAGE_BYTES;
+    for (int j = 0; j < GA; ++j)
+      asrc[j] = a.A + (int64_t)min(m0 + (wave * GA + j) * 16 + lrow, a.M - 1) * a.lda + lchunk;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      glds16(asrc[j] + kt * BK, base + (wave * 4 + j) * 1024);
-      glds16(wsrc[j] + kt * BK, base + BM * BK * 2 + (wave * 4 + j) * 1024);
+    for (int j = 0; j < GB; ++j) wsrc[j] = a.W + (int64_t)(n0 + (wave * GB + j) * 16 + lrow) * a.ldw + lchunk;
+  };
+  auto issue = [&]() {
+    char* base = smem + (is_g % RING) * STAGE_BYTES;
+#pragma unroll
+    for (int j = 0; j < GA; ++j) glds16(asrc[j] + is_kt * BK, base + (wave * GA + j) * 1024);
+#pragma unroll
+    for (int j = 0; j < GB; ++j) glds16(wsrc[j] + is_kt * BK, base + A_BYTES + (wave * GB + j) * 1024);
+    ++is_g;
+    if (++is_kt == nk) {
+      is_kt = 0;
+      if (++is_tile < my_tiles) set_src(slot + is_tile * G);
     }
   };
+  set_src(slot);
+  for (int s = 0; s < LEAD; ++s)
+    if (is_g < T) issue();
 
-  const int wr = wave >> 1, wc = wave & 1;
-  f32x4 acc[4][4];
+  // ---- consumer
+  const int wr = wave / WAVES_N, wc = wave % WAVES_N;
+  // fragment read: row (lane&15) of a 16-row block, chunk (lane>>4)
+  const int rd = (lane & 15) * 64 + (((lane >> 4) ^ swz((lane >> 2) & 3)) * 16);
+  bool pend = false;  // previous tile's S stores are still counted in vmcnt
+  int g = 0;
+  for (int ti = 0; ti < my_tiles; ++ti) {
+    const int t = slot + ti * G;
+    const int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
+    f32x4 acc[MI][NI];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = a.K / BK;
-  stage(0, 0);
-  vm_wait_all();
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) stage(kt + 1, (kt + 1) & 1);
-    const char* As = smem + (kt & 1) * STAGE_BYTES;
-    const char* Ws = As + BM * BK * 2;
+    for (int kt = 0; kt < nk; ++kt, ++g) {
+      // stage g must have landed; younger ops: up to LEAD-1 stages, plus the
+      // previous epilogue's stores while stage g predates them (kt < LEAD)
+      const int ys = min(LEAD - 1, T - 1 - g);
+      const bool st = pend && kt < LEAD;
+      if (nk < LEAD) wait_vm_barrier<0>();
+      else if (ys == 2) { if (st) wait_vm_barrier<2 * PS + S>(); else wait_vm_barrier<2 * PS>(); }
+      else if (ys == 1) { if (st) wait_vm_barrier<PS + S>(); else wait_vm_barrier<PS>(); }
+      else { if (st) wait_vm_barrier<S>(); else wait_vm_barrier<0>(); }
+      if (is_g < T) issue();
+      const char* As = smem + (g % RING) * STAGE_BYTES;
+      const char* Ws = As + A_BYTES;
+      bf16x8 bfr[NI], af[MI];
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      // fragment: row (lane&15) of a 16-row block, k chunk 4s + (lane>>4)
-      const int slot = ((4 * s + (lane >> 4)) ^ (lane & 7)) * 16;
-      bf16x8 af[4], bfr[4];
+      for (int ni = 0; ni < NI; ++ni) bfr[ni] = *(const bf16x8*)(Ws + (wc * WTN + ni * 16) * 64 + rd);
 #pragma unroll
-      for (int mi = 0; mi < 4; ++mi)
-        af[mi] = *(const bf16x8*)(As + (wr * 64 + mi * 16 + (lane & 15)) * 128 + slot);
+      for (int mi = 0; mi < MI; ++mi) af[mi] = *(const bf16x8*)(As + (wr * WTM + mi * 16) * 64 + rd);
 #pragma unroll
-      for (int ni = 0; ni < 4; ++ni)
-        bfr[ni] = *(const bf16x8*)(Ws + (wc * 64 + ni * 16 + (lane & 15)) * 128 + slot);
+      for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
-      for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < 4; ++ni)
-          acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], bfr[ni], acc[mi][ni], 0, 0, 0);
+        for (int ni = 0; ni < NI; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[ni], af[mi], acc[mi][ni], 0, 0, 0);
     }
-    vm_wait_all();
-    __syncthreads();
-  }
 
-  // --- epilogue: C/D map col = lane&15, row = 4*(lane>>4) + j
-  float bias[4];
+    // ---------------------------------------------------------- epilogue
+    // lane: output row m = m0 + wr*WTM + mi*16 + (lane&15),
+    //       columns  n = n0 + wc*WTN + ni*16 + 4*(lane>>4) + 0..3
+    const bool tail = m0 + BM > a.M;
+    float4 bias[NI];
 #pragma unroll
-  for (int ni = 0; ni < 4; ++ni) {
-    const int n = n0 + wc * 64 + ni * 16 + (lane & 15);
-    bias[ni] = a.bias ? a.bias[n] : 0.f;
-  }
+    for (int ni = 0; ni < NI; ++ni) bias[ni] = lds_read_f4(sbias + n0 + wc * WTN + ni * 16 + 4 * (lane >> 4));
 #pragma unroll
-  for (int mi = 0; mi < 4; ++mi) {
+    for (int mi = 0; mi < MI; ++mi) {
+      const int m = m0 + wr * WTM + mi * 16 + (lane & 15);
+      if (tail && m >= a.M) continue;
+      int64_t orow = m;
+      if (a.group) orow = (int64_t)(m / a.group) * a.gstride + a.goffset + m % a.group;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int m = m0 + wr * 64 + mi * 16 + 4 * (lane >> 4) + j;
-      if (m >= a.M) continue;
-      const int64_t orow = a.group ? (int64_t)(m / a.group) * a.gstride + a.goffset + m % a.group : m;
-#pragma unroll
-      for (int ni = 0; ni < 4; ++ni) {
-        const int n = n0 + wc * 64 + ni * 16 + (lane & 15);
-        float v = acc[mi][ni][j] + bias[ni];
-        if (EPI == EPI_BF16) {
-          ((uint16_t*)a.out)[orow * a.ldo + n] = f2bf(v);
-        } else if (EPI == EPI_GELU_BF16) {
-          ((uint16_t*)a.out)[orow * a.ldo + n] = f2bf(quick_gelu(v));
-        } else if (EPI == EPI_RESID_F32) {
-          float* p = (float*)a.out + orow * a.ldo + n;
-          *p = *p + v;
-        } else {
-          ((float*)a.out)[orow * a.ldo + n] = v;
+      for (int ni = 0; ni < NI; ++ni) {
+        const int n = n0 + wc * WTN + ni * 16 + 4 * (lane >> 4);
+        float v0 = acc[mi][ni][0] + bias[ni].x, v1 = acc[mi][ni][1] + bias[ni].y;
+        float v2 = acc[mi][ni][2] + bias[ni].z, v3 = acc[mi][ni][3] + bias[ni].w;
+        if (EPI == EPI_BF16 || EPI == EPI_GELU_BF16) {
+          if (EPI == EPI_GELU_BF16) {
+            v0 = quick_gelu(v0); v1 = quick_gelu(v1); v2 = quick_gelu(v2); v3 = quick_gelu(v3);
+          }
+          *(uint2*)((uint16_t*)a.out + orow * a.ldo + n) = make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
+        } else if (EPI == EPI_F32) {
+          *(float4*)((float*)a.out + orow * a.ldo + n) = make_float4(v0, v1, v2, v3);
+        } else {  // EPI_RESID_F32 (operator API only): read-modify-write, not overlapped
+          float4* dst = (float4*)((float*)a.out + orow * a.ldo + n);
+          const float4 o = *dst;
+          *dst = make_float4(o.x + v0, o.y + v1, o.z + v2, o.w + v3);
         }
       }
     }
+    // a tail tile issues fewer than S stores (and the residual form issues
+    // loads): drain so the counted waits stay exact
+    if (tail || EPI == EPI_RESID_F32) {
+      vm_wait_all();
+      pend = false;
+    } else {
+      pend = true;
+    }
   }
+}
+
+int cu_count() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
+template <int EPI>
+hipError_t launch(const GemmArgs& a, hipStream_t s) {
+  const bool big = a.N % 256 == 0 && a.M >= 1024;
+  if (big) {
+    const int nt = ((a.M + 255) / 256) * (a.N / 256);
+    const int g = nt < cu_count() ? nt : cu_count();
+    hipLaunchKernelGGL((gemm_kernel<EPI, 256, 256, 2, 4>), dim3(g), dim3(512), 0, s, a);
+  } else {
+    const int nt = ((a.M + 127) / 128) * (a.N / 128);
+    const int g = nt < 2 * cu_count() ? nt : 2 * cu_count();
+    hipLaunchKernelGGL((gemm_kernel<EPI, 128, 128, 2, 2>), dim3(g), dim3(256), 0, s, a);
+  }
+  return hipGetLastError();
 }
 
 }  // namespace
 
 hipError_t gemm_bf16(const GemmArgs& a, int epi, hipStream_t s) {
   if (a.M <= 0) return hipSuccess;
-  if (a.K % BK || a.N % BN || a.K <= 0) return hipErrorInvalidValue;
-  const int nwg = ((a.M + BM - 1) / BM) * (a.N / BN);
+  if (a.K % BK || a.N % 128 || a.K <= 0 || a.N > MAX_N) return hipErrorInvalidValue;
+  if ((a.ldo % 8) || ((uintptr_t)a.out & 15)) return hipErrorInvalidValue;
   switch (epi) {
-    case EPI_BF16: hipLaunchKernelGGL(gemm_kernel<EPI_BF16>, dim3(nwg), dim3(256), 0, s, a); break;
-    case EPI_GELU_BF16: hipLaunchKernelGGL(gemm_kernel<EPI_GELU_BF16>, dim3(nwg), dim3(256), 0, s, a); break;
-    case EPI_RESID_F32: hipLaunchKernelGGL(gemm_kernel<EPI_RESID_F32>, dim3(nwg), dim3(256), 0, s, a); break;
-    case EPI_F32: hipLaunchKernelGGL(gemm_kernel<EPI_F32>, dim3(nwg), dim3(256), 0, s, a); break;
+    case EPI_BF16: return launch<EPI_BF16>(a, s);
+    case EPI_GELU_BF16: return launch<EPI_GELU_BF16>(a, s);
+    case EPI_RESID_F32: return launch<EPI_RESID_F32>(a, s);
+    case EPI_F32: return launch<EPI_F32>(a, s);
     default: return hipErrorInvalidValue;
   }
-  return hipGetLastError();
 }
 
 }  // namespace miclip

@@ -35,9 +35,12 @@ hipError_t vision_embed_ln(float* x, const float* cls, const float* pos, const f
 // x[q*S + t] = tok_emb[tokens[q*S + t]] + pos[t]
 hipError_t text_embed(const int32_t* tokens, const float* tok_emb, const float* pos, float* x,
                       int Q, int S, int W, int vocab, hipStream_t s);
-// out[q] = LN(x[q*S + argmax_t tokens[q*S + t]]) bf16
-hipError_t eot_gather_ln(const int32_t* tokens, const float* x, const float* g, const float* b,
-                         uint16_t* out, int Q, int S, int W, hipStream_t s);
+// out[q] = LN(x[r] (+ delta[r])), r = q*S + argmax_t tokens[q*S + t]; bf16
+hipError_t eot_gather_ln(const int32_t* tokens, const float* x, const uint16_t* delta, const float* g,
+                         const float* b, uint16_t* out, int Q, int S, int W, hipStream_t s);
+// row r = i*stride: xr = x[r] + delta[r] (bf16); if write_x: x[r] = xr; out[i] = LN(xr) bf16 [rows, W]
+hipError_t residual_ln(float* x, const uint16_t* delta, int64_t stride, int write_x, const float* g, const float* b,
+                       uint16_t* out, int rows, int W, hipStream_t s);
 // pixels [B,3,R,R] (f32 or bf16) -> patches [B*G*G, Kp] bf16, k = c*P*P + kh*P + kw, zero pad to Kp
 hipError_t im2col(const void* pixels, int in_bf16, uint16_t* out, int B, int R, int P, int Kp,
                   hipStream_t s);

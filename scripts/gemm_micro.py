@@ -1,0 +1,56 @@
+"""GEMM microbenchmark through mi_op_gemm (random bf16 operands, HIP events).
+
+usage: python scripts/gemm_micro.py [reps]
+Shapes: the four ViT-B/32 tower GEMMs at a 2000-frame chunk (M = 100000) and
+a long-K square-ish case that isolates main-loop efficiency.
+"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "event-retrival-in-video-learning-transferable-visual-model-from-supervised-natural-language_amd"))
+
+import torch  # noqa: E402
+
+from miclip import _native as N  # noqa: E402
+
+SHAPES = {
+    "qkv": (100000, 2304, 768, 0),
+    "out": (100000, 768, 768, 0),
+    "fc": (100000, 3072, 768, 1),
+    "proj": (100000, 768, 3072, 0),
+    "sq4096": (8192, 8192, 4096, 3),
+}
+
+
+def main():
+    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+    only = sys.argv[2].split(",") if len(sys.argv) > 2 else list(SHAPES)
+    L = N.lib()
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev).manual_seed(0)
+    sp = torch.cuda.current_stream().cuda_stream
+    for name in only:
+        M, Nn, K, epi = SHAPES[name]
+        A = (torch.rand(M, K, device=dev, generator=g) * 2 - 1).bfloat16()
+        W = ((torch.rand(Nn, K, device=dev, generator=g) * 2 - 1) * K ** -0.5).bfloat16()
+        bias = torch.zeros(Nn, device=dev)
+        out = torch.zeros(M, Nn, device=dev, dtype=torch.bfloat16 if epi in (0, 1) else torch.float32)
+        run = lambda: N.check(L.mi_op_gemm(A.data_ptr(), W.data_ptr(), bias.data_ptr(), out.data_ptr(), M, Nn, K,  # noqa
+                                           epi, sp), "gemm")
+        run()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            run()
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / reps
+        print(f"{name:7s} M={M} N={Nn} K={K} epi={epi}: {us:9.1f} us  {2.0 * M * Nn * K / us / 1e6:7.1f} TFLOP/s",
+              flush=True)
+        del A, W, out
+
+
+if __name__ == "__main__":
+    main()
