@@ -174,7 +174,12 @@ def main():
 
     from miclip import api, distributed, retrieval, weights
 
-    model, _ = api.load(args.model, device=dev, image_chunk=args.image_chunk)
+    chunk = args.image_chunk
+    if chunk is None:  # equal-size passes (so every GEMM launch has one shape)
+        from miclip.config import get_config
+        base = max(8, 100_000 // get_config(args.model).vision_tokens)
+        chunk = -(-args.frames // -(-args.frames // base))
+    model, _ = api.load(args.model, device=dev, image_chunk=chunk)
     cfg = model.cfg
     chunk = model._chunks[0]
     Nf, Q, k = args.frames, args.queries, args.k

@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdarg>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -321,11 +322,22 @@ int mi_clip_reserve(mi_clip* c, int64_t image_chunk, int64_t text_chunk) {
   return reserve_locked(c, image_chunk, text_chunk);
 }
 
+// GEMM main-loop schedule (gemm.hip): MICLIP_GEMM_VARIANT overrides the default.
+static int gemm_variant() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("MICLIP_GEMM_VARIANT");
+    v = e ? atoi(e) : 0;
+  }
+  return v;
+}
+
 static GemmArgs gargs(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, const float* bias, void* out,
                       int64_t ldo, int M, int N, int K) {
   GemmArgs g;
   g.A = A; g.lda = lda; g.W = W; g.ldw = ldw; g.bias = bias; g.out = out; g.ldo = ldo;
   g.M = M; g.N = N; g.K = K; g.group = 0; g.gstride = 0; g.goffset = 0;
+  g.variant = gemm_variant();
   return g;
 }
 
@@ -488,9 +500,12 @@ int mi_op_gemm(const void* A, const void* W, const float* bias, void* out, int32
                int32_t epi, void* stream) {
   if (!A || !W || !out || M < 0) return fail(MI_ERR_ARG, "mi_op_gemm: bad arguments");
   if (K % 64 || N % 128 || K <= 0) return fail(MI_ERR_UNSUPPORTED, "mi_op_gemm: needs K %% 64 == 0, N %% 128 == 0");
+  const int variant = epi >> 8;  // bits 8+: schedule override for A/B measurements
+  epi &= 0xff;
   if (epi < 0 || epi > 3) return fail(MI_ERR_ARG, "mi_op_gemm: bad epilogue");
-  HIP_TRY(gemm_bf16(gargs((const uint16_t*)A, K, (const uint16_t*)W, K, bias, out, N, M, N, K), epi,
-                    (hipStream_t)stream));
+  GemmArgs g = gargs((const uint16_t*)A, K, (const uint16_t*)W, K, bias, out, N, M, N, K);
+  if (variant) g.variant = variant;
+  HIP_TRY(gemm_bf16(g, epi, (hipStream_t)stream));
   return MI_OK;
 }
 

@@ -217,6 +217,214 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_kernel(GemmArgs a
   }
 }
 
+// ---------------------------------------------------------------------------
+// Ping-pong schedule (variant 2): the 8 waves form two groups (waves 0-3 and
+// 4-7; waves w and w+4 share a SIMD), each owning 128 rows of the 256x256
+// tile.  A wave alternates LOAD sections (issue its share of the LDS-DMA for a
+// stage three ahead, ds_read the fragments of its next MFMA cluster,
+// lgkmcnt(0)) and COMPUTE sections (16 MFMAs); every section ends at a
+// workgroup barrier.  Group 1 runs one section behind group 0, so in every
+// section one wave of each SIMD feeds the matrix pipe while its partner loads
+// (cdna_hip_programming.md §5 "8-phase template", MI355X_MICROARCH.md "Two
+// waves per SIMD").  Per BK=32 stage: L_a (A frags 0-3, B frags) | C_a (16
+// MFMA) | L_b (A frags 4-7) | C_b (16 MFMA).  RAW on a stage: every wave
+// retires its DMA for stage g+1 (counted vmcnt) before the barrier that opens
+// stage g+1's first LOAD section — group 0 at the end of C_b(g), group 1 at
+// the end of L_b(g).  WAR: stage g+3 is issued in L sections of stage g, after
+// every read of the buffer it overwrites (stage g-1, last read by group 1 in
+// L_b(g-1), which ends with lgkmcnt(0) + barrier).
+template <int EPI, int CL, bool PRIO>
+__global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs a) {
+  constexpr int BM = 256, BN = 256, NT = 512;
+  constexpr int WTM = 128, WTN = 64;
+  constexpr int A_BYTES = BM * BK * 2, STAGE_BYTES = (BM + BN) * BK * 2;
+  constexpr int LDS = (RING * STAGE_BYTES > BM * (BN * 2 + 16) ? RING * STAGE_BYTES : BM * (BN * 2 + 16)) >
+                              (WTM * (BN * 4 + 16))
+                          ? (RING * STAGE_BYTES > BM * (BN * 2 + 16) ? RING * STAGE_BYTES : BM * (BN * 2 + 16))
+                          : (WTM * (BN * 4 + 16));
+  __shared__ __attribute__((aligned(16))) char smem[LDS];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int grp = __builtin_amdgcn_readfirstlane(wave >> 2), wc = wave & 3;
+  const int tiles_n = a.N / BN;
+  const int tiles_m = (a.M + BM - 1) / BM;
+  const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
+  const int nk = a.K / BK;
+
+  // DMA: per stage each wave issues A rows (wave*2+j)*16.. and W rows likewise (j = 0,1)
+  const int lrow = lane >> 2;
+  const int lchunk = ((lane & 3) ^ swz(lane >> 4)) * 8;
+  const uint16_t* asrc[2];
+  const uint16_t* wsrc[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    asrc[j] = a.A + (int64_t)min(m0 + (wave * 2 + j) * 16 + lrow, a.M - 1) * a.lda + lchunk;
+    wsrc[j] = a.W + (int64_t)(n0 + (wave * 2 + j) * 16 + lrow) * a.ldw + lchunk;
+  }
+  auto issue_half = [&](int st, int j) {
+    char* base = smem + (st % RING) * STAGE_BYTES;
+    glds16(asrc[j] + st * BK, base + (wave * 2 + j) * 1024);
+    glds16(wsrc[j] + st * BK, base + A_BYTES + (wave * 2 + j) * 1024);
+  };
+  auto wait_stage = [&](int g1) {  // retire this wave's DMA for stage g1
+    const int younger = min(LEAD - 1, nk - 1 - g1);
+    if (younger >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (younger == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+  auto barrier = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto lgkm_barrier = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+#pragma unroll
+  for (int s = 0; s < LEAD; ++s)
+    if (s < nk) { issue_half(s, 0); issue_half(s, 1); }
+  wait_stage(0);
+  barrier();
+  if (grp == 1) barrier();
+
+  const int rd = (lane & 15) * 64 + (((lane >> 4) ^ swz((lane >> 2) & 3)) * 16);
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 bfr[4], af[8 / CL];
+
+  auto mfma_cluster = [&](int mbase, int count) {
+    if (PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni)
+        acc[mbase + mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[ni], af[(mbase % (8 / CL)) + mi], acc[mbase + mi][ni], 0, 0, 0);
+    if (PRIO) __builtin_amdgcn_s_setprio(0);
+    (void)count;
+  };
+  for (int g = 0; g < nk; ++g) {
+    const char* As = smem + (g % RING) * STAGE_BYTES + (grp * WTM) * 64;
+    const char* Ws = smem + (g % RING) * STAGE_BYTES + A_BYTES + (wc * WTN) * 64;
+    if (CL == 2) {
+      // ---- L_a
+      if (g + LEAD < nk) issue_half(g + LEAD, 0);
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) bfr[ni] = *(const bf16x8*)(Ws + ni * 16 * 64 + rd);
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) af[mi] = *(const bf16x8*)(As + mi * 16 * 64 + rd);
+      lgkm_barrier();
+      // ---- C_a
+      mfma_cluster(0, 16);
+      barrier();
+      // ---- L_b
+      if (g + LEAD < nk) issue_half(g + LEAD, 1);
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) af[mi] = *(const bf16x8*)(As + (mi + 4) * 16 * 64 + rd);
+      if (grp == 1 && g + 1 < nk) wait_stage(g + 1);
+      lgkm_barrier();
+      // ---- C_b
+      mfma_cluster(4, 16);
+      if (grp == 0 && g + 1 < nk) wait_stage(g + 1);
+      barrier();
+    } else {
+      // ---- L: all fragments of the stage + the whole DMA share of stage g+3
+      if (g + LEAD < nk) { issue_half(g + LEAD, 0); issue_half(g + LEAD, 1); }
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) bfr[ni] = *(const bf16x8*)(Ws + ni * 16 * 64 + rd);
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi) af[mi] = *(const bf16x8*)(As + mi * 16 * 64 + rd);
+      if (grp == 1 && g + 1 < nk) wait_stage(g + 1);
+      lgkm_barrier();
+      // ---- C: 32 MFMAs
+      mfma_cluster(0, 16);
+      mfma_cluster(4, 16);
+      if (grp == 0 && g + 1 < nk) wait_stage(g + 1);
+      barrier();
+    }
+  }
+  if (grp == 0) barrier();
+  __syncthreads();
+
+  // ------------------------------------------------ epilogue (LDS-staged rows)
+  const int wr = grp;
+  float4 bias[4];
+#pragma unroll
+  for (int ni = 0; ni < 4; ++ni) {
+    const int n = n0 + wc * WTN + ni * 16 + 4 * (lane >> 4);
+    bias[ni] = a.bias ? *(const float4*)(a.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  auto out_row = [&](int m) -> int64_t {
+    return a.group ? (int64_t)(m / a.group) * a.gstride + a.goffset + m % a.group : (int64_t)m;
+  };
+  if (EPI == EPI_BF16 || EPI == EPI_GELU_BF16) {
+    constexpr int RS = BN * 2 + 16;
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        float v0 = acc[mi][ni][0] + bias[ni].x, v1 = acc[mi][ni][1] + bias[ni].y;
+        float v2 = acc[mi][ni][2] + bias[ni].z, v3 = acc[mi][ni][3] + bias[ni].w;
+        if (EPI == EPI_GELU_BF16) {
+          v0 = quick_gelu(v0); v1 = quick_gelu(v1); v2 = quick_gelu(v2); v3 = quick_gelu(v3);
+        }
+        const int r = wr * WTM + mi * 16 + (lane & 15);
+        const int c = wc * WTN + ni * 16 + 4 * (lane >> 4);
+        *(uint2*)(smem + r * RS + c * 2) = make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
+      }
+    __syncthreads();
+    constexpr int CH = BN / 8;
+#pragma unroll 4
+    for (int f = tid; f < BM * CH; f += NT) {
+      const int r = f / CH, c8 = f % CH;
+      const int m = m0 + r;
+      if (m < a.M)
+        *(uint4*)((uint16_t*)a.out + out_row(m) * a.ldo + n0 + c8 * 8) = *(const uint4*)(smem + r * RS + c8 * 16);
+    }
+  } else {
+    constexpr int RS = BN * 4 + 16;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      if (wr == p) {
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < 4; ++ni) {
+            const int r = mi * 16 + (lane & 15);
+            const int c = wc * WTN + ni * 16 + 4 * (lane >> 4);
+            *(float4*)(smem + r * RS + c * 4) =
+                make_float4(acc[mi][ni][0] + bias[ni].x, acc[mi][ni][1] + bias[ni].y, acc[mi][ni][2] + bias[ni].z,
+                            acc[mi][ni][3] + bias[ni].w);
+          }
+      }
+      __syncthreads();
+      constexpr int C4 = BN / 4;
+#pragma unroll 4
+      for (int f = tid; f < WTM * C4; f += NT) {
+        const int r = f / C4, c4 = f % C4;
+        const int m = m0 + p * WTM + r;
+        if (m < a.M) {
+          const float4 v = *(const float4*)(smem + r * RS + c4 * 16);
+          float4* dst = (float4*)((float*)a.out + out_row(m) * a.ldo + n0 + c4 * 4);
+          if (EPI == EPI_RESID_F32) {
+            const float4 o = *dst;
+            *dst = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + v.w);
+          } else {
+            *dst = v;
+          }
+        }
+      }
+      if (p == 0) __syncthreads();
+    }
+  }
+}
+
 int cu_count() {
   static int n = 0;
   if (!n) {
@@ -231,7 +439,16 @@ int cu_count() {
 template <int EPI>
 hipError_t launch(const GemmArgs& a, hipStream_t s) {
   const bool big = a.N % 256 == 0 && a.M >= 1024;
-  if (big) {
+  // variant 0 (default) = 3: ping-pong, one 32-MFMA cluster per stage (fastest
+  // on every tower shape measured, scripts/gemm_micro.py); 1 = persistent ring
+  const int v = a.variant == 0 ? 3 : a.variant;
+  if (big && v >= 2 && v <= 5 && a.K / BK >= LEAD) {
+    const int nt = ((a.M + 255) / 256) * (a.N / 256);
+    if (v == 2) hipLaunchKernelGGL((gemm_pp_kernel<EPI, 2, false>), dim3(nt), dim3(512), 0, s, a);
+    else if (v == 3) hipLaunchKernelGGL((gemm_pp_kernel<EPI, 1, false>), dim3(nt), dim3(512), 0, s, a);
+    else if (v == 4) hipLaunchKernelGGL((gemm_pp_kernel<EPI, 2, true>), dim3(nt), dim3(512), 0, s, a);
+    else hipLaunchKernelGGL((gemm_pp_kernel<EPI, 1, true>), dim3(nt), dim3(512), 0, s, a);
+  } else if (big) {
     const int nt = ((a.M + 255) / 256) * (a.N / 256);
     const int g = nt < cu_count() ? nt : cu_count();
     hipLaunchKernelGGL((gemm_kernel<EPI, 256, 256, 2, 4>), dim3(g), dim3(512), 0, s, a);

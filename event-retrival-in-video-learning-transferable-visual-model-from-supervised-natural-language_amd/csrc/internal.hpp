@@ -21,6 +21,7 @@ struct GemmArgs {
   int M, N, K;
   // output row remap: r -> (r / group) * gstride + goffset + r % group (group == 0: identity)
   int group, gstride, goffset;
+  int variant;  // main-loop schedule (0 = default choice; see gemm.hip)
 };
 
 // Requirements: K % 64 == 0, N % 128 == 0, A/W 16-byte aligned rows.

@@ -53,8 +53,9 @@ class CLIP:
         self._out_dtype = torch.float32
         self._lock = threading.Lock()
         if image_chunk is None:
-            # ~50-60k token rows per pass keeps one pass's activations near the Infinity Cache size
-            image_chunk = max(8, 51200 // cfg.vision_tokens)
+            # ~100k token rows per pass: enough 256x256 GEMM tiles for 256 CUs
+            # even at N = 768 (391 x 3), measured best with 20k-100k rows
+            image_chunk = max(8, 100_000 // cfg.vision_tokens)
         self._chunks = (int(image_chunk), int(text_chunk))
         self._ctx = None
         self._build()

@@ -1,8 +1,10 @@
 """GEMM microbenchmark through mi_op_gemm (random bf16 operands, HIP events).
 
-usage: python scripts/gemm_micro.py [reps]
+usage: python scripts/gemm_micro.py [reps] [shapes,comma] [variants,comma]
 Shapes: the four ViT-B/32 tower GEMMs at a 2000-frame chunk (M = 100000) and
-a long-K square-ish case that isolates main-loop efficiency.
+a long-K case that isolates main-loop efficiency.  Variants are main-loop
+schedules (gemm.hip; 0 = default); each variant's output is checked against
+the first one and timed in interleaved rounds in ONE process (guide §5.4 rule 24).
 """
 import os
 import sys
@@ -19,13 +21,16 @@ SHAPES = {
     "out": (100000, 768, 768, 0),
     "fc": (100000, 3072, 768, 1),
     "proj": (100000, 768, 3072, 0),
-    "sq4096": (8192, 8192, 4096, 3),
+    "long": (16384, 4096, 4096, 0),
+    "qkv20k": (20000, 2304, 768, 0),
+    "fc20k": (20000, 3072, 768, 1),
 }
 
 
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
     only = sys.argv[2].split(",") if len(sys.argv) > 2 else list(SHAPES)
+    variants = [int(v) for v in sys.argv[3].split(",")] if len(sys.argv) > 3 else [0]
     L = N.lib()
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
@@ -34,22 +39,33 @@ def main():
         M, Nn, K, epi = SHAPES[name]
         A = (torch.rand(M, K, device=dev, generator=g) * 2 - 1).bfloat16()
         W = ((torch.rand(Nn, K, device=dev, generator=g) * 2 - 1) * K ** -0.5).bfloat16()
-        bias = torch.zeros(Nn, device=dev)
-        out = torch.zeros(M, Nn, device=dev, dtype=torch.bfloat16 if epi in (0, 1) else torch.float32)
-        run = lambda: N.check(L.mi_op_gemm(A.data_ptr(), W.data_ptr(), bias.data_ptr(), out.data_ptr(), M, Nn, K,  # noqa
-                                           epi, sp), "gemm")
-        run()
+        bias = torch.rand(Nn, device=dev, generator=g)
+        outs = {v: torch.zeros(M, Nn, device=dev, dtype=torch.bfloat16 if epi in (0, 1) else torch.float32)
+                for v in variants}
+
+        def run(v):
+            N.check(L.mi_op_gemm(A.data_ptr(), W.data_ptr(), bias.data_ptr(), outs[v].data_ptr(), M, Nn, K,
+                                 epi | (v << 8), sp), "gemm")
+        for v in variants:
+            run(v)
         torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(reps):
-            run()
-        e1.record()
-        torch.cuda.synchronize()
-        us = e0.elapsed_time(e1) * 1e3 / reps
-        print(f"{name:7s} M={M} N={Nn} K={K} epi={epi}: {us:9.1f} us  {2.0 * M * Nn * K / us / 1e6:7.1f} TFLOP/s",
-              flush=True)
-        del A, W, out
+        ref = outs[variants[0]].float()
+        times = {v: [] for v in variants}
+        for _ in range(3):
+            for v in variants:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(reps):
+                    run(v)
+                e1.record()
+                torch.cuda.synchronize()
+                times[v].append(e0.elapsed_time(e1) * 1e3 / reps)
+        for v in variants:
+            us = min(times[v])
+            err = (outs[v].float() - ref).abs().max().item()
+            print(f"{name:7s} v{v} M={M} N={Nn} K={K} epi={epi}: {us:9.1f} us {2.0 * M * Nn * K / us / 1e6:7.1f} "
+                  f"TFLOP/s  maxdiff vs v{variants[0]} {err:.3g}", flush=True)
+        del A, W, outs, ref
 
 
 if __name__ == "__main__":
