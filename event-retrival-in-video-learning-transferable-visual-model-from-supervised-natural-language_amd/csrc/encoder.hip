@@ -221,6 +221,36 @@ __global__ __launch_bounds__(256) void eot_gather_ln_kernel(const int32_t* __res
 
 // ------------------------------------------------------------------ im2col
 // One thread per 8 consecutive k of one patch row.
+// Vector form for P % 8 == 0 (B/32, B/16): the 8 k of a thread are 8
+// consecutive pixels of one image row -> one 16-byte (bf16) or two 16-byte
+// (f32) loads and one 16-byte store; consecutive threads walk a patch row.
+template <bool IN_BF16>
+__global__ __launch_bounds__(256) void im2col8_kernel(const void* __restrict__ pixels, uint16_t* __restrict__ out,
+                                                      int64_t total8, int R, int P, int G, int Kp) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total8) return;
+  const int k8 = Kp >> 3;
+  const int64_t prow = i / k8;
+  const int kb = (int)(i % k8) * 8;
+  const int PP = P * P;
+  uint4 o = make_uint4(0, 0, 0, 0);
+  if (kb < 3 * PP) {
+    const int64_t bimg = prow / (G * G);
+    const int p = (int)(prow % (G * G));
+    const int gy = p / G, gx = p % G;
+    const int c = kb / PP, rem = kb % PP, kh = rem / P, kw = rem % P;
+    const int64_t off = ((bimg * 3 + c) * R + (gy * P + kh)) * (int64_t)R + gx * P + kw;
+    if (IN_BF16) {
+      o = *(const uint4*)((const uint16_t*)pixels + off);
+    } else {
+      const float4 a = *(const float4*)((const float*)pixels + off);
+      const float4 b = *(const float4*)((const float*)pixels + off + 4);
+      o = make_uint4(pack_bf16x2(a.x, a.y), pack_bf16x2(a.z, a.w), pack_bf16x2(b.x, b.y), pack_bf16x2(b.z, b.w));
+    }
+  }
+  *(uint4*)(out + prow * Kp + kb) = o;
+}
+
 template <bool IN_BF16>
 __global__ __launch_bounds__(256) void im2col_kernel(const void* __restrict__ pixels, uint16_t* __restrict__ out,
                                                      int64_t total8, int R, int P, int G, int Kp) {
@@ -254,73 +284,75 @@ __global__ __launch_bounds__(256) void im2col_kernel(const void* __restrict__ pi
 }
 
 // --------------------------------------------------------------- attention
-// One workgroup (4 waves) per (sequence, head); head dim 64; the whole padded
-// sequence (SP rows, multiple of 32) is resident in LDS: Q and K row-major,
-// V transposed (so P.V's B operand is a contiguous 16-byte read), P per wave.
-// Rows are padded to an odd number of 16-byte slots (bank-conflict free
-// ds_read_b128).  S = Q K^T and O = P V on mfma_f32_16x16x32_bf16; softmax in
-// fp32 registers, rows reduced across the 16 lanes that share them.
+// One wave per (sequence, head), head dim 64, whole padded sequence (SP rows,
+// multiple of 32) per wave; no workgroup barriers.
+//   S = Q K^T : Q (A operand) and K (B operand) fragments are loaded straight
+//     from the packed qkv rows as 16-byte pieces (the 16x16x32 operand map
+//     wants 8 consecutive head dims of one row per lane), rows past S clamped;
+//   softmax over keys in f32 registers (scale 1/8, key >= S and causal masks),
+//     rows reduced across the 16 lanes that hold them; P normalised, to bf16,
+//     through a per-wave LDS tile (C layout -> operand layout);
+//   O^T = V^T P^T with V^T (A operand) from a per-wave transposed LDS image
+//     and P (B operand), so each lane holds 4 consecutive head dims of one
+//     query row -> one 8-byte store.
+// LDS rows are padded to an odd number of 16-byte slots.
 template <int SP>
-__global__ __launch_bounds__(256) void attention_kernel(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ out,
-                                                        int S, int W, int H, int causal) {
-  constexpr int QK_STRIDE = 72;        // bf16 per Q/K row (144 B = 9 slots)
-  constexpr int VT_STRIDE = SP + 8;    // bf16 per V^T / P row
-  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * SP * QK_STRIDE + 64 * VT_STRIDE + 4 * 16 * VT_STRIDE];
-  uint16_t* Qs = lds;
-  uint16_t* Ks = Qs + SP * QK_STRIDE;
-  uint16_t* Vt = Ks + SP * QK_STRIDE;
-  uint16_t* Ps = Vt + 64 * VT_STRIDE;
-
-  const int bh = blockIdx.x;
-  const int bseq = bh / H, h = bh % H;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+__global__ __launch_bounds__(64) void attention_kernel(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ out,
+                                                       int S, int W, int H, int causal, int items) {
+  constexpr int TS = SP + 8;  // bf16 per V^T / P row (odd number of 16-byte slots)
+  __shared__ __attribute__((aligned(16))) uint16_t lds[64 * TS + 16 * TS];
+  uint16_t* Vt = lds;
+  uint16_t* Pw = lds + 64 * TS;
+  const int item = blockIdx.x;
+  if (item >= items) return;
+  const int bseq = item / H, h = item % H;
+  const int lane = threadIdx.x;
   const int64_t ld = 3 * (int64_t)W;
-  const uint16_t* base = qkv + (int64_t)bseq * S * ld + h * 64;
+  const uint16_t* qb = qkv + (int64_t)bseq * S * ld + h * 64;
+  const uint16_t* kb = qb + W;
+  const uint16_t* vb = qb + 2 * W;
 
-  // load Q, K (row-major) and V (transposed); zero the padding rows
-  for (int c = tid; c < SP * 8; c += 256) {
-    const int r = c >> 3, ch = c & 7;
-    uint4 q = make_uint4(0, 0, 0, 0), k = q, v = q;
-    if (r < S) {
-      const uint16_t* src = base + (int64_t)r * ld + ch * 8;
-      q = *(const uint4*)src;
-      k = *(const uint4*)(src + W);
-      v = *(const uint4*)(src + 2 * W);
-    }
-    *(uint4*)(Qs + r * QK_STRIDE + ch * 8) = q;
-    *(uint4*)(Ks + r * QK_STRIDE + ch * 8) = k;
+  // V^T image: lane (ch = lane>>3, r8 = lane&7) loads 8 head dims of key
+  // row r and scatters them down column r of V^T (consecutive lanes ->
+  // consecutive keys, so the 2-byte writes of an instruction are contiguous).
+  for (int r0 = 0; r0 < SP; r0 += 8) {
+    const int r = r0 + (lane & 7), ch = lane >> 3;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (r < S) v = *(const uint4*)(vb + (int64_t)r * ld + ch * 8);
     const uint16_t* vv = (const uint16_t*)&v;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) Vt[(ch * 8 + e) * VT_STRIDE + r] = vv[e];
+    for (int e = 0; e < 8; ++e) Vt[(ch * 8 + e) * TS + r] = vv[e];
   }
-  __syncthreads();
 
   constexpr int NKT = SP / 16;
   const float scale = 0.125f;  // 64 ** -0.5
-  uint16_t* Pw = Ps + wave * 16 * VT_STRIDE;
+  const int fr = lane & 15, fk = 8 * (lane >> 4);
   const int nqt = (S + 15) / 16;
-  for (int qt = wave; qt < nqt; qt += 4) {
+  for (int qt = 0; qt < nqt; ++qt) {
+    const int64_t qrow = min(qt * 16 + fr, S - 1);
+    bf16x8 qa[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) qa[s] = *(const bf16x8*)(qb + qrow * ld + 32 * s + fk);
     f32x4 sc[NKT];
 #pragma unroll
     for (int kt = 0; kt < NKT; ++kt) {
+      const int64_t krow = min(kt * 16 + fr, S - 1);
       f32x4 c = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const bf16x8 a = *(const bf16x8*)(Qs + (qt * 16 + (lane & 15)) * QK_STRIDE + 32 * s + 8 * (lane >> 4));
-        const bf16x8 bb = *(const bf16x8*)(Ks + (kt * 16 + (lane & 15)) * QK_STRIDE + 32 * s + 8 * (lane >> 4));
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bb, c, 0, 0, 0);
+        const bf16x8 kf = *(const bf16x8*)(kb + krow * ld + 32 * s + fk);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa[s], kf, c, 0, 0, 0);
       }
       sc[kt] = c;
     }
-    // row = qt*16 + 4*(lane>>4) + j, key = kt*16 + (lane&15)
-    float mx[4], sum[4];
+    // sc[kt][j]: query row qt*16 + 4*(lane>>4) + j, key kt*16 + (lane&15)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int row = qt * 16 + 4 * (lane >> 4) + j;
       float m = -INFINITY;
 #pragma unroll
       for (int kt = 0; kt < NKT; ++kt) {
-        const int key = kt * 16 + (lane & 15);
+        const int key = kt * 16 + fr;
         float v = sc[kt][j] * scale;
         if (key >= S || (causal && key > row)) v = -INFINITY;
         sc[kt][j] = v;
@@ -328,43 +360,40 @@ __global__ __launch_bounds__(256) void attention_kernel(const uint16_t* __restri
       }
 #pragma unroll
       for (int o = 1; o < 16; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-      mx[j] = m;
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float s = 0.f;
+      float sum = 0.f;
 #pragma unroll
       for (int kt = 0; kt < NKT; ++kt) {
-        const float p = __expf(sc[kt][j] - mx[j]);
+        const float p = __expf(sc[kt][j] - m);
         sc[kt][j] = p;
-        s += p;
+        sum += p;
       }
 #pragma unroll
-      for (int o = 1; o < 16; o <<= 1) s += __shfl_xor(s, o, 64);
-      sum[j] = s;
+      for (int o = 1; o < 16; o <<= 1) sum += __shfl_xor(sum, o, 64);
+      const float inv = 1.0f / sum;
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt) Pw[(4 * (lane >> 4) + j) * TS + kt * 16 + fr] = f2bf_hw(sc[kt][j] * inv);
     }
-#pragma unroll
-    for (int kt = 0; kt < NKT; ++kt)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) Pw[(4 * (lane >> 4) + j) * VT_STRIDE + kt * 16 + (lane & 15)] = f2bf(sc[kt][j]);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
-
+    // O^T[d][q] = sum_key V^T[d][key] P[q][key]
+    uint2 ov[4];
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
       f32x4 o = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < SP / 32; ++s) {
-        const bf16x8 a = *(const bf16x8*)(Pw + (lane & 15) * VT_STRIDE + 32 * s + 8 * (lane >> 4));
-        const bf16x8 bb = *(const bf16x8*)(Vt + (dt * 16 + (lane & 15)) * VT_STRIDE + 32 * s + 8 * (lane >> 4));
-        o = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bb, o, 0, 0, 0);
+        const bf16x8 va = *(const bf16x8*)(Vt + (dt * 16 + fr) * TS + 32 * s + fk);
+        const bf16x8 pb = *(const bf16x8*)(Pw + fr * TS + 32 * s + fk);
+        o = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pb, o, 0, 0, 0);
       }
+      ov[dt] = make_uint2(pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3]));
+    }
+    // lane: query row qt*16 + (lane&15), head dims dt*16 + 4*(lane>>4) + 0..3
+    const int row = qt * 16 + fr;
+    if (row < S) {
+      uint16_t* dst = out + ((int64_t)bseq * S + row) * W + h * 64 + 4 * (lane >> 4);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int row = qt * 16 + 4 * (lane >> 4) + j;
-        if (row < S)
-          out[((int64_t)bseq * S + row) * W + h * 64 + dt * 16 + (lane & 15)] = f2bf(o[j] / sum[j]);
-      }
+      for (int dt = 0; dt < 4; ++dt) *(uint2*)(dst + dt * 16) = ov[dt];
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
@@ -444,7 +473,12 @@ hipError_t im2col(const void* pixels, int in_bf16, uint16_t* out, int B, int R, 
   const int64_t total8 = (int64_t)B * G * G * (Kp / 8);
   if (total8 <= 0) return hipSuccess;
   const dim3 grid((unsigned)((total8 + 255) / 256));
-  if (in_bf16)
+  const bool vec = P % 8 == 0 && ((uintptr_t)pixels & 15) == 0;
+  if (vec && in_bf16)
+    hipLaunchKernelGGL(im2col8_kernel<true>, grid, dim3(256), 0, s, pixels, out, total8, R, P, G, Kp);
+  else if (vec)
+    hipLaunchKernelGGL(im2col8_kernel<false>, grid, dim3(256), 0, s, pixels, out, total8, R, P, G, Kp);
+  else if (in_bf16)
     hipLaunchKernelGGL(im2col_kernel<true>, grid, dim3(256), 0, s, pixels, out, total8, R, P, G, Kp);
   else
     hipLaunchKernelGGL(im2col_kernel<false>, grid, dim3(256), 0, s, pixels, out, total8, R, P, G, Kp);
@@ -453,14 +487,15 @@ hipError_t im2col(const void* pixels, int in_bf16, uint16_t* out, int B, int R, 
 
 hipError_t attention(const uint16_t* qkv, uint16_t* out, int B, int S, int W, int causal, hipStream_t s) {
   const int H = W / 64;
-  const dim3 grid(B * H), block(256);
-  if (B <= 0) return hipSuccess;
-  if (S <= 32) hipLaunchKernelGGL(attention_kernel<32>, grid, block, 0, s, qkv, out, S, W, H, causal);
-  else if (S <= 64) hipLaunchKernelGGL(attention_kernel<64>, grid, block, 0, s, qkv, out, S, W, H, causal);
-  else if (S <= 96) hipLaunchKernelGGL(attention_kernel<96>, grid, block, 0, s, qkv, out, S, W, H, causal);
-  else if (S <= 128) hipLaunchKernelGGL(attention_kernel<128>, grid, block, 0, s, qkv, out, S, W, H, causal);
-  else if (S <= 224) hipLaunchKernelGGL(attention_kernel<224>, grid, block, 0, s, qkv, out, S, W, H, causal);
-  else if (S <= 288) hipLaunchKernelGGL(attention_kernel<288>, grid, block, 0, s, qkv, out, S, W, H, causal);
+  const int items = B * H;
+  if (items <= 0) return hipSuccess;
+  const dim3 grid(items), block(64);
+  if (S <= 32) hipLaunchKernelGGL(attention_kernel<32>, grid, block, 0, s, qkv, out, S, W, H, causal, items);
+  else if (S <= 64) hipLaunchKernelGGL(attention_kernel<64>, grid, block, 0, s, qkv, out, S, W, H, causal, items);
+  else if (S <= 96) hipLaunchKernelGGL(attention_kernel<96>, grid, block, 0, s, qkv, out, S, W, H, causal, items);
+  else if (S <= 128) hipLaunchKernelGGL(attention_kernel<128>, grid, block, 0, s, qkv, out, S, W, H, causal, items);
+  else if (S <= 224) hipLaunchKernelGGL(attention_kernel<224>, grid, block, 0, s, qkv, out, S, W, H, causal, items);
+  else if (S <= 288) hipLaunchKernelGGL(attention_kernel<288>, grid, block, 0, s, qkv, out, S, W, H, causal, items);
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }
