@@ -103,6 +103,22 @@ def kernel_timing(model, cfg, chunk, reps=20):
     return res
 
 
+def pmc_traffic(shape):
+    """HBM bytes per launch of the GEMM at `shape` [M, N, K] from the newest
+    committed PMC summary (profiles/*_gemm_traffic.json, made by
+    scripts/gpu_traffic.sh + scripts/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE,
+    the gfx950 corrections of MI355X_MICROARCH.md "HBM").  None if absent."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_gemm_traffic.json")), reverse=True):
+        try:
+            for v in json.load(open(f)).values():
+                if list(v["shape"]) == list(shape):
+                    return v["traffic_bytes"], os.path.relpath(f, ROOT)
+        except (OSError, ValueError, KeyError):
+            continue
+    return None, None
+
+
 def rank_timing(corpus, txt, k, reps=50):
     import torch
     from miclip import retrieval
@@ -235,9 +251,13 @@ def main():
         if dom:
             fl = 2.0 * M * 4 * cfg.vision_width * cfg.vision_width
             ach = fl / (dom["us"] * 1e-6) / 1e12
-            roof = {"bound": "mfma", "kernel": "gemm_kernel<EPI_GELU_BF16> (mlp.c_fc + QuickGELU)",
+            shape = [M, 4 * cfg.vision_width, cfg.vision_width]
+            traffic, tsrc = pmc_traffic(shape)
+            roof = {"bound": "mfma", "kernel": "gemm_pp_kernel<EPI_GELU_BF16> (mlp.c_fc + QuickGELU)",
                     "achieved": round(ach, 1), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(ach / BF16_PEAK_TFLOPS, 4), "traffic": None,
+                    "frac": round(ach / BF16_PEAK_TFLOPS, 4), "traffic": traffic, "traffic_source": tsrc,
+                    "algorithmic_bytes": 2 * (M * 4 * cfg.vision_width + 4 * cfg.vision_width ** 2
+                                              + M * cfg.vision_width),
                     "flops_per_launch": fl, "launch_shape": [M, 4 * cfg.vision_width, cfg.vision_width],
                     "avg_launch_us": dom["us"]}
         cpu = None
@@ -252,7 +272,7 @@ def main():
             "config": {"workload": f"{cfg.name} bf16, {Nf} frames/GPU x {Q} text queries, top-{k}"
                                    + (" (BASELINE configs[1])" if world == 1 and Nf == 10_000 else
                                       f" ({world} shards, RCCL all-gather top-k)"),
-                       "model": cfg.name, "global_batch": Nf * world, "queries": Q, "k": k,
+                       "frames_per_gpu": Nf, "global_frames": Nf * world, "queries": Q, "k": k,
                        "image_chunk": chunk, "parallelism": f"dp{world}"},
             "roofline": roof,
             "mfma_frac_end_to_end": round(mfma_frac, 4),

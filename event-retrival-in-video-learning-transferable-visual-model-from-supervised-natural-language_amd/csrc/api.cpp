@@ -185,8 +185,8 @@ int mi_clip_create(const mi_clip_arch* arch, const float* weights, int64_t numel
   if (a.image_resolution % a.vision_patch_size) return fail(MI_ERR_ARG, "resolution not divisible by patch");
   if (a.text_heads * 64 != a.text_width) return fail(MI_ERR_UNSUPPORTED, "text head dim must be 64");
   const int G = a.image_resolution / a.vision_patch_size;
-  if (G * G + 1 > 288 || a.context_length > 288)
-    return fail(MI_ERR_UNSUPPORTED, "sequence longer than 288 tokens not supported yet");
+  if (G * G + 1 > 640 || a.context_length > 640)
+    return fail(MI_ERR_UNSUPPORTED, "sequences longer than 640 tokens are not supported");
   const int64_t expect = mi_clip_weights_numel(arch);
   if (numel != expect) return fail(MI_ERR_ARG, "weight blob has %lld elements, expected %lld", (long long)numel,
                                    (long long)expect);
@@ -336,7 +336,7 @@ static GemmArgs gargs(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t
                       int64_t ldo, int M, int N, int K) {
   GemmArgs g;
   g.A = A; g.lda = lda; g.W = W; g.ldw = ldw; g.bias = bias; g.out = out; g.ldo = ldo;
-  g.M = M; g.N = N; g.K = K; g.group = 0; g.gstride = 0; g.goffset = 0;
+  g.M = M; g.N = N; g.K = K; g.group = 0; g.gstride = 0; g.goffset = 0; g.ngroup = 0;
   g.variant = gemm_variant();
   return g;
 }
@@ -519,7 +519,7 @@ int mi_op_layernorm(const float* x, const float* g, const float* b, void* out, i
 
 int mi_op_attention(const void* qkv, void* out, int32_t B, int32_t S, int32_t W, int32_t causal, void* stream) {
   if (!qkv || !out || B < 0 || S < 1) return fail(MI_ERR_ARG, "mi_op_attention: bad arguments");
-  if (W % 64 || S > 288) return fail(MI_ERR_UNSUPPORTED, "mi_op_attention: W %% 64 == 0 and S <= 288");
+  if (W % 64 || S > 640) return fail(MI_ERR_UNSUPPORTED, "mi_op_attention: W %% 64 == 0 and S <= 640");
   HIP_TRY(attention((const uint16_t*)qkv, (uint16_t*)out, B, S, W, causal, (hipStream_t)stream));
   return MI_OK;
 }

@@ -400,6 +400,162 @@ __global__ __launch_bounds__(64) void attention_kernel(const uint16_t* __restric
   }
 }
 
+// ------------------------------------------------- attention, long sequences
+// One 512-thread workgroup (8 waves) per (sequence, head) for S > 96
+// (B/16: 197, L/14: 257, L/14@336: 577 tokens).  V^T of the whole padded
+// sequence (SP keys, multiple of 64) is staged once in LDS and shared by the 8
+// waves; wave w takes query tiles w, w+8, ... and streams the keys in chunks
+// of 64 with an online (flash) softmax:
+//   S_c = Q K_c^T      A = Q rows, B = K rows (16-byte loads straight from the
+//                      packed qkv rows; the next chunk's K is loaded before the
+//                      current chunk's softmax so its latency hides);
+//   m' = max(m, rowmax S_c); alpha = e^(m - m'); P = e^(S_c - m');
+//   l = alpha l + rowsum P;  O = alpha O + P V_c
+//   O = P V            A = P (bf16, per-wave LDS tile), B = V^T rows from LDS,
+//                      so O's C layout (query rows 4*(lane>>4)+j) matches the
+//                      row statistics of S — the rescale is per register.
+// The 16x64 output tile is transposed through the P tile into row-contiguous
+// 16-byte stores.  Keys >= S are masked to -inf (and their V^T columns are 0).
+template <int SP>
+__global__ __launch_bounds__(512) void attention_long_kernel(const uint16_t* __restrict__ qkv,
+                                                             uint16_t* __restrict__ out, int S, int W, int H,
+                                                             int causal) {
+  constexpr int TS = SP + 8;  // V^T row (odd number of 16-byte slots)
+  constexpr int PS = 72;      // P row: 64 keys + pad (9 slots)
+  __shared__ __attribute__((aligned(16))) uint16_t lds[64 * TS + 8 * 16 * PS];
+  uint16_t* Vt = lds;
+  const int item = blockIdx.x;
+  const int bseq = item / H, h = item % H;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  uint16_t* Pw = lds + 64 * TS + wave * 16 * PS;
+  const int64_t ld = 3 * (int64_t)W;
+  const uint16_t* qb = qkv + (int64_t)bseq * S * ld + h * 64;
+  const uint16_t* kb = qb + W;
+  const uint16_t* vb = qb + 2 * W;
+
+  for (int r0 = 0; r0 < SP; r0 += 64) {
+    const int r = r0 + lane, ch = wave;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (r < S) v = *(const uint4*)(vb + (int64_t)r * ld + ch * 8);
+    const uint16_t* vv = (const uint16_t*)&v;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) Vt[(ch * 8 + e) * TS + r] = vv[e];
+  }
+  __syncthreads();
+
+  const float scale = 0.125f;
+  const int fr = lane & 15, fk = 8 * (lane >> 4), qg = lane >> 4;
+  const int nqt = (S + 15) / 16;
+  for (int qt = wave; qt < nqt; qt += 8) {
+    const int64_t qrow = min(qt * 16 + fr, S - 1);
+    bf16x8 qa[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) qa[s] = *(const bf16x8*)(qb + qrow * ld + 32 * s + fk);
+    const int last_key = causal ? min(qt * 16 + 15, S - 1) : S - 1;
+    const int nch = last_key / 64 + 1;
+    float m[4], l[4];
+    f32x4 o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      m[j] = -INFINITY;
+      l[j] = 0.f;
+      o[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    bf16x8 kf[4][2];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      const int64_t krow = min(kt * 16 + fr, S - 1);
+#pragma unroll
+      for (int s = 0; s < 2; ++s) kf[kt][s] = *(const bf16x8*)(kb + krow * ld + 32 * s + fk);
+    }
+    for (int c = 0; c < nch; ++c) {
+      f32x4 sc[4];
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 2; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa[s], kf[kt][s], acc, 0, 0, 0);
+        sc[kt] = acc;
+      }
+      if (c + 1 < nch) {  // prefetch the next chunk's K fragments
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt) {
+          const int64_t krow = min((c + 1) * 64 + kt * 16 + fr, S - 1);
+#pragma unroll
+          for (int s = 0; s < 2; ++s) kf[kt][s] = *(const bf16x8*)(kb + krow * ld + 32 * s + fk);
+        }
+      }
+      // sc[kt][j]: query row qt*16 + 4*qg + j, key c*64 + kt*16 + fr
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = qt * 16 + 4 * qg + j;
+        float cm = -INFINITY;
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt) {
+          const int key = c * 64 + kt * 16 + fr;
+          float v = sc[kt][j] * scale;
+          if (key >= S || (causal && key > row)) v = -INFINITY;
+          sc[kt][j] = v;
+          cm = fmaxf(cm, v);
+        }
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) cm = fmaxf(cm, __shfl_xor(cm, off, 64));
+        const float mn = fmaxf(m[j], cm);
+        // mn is finite: chunk 0 always holds key 0 <= row (rows past S are clamped copies)
+        const float alpha = __expf(m[j] - mn);
+        m[j] = mn;
+        float sum = 0.f;
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt) {
+          const float p = __expf(sc[kt][j] - mn);
+          sum += p;
+          Pw[(4 * qg + j) * PS + kt * 16 + fr] = f2bf_hw(p);
+        }
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) sum += __shfl_xor(sum, off, 64);
+        l[j] = l[j] * alpha + sum;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) o[dt][j] *= alpha;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 pa = *(const bf16x8*)(Pw + fr * PS + 32 * s + fk);
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          const bf16x8 vf = *(const bf16x8*)(Vt + (dt * 16 + fr) * TS + c * 64 + 32 * s + fk);
+          o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, vf, o[dt], 0, 0, 0);
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+    }
+    // o[dt][j]: query row 4*qg + j, head dim dt*16 + fr -> P tile -> rows
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float inv = 1.0f / l[j];
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) Pw[(4 * qg + j) * PS + dt * 16 + fr] = f2bf_hw(o[dt][j] * inv);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    {
+      const int r = lane >> 2, c16 = (lane & 3) * 16;  // row r, head dims c16..c16+15
+      const uint4 a0 = *(const uint4*)(Pw + r * PS + c16);
+      const uint4 a1 = *(const uint4*)(Pw + r * PS + c16 + 8);
+      const int row = qt * 16 + r;
+      if (row < S) {
+        uint16_t* dst = out + ((int64_t)bseq * S + row) * W + h * 64 + c16;
+        *(uint4*)dst = a0;
+        *(uint4*)(dst + 8) = a1;
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
 // ---------------------------------------------------------------- finalize
 __global__ __launch_bounds__(256) void finalize_kernel(const float* __restrict__ y, void* __restrict__ out,
                                                        int out_dtype, int rows, int D, int l2) {
@@ -490,12 +646,14 @@ hipError_t attention(const uint16_t* qkv, uint16_t* out, int B, int S, int W, in
   const int items = B * H;
   if (items <= 0) return hipSuccess;
   const dim3 grid(items), block(64);
+  const dim3 lblock(512);
   if (S <= 32) hipLaunchKernelGGL(attention_kernel<32>, grid, block, 0, s, qkv, out, S, W, H, causal, items);
   else if (S <= 64) hipLaunchKernelGGL(attention_kernel<64>, grid, block, 0, s, qkv, out, S, W, H, causal, items);
   else if (S <= 96) hipLaunchKernelGGL(attention_kernel<96>, grid, block, 0, s, qkv, out, S, W, H, causal, items);
-  else if (S <= 128) hipLaunchKernelGGL(attention_kernel<128>, grid, block, 0, s, qkv, out, S, W, H, causal, items);
-  else if (S <= 224) hipLaunchKernelGGL(attention_kernel<224>, grid, block, 0, s, qkv, out, S, W, H, causal, items);
-  else if (S <= 288) hipLaunchKernelGGL(attention_kernel<288>, grid, block, 0, s, qkv, out, S, W, H, causal, items);
+  else if (S <= 128) hipLaunchKernelGGL(attention_long_kernel<128>, grid, lblock, 0, s, qkv, out, S, W, H, causal);
+  else if (S <= 256) hipLaunchKernelGGL(attention_long_kernel<256>, grid, lblock, 0, s, qkv, out, S, W, H, causal);
+  else if (S <= 384) hipLaunchKernelGGL(attention_long_kernel<384>, grid, lblock, 0, s, qkv, out, S, W, H, causal);
+  else if (S <= 640) hipLaunchKernelGGL(attention_long_kernel<640>, grid, lblock, 0, s, qkv, out, S, W, H, causal);
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }

@@ -67,6 +67,25 @@ __device__ __forceinline__ float4 lds_read_f4(const float* p) {
   return v;
 }
 
+// Logical tile t -> (m-block, n-block).  Tiles are taken in groups of `ng`
+// n-blocks (ng >= tiles_n: plain m-major raster): within a group all m-blocks
+// are swept with the group's n-blocks innermost, so the W column panel of the
+// group stays L2-resident while the XCD streams A (each A panel is re-read by
+// the ng concurrent tiles of its row).  With xcd_remap each XCD owns a
+// contiguous run of t, i.e. one group and a contiguous range of m-blocks.
+__device__ __forceinline__ void tile_coords(int t, int tiles_m, int tiles_n, int ng, int& mb, int& nb) {
+  if (ng <= 0 || ng >= tiles_n) {
+    mb = t / tiles_n;
+    nb = t % tiles_n;
+    return;
+  }
+  const int per = tiles_m * ng;
+  const int g = t / per, r = t - g * per;
+  const int ngg = min(ng, tiles_n - g * ng);
+  mb = r / ngg;
+  nb = g * ng + r % ngg;
+}
+
 template <int N>
 __device__ __forceinline__ void wait_vm_barrier() {
   // retire all but the N youngest vector-memory ops of this wave, then a raw
@@ -248,8 +267,10 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs a) {
   const int grp = __builtin_amdgcn_readfirstlane(wave >> 2), wc = wave & 3;
   const int tiles_n = a.N / BN;
   const int tiles_m = (a.M + BM - 1) / BM;
-  const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
-  const int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
+  int m0, n0;
+  tile_coords(xcd_remap(blockIdx.x, tiles_m * tiles_n), tiles_m, tiles_n, a.ngroup, m0, n0);
+  m0 *= BM;
+  n0 *= BN;
   const int nk = a.K / BK;
 
   // DMA: per stage each wave issues A rows (wave*2+j)*16.. and W rows likewise (j = 0,1)
@@ -436,13 +457,30 @@ int cu_count() {
   return n;
 }
 
+// n-blocks per tile group (tile_coords): the largest divisor of tiles_n whose
+// W panel (ng x 256 rows x K bf16) fits ~1.6 MB of the XCD's 4 MB L2; 0 (plain
+// m-major) when even one n-block's panel does not fit or all of W fits.
+int n_group(int tiles_n, int K) {
+  const int64_t panel = 256LL * K * 2;
+  if (tiles_n * panel <= (1 << 21)) return 0;
+  for (int ng = tiles_n - 1; ng >= 2; --ng)
+    if (tiles_n % ng == 0 && ng * panel <= 1677722) return ng;
+  return 0;
+}
+
 template <int EPI>
 hipError_t launch(const GemmArgs& a, hipStream_t s) {
   const bool big = a.N % 256 == 0 && a.M >= 1024;
   // variant 0 (default) = 3: ping-pong, one 32-MFMA cluster per stage (fastest
   // on every tower shape measured, scripts/gemm_micro.py); 1 = persistent ring
-  const int v = a.variant == 0 ? 3 : a.variant;
+  int v = a.variant == 0 ? 3 : a.variant;
+  GemmArgs ga = a;
+  if (v == 6) {  // ping-pong with the grouped (L2-resident W panel) tile order
+    v = 3;
+    ga.ngroup = n_group(a.N / 256, a.K);
+  }
   if (big && v >= 2 && v <= 5 && a.K / BK >= LEAD) {
+    const GemmArgs& a = ga;
     const int nt = ((a.M + 255) / 256) * (a.N / 256);
     if (v == 2) hipLaunchKernelGGL((gemm_pp_kernel<EPI, 2, false>), dim3(nt), dim3(512), 0, s, a);
     else if (v == 3) hipLaunchKernelGGL((gemm_pp_kernel<EPI, 1, false>), dim3(nt), dim3(512), 0, s, a);

@@ -22,6 +22,7 @@ struct GemmArgs {
   // output row remap: r -> (r / group) * gstride + goffset + r % group (group == 0: identity)
   int group, gstride, goffset;
   int variant;  // main-loop schedule (0 = default choice; see gemm.hip)
+  int ngroup;   // tile order: n-blocks per group (0 = m-major raster; gemm.hip tile_coords)
 };
 
 // Requirements: K % 64 == 0, N % 128 == 0, A/W 16-byte aligned rows.

@@ -1,7 +1,7 @@
 # GPU-box check: parity tests, smoke, short bench.  Each GPU step has its own
 # time limit; a crash/timeout (not a plain test failure) stops the script.
 mkdir -p gpurun_out
-timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
 rc=$?
 echo "pytest rc=$rc"
 tail -5 gpurun_out/pytest_gpu.log

@@ -120,10 +120,14 @@ def rk_golden():
 
 
 if __name__ == "__main__":
+    if "--only" in sys.argv:  # one encoder golden, e.g. --only ViT-L/14@336px
+        encoder_golden(sys.argv[sys.argv.index("--only") + 1], 2, 2)
+        sys.exit(0)
     encoder_golden("test-tiny", 3, 4)
     encoder_golden("test-small", 3, 4)
     encoder_golden("ViT-B/32", 4, 4)
     if "--large" in sys.argv:
         encoder_golden("ViT-L/14", 2, 2)
+        encoder_golden("ViT-L/14@336px", 2, 2)
     rank_golden()
     rk_golden()

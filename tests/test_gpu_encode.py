@@ -61,6 +61,23 @@ def test_encode_b32_golden(gpu):
     _check(txt, g["text"], "B/32 text")
 
 
+@pytest.mark.parametrize("name,fname", [("ViT-L/14", "vit_l14.npz"), ("ViT-L/14@336px", "vit_l14_336px.npz")])
+def test_encode_l14_golden(gpu, name, fname):
+    """ViT-L/14 (257 tokens, BASELINE configs[2]) and ViT-L/14@336px (577
+    tokens, configs[4]; the flash attention kernel) against the HF-pinned
+    fixtures."""
+    import torch
+    from miclip import config, weights
+    cfg = config.get_config(name)
+    g = golden(fname)
+    m = _model(name, gpu, image_chunk=2, text_chunk=2)
+    px = weights.synthetic_pixels(int(g["n_images"]), cfg.image_resolution)
+    img = m.encode_image(torch.from_numpy(px)).cpu().numpy()
+    txt = m.encode_text(torch.from_numpy(g["tokens"])).cpu().numpy()
+    _check(img, g["image"], f"{name} image")
+    _check(txt, g["text"], f"{name} text")
+
+
 def test_encode_chunking_and_dtypes(gpu):
     """Batches larger than the internal chunk, bf16 input, fp16/bf16 output,
     in-kernel L2 normalisation: all consistent with the fp32 single-chunk run."""

@@ -76,7 +76,11 @@ def test_layernorm(gpu, rows, W):
 
 
 @pytest.mark.parametrize("B,S,W,causal", [(1, 50, 768, 0), (7, 50, 768, 0), (3, 77, 512, 1), (2, 17, 128, 0),
-                                          (2, 10, 256, 1), (1, 257, 1024, 0), (4, 197, 768, 0)])
+                                          (2, 10, 256, 1), (1, 257, 1024, 0), (4, 197, 768, 0),
+                                          # long-sequence (flash) kernel: L/14@336 = 577 tokens, ragged tails,
+                                          # causal, chunk boundaries
+                                          (2, 577, 1024, 0), (1, 300, 256, 1), (3, 130, 128, 0), (1, 640, 128, 1),
+                                          (2, 97, 256, 0), (1, 128, 192, 1), (2, 385, 128, 0)])
 def test_attention(gpu, B, S, W, causal):
     import torch
     N_ = _lib()
