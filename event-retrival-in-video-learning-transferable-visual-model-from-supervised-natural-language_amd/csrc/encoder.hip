@@ -404,63 +404,65 @@ __global__ __launch_bounds__(64) void attention_kernel(const uint16_t* __restric
 // One 512-thread workgroup (8 waves) per (sequence, head) for S > 96
 // (B/16: 197, L/14: 257, L/14@336: 577 tokens).  V^T of the whole padded
 // sequence (SP keys, multiple of 64) is staged once in LDS and shared by the 8
-// waves; wave w takes query tiles w, w+8, ... and streams the keys in chunks
-// of 64 with an online (flash) softmax:
-//   S_c = Q K_c^T      A = Q rows, B = K rows (16-byte loads straight from the
-//                      packed qkv rows; the next chunk's K is loaded before the
-//                      current chunk's softmax so its latency hides);
-//   m' = max(m, rowmax S_c); alpha = e^(m - m'); P = e^(S_c - m');
-//   l = alpha l + rowsum P;  O = alpha O + P V_c
-//   O = P V            A = P (bf16, per-wave LDS tile), B = V^T rows from LDS,
-//                      so O's C layout (query rows 4*(lane>>4)+j) matches the
-//                      row statistics of S — the rescale is per register.
-// The 16x64 output tile is transposed through the P tile into row-contiguous
-// 16-byte stores.  Keys >= S are masked to -inf (and their V^T columns are 0).
-template <int SP>
-__global__ __launch_bounds__(512) void attention_long_kernel(const uint16_t* __restrict__ qkv,
+// waves (SP multiple of 32 and <= 608 keeps two workgroups per CU for
+// L/14@336); wave w takes query tiles w, w+8, ... and streams the keys in chunks
+// of 64 with an online (flash) softmax.  Everything is computed TRANSPOSED so
+// that a lane owns one query row end to end:
+//   S^T = K Q^T   A = K rows, B = Q rows (16-byte loads straight from the
+//                 packed qkv rows; the next chunk's K is loaded before the
+//                 current chunk's softmax so its latency hides).  C layout:
+//                 lane -> query fr = lane&15, keys kt*16 + 4*(lane>>4) + j.
+//   row max / sum: 16 registers in-lane + two cross-group shuffles;
+//   m' = max(m, rowmax); alpha = 2^(m - m'); P = 2^(S^T - m')  (log2e/8 folded
+//   into the scores); l = alpha l + rowsum P;
+//   O^T = alpha O^T + V^T P^T   B = P^T straight from the S^T registers (the
+//                 MFMA k order is a permutation: lane group g holds keys
+//                 {32s + 4g + j, 32s + 16 + 4g + j}), A = V^T rows from LDS read
+//                 with the same key permutation (two 8-byte reads).
+// O^T's C layout gives each lane 4 consecutive head dims of its query row per
+// 16-dim tile: 8-byte row stores.  Keys >= S are masked to -inf (and their V^T
+// columns are 0, so 0 * pad never makes a NaN).
+template <int SP, int NW>
+__global__ __launch_bounds__(64 * NW) void attention_long_kernel(const uint16_t* __restrict__ qkv,
                                                              uint16_t* __restrict__ out, int S, int W, int H,
                                                              int causal) {
-  constexpr int TS = SP + 8;  // V^T row (odd number of 16-byte slots)
-  constexpr int PS = 72;      // P row: 64 keys + pad (9 slots)
-  __shared__ __attribute__((aligned(16))) uint16_t lds[64 * TS + 8 * 16 * PS];
-  uint16_t* Vt = lds;
+  static_assert(SP % 32 == 0, "key padding");
+  constexpr int TS = SP + 4;  // V^T row: +8 bytes staggers the banks of consecutive head dims
+  __shared__ __attribute__((aligned(16))) uint16_t Vt[64 * TS];
   const int item = blockIdx.x;
   const int bseq = item / H, h = item % H;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  uint16_t* Pw = lds + 64 * TS + wave * 16 * PS;
   const int64_t ld = 3 * (int64_t)W;
   const uint16_t* qb = qkv + (int64_t)bseq * S * ld + h * 64;
   const uint16_t* kb = qb + W;
   const uint16_t* vb = qb + 2 * W;
 
-  for (int r0 = 0; r0 < SP; r0 += 64) {
-    const int r = r0 + lane, ch = wave;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (r < S) v = *(const uint4*)(vb + (int64_t)r * ld + ch * 8);
-    const uint16_t* vv = (const uint16_t*)&v;
+  for (int i = wave; i < 8 * ((SP + 63) / 64); i += NW) {
+    const int r = (i >> 3) * 64 + lane, ch = i & 7;
+    if (r < SP) {
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (r < S) v = *(const uint4*)(vb + (int64_t)r * ld + ch * 8);
+      const uint16_t* vv = (const uint16_t*)&v;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) Vt[(ch * 8 + e) * TS + r] = vv[e];
+      for (int e = 0; e < 8; ++e) Vt[(ch * 8 + e) * TS + r] = vv[e];
+    }
   }
   __syncthreads();
 
-  const float scale = 0.125f;
-  const int fr = lane & 15, fk = 8 * (lane >> 4), qg = lane >> 4;
+  const float sl2 = 0.125f * 1.4426950408889634f;  // head_dim^-0.5 * log2(e)
+  const int fr = lane & 15, g = lane >> 4, fk = 8 * g;
   const int nqt = (S + 15) / 16;
-  for (int qt = wave; qt < nqt; qt += 8) {
-    const int64_t qrow = min(qt * 16 + fr, S - 1);
-    bf16x8 qa[2];
+  for (int qt = wave; qt < nqt; qt += NW) {
+    const int qrow = qt * 16 + fr;  // this lane's query row
+    bf16x8 qf[2];
 #pragma unroll
-    for (int s = 0; s < 2; ++s) qa[s] = *(const bf16x8*)(qb + qrow * ld + 32 * s + fk);
+    for (int s = 0; s < 2; ++s) qf[s] = *(const bf16x8*)(qb + (int64_t)min(qrow, S - 1) * ld + 32 * s + fk);
     const int last_key = causal ? min(qt * 16 + 15, S - 1) : S - 1;
     const int nch = last_key / 64 + 1;
-    float m[4], l[4];
+    float m = -INFINITY, l = 0.f;
     f32x4 o[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      m[j] = -INFINITY;
-      l[j] = 0.f;
-      o[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
+    for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
     bf16x8 kf[4][2];
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) {
@@ -474,10 +476,10 @@ __global__ __launch_bounds__(512) void attention_long_kernel(const uint16_t* __r
       for (int kt = 0; kt < 4; ++kt) {
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int s = 0; s < 2; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa[s], kf[kt][s], acc, 0, 0, 0);
+        for (int s = 0; s < 2; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kt][s], qf[s], acc, 0, 0, 0);
         sc[kt] = acc;
       }
-      if (c + 1 < nch) {  // prefetch the next chunk's K fragments
+      if (SP > 64 && c + 1 < nch) {  // prefetch the next chunk's K fragments
 #pragma unroll
         for (int kt = 0; kt < 4; ++kt) {
           const int64_t krow = min((c + 1) * 64 + kt * 16 + fr, S - 1);
@@ -485,74 +487,69 @@ __global__ __launch_bounds__(512) void attention_long_kernel(const uint16_t* __r
           for (int s = 0; s < 2; ++s) kf[kt][s] = *(const bf16x8*)(kb + krow * ld + 32 * s + fk);
         }
       }
-      // sc[kt][j]: query row qt*16 + 4*qg + j, key c*64 + kt*16 + fr
+      // sc[kt][j]: query qrow, key c*64 + kt*16 + 4g + j
+      float cm = -INFINITY;
+      const bool edge = (c + 1) * 64 > S || (causal && (c + 1) * 64 > qt * 16);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int row = qt * 16 + 4 * qg + j;
-        float cm = -INFINITY;
+      for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-        for (int kt = 0; kt < 4; ++kt) {
-          const int key = c * 64 + kt * 16 + fr;
-          float v = sc[kt][j] * scale;
-          if (key >= S || (causal && key > row)) v = -INFINITY;
+        for (int j = 0; j < 4; ++j) {
+          float v = sc[kt][j] * sl2;
+          if (edge) {
+            const int key = c * 64 + kt * 16 + 4 * g + j;
+            if (key >= S || (causal && key > qrow)) v = -INFINITY;
+          }
           sc[kt][j] = v;
           cm = fmaxf(cm, v);
         }
+      cm = fmaxf(cm, __shfl_xor(cm, 16, 64));
+      cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
+      // finite: chunk 0 holds key 0 <= every row
+      const float mn = fmaxf(m, cm);
+      const float alpha = exp2f(m - mn);
+      m = mn;
+      float sum = 0.f;
 #pragma unroll
-        for (int off = 1; off < 16; off <<= 1) cm = fmaxf(cm, __shfl_xor(cm, off, 64));
-        const float mn = fmaxf(m[j], cm);
-        // mn is finite: chunk 0 always holds key 0 <= row (rows past S are clamped copies)
-        const float alpha = __expf(m[j] - mn);
-        m[j] = mn;
-        float sum = 0.f;
+      for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-        for (int kt = 0; kt < 4; ++kt) {
-          const float p = __expf(sc[kt][j] - mn);
+        for (int j = 0; j < 4; ++j) {
+          const float p = exp2f(sc[kt][j] - mn);
+          sc[kt][j] = p;
           sum += p;
-          Pw[(4 * qg + j) * PS + kt * 16 + fr] = f2bf_hw(p);
         }
+      l = l * alpha + sum;  // partial (this lane group's keys); reduced once at the end
 #pragma unroll
-        for (int off = 1; off < 16; off <<= 1) sum += __shfl_xor(sum, off, 64);
-        l[j] = l[j] * alpha + sum;
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) o[dt][j] *= alpha;
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_wave_barrier();
+      for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const bf16x8 pa = *(const bf16x8*)(Pw + fr * PS + 32 * s + fk);
+        if (s == 1 && c * 64 + 32 >= S) break;  // keys past round32(S) <= SP: P = 0, no V^T columns
+        bf16x8 pb;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          pb[j] = (__bf16)sc[2 * s][j];
+          pb[4 + j] = (__bf16)sc[2 * s + 1][j];
+        }
+        const uint16_t* vrow = Vt + fr * TS + c * 64 + 32 * s + 4 * g;
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) {
-          const bf16x8 vf = *(const bf16x8*)(Vt + (dt * 16 + fr) * TS + c * 64 + 32 * s + fk);
-          o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, vf, o[dt], 0, 0, 0);
+          const uint2 lo = *(const uint2*)(vrow + dt * 16 * TS);
+          const uint2 hi = *(const uint2*)(vrow + dt * 16 * TS + 16);
+          const uint4 va4 = make_uint4(lo.x, lo.y, hi.x, hi.y);
+          o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, va4), pb, o[dt], 0, 0, 0);
         }
       }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_wave_barrier();
     }
-    // o[dt][j]: query row 4*qg + j, head dim dt*16 + fr -> P tile -> rows
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    const float inv = 1.0f / l;
+    // o[dt][j]: query qrow, head dim dt*16 + 4g + j
+    if (qrow < S) {
+      uint16_t* dst = out + ((int64_t)bseq * S + qrow) * W + h * 64 + 4 * g;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float inv = 1.0f / l[j];
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) Pw[(4 * qg + j) * PS + dt * 16 + fr] = f2bf_hw(o[dt][j] * inv);
+      for (int dt = 0; dt < 4; ++dt)
+        *(uint2*)(dst + dt * 16) = make_uint2(pack_bf16x2(o[dt][0] * inv, o[dt][1] * inv),
+                                              pack_bf16x2(o[dt][2] * inv, o[dt][3] * inv));
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-    {
-      const int r = lane >> 2, c16 = (lane & 3) * 16;  // row r, head dims c16..c16+15
-      const uint4 a0 = *(const uint4*)(Pw + r * PS + c16);
-      const uint4 a1 = *(const uint4*)(Pw + r * PS + c16 + 8);
-      const int row = qt * 16 + r;
-      if (row < S) {
-        uint16_t* dst = out + ((int64_t)bseq * S + row) * W + h * 64 + c16;
-        *(uint4*)dst = a0;
-        *(uint4*)(dst + 8) = a1;
-      }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
   }
 }
 
@@ -645,16 +642,29 @@ hipError_t attention(const uint16_t* qkv, uint16_t* out, int B, int S, int W, in
   const int H = W / 64;
   const int items = B * H;
   if (items <= 0) return hipSuccess;
-  const dim3 grid(items), block(64);
-  const dim3 lblock(512);
-  if (S <= 32) hipLaunchKernelGGL(attention_kernel<32>, grid, block, 0, s, qkv, out, S, W, H, causal, items);
-  else if (S <= 64) hipLaunchKernelGGL(attention_kernel<64>, grid, block, 0, s, qkv, out, S, W, H, causal, items);
-  else if (S <= 96) hipLaunchKernelGGL(attention_kernel<96>, grid, block, 0, s, qkv, out, S, W, H, causal, items);
-  else if (S <= 128) hipLaunchKernelGGL(attention_long_kernel<128>, grid, lblock, 0, s, qkv, out, S, W, H, causal);
-  else if (S <= 256) hipLaunchKernelGGL(attention_long_kernel<256>, grid, lblock, 0, s, qkv, out, S, W, H, causal);
-  else if (S <= 384) hipLaunchKernelGGL(attention_long_kernel<384>, grid, lblock, 0, s, qkv, out, S, W, H, causal);
-  else if (S <= 640) hipLaunchKernelGGL(attention_long_kernel<640>, grid, lblock, 0, s, qkv, out, S, W, H, causal);
+  // S <= 96 (B/32 50, text 77): the one-wave LDS-P kernel, measured faster there
+  // (scripts/attn_micro.py: 179 vs 195-203 us at B/32) than the flash kernel
+  // with 1, 2 or 4 waves; causal bit 8 selects the 4-wave flash kernel instead
+  // (A/B measurements, parity tests of both paths).
+  const bool flash_short = (causal >> 8) & 1;
+  causal &= 1;
+  const dim3 grid(items), b64(64), b256(256), b512(512);
+#define LONG_ATTN(SP, NW, blk) hipLaunchKernelGGL((attention_long_kernel<SP, NW>), grid, blk, 0, s, qkv, out, S, W, H, causal)
+  if (!flash_short && S <= 96) {
+    if (S <= 32) hipLaunchKernelGGL(attention_kernel<32>, grid, b64, 0, s, qkv, out, S, W, H, causal, items);
+    else if (S <= 64) hipLaunchKernelGGL(attention_kernel<64>, grid, b64, 0, s, qkv, out, S, W, H, causal, items);
+    else hipLaunchKernelGGL(attention_kernel<96>, grid, b64, 0, s, qkv, out, S, W, H, causal, items);
+  } else if (S <= 32) LONG_ATTN(32, 4, b256);
+  else if (S <= 64) LONG_ATTN(64, 4, b256);
+  else if (S <= 96) LONG_ATTN(96, 4, b256);
+  else if (S <= 128) LONG_ATTN(128, 8, b512);
+  else if (S <= 224) LONG_ATTN(224, 8, b512);
+  else if (S <= 288) LONG_ATTN(288, 8, b512);
+  else if (S <= 384) LONG_ATTN(384, 8, b512);
+  else if (S <= 608) LONG_ATTN(608, 8, b512);
+  else if (S <= 640) LONG_ATTN(640, 8, b512);
   else return hipErrorInvalidValue;
+#undef LONG_ATTN
   return hipGetLastError();
 }
 

@@ -1,0 +1,47 @@
+"""Attention microbenchmark through mi_op_attention (random bf16 qkv, HIP events).
+Shapes: the bench chunk of each tower.  S <= 96 runs the one-wave LDS-P kernel by default and the
+flash kernel with causal bit 8.  usage: python scripts/attn_micro.py [reps]"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "event-retrival-in-video-learning-transferable-visual-model-from-supervised-natural-language_amd"))
+
+import torch  # noqa: E402
+
+from miclip import _native as N  # noqa: E402
+
+SHAPES = [("B/32", 2000, 50, 768, 0), ("text", 256, 77, 512, 1), ("L/14", 385, 257, 1024, 0),
+          ("L/14@336", 173, 577, 1024, 0)]
+
+
+def main():
+    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+    L = N.lib()
+    dev = torch.device("cuda:0")
+    sp = torch.cuda.current_stream().cuda_stream
+    for name, B, S, W, causal in SHAPES:
+        qkv = (torch.randn(B * S, 3 * W, device=dev) * 1.5).bfloat16()
+        outs = {}
+        for mode in ([0, 0x100] if S <= 96 else [0]):
+            out = torch.empty(B * S, W, dtype=torch.bfloat16, device=dev)
+            run = lambda: N.check(L.mi_op_attention(qkv.data_ptr(), out.data_ptr(), B, S, W, causal | mode, sp), "attn")
+            run()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(reps):
+                run()
+            e1.record()
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) * 1e3 / reps
+            outs[mode] = out
+            fl = 4.0 * B * S * S * W * (0.5 if causal else 1.0)
+            by = B * S * 4 * W * 2
+            d = (out.float() - outs[0].float()).abs().max().item()
+            print(f"{name:9s} {'one-wave' if (S <= 96 and not mode) else 'flash'} B={B} S={S} W={W}: {us:8.1f} us "
+                  f"{fl / us / 1e6:6.1f} TFLOP/s {by / us / 1e3:7.1f} GB/s  maxdiff {d:.3g}", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -81,13 +81,14 @@ def test_layernorm(gpu, rows, W):
                                           # causal, chunk boundaries
                                           (2, 577, 1024, 0), (1, 300, 256, 1), (3, 130, 128, 0), (1, 640, 128, 1),
                                           (2, 97, 256, 0), (1, 128, 192, 1), (2, 385, 128, 0)])
-def test_attention(gpu, B, S, W, causal):
+@pytest.mark.parametrize("flash", [0, 0x100])
+def test_attention(gpu, B, S, W, causal, flash):
     import torch
     N_ = _lib()
     g = torch.Generator(device="cpu").manual_seed(B * S + W + causal)
     qkv = (torch.randn(B * S, 3 * W, generator=g) * 1.5).bfloat16().to(gpu)
     out = torch.empty(B * S, W, dtype=torch.bfloat16, device=gpu)
-    N_.check(N_.lib().mi_op_attention(qkv.data_ptr(), out.data_ptr(), B, S, W, causal, _stream()), "attention")
+    N_.check(N_.lib().mi_op_attention(qkv.data_ptr(), out.data_ptr(), B, S, W, causal | flash, _stream()), "attention")
     torch.cuda.synchronize()
     H = W // 64
     x = qkv.double().reshape(B, S, 3, H, 64)
