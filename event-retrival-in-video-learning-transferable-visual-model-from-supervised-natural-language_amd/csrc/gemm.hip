@@ -49,6 +49,7 @@ constexpr int BK = 32;       // k per stage
 constexpr int RING = 4;      // LDS stages
 constexpr int LEAD = 3;      // stages in flight ahead of the one being read
 constexpr int MAX_N = 4096;  // bias staged in LDS
+constexpr int EPI_NONE = 9;  // timing probe (variant 8): main loop only
 
 // QuickGELU x * sigmoid(1.702 x) with the hardware exp/rcp (~1 ulp; output is bf16)
 __device__ __forceinline__ float quick_gelu(float v) {
@@ -252,7 +253,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_kernel(GemmArgs a
 // the end of L_b(g).  WAR: stage g+3 is issued in L sections of stage g, after
 // every read of the buffer it overwrites (stage g-1, last read by group 1 in
 // L_b(g-1), which ends with lgkmcnt(0) + barrier).
-template <int EPI, int CL, bool PRIO>
+template <int EPI, int CL, bool PRIO, bool DIRECT = false>
 __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs a) {
   constexpr int BM = 256, BN = 256, NT = 512;
   constexpr int WTM = 128, WTN = 64;
@@ -371,9 +372,18 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs a) {
     }
   }
   if (grp == 0) barrier();
-  __syncthreads();
+  if (!DIRECT) __syncthreads();
+  if (EPI == EPI_NONE) {  // timing probe: nothing stored, every accumulator kept live
+    float t = 0.f;
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) t += acc[mi][ni][0] + acc[mi][ni][1] + acc[mi][ni][2] + acc[mi][ni][3];
+    if (t == 12345.f && a.M < 0) *(float*)a.out = t;
+    return;
+  }
 
-  // ------------------------------------------------ epilogue (LDS-staged rows)
+  // ------------------------------------------------ epilogue
   const int wr = grp;
   float4 bias[4];
 #pragma unroll
@@ -384,7 +394,40 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs a) {
   auto out_row = [&](int m) -> int64_t {
     return a.group ? (int64_t)(m / a.group) * a.gstride + a.goffset + m % a.group : (int64_t)m;
   };
-  if (EPI == EPI_BF16 || EPI == EPI_GELU_BF16) {
+  if (DIRECT && (EPI == EPI_BF16 || EPI == EPI_GELU_BF16)) {
+    // Direct row stores, no LDS round trip or workgroup barrier.  Fragments
+    // ni and ni+1 of a 16-row block are exchanged across 16-lane rows with
+    // v_permlane16_swap (odd row of the first <-> even row of the second), so
+    // lane (r, g) ends up with 8 consecutive bf16 columns of row r:
+    //   g = 0: ni*16 + 0..7   g = 1: (ni+1)*16 + 0..7
+    //   g = 2: ni*16 + 8..15  g = 3: (ni+1)*16 + 8..15
+    // -> one 16-byte store per lane per fragment pair, 64 contiguous bytes per
+    // row per instruction (cdna_hip_programming.md T21, 16-lane form).
+    const int g = lane >> 4;
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi) {
+      const int m = m0 + wr * WTM + mi * 16 + (lane & 15);
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        uint2 pk[2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int ni = 2 * p + q;
+          float v0 = acc[mi][ni][0] + bias[ni].x, v1 = acc[mi][ni][1] + bias[ni].y;
+          float v2 = acc[mi][ni][2] + bias[ni].z, v3 = acc[mi][ni][3] + bias[ni].w;
+          if (EPI == EPI_GELU_BF16) {
+            v0 = quick_gelu(v0); v1 = quick_gelu(v1); v2 = quick_gelu(v2); v3 = quick_gelu(v3);
+          }
+          pk[q] = make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
+        }
+        const auto sx = __builtin_amdgcn_permlane16_swap(pk[0].x, pk[1].x, false, false);
+        const auto sy = __builtin_amdgcn_permlane16_swap(pk[0].y, pk[1].y, false, false);
+        const int col = n0 + wc * WTN + (2 * p + (g & 1)) * 16 + (g >> 1) * 8;
+        if (m < a.M)
+          *(uint4*)((uint16_t*)a.out + out_row(m) * a.ldo + col) = make_uint4(sx[0], sy[0], sx[1], sy[1]);
+      }
+    }
+  } else if (EPI == EPI_BF16 || EPI == EPI_GELU_BF16) {
     constexpr int RS = BN * 2 + 16;
 #pragma unroll
     for (int mi = 0; mi < 8; ++mi)
@@ -471,9 +514,24 @@ int n_group(int tiles_n, int K) {
 template <int EPI>
 hipError_t launch(const GemmArgs& a, hipStream_t s) {
   const bool big = a.N % 256 == 0 && a.M >= 1024;
-  // variant 0 (default) = 3: ping-pong, one 32-MFMA cluster per stage (fastest
-  // on every tower shape measured, scripts/gemm_micro.py); 1 = persistent ring
-  int v = a.variant == 0 ? 3 : a.variant;
+  // variant 0 (default): ping-pong, one 32-MFMA cluster per stage, direct
+  // permlane-swapped row stores for bf16 outputs (16) / LDS-staged rows for f32
+  // (3) — the fastest on every tower shape measured (scripts/gemm_micro.py);
+  // 1 = persistent ring; 8 = main-loop-only timing probe (no epilogue).
+  const bool bf16_out = EPI == EPI_BF16 || EPI == EPI_GELU_BF16;
+  int v = a.variant == 0 ? (bf16_out ? 16 : 3) : a.variant;
+  if (v == 16 && !bf16_out) v = 3;
+  if (big && v == 16 && a.K / BK >= LEAD) {
+    const int nt = ((a.M + 255) / 256) * (a.N / 256);
+    hipLaunchKernelGGL((gemm_pp_kernel<EPI, 1, false, true>), dim3(nt), dim3(512), 0, s, a);
+    return hipGetLastError();
+  }
+  if (big && v == 8 && a.K / BK >= LEAD) {
+    const int nt = ((a.M + 255) / 256) * (a.N / 256);
+    hipLaunchKernelGGL((gemm_pp_kernel<EPI_NONE, 1, false>), dim3(nt), dim3(512), 0, s, a);
+    return hipGetLastError();
+  }
+  if (v == 16) v = 3;
   GemmArgs ga = a;
   if (v == 6) {  // ping-pong with the grouped (L2-resident W panel) tile order
     v = 3;

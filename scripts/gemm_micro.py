@@ -24,6 +24,11 @@ SHAPES = {
     "long": (16384, 4096, 4096, 0),
     "qkv20k": (20000, 2304, 768, 0),
     "fc20k": (20000, 3072, 768, 1),
+    # K sweep at the fc shape (per-tile fixed cost = intercept)
+    "fcK384": (100000, 3072, 384, 0),
+    "fcK768": (100000, 3072, 768, 0),
+    "fcK1536": (100000, 3072, 1536, 0),
+    "fcK3072": (100000, 3072, 3072, 0),
 }
 
 
