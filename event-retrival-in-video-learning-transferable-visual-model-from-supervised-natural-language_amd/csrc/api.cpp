@@ -524,4 +524,35 @@ int mi_op_attention(const void* qkv, void* out, int32_t B, int32_t S, int32_t W,
   return MI_OK;
 }
 
+int mi_resample_coeffs(int32_t in_size, double in0, double in1, int32_t out_size, int filter, int32_t* kk,
+                       int64_t kk_cap, int32_t* bounds) {
+  if (!kk || !bounds || in_size < 1 || out_size < 1 || (filter != MI_RESAMPLE_BICUBIC && filter != MI_RESAMPLE_BILINEAR))
+    return fail(MI_ERR_ARG, "mi_resample_coeffs: bad arguments");
+  std::vector<int32_t> k, b;
+  const int ks = resample_coeffs(in_size, in0, in1, out_size, filter, k, b);
+  if (ks < 0) return fail(MI_ERR_ARG, "mi_resample_coeffs: bad arguments");
+  if ((int64_t)k.size() > kk_cap) return fail(MI_ERR_ARG, "mi_resample_coeffs: kk needs %zu entries", k.size());
+  memcpy(kk, k.data(), k.size() * 4);
+  memcpy(bounds, b.data(), b.size() * 4);
+  return ks;
+}
+
+size_t mi_preprocess_workspace_bytes(int64_t B, int32_t H, int32_t W, int32_t n, int mode) {
+  return preprocess_workspace_bytes(B, H, W, n, mode);
+}
+
+int mi_preprocess_frames(const uint8_t* frames, int64_t B, int32_t H, int32_t W, int32_t n, int mode, void* out,
+                         int out_dtype, void* workspace, size_t workspace_bytes, void* stream) {
+  if (B < 0 || H < 1 || W < 1 || n < 1 || n > 4096) return fail(MI_ERR_ARG, "mi_preprocess_frames: bad sizes");
+  if (mode != MI_PREP_CLIP && mode != MI_PREP_SQUASH) return fail(MI_ERR_ARG, "mi_preprocess_frames: bad mode");
+  if (out_dtype != MI_F32 && out_dtype != MI_BF16) return fail(MI_ERR_ARG, "mi_preprocess_frames: out_dtype f32/bf16");
+  if (B == 0) return MI_OK;
+  if (!frames || !out) return fail(MI_ERR_ARG, "mi_preprocess_frames: null pointer");
+  const size_t need = preprocess_workspace_bytes(B, H, W, n, mode);
+  if (!workspace || workspace_bytes < need)
+    return fail(MI_ERR_ARG, "mi_preprocess_frames: workspace too small (%zu < %zu)", workspace_bytes, need);
+  HIP_TRY(preprocess_frames(frames, B, H, W, n, mode, out, out_dtype == MI_BF16, workspace, (hipStream_t)stream));
+  return MI_OK;
+}
+
 }  // extern "C"

@@ -67,3 +67,16 @@ hipError_t score_matrix(const void* corpus, int64_t N, int64_t D, int dt, const 
 hipError_t rank_of_targets(const float* S, int64_t Q, int64_t N, const int64_t* pq, const int64_t* pt, int64_t T,
                            int64_t* out, hipStream_t s);
 }  // namespace miclip
+
+#include <vector>
+namespace miclip {
+// Pillow ImagingResample coefficients (csrc/preprocess.hip): filter 0 bicubic,
+// 1 bilinear; returns ksize (< 0 on error), kk [out_size][ksize] int32 (22
+// fractional bits), bounds [out_size][2] = (first tap, tap count).
+int resample_coeffs(int in_size, double in0, double in1, int out_size, int filter, std::vector<int32_t>& kk,
+                    std::vector<int32_t>& bounds);
+size_t preprocess_workspace_bytes(int64_t B, int H, int W, int n, int mode);
+// frames uint8 [B,H,W,3] -> out [B,3,n,n] f32 / bf16; mode 0 CLIP _transform, 1 squash (bilinear)
+hipError_t preprocess_frames(const uint8_t* frames, int64_t B, int H, int W, int n, int mode, void* out,
+                             int out_bf16, void* ws, hipStream_t s);
+}  // namespace miclip

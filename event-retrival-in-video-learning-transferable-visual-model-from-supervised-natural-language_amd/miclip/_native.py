@@ -19,6 +19,8 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 MI_F32, MI_BF16, MI_F16 = 0, 1, 2
 MI_NAN_FIRST, MI_NAN_LAST = 0, 1
 MI_NORM_L2, MI_NORM_L2_GUARD, MI_NORM_NONE = 0, 1, 2
+MI_PREP_CLIP, MI_PREP_SQUASH = 0, 1
+MI_RESAMPLE_BICUBIC, MI_RESAMPLE_BILINEAR = 0, 1
 
 # every symbol include/miclip.h declares (checked by tests/test_abi.py)
 EXPORTS = (
@@ -26,6 +28,7 @@ EXPORTS = (
     "mi_clip_reserve", "mi_clip_encode_image", "mi_clip_encode_text", "mi_rank_workspace_bytes",
     "mi_rank_topk", "mi_rank_merge", "mi_score_matrix", "mi_rank_of_targets",
     "mi_op_gemm", "mi_op_layernorm", "mi_op_attention",
+    "mi_resample_coeffs", "mi_preprocess_workspace_bytes", "mi_preprocess_frames",
 )
 
 
@@ -83,6 +86,9 @@ def lib():
         "mi_op_gemm": (ctypes.c_int, [P, P, P, P, I32, I32, I32, I32, P]),
         "mi_op_layernorm": (ctypes.c_int, [P, P, P, P, I32, I32, P]),
         "mi_op_attention": (ctypes.c_int, [P, P, I32, I32, I32, I32, P]),
+        "mi_resample_coeffs": (ctypes.c_int, [I32, ctypes.c_double, ctypes.c_double, I32, ctypes.c_int, P, I64, P]),
+        "mi_preprocess_workspace_bytes": (SZ, [I64, I32, I32, I32, ctypes.c_int]),
+        "mi_preprocess_frames": (ctypes.c_int, [P, I64, I32, I32, I32, ctypes.c_int, P, ctypes.c_int, P, SZ, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

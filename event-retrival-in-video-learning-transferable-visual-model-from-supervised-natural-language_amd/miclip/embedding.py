@@ -16,6 +16,7 @@ from pathlib import Path
 import numpy as np
 
 from . import api
+from .preprocess import Transform, load_frames
 
 
 def extract_and_save_embeddings_from_folder(folder_path, model_name, video_name=None, output_dir="embedding",
@@ -36,7 +37,11 @@ def extract_and_save_embeddings_from_folder(folder_path, model_name, video_name=
                 paths.append(os.path.join(root, file))
     rows = []
     for i in range(0, len(paths), batch_size):
-        batch = torch.stack([preprocess(Image.open(p).convert("RGB")) for p in paths[i:i + batch_size]])
+        chunk = paths[i:i + batch_size]
+        if isinstance(preprocess, Transform):  # this package's transform: GPU resize/crop/normalise
+            batch, _ = load_frames(chunk, preprocess.n_px, device=model.device, squash=preprocess.squash)
+        else:
+            batch = torch.stack([preprocess(Image.open(p).convert("RGB")) for p in chunk])
         rows.append(model.encode_image(batch, out_dtype=torch.float32).cpu().numpy())
     all_embeddings = np.vstack(rows) if rows else np.zeros((0, model.visual.output_dim), np.float32)
     np.save(output_file, all_embeddings)

@@ -5,12 +5,18 @@
               RGB -> ToTensor -> Normalize(CLIP mean/std)
               (used at Backend/embedding.py:46, embedding_service.py:406,475)
   squash:     Resize((n_px, n_px)) -> ToTensor -> Normalize
-              (compare_models.py:387-391)
+              (compare_models.py:387-391; torchvision's default interpolation
+              there is BILINEAR)
 
-torchvision is not installed here, so both are restated on PIL + numpy with
-torchvision's size arithmetic (short side scaled, long side truncated;
-crop offsets rounded).  Host-side like the reference; a GPU decode/resize
-kernel is SURVEY.md §8(f) item 1 ("next").
+``Transform`` is the reference's host path, restated on PIL + numpy with
+torchvision's size arithmetic (short side scaled, long side truncated; crop
+offsets rounded half to even) since torchvision is not installed here.
+
+``preprocess_frames`` is the same transform on the GPU for a batch of decoded
+frames: ``mi_preprocess_frames`` resamples with
+Pillow's exact integer algorithm, so its output equals ``Transform``'s bit for
+bit (tests/test_preprocess.py).  JPEG decoding stays on the host (PIL; there
+is no GPU JPEG decoder in this image).
 """
 from __future__ import annotations
 
@@ -36,7 +42,7 @@ class Transform:
         from PIL import Image
         n = self.n_px
         if self.squash:
-            img = img.resize((n, n), Image.BICUBIC)
+            img = img.resize((n, n), Image.BILINEAR)
             return _to_tensor(img)
         w, h = img.size
         if w <= h:
@@ -50,5 +56,70 @@ class Transform:
         img = img.crop((left, top, left + n, top + n))
         return _to_tensor(img)
 
+    def batch(self, images, device="cuda", out_dtype=None):
+        """GPU path for a list of PIL images of ONE size: host decode/convert,
+        one upload of the uint8 frames, ``preprocess_frames`` on the device."""
+        import torch
+        frames = np.stack([np.asarray(im.convert("RGB"), dtype=np.uint8) for im in images])
+        t = torch.from_numpy(frames).to(device)
+        return preprocess_frames(t, self.n_px, squash=self.squash, out_dtype=out_dtype or torch.float32)
+
     def __repr__(self):
         return f"Transform(n_px={self.n_px}, squash={self.squash})"
+
+
+def preprocess_frames(frames, n_px: int = 224, squash: bool = False, out_dtype=None):
+    """frames: uint8 CUDA tensor [B, H, W, 3] (RGB) -> [B, 3, n_px, n_px]
+    (float32 or bfloat16) through ``mi_preprocess_frames``; no CPU fallback."""
+    import torch
+    from . import _native as N
+    if out_dtype is None:
+        out_dtype = torch.float32
+    if frames.dtype != torch.uint8 or frames.dim() != 4 or frames.shape[-1] != 3:
+        raise N.MiClipError("preprocess_frames expects a uint8 tensor [B, H, W, 3]")
+    if frames.device.type != "cuda":
+        raise N.MiClipError("preprocess_frames runs on the GPU; host preprocessing is Transform")
+    frames = frames.contiguous()
+    B, H, W, _ = frames.shape
+    mode = N.MI_PREP_SQUASH if squash else N.MI_PREP_CLIP
+    L = N.lib()
+    out = torch.empty(B, 3, n_px, n_px, dtype=out_dtype, device=frames.device)
+    nb = L.mi_preprocess_workspace_bytes(B, H, W, n_px, mode)
+    ws = torch.empty(max(nb, 1), dtype=torch.uint8, device=frames.device)
+    with torch.cuda.device(frames.device):
+        N.check(L.mi_preprocess_frames(frames.data_ptr(), B, H, W, n_px, mode, out.data_ptr(),
+                                       N.dtype_code(out_dtype), ws.data_ptr(), nb, N.stream_ptr(frames.device)),
+                "mi_preprocess_frames")
+    return out
+
+
+def load_frames(paths, n_px: int = 224, device="cuda", squash: bool = False, out_dtype=None, threads: int = 8):
+    """Decode frame files on host threads (PIL; decoding releases the GIL),
+    upload each same-size group once as uint8, preprocess it on the GPU.
+    Returns ([len(paths), 3, n_px, n_px] tensor in path order, list of failed
+    indices).  A frame that cannot be read is left as zeros, as the
+    reference's ingest does (Backend/services/embedding_service.py:476-480)."""
+    import torch
+    from concurrent.futures import ThreadPoolExecutor
+    from PIL import Image
+
+    def load(p):
+        try:
+            with Image.open(p) as im:
+                return np.asarray(im.convert("RGB"), dtype=np.uint8)
+        except Exception as e:  # reference: print and substitute a zero frame
+            print(f"Error preprocessing image {p}: {e}")
+            return None
+
+    with ThreadPoolExecutor(max(1, threads)) as ex:
+        arrs = list(ex.map(load, paths))
+    out = torch.zeros(len(paths), 3, n_px, n_px, dtype=out_dtype or torch.float32, device=device)
+    groups = {}
+    for i, a in enumerate(arrs):
+        if a is not None:
+            groups.setdefault(a.shape, []).append(i)
+    for idx in groups.values():
+        frames = torch.from_numpy(np.stack([arrs[i] for i in idx])).to(device)
+        out[torch.tensor(idx, device=out.device)] = preprocess_frames(frames, n_px, squash=squash,
+                                                                       out_dtype=out.dtype)
+    return out, [i for i, a in enumerate(arrs) if a is None]

@@ -26,6 +26,7 @@ import os
 import numpy as np
 
 from . import api
+from .preprocess import load_frames
 from .retrieval import MAX_K, rank_topk, score_matrix
 from .weights import load_state_dict
 
@@ -243,7 +244,6 @@ class EmbeddingService:
     def extract_and_save_embeddings_from_folder(self, folder_path, model_name=None, video_name=None,
                                                 batch_size=256):
         import torch
-        from PIL import Image
 
         current = self.active_model
         if model_name:
@@ -259,17 +259,10 @@ class EmbeddingService:
         model = self._clip()
         R = model.cfg.image_resolution
         out = []
-        last = None
         for i in range(0, len(frame_files), batch_size):
-            imgs = []
-            for f in frame_files[i:i + batch_size]:
-                try:
-                    last = self.preprocess(Image.open(os.path.join(folder_path, f)).convert("RGB"))
-                    imgs.append(last)
-                except Exception as e:
-                    print(f"Error preprocessing image {f}: {e}")
-                    imgs.append(torch.zeros(3, R, R))
-            batch = torch.stack(imgs)
+            # host decode + GPU resize/crop/normalise (Pillow-exact, miclip.preprocess.load_frames)
+            batch, _ = load_frames([os.path.join(folder_path, f) for f in frame_files[i:i + batch_size]], R,
+                                   device=model.device)
             out.append(model.encode_image(batch, normalize=True, out_dtype=torch.float32).cpu().numpy())
         embeddings = np.vstack(out)
         np.save(embeddings_path, embeddings)

@@ -47,6 +47,13 @@ enum mi_norm_mode {
   MI_NORM_NONE = 2      /* raw dot products (features already normalised, compare_models:999) */
 };
 
+/* image preprocessing (mi_preprocess_frames) */
+enum mi_prep_mode {
+  MI_PREP_CLIP = 0,   /* openai/CLIP _transform: Resize(n, bicubic) short side + CenterCrop(n) + ToTensor + Normalize */
+  MI_PREP_SQUASH = 1  /* compare_models.py:387-391: Resize((n, n)) (bilinear) + ToTensor + Normalize            */
+};
+enum mi_resample_filter { MI_RESAMPLE_BICUBIC = 0, MI_RESAMPLE_BILINEAR = 1 };
+
 /* Architecture of a ViT CLIP (openai/CLIP build_model inference; miclip/config.py). */
 typedef struct mi_clip_arch {
   int32_t embed_dim;         /* D: 512 (B/32), 768 (L/14)      */
@@ -134,6 +141,30 @@ int mi_score_matrix(const void* corpus, int64_t N, int64_t D, int corpus_dtype,
  * q = pair_query[t], g = pair_target[t]; NaN sorts last (argsort(-s)). */
 int mi_rank_of_targets(const float* scores, int64_t Q, int64_t N, const int64_t* pair_query,
                        const int64_t* pair_target, int64_t T, int64_t* out_rank, void* stream);
+
+/* Pillow ImagingResample coefficients (host only, no GPU): the resize of
+ * in_size -> out_size over the source box [in0, in1) with `filter`, exactly as
+ * Pillow computes them (libImaging/Resample.c precompute_coeffs +
+ * normalize_coeffs_8bpc; restated in oracle/preprocess_ref.py).  Writes
+ * kk [out_size][ksize] int32 (22 fractional bits) and bounds [out_size][2] =
+ * (first tap, tap count); returns ksize (> 0) or a negative MI_ERR_*.
+ * Exposed so the host side of the preprocessing can be checked on a CPU. */
+int mi_resample_coeffs(int32_t in_size, double in0, double in1, int32_t out_size, int filter, int32_t* kk,
+                       int64_t kk_cap, int32_t* bounds);
+
+/* Workspace bytes mi_preprocess_frames needs. */
+size_t mi_preprocess_workspace_bytes(int64_t B, int32_t H, int32_t W, int32_t n, int mode);
+
+/* Replaces the per-frame host preprocessing before encode_image
+ * (openai/CLIP `preprocess(Image.open(p))`: Backend/embedding.py:46,
+ * Backend/services/embedding_service.py:406,475; and the squash transform of
+ * compare_models.py:387-391) for a batch of decoded frames of one size.
+ * frames: device uint8 [B,H,W,3] (RGB, row-major HWC); out: device [B,3,n,n]
+ * in MI_F32 / MI_BF16.  Resampling is Pillow-exact (the uint8 image before
+ * ToTensor is bit-identical to PIL.Image.resize), ToTensor/Normalize are f32
+ * as torchvision computes them. */
+int mi_preprocess_frames(const uint8_t* frames, int64_t B, int32_t H, int32_t W, int32_t n, int mode, void* out,
+                         int out_dtype, void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---- operator-level entry points (per-kernel parity tests) ----
  * mi_op_gemm: out = A[M,K] . W[N,K]^T (+bias) with epilogue

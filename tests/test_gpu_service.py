@@ -1,0 +1,163 @@
+"""EmbeddingService mirror end to end on the GPU:
+folder ingest (host decode + GPU preprocessing + encode_image + L2) -> .npy,
+then search_top_frames / extract_query_confidence / search_top_frames_by_image
+over the HBM-resident corpus, against the oracle restatement of
+Backend/services/embedding_service.py:151-392 on the same rows.
+
+The injected services are minimal in-memory stand-ins with the reference's
+method names (cache_service.py, path_service.py, data_service.py:24-55 —
+frame list = sorted file names).  clip.tokenize needs a BPE vocabulary that is
+not in this image (tokenizer parity unpinned), so the query -> token ids step
+is replaced by the deterministic synthetic tokenizer of miclip.weights."""
+import json
+import os
+import zlib
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+class Cache:
+    def __init__(self):
+        self.d = {}
+
+    def _get(self, *k):
+        return self.d.get(k)
+
+    def _set(self, v, *k):
+        self.d[k] = v
+
+    def get_text_features(self, key, video):
+        return self._get("t", key, video)
+
+    def set_text_features(self, key, video, v):
+        self._set(v, "t", key, video)
+
+    def get_embeddings(self, path):
+        return self._get("e", path)
+
+    def set_embeddings(self, path, v):
+        self._set(v, "e", path)
+
+    def get_frames_list(self, path):
+        return self._get("f", path)
+
+    def set_frames_list(self, path, v):
+        self._set(v, "f", path)
+
+    def get_search_results(self, key, video):
+        return self._get("s", key, video)
+
+    def set_search_results(self, key, video, v):
+        self._set(v, "s", key, video)
+
+
+class Paths:
+    def __init__(self, root):
+        self.root = root
+
+    def get_embeddings_path(self, video):
+        return os.path.join(self.root, "embedding", f"{video}_embeddings.npy")
+
+    def get_metadata_path(self, video):
+        return os.path.join(self.root, "metadata", f"{video}_metadata.json")
+
+
+class Data:
+    def __init__(self, paths, frame_dir):
+        self.paths, self.frame_dir = paths, frame_dir
+
+    def load_frames_from_json(self, video):
+        with open(self.paths.get_metadata_path(video)) as f:
+            return [item["frame"] for item in json.load(f)]
+
+
+def _frames(tmp_path, n=24):
+    from PIL import Image
+    d = tmp_path / "frames"
+    d.mkdir()
+    rng = np.random.default_rng(5)
+    names = []
+    for i in range(n):
+        h, w = (90, 160) if i % 3 else (120, 120)    # two frame sizes -> two upload groups
+        yy, xx = np.mgrid[0:h, 0:w]
+        base = (127 + 100 * np.sin(xx / (3.0 + i) + yy / (5.0 + i)))[..., None] * np.array([1.0, 0.8, 0.5])
+        img = np.clip(base + rng.normal(0, 30, (h, w, 3)), 0, 255).astype(np.uint8)
+        names.append(f"{i:04d}.png")
+        Image.fromarray(img).save(d / names[-1])
+    (d / "broken.png").write_bytes(b"not an image")   # unreadable frame -> zero row (embedding_service.py:476-480)
+    names.append("broken.png")
+    return d, sorted(names)
+
+
+def _tokens(q, cfg):
+    from miclip import weights
+    seed = zlib.crc32(q.encode()) % 1000
+    return weights.synthetic_tokens(1, cfg.context_length, cfg.vocab_size, seed=seed)
+
+
+@pytest.fixture()
+def service(gpu, tmp_path, monkeypatch):
+    import torch
+    from miclip import api, service as S
+    root = tmp_path / "state"
+    (root / "metadata").mkdir(parents=True)
+    frame_dir, names = _frames(tmp_path)
+    with open(root / "metadata" / "vid_metadata.json", "w") as f:
+        json.dump([{"frame": n} for n in names], f)
+    paths = Paths(str(root))
+    svc = S.EmbeddingService(Cache(), paths, Data(paths, frame_dir), device="cuda", model_name="test-small")
+    cfg = svc.original_model.cfg
+    monkeypatch.setattr(api, "tokenize", lambda texts, *a, **k: torch.from_numpy(
+        np.concatenate([_tokens(t, cfg) for t in texts])))
+    return svc, frame_dir, names, paths
+
+
+def test_ingest_rows_match_host_preprocessing(service):
+    import torch
+    from PIL import Image
+    svc, frame_dir, names, paths = service
+    out = svc.extract_and_save_embeddings_from_folder(str(frame_dir), video_name="vid", batch_size=10)
+    rows = np.load(out)
+    assert rows.shape == (len(names), svc.original_model.cfg.embed_dim)
+    tf = svc.preprocess
+    for i, name in enumerate(names):
+        if name == "broken.png":
+            x = torch.zeros(1, 3, tf.n_px, tf.n_px)
+        else:
+            x = tf(Image.open(frame_dir / name).convert("RGB")).unsqueeze(0)
+        ref = svc.original_model.encode_image(x, normalize=True, out_dtype=torch.float32).cpu().numpy()[0]
+        np.testing.assert_allclose(rows[i], ref, rtol=0, atol=2e-6)
+    np.testing.assert_allclose(np.linalg.norm(rows, axis=1), 1.0, atol=1e-5)
+
+
+def test_search_confidence_and_image_query_match_oracle(service):
+    from oracle import rank_ref
+    svc, frame_dir, names, paths = service
+    svc.extract_and_save_embeddings_from_folder(str(frame_dir), video_name="vid")
+    rows = np.load(paths.get_embeddings_path("vid"))
+    for q in ("a red car at night", "people walking"):
+        k = 7
+        got = svc.search_top_frames(q, k, "vid")
+        t = svc.get_text_features(q, "vid")
+        ref_frames, _ = rank_ref.search_top_frames_ref(rows, t, k, names)
+        assert got == ref_frames[:k]
+        assert svc.search_top_frames(q, k, "vid") == got          # cached path
+        conf = svc.extract_query_confidence(got[0], q, "vid")
+        i = names.index(got[0])
+        e = rows / np.linalg.norm(rows, axis=1, keepdims=True)
+        assert abs(conf - float(e[i] @ t[0])) < 1e-5
+    img_q = rows[3]
+    got = svc.search_top_frames_by_image(img_q, 5, "vid")
+    ref_frames, _ = rank_ref.search_top_frames_ref(rows, img_q[None], 5, names)
+    assert got == ref_frames[:5] and got[0] == names[3]
+
+
+def test_error_semantics(service):
+    svc, frame_dir, names, paths = service
+    assert svc.search_top_frames("anything", 5, "missing_video") == []      # embedding_service.py:342-344
+    assert svc.extract_query_confidence("nope.png", "x", "missing_video") == 0.0  # :280-282
+    svc.extract_and_save_embeddings_from_folder(str(frame_dir), video_name="vid")
+    assert svc.extract_query_confidence("not_a_frame.png", "x", "vid") == 0.0
