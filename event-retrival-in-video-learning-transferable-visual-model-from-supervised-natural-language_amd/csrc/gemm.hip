@@ -253,7 +253,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_kernel(GemmArgs a
 // the end of L_b(g).  WAR: stage g+3 is issued in L sections of stage g, after
 // every read of the buffer it overwrites (stage g-1, last read by group 1 in
 // L_b(g-1), which ends with lgkmcnt(0) + barrier).
-template <int EPI, int CL, bool PRIO, bool DIRECT = false>
+template <int EPI, int CL, bool PRIO, bool DIRECT = false, bool NTS = false>
 __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs a) {
   constexpr int BM = 256, BN = 256, NT = 512;
   constexpr int WTM = 128, WTN = 64;
@@ -423,8 +423,13 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs a) {
         const auto sx = __builtin_amdgcn_permlane16_swap(pk[0].x, pk[1].x, false, false);
         const auto sy = __builtin_amdgcn_permlane16_swap(pk[0].y, pk[1].y, false, false);
         const int col = n0 + wc * WTN + (2 * p + (g & 1)) * 16 + (g >> 1) * 8;
-        if (m < a.M)
-          *(uint4*)((uint16_t*)a.out + out_row(m) * a.ldo + col) = make_uint4(sx[0], sy[0], sx[1], sy[1]);
+        if (m < a.M) {
+          typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+          u32x4* dst = (u32x4*)((uint16_t*)a.out + out_row(m) * a.ldo + col);
+          const u32x4 val = {sx[0], sy[0], sx[1], sy[1]};
+          if (NTS) __builtin_nontemporal_store(val, dst);
+          else *dst = val;
+        }
       }
     }
   } else if (EPI == EPI_BF16 || EPI == EPI_GELU_BF16) {
@@ -524,6 +529,11 @@ hipError_t launch(const GemmArgs& a, hipStream_t s) {
   if (big && v == 16 && a.K / BK >= LEAD) {
     const int nt = ((a.M + 255) / 256) * (a.N / 256);
     hipLaunchKernelGGL((gemm_pp_kernel<EPI, 1, false, true>), dim3(nt), dim3(512), 0, s, a);
+    return hipGetLastError();
+  }
+  if (big && v == 17 && bf16_out && a.K / BK >= LEAD) {  // experiment: non-temporal output stores
+    const int nt = ((a.M + 255) / 256) * (a.N / 256);
+    hipLaunchKernelGGL((gemm_pp_kernel<EPI, 1, false, true, true>), dim3(nt), dim3(512), 0, s, a);
     return hipGetLastError();
   }
   if (big && v == 8 && a.K / BK >= LEAD) {
