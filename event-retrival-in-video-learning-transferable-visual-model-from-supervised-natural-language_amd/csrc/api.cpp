@@ -336,7 +336,7 @@ static GemmArgs gargs(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t
                       int64_t ldo, int M, int N, int K) {
   GemmArgs g;
   g.A = A; g.lda = lda; g.W = W; g.ldw = ldw; g.bias = bias; g.out = out; g.ldo = ldo;
-  g.M = M; g.N = N; g.K = K; g.group = 0; g.gstride = 0; g.goffset = 0; g.ngroup = 0;
+  g.M = M; g.N = N; g.K = K; g.group = 0; g.gstride = 0; g.goffset = 0; g.ngroup = 0; g.a_scale = nullptr; g.w_scale = nullptr;
   g.variant = gemm_variant();
   return g;
 }
@@ -521,6 +521,25 @@ int mi_op_attention(const void* qkv, void* out, int32_t B, int32_t S, int32_t W,
   if (!qkv || !out || B < 0 || S < 1) return fail(MI_ERR_ARG, "mi_op_attention: bad arguments");
   if (W % 64 || S > 640 || (causal & ~0x101)) return fail(MI_ERR_UNSUPPORTED, "mi_op_attention: W %% 64 == 0 and S <= 640");
   HIP_TRY(attention((const uint16_t*)qkv, (uint16_t*)out, B, S, W, causal, (hipStream_t)stream));
+  return MI_OK;
+}
+
+int mi_op_gemm_mx(const void* A, const void* a_scale, const void* W, const void* w_scale, const float* bias, void* out,
+                  int32_t M, int32_t N, int32_t K, int32_t epi, void* stream) {
+  if (!A || !W || !a_scale || !w_scale || !out || M < 0) return fail(MI_ERR_ARG, "mi_op_gemm_mx: bad arguments");
+  if (K % 128 || N % 256 || K <= 0) return fail(MI_ERR_UNSUPPORTED, "mi_op_gemm_mx: needs K %% 128 == 0, N %% 256 == 0");
+  if (epi != 0 && epi != 1 && epi != 3) return fail(MI_ERR_ARG, "mi_op_gemm_mx: epilogue 0 (bf16), 1 (GELU) or 3 (f32)");
+  GemmArgs g = gargs((const uint16_t*)A, K, (const uint16_t*)W, K, bias, out, N, M, N, K);
+  g.a_scale = (const uint8_t*)a_scale;
+  g.w_scale = (const uint8_t*)w_scale;
+  HIP_TRY(gemm_mx(g, epi, (hipStream_t)stream));
+  return MI_OK;
+}
+
+int mi_op_quantize_mx(const void* in, void* q, void* scales, int32_t rows, int32_t K, void* stream) {
+  if (!in || !q || !scales || rows < 0) return fail(MI_ERR_ARG, "mi_op_quantize_mx: bad arguments");
+  if (K % 128 || K <= 0) return fail(MI_ERR_UNSUPPORTED, "mi_op_quantize_mx: K %% 128 == 0");
+  HIP_TRY(quantize_mx((const uint16_t*)in, K, (uint8_t*)q, K, (uint8_t*)scales, rows, K, (hipStream_t)stream));
   return MI_OK;
 }
 

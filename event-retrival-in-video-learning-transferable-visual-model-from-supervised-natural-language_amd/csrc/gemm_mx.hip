@@ -1,0 +1,263 @@
+// MX-fp8 GEMM (gfx950 block-scaled MFMA) for the "fp8 MFMA weights" tower
+// configuration (BASELINE.json configs[4]: ViT-L/14@336px).
+//
+//   C[M,N] = (A[M,K] * 2^sa) . (W[N,K] * 2^sw)^T  (+ bias, QuickGELU)
+//
+// A and W are OCP e4m3 with one e8m0 scale per 64 consecutive k of a row;
+// v_mfma_scale_f32_16x16x128_f8f6f4 applies the scales in hardware and runs at
+// twice the bf16 MFMA rate (MI355X_MICROARCH.md "Matrix cores").  Probed on
+// hardware (scripts/probes/):
+//   operands (mx_layout.hip): lane l holds row (l & 15) and k = 32 (l >> 4) ..
+//     +31 of the 128-k step, dword d = k 4d..4d+3; C/D is the common 16x16 map;
+//   scales (mx_scale_map.hip, .out.txt): with opsel 0, byte 0 of lane l < 32
+//     scales row (l & 15) over k = 64 (l >> 4) .. +63 — one e8m0 per 64 k, so
+//     that is this format's block (the OCP MX block is 32);
+//   LDS-DMA of 1- or 2-byte elements lands at a 4-byte lane stride, so scales
+//     are moved as dwords: the scale tensor is stage-major, [K/128][rows_pad][2]
+//     (rows_pad = rows rounded up to even; byte (kb & 1) of row r in stage
+//     kb >> 1 is the e8m0 of k-block kb), one dword = 2 rows of one stage.
+//
+// Tile 256x256, 512 threads = 8 waves (2 M x 4 N), 128x64 per wave; the MFMA
+// computes C^T (A operand = W fragment, B operand = activation fragment) so a
+// lane holds 4 consecutive output columns (same epilogue as gemm.hip).
+// Stage = 128 k = 128 bytes per row: 64 KB of operands + 2 KB of scales,
+// double buffered by LDS-DMA one stage ahead; one barrier per stage.
+// LDS row image: 16-byte chunk c of row r sits in slot c ^ ((r >> 1) & 5), so
+// the two 16-byte reads of every fragment (chunks 2g, 2g+1 for lane group g)
+// hit 16 distinct bank quads per ds_read_b128 lane group (exhaustive search).
+#include "common.hpp"
+#include "internal.hpp"
+
+namespace miclip {
+
+namespace {
+
+constexpr int MX_BK = 128;                              // k (bytes) per stage
+constexpr int MX_STAGE = 512 * MX_BK;                   // 256 A rows + 256 W rows
+constexpr int MX_SC_STAGE = 512 * 2;                    // 2 e8m0 (64-k blocks) per row per stage
+
+typedef int v8i __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ int mx_swz(int r) { return (r >> 1) & 5; }
+
+__device__ __forceinline__ float mx_gelu(float v) { return v * __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * v)); }
+
+__device__ __forceinline__ void glds4(const void* gsrc, void* lds_base) {
+  __builtin_amdgcn_global_load_lds((const GLB_AS void*)gsrc, (LDS_AS void*)lds_base, 4, 0, 0);
+}
+
+template <int EPI>
+__global__ __launch_bounds__(512) void gemm_mx_kernel(GemmArgs a) {
+  constexpr int BM = 256, BN = 256, WTM = 128, WTN = 64;
+  __shared__ __attribute__((aligned(16))) char smem[2 * MX_STAGE + 2 * MX_SC_STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int tiles_n = a.N / BN;
+  const int tiles_m = (a.M + BM - 1) / BM;
+  const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
+  const int nk = a.K / MX_BK;
+  const int m_pad = (a.M + 1) & ~1;
+  const uint8_t* A = (const uint8_t*)a.A;
+  const uint8_t* Wt = (const uint8_t*)a.W;
+
+  // ---- DMA geometry: instruction j (0..3) of wave w moves 8 rows x 128 B:
+  // rows (w*4 + j)*8 + (lane >> 3), LDS slot lane & 7 <- global chunk slot ^ swz
+  const uint8_t* asrc[4];
+  const uint8_t* wsrc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int r = (wave * 4 + j) * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ mx_swz(r);
+    asrc[j] = A + (int64_t)min(m0 + r, a.M - 1) * a.lda + c * 16;
+    wsrc[j] = Wt + (int64_t)(n0 + r) * a.ldw + c * 16;
+  }
+  // scales: waves 0-1 move A row pairs, waves 2-3 W row pairs (one dword = 2 rows)
+  const int spair = (wave & 1) * 64 + lane;
+  const uint8_t* ssrc = wave < 2 ? a.a_scale + (int64_t)min(m0 + 2 * spair, m_pad - 2) * 2
+                                 : a.w_scale + (int64_t)(n0 + 2 * spair) * 2;
+  const int64_t sstage = wave < 2 ? (int64_t)m_pad * 2 : (int64_t)a.N * 2;  // bytes per stage
+  auto issue = [&](int st) {
+    char* base = smem + (st & 1) * MX_STAGE;
+    const int kofs = st * MX_BK;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) glds16(asrc[j] + kofs, base + (wave * 4 + j) * 1024);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) glds16(wsrc[j] + kofs, base + 256 * MX_BK + (wave * 4 + j) * 1024);
+    if (wave < 4) glds4(ssrc + st * sstage, smem + 2 * MX_STAGE + (st & 1) * MX_SC_STAGE + wave * 256);
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // fragment read: row fr of a 16-row block, chunks 2g and 2g+1
+  const int fr = lane & 15, g = lane >> 4;
+  const int rdo0 = fr * MX_BK + (((2 * g) ^ mx_swz(fr)) * 16);
+  const int rdo1 = fr * MX_BK + (((2 * g + 1) ^ mx_swz(fr)) * 16);
+
+  issue(0);
+  for (int st = 0; st < nk; ++st) {
+    // stage st landed (this wave's share), every wave's reads of the other
+    // buffer (stage st-1) are done -> barrier -> prefetch st+1 into it
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (st + 1 < nk) issue(st + 1);
+    const char* As = smem + (st & 1) * MX_STAGE + (wr * WTM) * MX_BK;
+    const char* Ws = smem + (st & 1) * MX_STAGE + 256 * MX_BK + (wc * WTN) * MX_BK;
+    const uint16_t* Ssa = (const uint16_t*)(smem + 2 * MX_STAGE + (st & 1) * MX_SC_STAGE) + wr * WTM;
+    const uint16_t* Ssw = (const uint16_t*)(smem + 2 * MX_STAGE + (st & 1) * MX_SC_STAGE) + 256 + wc * WTN;
+    v8i bw[4];
+    int sw[4];
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const char* p = Ws + ni * 16 * MX_BK;
+      const uint4 lo = *(const uint4*)(p + rdo0), hi = *(const uint4*)(p + rdo1);
+      bw[ni] = v8i{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+      sw[ni] = (int)((Ssw[ni * 16 + fr] >> (8 * (g & 1))) & 0xff);  // lanes >= 32: unused
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      v8i av[4];
+      int sa[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int mi = 4 * h + q;
+        const char* p = As + mi * 16 * MX_BK;
+        const uint4 lo = *(const uint4*)(p + rdo0), hi = *(const uint4*)(p + rdo1);
+        av[q] = v8i{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+        sa[q] = (int)((Ssa[mi * 16 + fr] >> (8 * (g & 1))) & 0xff);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni)
+          acc[4 * h + q][ni] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bw[ni], av[q], acc[4 * h + q][ni], 0,
+                                                                                0, 0, sw[ni], 0, sa[q]);
+    }
+  }
+
+  // ---- epilogue: lane holds rows m0 + wr*128 + mi*16 + fr, columns n0 + wc*64 + ni*16 + 4g .. +3
+  float4 bias[4];
+#pragma unroll
+  for (int ni = 0; ni < 4; ++ni) {
+    const int n = n0 + wc * WTN + ni * 16 + 4 * g;
+    bias[ni] = a.bias ? *(const float4*)(a.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+#pragma unroll
+  for (int mi = 0; mi < 8; ++mi) {
+    const int m = m0 + wr * WTM + mi * 16 + fr;
+    if (EPI == EPI_F32) {
+      if (m < a.M)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+          const int n = n0 + wc * WTN + ni * 16 + 4 * g;
+          *(float4*)((float*)a.out + (int64_t)m * a.ldo + n) =
+              make_float4(acc[mi][ni][0] + bias[ni].x, acc[mi][ni][1] + bias[ni].y, acc[mi][ni][2] + bias[ni].z,
+                          acc[mi][ni][3] + bias[ni].w);
+        }
+      continue;
+    }
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      uint2 pk[2];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int ni = 2 * p + q;
+        float v0 = acc[mi][ni][0] + bias[ni].x, v1 = acc[mi][ni][1] + bias[ni].y;
+        float v2 = acc[mi][ni][2] + bias[ni].z, v3 = acc[mi][ni][3] + bias[ni].w;
+        if (EPI == EPI_GELU_BF16) {
+          v0 = mx_gelu(v0); v1 = mx_gelu(v1); v2 = mx_gelu(v2); v3 = mx_gelu(v3);
+        }
+        pk[q] = make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
+      }
+      // 16-lane-row exchange -> 8 consecutive columns per lane (gemm.hip DIRECT epilogue)
+      const auto sx = __builtin_amdgcn_permlane16_swap(pk[0].x, pk[1].x, false, false);
+      const auto sy = __builtin_amdgcn_permlane16_swap(pk[0].y, pk[1].y, false, false);
+      const int col = n0 + wc * WTN + (2 * p + (g & 1)) * 16 + (g >> 1) * 8;
+      if (m < a.M) *(uint4*)((uint16_t*)a.out + (int64_t)m * a.ldo + col) = make_uint4(sx[0], sy[0], sx[1], sy[1]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// bf16 -> MX-fp8 (OCP e4m3 + one e8m0 scale per 64 consecutive k): one lane
+// per 64-element block.  Shared exponent X = floor(log2(amax)) - 8 (e4m3's
+// largest exponent), element = RNE e4m3 of v * 2^-X, saturated to +-448;
+// scale byte = X + 127 (amax = 0 -> X = -127).
+__global__ __launch_bounds__(256) void quantize_mx_kernel(const uint16_t* __restrict__ in, int64_t ld_in,
+                                                          uint8_t* __restrict__ q, int64_t ld_q,
+                                                          uint8_t* __restrict__ s, int rows, int K) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int nb = K / 64;
+  if (i >= (int64_t)rows * nb) return;
+  const int64_t r = i / nb;
+  const int b = (int)(i % nb);
+  const uint4* src = (const uint4*)(in + r * ld_in + b * 64);
+  const int rows_pad = (rows + 1) & ~1;
+  float v[64];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const uint4 u = src[c];
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v[8 * c + 2 * e] = bf2f((uint16_t)(w[e] & 0xffff));
+      v[8 * c + 2 * e + 1] = bf2f((uint16_t)(w[e] >> 16));
+    }
+  }
+  float amax = 0.f;
+#pragma unroll
+  for (int e = 0; e < 64; ++e) amax = fmaxf(amax, fabsf(v[e]));
+  int X = -127;
+  if (amax > 0.f) {
+    int ex;
+    (void)frexpf(amax, &ex);  // amax = f * 2^ex, f in [0.5, 1): floor(log2 amax) = ex - 1
+    X = ex - 1 - 8;
+    X = X < -127 ? -127 : (X > 127 ? 127 : X);
+  }
+  const float inv = ldexpf(1.0f, -X);
+  uint32_t packed[16];
+#pragma unroll
+  for (int d = 0; d < 16; ++d) {
+    float f[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) f[e] = fminf(fmaxf(v[4 * d + e] * inv, -448.f), 448.f);
+    uint32_t w = __builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], 0, false);
+    w = __builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], w, true);
+    packed[d] = w;
+  }
+  uint4* dst = (uint4*)(q + r * ld_q + b * 64);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) dst[c] = make_uint4(packed[4 * c], packed[4 * c + 1], packed[4 * c + 2], packed[4 * c + 3]);
+  s[((int64_t)(b >> 1) * rows_pad + r) * 2 + (b & 1)] = (uint8_t)(X + 127);
+}
+
+}  // namespace
+
+hipError_t gemm_mx(const GemmArgs& a, int epi, hipStream_t s) {
+  if (a.M <= 0) return hipSuccess;
+  if (a.K % MX_BK || a.N % 256 || a.K <= 0 || !a.a_scale || !a.w_scale) return hipErrorInvalidValue;
+  if ((a.lda % 16) || (a.ldw % 16) || (a.ldo % 8) || ((uintptr_t)a.out & 15)) return hipErrorInvalidValue;
+  const int nt = ((a.M + 255) / 256) * (a.N / 256);
+  switch (epi) {
+    case EPI_BF16: hipLaunchKernelGGL(gemm_mx_kernel<EPI_BF16>, dim3(nt), dim3(512), 0, s, a); break;
+    case EPI_GELU_BF16: hipLaunchKernelGGL(gemm_mx_kernel<EPI_GELU_BF16>, dim3(nt), dim3(512), 0, s, a); break;
+    case EPI_F32: hipLaunchKernelGGL(gemm_mx_kernel<EPI_F32>, dim3(nt), dim3(512), 0, s, a); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t quantize_mx(const uint16_t* in, int64_t ld_in, uint8_t* q, int64_t ld_q, uint8_t* sc, int rows, int K,
+                       hipStream_t s) {
+  if (rows <= 0) return hipSuccess;
+  if (K % 128 || (ld_in % 8) || (ld_q % 16)) return hipErrorInvalidValue;
+  const int64_t n = (int64_t)rows * (K / 64);
+  hipLaunchKernelGGL(quantize_mx_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, in, ld_in, q, ld_q, sc,
+                     rows, K);
+  return hipGetLastError();
+}
+
+}  // namespace miclip

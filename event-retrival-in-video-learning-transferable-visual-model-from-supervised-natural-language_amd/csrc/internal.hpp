@@ -22,11 +22,17 @@ struct GemmArgs {
   // output row remap: r -> (r / group) * gstride + goffset + r % group (group == 0: identity)
   int group, gstride, goffset;
   int variant;  // main-loop schedule (0 = default choice; see gemm.hip)
+  const uint8_t *a_scale, *w_scale;  // MX-fp8 GEMM: e8m0 per 64 k, stage-major [K/128][rows_pad][2] (gemm_mx.hip)
   int ngroup;   // tile order: n-blocks per group (0 = m-major raster; gemm.hip tile_coords)
 };
 
 // Requirements: K % 64 == 0, N % 128 == 0, A/W 16-byte aligned rows.
 hipError_t gemm_bf16(const GemmArgs& a, int epi, hipStream_t s);
+// MX-fp8: A, W e4m3 bytes (row strides lda/ldw in BYTES), a_scale/w_scale e8m0; K % 128 == 0, N % 256 == 0
+hipError_t gemm_mx(const GemmArgs& a, int epi, hipStream_t s);
+// bf16 [rows][K] -> e4m3 [rows][K] + e8m0 scales [K/128][rows_pad][2] (one per 64 k; K % 128 == 0)
+hipError_t quantize_mx(const uint16_t* in, int64_t ld_in, uint8_t* q, int64_t ld_q, uint8_t* sc, int rows, int K,
+                       hipStream_t s);
 
 // out[r] = LN(x[r * in_stride]) over W features; out is bf16 (row stride out_stride).
 hipError_t layernorm_bf16(const float* x, int64_t in_stride, const float* g, const float* b,

@@ -179,6 +179,20 @@ int mi_op_layernorm(const float* x, const float* gamma, const float* beta, void*
                     void* stream);
 int mi_op_attention(const void* qkv, void* out, int32_t B, int32_t S, int32_t W, int32_t causal, void* stream);
 
+/* MX-fp8 operator entry points (the "fp8 MFMA weights" configuration,
+ * BASELINE.json configs[4]; OCP e4m3 elements with one e8m0 scale per 64
+ * consecutive k of a row — the block the gfx950 16x16x128 block-scaled MFMA
+ * applies, probed in scripts/probes/mx_scale_map.hip):
+ * mi_op_quantize_mx: bf16 [rows][K] -> e4m3 q [rows][K] + e8m0 scales, stage-major
+ *   [K/128][rows_pad][2] (rows_pad = rows rounded up to even; byte kb & 1 of
+ *   row r in stage kb >> 1 scales k-block kb); K % 128 == 0
+ * mi_op_gemm_mx: out = (A * 2^sA) . (W * 2^sW)^T (+bias) on the block-scaled MFMA,
+ *   A [M][K] / W [N][K] e4m3 with their scales; epilogue 0 bf16, 1 bf16 QuickGELU, 3 f32.
+ *   K % 128 == 0, N % 256 == 0. */
+int mi_op_quantize_mx(const void* in, void* q, void* scales, int32_t rows, int32_t K, void* stream);
+int mi_op_gemm_mx(const void* A, const void* a_scale, const void* W, const void* w_scale, const float* bias, void* out,
+                  int32_t M, int32_t N, int32_t K, int32_t epi, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

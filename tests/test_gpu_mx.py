@@ -1,0 +1,86 @@
+"""MX-fp8 operators (configs[4] "fp8 MFMA weights"): the bf16 -> MX quantiser
+and the block-scaled MFMA GEMM against oracle/mx_ref.py (float64)."""
+import numpy as np
+import pytest
+
+from oracle import mx_ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _lib():
+    from miclip import _native
+    return _native
+
+
+def _stream():
+    import torch
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _quant_gpu(x_bf16):
+    import torch
+    N_ = _lib()
+    rows, K = x_bf16.shape
+    q = torch.empty(rows, K, dtype=torch.uint8, device=x_bf16.device)
+    s = torch.zeros((K // 128) * (rows + (rows & 1)) * 2, dtype=torch.uint8, device=x_bf16.device)
+    N_.check(N_.lib().mi_op_quantize_mx(x_bf16.data_ptr(), q.data_ptr(), s.data_ptr(), rows, K, _stream()), "quant")
+    return q, s
+
+
+def test_quantize_matches_oracle(gpu):
+    import torch
+    g = torch.Generator(device="cpu").manual_seed(3)
+    x = (torch.randn(97, 256, generator=g) * torch.logspace(-3, 3, 256)).bfloat16()
+    x[5, :64] = 0                                 # all-zero block -> scale 2^-127, codes 0
+    x[7, 40] = 1e4                                # one large outlier in a block
+    q, s = _quant_gpu(x.to(gpu))
+    torch.cuda.synchronize()
+    rq, rs = mx_ref.quantize(x.float().numpy())
+    assert np.array_equal(mx_ref.from_stage_major(s.cpu().numpy(), 97, 256), rs)
+    got = mx_ref.E4M3[q.cpu().numpy()]
+    ref = mx_ref.E4M3[rq]
+    assert np.array_equal(got, ref)               # same values (+0 / -0 codes may differ)
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (301, 512, 1024), (1000, 768, 256), (4096, 1024, 4096)])
+@pytest.mark.parametrize("epi", [3, 0, 1])
+def test_gemm_mx_matches_oracle(gpu, M, N, K, epi):
+    import torch
+    N_ = _lib()
+    g = torch.Generator(device="cpu").manual_seed(M + N + K + epi)
+    a = (torch.randn(M, K, generator=g) * 2).bfloat16()
+    w = (torch.randn(N, K, generator=g) * K ** -0.5).bfloat16()
+    bias = torch.randn(N, generator=g)
+    qa, sa = _quant_gpu(a.to(gpu))
+    qw, sw = _quant_gpu(w.to(gpu))
+    out = torch.empty(M, N, dtype=torch.float32 if epi == 3 else torch.bfloat16, device=gpu)
+    bd = bias.to(gpu)
+    N_.check(N_.lib().mi_op_gemm_mx(qa.data_ptr(), sa.data_ptr(), qw.data_ptr(), sw.data_ptr(), bd.data_ptr(),
+                                    out.data_ptr(), M, N, K, epi, _stream()), "gemm_mx")
+    torch.cuda.synchronize()
+    sa_, sw_ = (mx_ref.from_stage_major(x.cpu().numpy(), r, K) for x, r in ((sa, M), (sw, N)))
+    ref = mx_ref.gemm(qa.cpu().numpy(), sa_, qw.cpu().numpy(), sw_) + bias.double().numpy()
+    if epi == 1:
+        ref = ref / (1 + np.exp(-1.702 * ref))
+    got = out.double().cpu().numpy()
+    scale = np.abs(ref).max()
+    tol = (1e-4 if epi == 3 else 1e-2) * scale
+    assert np.abs(got - ref).max() < tol, (np.abs(got - ref).max(), tol)
+
+
+def test_gemm_mx_asymmetric_identity(gpu):
+    """A = I (exact in e4m3) with an asymmetric W catches a transposed C write."""
+    import torch
+    N_ = _lib()
+    M = N = 256
+    K = 256
+    a = torch.eye(M, K).bfloat16()
+    w = ((torch.arange(N * K).reshape(N, K) % 7) - 3).float().bfloat16()
+    qa, sa = _quant_gpu(a.to(gpu))
+    qw, sw = _quant_gpu(w.to(gpu))
+    out = torch.empty(M, N, device=gpu)
+    N_.check(N_.lib().mi_op_gemm_mx(qa.data_ptr(), sa.data_ptr(), qw.data_ptr(), sw.data_ptr(), None,
+                                    out.data_ptr(), M, N, K, 3, _stream()), "gemm_mx")
+    torch.cuda.synchronize()
+    assert torch.equal(out.cpu(), w.float().t().contiguous())
