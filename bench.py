@@ -29,6 +29,7 @@ for _p in (PKG, ROOT):
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md (spec)
 BF16_PEAK_TFLOPS = 2500.0      # dense bf16 MFMA (spec, no sparsity)
+FP8_PEAK_TFLOPS = 5000.0       # dense fp8 / MX-fp8 MFMA (spec, no sparsity)
 F32_MFMA_PEAK_TFLOPS = 157.3
 
 
@@ -42,6 +43,8 @@ def parse():
     ap.add_argument("--queries", type=int, default=32)
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--image-chunk", type=int, default=None)
+    ap.add_argument("--weights", choices=["bf16", "fp8"], default="bf16",
+                    help="fp8: vision GEMMs on the MX-fp8 block-scaled MFMA (BASELINE configs[4])")
     ap.add_argument("--cpu-frames", type=int, default=64, help="CPU baseline sample (BASELINE configs[0])")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
@@ -87,10 +90,25 @@ def kernel_timing(model, cfg, chunk, reps=20):
 
     gemms = [("gemm_qkv", 3 * W, W, 0, outb), ("gemm_out", W, W, 0, outb), ("gemm_fc", 4 * W, W, 1, outb),
              ("gemm_proj", W, 4 * W, 0, outb)]
-    for name, Nn, K, epi, out in gemms:
-        timed(name, lambda Nn=Nn, K=K, epi=epi, out=out: N.check(
-            L.mi_op_gemm(A.data_ptr(), Wt.data_ptr(), bias.data_ptr(), out.data_ptr(), M, Nn, K, epi, sp), "gemm"),
-            flops=2.0 * M * Nn * K)
+    if getattr(model, "weights", "bf16") == "fp8":
+        # MX-fp8 operands: e4m3 codes + stage-major e8m0 scales (mi_op_quantize_mx)
+        def mx(t):
+            rows, K = t.shape
+            q = torch.empty(rows, K, dtype=torch.uint8, device=dev)
+            sc = torch.empty((K // 128) * ((rows + 1) & ~1) * 2, dtype=torch.uint8, device=dev)
+            N.check(L.mi_op_quantize_mx(t.data_ptr(), q.data_ptr(), sc.data_ptr(), rows, K, sp), "quantize_mx")
+            return q, sc
+        for name, Nn, K, epi, out in gemms:
+            Aq, As = mx(A[:, :K].contiguous())
+            Wq, Ws = mx(Wt[:Nn, :K].contiguous())
+            timed(name, lambda Nn=Nn, K=K, epi=epi, out=out, Aq=Aq, As=As, Wq=Wq, Ws=Ws: N.check(
+                L.mi_op_gemm_mx(Aq.data_ptr(), As.data_ptr(), Wq.data_ptr(), Ws.data_ptr(), bias.data_ptr(),
+                                out.data_ptr(), M, Nn, K, epi, sp), "gemm_mx"), flops=2.0 * M * Nn * K)
+    else:
+        for name, Nn, K, epi, out in gemms:
+            timed(name, lambda Nn=Nn, K=K, epi=epi, out=out: N.check(
+                L.mi_op_gemm(A.data_ptr(), Wt.data_ptr(), bias.data_ptr(), out.data_ptr(), M, Nn, K, epi, sp),
+                "gemm"), flops=2.0 * M * Nn * K)
     qkv = torch.randn(M, 3 * W, device=dev, generator=g).bfloat16()
     att = torch.empty(M, W, dtype=torch.bfloat16, device=dev)
     timed("attention", lambda: N.check(L.mi_op_attention(qkv.data_ptr(), att.data_ptr(), chunk, S, W, 0, sp),
@@ -218,7 +236,7 @@ def main():
         from miclip.config import get_config
         base = max(8, 100_000 // get_config(args.model).vision_tokens)
         chunk = -(-args.frames // -(-args.frames // base))
-    model, _ = api.load(args.model, device=dev, image_chunk=chunk)
+    model, _ = api.load(args.model, device=dev, image_chunk=chunk, weights=args.weights)
     cfg = model.cfg
     chunk = model._chunks[0]
     Nf, Q, k = args.frames, args.queries, args.k
@@ -277,11 +295,17 @@ def main():
             ach = fl / (dom["us"] * 1e-6) / 1e12
             shape = [M, 4 * cfg.vision_width, cfg.vision_width]
             traffic, tsrc = pmc_traffic(shape)
-            roof = {"bound": "mfma", "kernel": "gemm_pp_kernel<EPI_GELU_BF16> (mlp.c_fc + QuickGELU)",
-                    "achieved": round(ach, 1), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(ach / BF16_PEAK_TFLOPS, 4), "traffic": traffic, "traffic_source": tsrc,
-                    "algorithmic_bytes": 2 * (M * 4 * cfg.vision_width + 4 * cfg.vision_width ** 2
-                                              + M * cfg.vision_width),
+            fp8 = args.weights == "fp8"
+            peak = FP8_PEAK_TFLOPS if fp8 else BF16_PEAK_TFLOPS
+            eb = 1 if fp8 else 2            # operand element bytes (fp8 adds 1/64 B of scales per element)
+            roof = {"bound": "mfma",
+                    "kernel": ("gemm_mx_kernel<EPI_GELU_BF16> (mlp.c_fc + QuickGELU, MX-fp8 operands)" if fp8
+                               else "gemm_pp_kernel<EPI_GELU_BF16> (mlp.c_fc + QuickGELU)"),
+                    "achieved": round(ach, 1), "peak": peak, "unit": "TFLOP/s",
+                    "frac": round(ach / peak, 4), "traffic": None if fp8 else traffic,
+                    "traffic_source": None if fp8 else tsrc,
+                    "algorithmic_bytes": int(eb * (1 + fp8 / 64) * (M * cfg.vision_width + 4 * cfg.vision_width ** 2)
+                                             + 2 * M * 4 * cfg.vision_width),
                     "flops_per_launch": fl, "launch_shape": [M, 4 * cfg.vision_width, cfg.vision_width],
                     "avg_launch_us": dom["us"]}
         cpu = None
@@ -291,9 +315,9 @@ def main():
             "metric": "frames/sec embedded+ranked, ViT-B/32 224², 1/2/4/8 MI355X; R@1/5/10 parity",
             "value": round(value, 1), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "bf16", "data": "synthetic (random pixels/tokens, deterministic "
+            "vs_baseline": None, "dtype": "bf16" if args.weights == "bf16" else "fp8-e4m3(MX) vision GEMMs, bf16 rest", "data": "synthetic (random pixels/tokens, deterministic "
                                                           "random-init weights of the real architecture)",
-            "config": {"workload": f"{cfg.name} bf16, {Nf} frames/GPU x {Q} text queries, top-{k}"
+            "config": {"workload": f"{cfg.name} {args.weights}, {Nf} frames/GPU x {Q} text queries, top-{k}"
                                    + (f" ({world} shards, RCCL all-gather top-k)" if world > 1 else
                                       " (BASELINE configs[1])" if (cfg.name, Nf, Q, k) == ("ViT-B/32", 10_000, 32, 10)
                                       else ""),

@@ -54,6 +54,9 @@ uint16_t f2bf_host(float f) {
 struct Layer {
   const float *ln1_g, *ln1_b, *b_qkv, *b_out, *ln2_g, *ln2_b, *b_fc, *b_proj;
   const uint16_t *w_qkv, *w_out, *w_fc, *w_proj;
+  // MX-fp8 copies (weight_dtype MI_FP8, vision tower): e4m3 codes + stage-major e8m0 scales
+  const uint8_t *q_qkv = nullptr, *s_qkv = nullptr, *q_out = nullptr, *s_out = nullptr;
+  const uint8_t *q_fc = nullptr, *s_fc = nullptr, *q_proj = nullptr, *s_proj = nullptr;
 };
 
 // Device weight image: bf16 GEMM weights and f32 vectors in one allocation.
@@ -137,6 +140,8 @@ struct mi_clip {
   int device = 0;
   int S_v = 0, G = 0, Kp = 0;
   char* wdev = nullptr;
+  bool fp8 = false;       // vision tower GEMMs on the MX-fp8 MFMA
+  char* wq = nullptr;     // MX-fp8 weight copies
   // vision
   const uint16_t* conv_w = nullptr;
   const float *cls = nullptr, *vpos = nullptr, *ln_pre_g = nullptr, *ln_pre_b = nullptr, *ln_post_g = nullptr,
@@ -153,6 +158,8 @@ struct mi_clip {
   uint16_t *h = nullptr, *qkv = nullptr, *att = nullptr, *mlp = nullptr, *patches = nullptr, *cls_ln = nullptr;
   uint16_t* delta = nullptr;  // bf16 GEMM output added to x by the next residual_ln
   float* y = nullptr;
+  // MX-fp8 activations (fp8 mode): LN outputs, attention output, QuickGELU(c_fc) + their scales
+  uint8_t *hq = nullptr, *hqs = nullptr, *attq = nullptr, *attqs = nullptr, *mlpq = nullptr, *mlpqs = nullptr;
   std::mutex mu;
 };
 
@@ -176,12 +183,15 @@ int mi_clip_create(const mi_clip_arch* arch, const float* weights, int64_t numel
                    mi_clip** out) {
   if (!arch || !weights || !out) return fail(MI_ERR_ARG, "mi_clip_create: null argument");
   *out = nullptr;
-  if (weight_dtype != MI_BF16) return fail(MI_ERR_UNSUPPORTED, "mi_clip_create: only MI_BF16 weights are supported");
+  if (weight_dtype != MI_BF16 && weight_dtype != MI_FP8)
+    return fail(MI_ERR_UNSUPPORTED, "mi_clip_create: weight_dtype must be MI_BF16 or MI_FP8");
   const mi_clip_arch& a = *arch;
   if (a.vision_width % 128 || a.text_width % 128 || a.vision_width > 1024 || a.text_width > 1024)
     return fail(MI_ERR_UNSUPPORTED, "widths must be multiples of 128 and <= 1024 (got %d/%d)", a.vision_width,
                 a.text_width);
   if (a.embed_dim % 128) return fail(MI_ERR_UNSUPPORTED, "embed_dim must be a multiple of 128");
+  if (weight_dtype == MI_FP8 && a.vision_width % 256)
+    return fail(MI_ERR_UNSUPPORTED, "MI_FP8 needs vision_width %% 256 == 0 (MX GEMM N tiles), got %d", a.vision_width);
   if (a.image_resolution % a.vision_patch_size) return fail(MI_ERR_ARG, "resolution not divisible by patch");
   if (a.text_heads * 64 != a.text_width) return fail(MI_ERR_UNSUPPORTED, "text head dim must be 64");
   const int G = a.image_resolution / a.vision_patch_size;
@@ -257,6 +267,40 @@ int mi_clip_create(const mi_clip_arch* arch, const float* weights, int64_t numel
   };
   conv_layers(vlo, c->vl);
   conv_layers(tlo, c->tl);
+  if (weight_dtype == MI_FP8) {
+    // MX-fp8 copies of the vision tower GEMM weights, quantised on the device
+    // from the bf16 image (the text tower and the projections stay bf16)
+    const int64_t Wv = a.vision_width;
+    const int64_t per_layer = 12 * Wv * Wv + 4 * (12 * Wv * Wv / 64) + 4 * 256;
+    e = hipMalloc(&c->wq, per_layer * c->vl.size() + 256);
+    if (e != hipSuccess) {
+      (void)hipFree(c->wdev);
+      delete c;
+      return fail(MI_ERR_HIP, "fp8 weight allocation: %s", hipGetErrorString(e));
+    }
+    size_t off = 0;
+    auto carve = [&](size_t bytes) { char* p = c->wq + off; off += (bytes + 255) & ~(size_t)255; return (uint8_t*)p; };
+    for (Layer& L : c->vl) {
+      struct { const uint16_t* w; int64_t n, k; const uint8_t** q; const uint8_t** sc; } mats[4] = {
+          {L.w_qkv, 3 * Wv, Wv, &L.q_qkv, &L.s_qkv}, {L.w_out, Wv, Wv, &L.q_out, &L.s_out},
+          {L.w_fc, 4 * Wv, Wv, &L.q_fc, &L.s_fc}, {L.w_proj, Wv, 4 * Wv, &L.q_proj, &L.s_proj}};
+      for (auto& m : mats) {
+        uint8_t* q = carve(m.n * m.k);
+        uint8_t* sc = carve((m.k / 128) * ((m.n + 1) & ~1) * 2);
+        if (e == hipSuccess) e = quantize_mx(m.w, m.k, q, m.k, sc, (int)m.n, (int)m.k, nullptr);
+        *m.q = q;
+        *m.sc = sc;
+      }
+    }
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e != hipSuccess) {
+      (void)hipFree(c->wq);
+      (void)hipFree(c->wdev);
+      delete c;
+      return fail(MI_ERR_HIP, "fp8 weight quantisation: %s", hipGetErrorString(e));
+    }
+    c->fp8 = true;
+  }
   *out = c;
   return MI_OK;
 }
@@ -268,6 +312,7 @@ int mi_clip_destroy(mi_clip* c) {
     (void)hipSetDevice(c->device);
     if (c->ws) (void)hipFree(c->ws);
     if (c->wdev) (void)hipFree(c->wdev);
+    if (c->wq) (void)hipFree(c->wq);
   }
   delete c;
   return MI_OK;
@@ -294,6 +339,16 @@ static int reserve_locked(mi_clip* c, int64_t ic, int64_t tc) {
   const size_t o_pat = carve((size_t)ic * c->G * c->G * c->Kp * 2);
   const size_t o_cls = carve((size_t)rows_max * mx(Wv, Wt) * 2);
   const size_t o_y = carve((size_t)rows_max * a.embed_dim * 4);
+  size_t o_hq = 0, o_hqs = 0, o_attq = 0, o_attqs = 0, o_mlpq = 0, o_mlpqs = 0;
+  if (c->fp8) {
+    const size_t mp = (size_t)((Mv + 1) & ~1);
+    o_hq = carve(Mv * Wv);
+    o_hqs = carve((Wv / 128) * mp * 2);
+    o_attq = carve(Mv * Wv);
+    o_attqs = carve((Wv / 128) * mp * 2);
+    o_mlpq = carve(4 * Mv * Wv);
+    o_mlpqs = carve((4 * Wv / 128) * mp * 2);
+  }
   HIP_TRY(hipSetDevice(c->device));
   char* ws = nullptr;
   HIP_TRY(hipMalloc(&ws, off));
@@ -311,6 +366,14 @@ static int reserve_locked(mi_clip* c, int64_t ic, int64_t tc) {
   c->patches = (uint16_t*)(ws + o_pat);
   c->cls_ln = (uint16_t*)(ws + o_cls);
   c->y = (float*)(ws + o_y);
+  if (c->fp8) {
+    c->hq = (uint8_t*)(ws + o_hq);
+    c->hqs = (uint8_t*)(ws + o_hqs);
+    c->attq = (uint8_t*)(ws + o_attq);
+    c->attqs = (uint8_t*)(ws + o_attqs);
+    c->mlpq = (uint8_t*)(ws + o_mlpq);
+    c->mlpqs = (uint8_t*)(ws + o_mlpqs);
+  }
   c->img_chunk = ic;
   c->txt_chunk = tc;
   return MI_OK;
@@ -336,7 +399,7 @@ static GemmArgs gargs(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t
                       int64_t ldo, int M, int N, int K) {
   GemmArgs g;
   g.A = A; g.lda = lda; g.W = W; g.ldw = ldw; g.bias = bias; g.out = out; g.ldo = ldo;
-  g.M = M; g.N = N; g.K = K; g.group = 0; g.gstride = 0; g.goffset = 0; g.ngroup = 0; g.a_scale = nullptr; g.w_scale = nullptr;
+  g.M = M; g.N = N; g.K = K; g.group = 0; g.gstride = 0; g.goffset = 0; g.ngroup = 0; g.a_scale = nullptr; g.w_scale = nullptr; g.o_scale = nullptr;
   g.variant = gemm_variant();
   return g;
 }
@@ -361,6 +424,39 @@ static int run_tower(mi_clip* c, const std::vector<Layer>& layers, int B, int S,
     HIP_TRY(gemm_bf16(gargs(c->mlp, 4 * W, L.w_proj, 4 * W, L.b_proj, c->delta, W, M, W, 4 * W), EPI_BF16, s));
     if (l + 1 < layers.size())
       HIP_TRY(residual_ln(c->x, c->delta, W, 1, layers[l + 1].ln1_g, layers[l + 1].ln1_b, c->h, M, W, s));
+  }
+  return MI_OK;
+}
+
+// MX-fp8 GEMM arguments: A / W e4m3 with their stage-major scales
+static GemmArgs margs(const uint8_t* A, const uint8_t* as, const uint8_t* W, const uint8_t* ws, const float* bias,
+                      void* out, int64_t ldo, int M, int N, int K) {
+  GemmArgs g = gargs((const uint16_t*)A, K, (const uint16_t*)W, K, bias, out, ldo, M, N, K);
+  g.a_scale = as;
+  g.w_scale = ws;
+  return g;
+}
+
+// The vision tower with MX-fp8 GEMMs (weight_dtype MI_FP8): the same block as
+// run_tower, every GEMM on the block-scaled MFMA; the producers of GEMM A
+// operands (the LayerNorms, attention, c_fc's QuickGELU epilogue) emit MX-fp8
+// directly, so no separate quantisation pass runs.
+static int run_tower_mx(mi_clip* c, const std::vector<Layer>& layers, int B, int S, int W, hipStream_t s) {
+  const int M = B * S;
+  HIP_TRY(layernorm_bf16(c->x, W, layers[0].ln1_g, layers[0].ln1_b, c->h, W, M, W, s, c->hq, c->hqs));
+  for (size_t l = 0; l < layers.size(); ++l) {
+    const Layer& L = layers[l];
+    HIP_TRY(gemm_mx(margs(c->hq, c->hqs, L.q_qkv, L.s_qkv, L.b_qkv, c->qkv, 3 * W, M, 3 * W, W), EPI_BF16, s));
+    HIP_TRY(attention(c->qkv, c->att, B, S, W, 0, s, c->attq, c->attqs));
+    HIP_TRY(gemm_mx(margs(c->attq, c->attqs, L.q_out, L.s_out, L.b_out, c->delta, W, M, W, W), EPI_BF16, s));
+    HIP_TRY(residual_ln(c->x, c->delta, W, 1, L.ln2_g, L.ln2_b, c->h, M, W, s, c->hq, c->hqs));
+    GemmArgs fc = margs(c->hq, c->hqs, L.q_fc, L.s_fc, L.b_fc, c->mlpq, 4 * W, M, 4 * W, W);
+    fc.o_scale = c->mlpqs;
+    HIP_TRY(gemm_mx(fc, EPI_GELU_MX, s));
+    HIP_TRY(gemm_mx(margs(c->mlpq, c->mlpqs, L.q_proj, L.s_proj, L.b_proj, c->delta, W, M, W, 4 * W), EPI_BF16, s));
+    if (l + 1 < layers.size())
+      HIP_TRY(residual_ln(c->x, c->delta, W, 1, layers[l + 1].ln1_g, layers[l + 1].ln1_b, c->h, M, W, s, c->hq,
+                          c->hqs));
   }
   return MI_OK;
 }
@@ -392,7 +488,7 @@ int mi_clip_encode_image(mi_clip* c, const void* pixels, int64_t B, int in_dtype
     pg.goffset = 1;
     HIP_TRY(gemm_bf16(pg, EPI_F32, s));
     HIP_TRY(vision_embed_ln(c->x, c->cls, c->vpos, c->ln_pre_g, c->ln_pre_b, nb, S, W, s));
-    int r = run_tower(c, c->vl, nb, S, W, 0, s);
+    int r = c->fp8 ? run_tower_mx(c, c->vl, nb, S, W, s) : run_tower(c, c->vl, nb, S, W, 0, s);
     if (r) return r;
     // ln_post(x[:, 0] + last c_proj delta) over the CLS rows only
     HIP_TRY(residual_ln(c->x, c->delta, (int64_t)S * W, 0, c->ln_post_g, c->ln_post_b, c->cls_ln, nb, W, s));

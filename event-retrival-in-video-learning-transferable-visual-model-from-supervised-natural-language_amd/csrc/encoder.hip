@@ -41,9 +41,47 @@ __device__ __forceinline__ void ln_stats(RowVals& r, int n4, int lane, int W, fl
   rstd = 1.0f / sqrtf(var + LN_EPS);
 }
 
+// LN output of one row: bf16 (out) or, when q != nullptr, MX-fp8 for the MX
+// GEMM (q codes + stage-major e8m0 scales, one per 64 columns).  Lane holds
+// columns 4*(lane + 64 i) .. +3, so a 64-column block is 16 consecutive lanes:
+// its max is reduced with xor 1, 2, 4, 8.
+__device__ __forceinline__ void ln_store(const RowVals& r, float mean, float rstd, const float* __restrict__ g,
+                                         const float* __restrict__ b, uint16_t* __restrict__ out_row,
+                                         uint8_t* __restrict__ q, uint8_t* __restrict__ qs, int64_t row,
+                                         int64_t rows_pad, int lane, int n4) {
+  const float4* g4 = (const float4*)g;
+  const float4* b4 = (const float4*)b;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = lane + 64 * i;
+    float y0 = 0.f, y1 = 0.f, y2 = 0.f, y3 = 0.f;
+    if (idx < n4) {
+      const float4 gg = g4[idx], bb = b4[idx];
+      y0 = (r.v[i].x - mean) * rstd * gg.x + bb.x;
+      y1 = (r.v[i].y - mean) * rstd * gg.y + bb.y;
+      y2 = (r.v[i].z - mean) * rstd * gg.z + bb.z;
+      y3 = (r.v[i].w - mean) * rstd * gg.w + bb.w;
+    }
+    if (!q) {
+      if (idx < n4) ((uint2*)out_row)[idx] = make_uint2(pack_bf16x2(y0, y1), pack_bf16x2(y2, y3));
+      continue;
+    }
+    if (64 * i >= n4) continue;  // wave-uniform: no column of this lane group exists
+    float amax = fmaxf(fmaxf(fabsf(y0), fabsf(y1)), fmaxf(fabsf(y2), fabsf(y3)));
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) amax = fmaxf(amax, __shfl_xor(amax, o, 64));
+    const int X = mx_block_exp(amax);
+    if (idx < n4) {
+      ((uint32_t*)(q + row * (int64_t)(4 * n4)))[idx] = mx_pack4(y0, y1, y2, y3, ldexpf(1.0f, -X));
+      if ((idx & 15) == 0) qs[mx_scale_index(row, idx >> 4, rows_pad)] = (uint8_t)(X + 127);
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void ln_bf16_kernel(const float* __restrict__ x, int64_t in_stride,
                                                       const float* __restrict__ g, const float* __restrict__ b,
-                                                      uint16_t* __restrict__ out, int64_t out_stride, int rows, int W) {
+                                                      uint16_t* __restrict__ out, int64_t out_stride, int rows, int W,
+                                                      uint8_t* __restrict__ q, uint8_t* __restrict__ qs) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= rows) return;
   const int n4 = W >> 2;
@@ -53,22 +91,7 @@ __global__ __launch_bounds__(256) void ln_bf16_kernel(const float* __restrict__ 
   for (int i = 0; i < 4; ++i) r.v[i] = (lane + 64 * i < n4) ? xr[lane + 64 * i] : make_float4(0.f, 0.f, 0.f, 0.f);
   float mean, rstd;
   ln_stats(r, n4, lane, W, mean, rstd);
-  const float4* g4 = (const float4*)g;
-  const float4* b4 = (const float4*)b;
-  uint2* o = (uint2*)(out + (int64_t)row * out_stride);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int idx = lane + 64 * i;
-    if (idx < n4) {
-      const float4 gg = g4[idx], bb = b4[idx];
-      const float y0 = (r.v[i].x - mean) * rstd * gg.x + bb.x;
-      const float y1 = (r.v[i].y - mean) * rstd * gg.y + bb.y;
-      const float y2 = (r.v[i].z - mean) * rstd * gg.z + bb.z;
-      const float y3 = (r.v[i].w - mean) * rstd * gg.w + bb.w;
-      o[idx] = make_uint2((uint32_t)f2bf(y0) | ((uint32_t)f2bf(y1) << 16),
-                          (uint32_t)f2bf(y2) | ((uint32_t)f2bf(y3) << 16));
-    }
-  }
+  ln_store(r, mean, rstd, g, b, out + (int64_t)row * out_stride, q, qs, row, (rows + 1) & ~1, lane, n4);
 }
 
 // Residual add + LayerNorm: xr = x[r*stride] + delta[r*stride] (delta = the
@@ -79,7 +102,8 @@ __global__ __launch_bounds__(256) void ln_bf16_kernel(const float* __restrict__ 
 __global__ __launch_bounds__(256) void residual_ln_kernel(float* __restrict__ x, const uint16_t* __restrict__ delta,
                                                           int64_t stride, int write_x, const float* __restrict__ g,
                                                           const float* __restrict__ b, uint16_t* __restrict__ out,
-                                                          int rows, int W) {
+                                                          int rows, int W, uint8_t* __restrict__ q,
+                                                          uint8_t* __restrict__ qs) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= rows) return;
   const int n4 = W >> 2;
@@ -101,18 +125,7 @@ __global__ __launch_bounds__(256) void residual_ln_kernel(float* __restrict__ x,
   }
   float mean, rstd;
   ln_stats(r, n4, lane, W, mean, rstd);
-  const float4* g4 = (const float4*)g;
-  const float4* b4 = (const float4*)b;
-  uint2* o = (uint2*)(out + (int64_t)row * W);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int idx = lane + 64 * i;
-    if (idx < n4) {
-      const float4 gg = g4[idx], bb = b4[idx];
-      o[idx] = make_uint2(pack_bf16x2((r.v[i].x - mean) * rstd * gg.x + bb.x, (r.v[i].y - mean) * rstd * gg.y + bb.y),
-                          pack_bf16x2((r.v[i].z - mean) * rstd * gg.z + bb.z, (r.v[i].w - mean) * rstd * gg.w + bb.w));
-    }
-  }
+  ln_store(r, mean, rstd, g, b, out + (int64_t)row * W, q, qs, row, (rows + 1) & ~1, lane, n4);
 }
 
 __global__ __launch_bounds__(256) void vision_embed_ln_kernel(float* __restrict__ x, const float* __restrict__ cls,
@@ -425,7 +438,8 @@ __global__ __launch_bounds__(64) void attention_kernel(const uint16_t* __restric
 template <int SP, int NW>
 __global__ __launch_bounds__(64 * NW) void attention_long_kernel(const uint16_t* __restrict__ qkv,
                                                              uint16_t* __restrict__ out, int S, int W, int H,
-                                                             int causal) {
+                                                             int causal, uint8_t* __restrict__ q8,
+                                                             uint8_t* __restrict__ qs, int64_t rows_pad) {
   static_assert(SP % 32 == 0, "key padding");
   constexpr int TS = SP + 4;  // V^T row: +8 bytes staggers the banks of consecutive head dims
   __shared__ __attribute__((aligned(16))) uint16_t Vt[64 * TS];
@@ -543,6 +557,26 @@ __global__ __launch_bounds__(64 * NW) void attention_long_kernel(const uint16_t*
     l += __shfl_xor(l, 32, 64);
     const float inv = 1.0f / l;
     // o[dt][j]: query qrow, head dim dt*16 + 4g + j
+    if (q8) {  // MX-fp8 output: this head's 64 dims are one 64-k block of out_proj
+      float amax = 0.f;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) amax = fmaxf(amax, fabsf(o[dt][j] * inv));
+      amax = fmaxf(amax, __shfl_xor(amax, 16, 64));
+      amax = fmaxf(amax, __shfl_xor(amax, 32, 64));
+      const int X = mx_block_exp(amax);
+      const float sc = ldexpf(1.0f, -X);
+      if (qrow < S) {
+        const int64_t row = (int64_t)bseq * S + qrow;
+        uint8_t* dst = q8 + row * W + h * 64 + 4 * g;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+          *(uint32_t*)(dst + dt * 16) = mx_pack4(o[dt][0] * inv, o[dt][1] * inv, o[dt][2] * inv, o[dt][3] * inv, sc);
+        if (g == 0) qs[mx_scale_index(row, h, rows_pad)] = (uint8_t)(X + 127);
+      }
+      continue;
+    }
     if (qrow < S) {
       uint16_t* dst = out + ((int64_t)bseq * S + qrow) * W + h * 64 + 4 * g;
 #pragma unroll
@@ -578,11 +612,11 @@ __global__ __launch_bounds__(256) void finalize_kernel(const float* __restrict__
 }  // namespace
 
 hipError_t layernorm_bf16(const float* x, int64_t in_stride, const float* g, const float* b, uint16_t* out,
-                          int64_t out_stride, int rows, int W, hipStream_t s) {
+                          int64_t out_stride, int rows, int W, hipStream_t s, uint8_t* q, uint8_t* qs) {
   if (rows <= 0) return hipSuccess;
-  if (W % 4 || W > 1024) return hipErrorInvalidValue;
+  if (W % 4 || W > 1024 || (q && W % 128)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(ln_bf16_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, x, in_stride, g, b, out, out_stride,
-                     rows, W);
+                     rows, W, q, qs);
   return hipGetLastError();
 }
 
@@ -613,11 +647,11 @@ hipError_t eot_gather_ln(const int32_t* tokens, const float* x, const uint16_t* 
 }
 
 hipError_t residual_ln(float* x, const uint16_t* delta, int64_t stride, int write_x, const float* g, const float* b,
-                       uint16_t* out, int rows, int W, hipStream_t s) {
+                       uint16_t* out, int rows, int W, hipStream_t s, uint8_t* q, uint8_t* qs) {
   if (rows <= 0) return hipSuccess;
-  if (W % 4 || W > 1024) return hipErrorInvalidValue;
+  if (W % 4 || W > 1024 || (q && W % 128)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(residual_ln_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, x, delta, stride, write_x, g, b, out,
-                     rows, W);
+                     rows, W, q, qs);
   return hipGetLastError();
 }
 
@@ -638,7 +672,8 @@ hipError_t im2col(const void* pixels, int in_bf16, uint16_t* out, int B, int R, 
   return hipGetLastError();
 }
 
-hipError_t attention(const uint16_t* qkv, uint16_t* out, int B, int S, int W, int causal, hipStream_t s) {
+hipError_t attention(const uint16_t* qkv, uint16_t* out, int B, int S, int W, int causal, hipStream_t s, uint8_t* q8,
+                     uint8_t* qs) {
   const int H = W / 64;
   const int items = B * H;
   if (items <= 0) return hipSuccess;
@@ -646,10 +681,13 @@ hipError_t attention(const uint16_t* qkv, uint16_t* out, int B, int S, int W, in
   // (scripts/attn_micro.py: 179 vs 195-203 us at B/32) than the flash kernel
   // with 1, 2 or 4 waves; causal bit 8 selects the 4-wave flash kernel instead
   // (A/B measurements, parity tests of both paths).
-  const bool flash_short = (causal >> 8) & 1;
+  bool flash_short = (causal >> 8) & 1;
   causal &= 1;
   const dim3 grid(items), b64(64), b256(256), b512(512);
-#define LONG_ATTN(SP, NW, blk) hipLaunchKernelGGL((attention_long_kernel<SP, NW>), grid, blk, 0, s, qkv, out, S, W, H, causal)
+#define LONG_ATTN(SP, NW, blk)                                                                                   \
+  hipLaunchKernelGGL((attention_long_kernel<SP, NW>), grid, blk, 0, s, qkv, out, S, W, H, causal, q8, qs, \
+                     ((int64_t)B * S + 1) & ~1)
+  if (q8 && S <= 96) flash_short = true;  // the fp8 output lives in the flash kernel
   if (!flash_short && S <= 96) {
     if (S <= 32) hipLaunchKernelGGL(attention_kernel<32>, grid, b64, 0, s, qkv, out, S, W, H, causal, items);
     else if (S <= 64) hipLaunchKernelGGL(attention_kernel<64>, grid, b64, 0, s, qkv, out, S, W, H, causal, items);

@@ -145,6 +145,38 @@ __global__ __launch_bounds__(512) void gemm_mx_kernel(GemmArgs a) {
     const int n = n0 + wc * WTN + ni * 16 + 4 * g;
     bias[ni] = a.bias ? *(const float4*)(a.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
   }
+  if (EPI == EPI_GELU_MX) {
+    // fp8 output for the next MX GEMM (mlp.c_fc -> c_proj): a wave's 64
+    // columns of a row are exactly one 64-k block of the consumer: max over the
+    // lane's 16 values, then across the 4 lane groups (xor 16, 32)
+    const int blk = (n0 + wc * WTN) >> 6;
+    const int64_t m_pad = (a.M + 1) & ~1;
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi) {
+      const int m = m0 + wr * WTM + mi * 16 + fr;
+      float v[4][4];
+      float amax = 0.f;
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        v[ni][0] = mx_gelu(acc[mi][ni][0] + bias[ni].x);
+        v[ni][1] = mx_gelu(acc[mi][ni][1] + bias[ni].y);
+        v[ni][2] = mx_gelu(acc[mi][ni][2] + bias[ni].z);
+        v[ni][3] = mx_gelu(acc[mi][ni][3] + bias[ni].w);
+        amax = fmaxf(amax, fmaxf(fmaxf(fabsf(v[ni][0]), fabsf(v[ni][1])), fmaxf(fabsf(v[ni][2]), fabsf(v[ni][3]))));
+      }
+      amax = fmaxf(amax, __shfl_xor(amax, 16, 64));
+      amax = fmaxf(amax, __shfl_xor(amax, 32, 64));
+      const int X = mx_block_exp(amax);
+      const float inv = ldexpf(1.0f, -X);
+      if (m < a.M) {
+        uint8_t* o = (uint8_t*)a.out + (int64_t)m * a.ldo + n0 + wc * WTN + 4 * g;
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) *(uint32_t*)(o + ni * 16) = mx_pack4(v[ni][0], v[ni][1], v[ni][2], v[ni][3], inv);
+        if (g == 0) a.o_scale[mx_scale_index(m, blk, m_pad)] = (uint8_t)(X + 127);
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int mi = 0; mi < 8; ++mi) {
     const int m = m0 + wr * WTM + mi * 16 + fr;
@@ -210,28 +242,15 @@ __global__ __launch_bounds__(256) void quantize_mx_kernel(const uint16_t* __rest
   float amax = 0.f;
 #pragma unroll
   for (int e = 0; e < 64; ++e) amax = fmaxf(amax, fabsf(v[e]));
-  int X = -127;
-  if (amax > 0.f) {
-    int ex;
-    (void)frexpf(amax, &ex);  // amax = f * 2^ex, f in [0.5, 1): floor(log2 amax) = ex - 1
-    X = ex - 1 - 8;
-    X = X < -127 ? -127 : (X > 127 ? 127 : X);
-  }
+  const int X = mx_block_exp(amax);
   const float inv = ldexpf(1.0f, -X);
   uint32_t packed[16];
 #pragma unroll
-  for (int d = 0; d < 16; ++d) {
-    float f[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) f[e] = fminf(fmaxf(v[4 * d + e] * inv, -448.f), 448.f);
-    uint32_t w = __builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], 0, false);
-    w = __builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], w, true);
-    packed[d] = w;
-  }
+  for (int d = 0; d < 16; ++d) packed[d] = mx_pack4(v[4 * d], v[4 * d + 1], v[4 * d + 2], v[4 * d + 3], inv);
   uint4* dst = (uint4*)(q + r * ld_q + b * 64);
 #pragma unroll
   for (int c = 0; c < 4; ++c) dst[c] = make_uint4(packed[4 * c], packed[4 * c + 1], packed[4 * c + 2], packed[4 * c + 3]);
-  s[((int64_t)(b >> 1) * rows_pad + r) * 2 + (b & 1)] = (uint8_t)(X + 127);
+  s[mx_scale_index(r, b, rows_pad)] = (uint8_t)(X + 127);
 }
 
 }  // namespace
@@ -245,6 +264,10 @@ hipError_t gemm_mx(const GemmArgs& a, int epi, hipStream_t s) {
     case EPI_BF16: hipLaunchKernelGGL(gemm_mx_kernel<EPI_BF16>, dim3(nt), dim3(512), 0, s, a); break;
     case EPI_GELU_BF16: hipLaunchKernelGGL(gemm_mx_kernel<EPI_GELU_BF16>, dim3(nt), dim3(512), 0, s, a); break;
     case EPI_F32: hipLaunchKernelGGL(gemm_mx_kernel<EPI_F32>, dim3(nt), dim3(512), 0, s, a); break;
+    case EPI_GELU_MX:
+      if (!a.o_scale) return hipErrorInvalidValue;
+      hipLaunchKernelGGL(gemm_mx_kernel<EPI_GELU_MX>, dim3(nt), dim3(512), 0, s, a);
+      break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

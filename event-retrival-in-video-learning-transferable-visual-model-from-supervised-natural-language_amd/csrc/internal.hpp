@@ -9,8 +9,32 @@ enum GemmEpi {
   EPI_BF16 = 0,        // out bf16 = acc + bias
   EPI_GELU_BF16 = 1,   // out bf16 = quick_gelu(acc + bias)
   EPI_RESID_F32 = 2,   // out f32 += acc + bias   (residual stream, in place)
-  EPI_F32 = 3          // out f32 = acc (+ bias)
+  EPI_F32 = 3,         // out f32 = acc (+ bias)
+  EPI_GELU_MX = 4      // MX-fp8 GEMM only: out e4m3 = MX(quick_gelu(acc + bias)), scales -> o_scale
 };
+
+// MX block quantisation shared by the fp8 producers (gemm_mx.hip, encoder.hip):
+// X = floor(log2 amax) - 8 clamped to [-127, 127] (amax = 0 -> -127);
+// element = RNE e4m3 of clamp(v * 2^-X, +-448); scale byte = X + 127.
+__device__ __forceinline__ int mx_block_exp(float amax) {
+  if (!(amax > 0.f)) return -127;
+  int ex;
+  (void)frexpf(amax, &ex);
+  const int X = ex - 1 - 8;
+  return X < -127 ? -127 : (X > 127 ? 127 : X);
+}
+__device__ __forceinline__ uint32_t mx_pack4(float a, float b, float c, float d, float inv) {
+  a = fminf(fmaxf(a * inv, -448.f), 448.f);
+  b = fminf(fmaxf(b * inv, -448.f), 448.f);
+  c = fminf(fmaxf(c * inv, -448.f), 448.f);
+  d = fminf(fmaxf(d * inv, -448.f), 448.f);
+  uint32_t w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  return __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
+}
+// scale byte index of (row r, 64-k block b) in the stage-major layout [K/128][rows_pad][2]
+__device__ __forceinline__ int64_t mx_scale_index(int64_t r, int b, int64_t rows_pad) {
+  return ((int64_t)(b >> 1) * rows_pad + r) * 2 + (b & 1);
+}
 
 struct GemmArgs {
   const uint16_t* A;  // [M, K] bf16, row stride lda
@@ -23,6 +47,7 @@ struct GemmArgs {
   int group, gstride, goffset;
   int variant;  // main-loop schedule (0 = default choice; see gemm.hip)
   const uint8_t *a_scale, *w_scale;  // MX-fp8 GEMM: e8m0 per 64 k, stage-major [K/128][rows_pad][2] (gemm_mx.hip)
+  uint8_t* o_scale;                  // EPI_GELU_MX: scales of the fp8 output (same layout, rows = M)
   int ngroup;   // tile order: n-blocks per group (0 = m-major raster; gemm.hip tile_coords)
 };
 
@@ -35,8 +60,10 @@ hipError_t quantize_mx(const uint16_t* in, int64_t ld_in, uint8_t* q, int64_t ld
                        hipStream_t s);
 
 // out[r] = LN(x[r * in_stride]) over W features; out is bf16 (row stride out_stride).
+// q != nullptr: MX-fp8 output instead (q [rows][W] e4m3 + qs stage-major scales, W % 128 == 0)
 hipError_t layernorm_bf16(const float* x, int64_t in_stride, const float* g, const float* b,
-                          uint16_t* out, int64_t out_stride, int rows, int W, hipStream_t s);
+                          uint16_t* out, int64_t out_stride, int rows, int W, hipStream_t s,
+                          uint8_t* q = nullptr, uint8_t* qs = nullptr);
 // x[b*S + t] = LN((t == 0 ? cls : x[b*S + t]) + pos[t]) in place (f32)
 hipError_t vision_embed_ln(float* x, const float* cls, const float* pos, const float* g,
                            const float* b, int B, int S, int W, hipStream_t s);
@@ -48,13 +75,14 @@ hipError_t eot_gather_ln(const int32_t* tokens, const float* x, const uint16_t* 
                          const float* b, uint16_t* out, int Q, int S, int W, hipStream_t s);
 // row r = i*stride: xr = x[r] + delta[r] (bf16); if write_x: x[r] = xr; out[i] = LN(xr) bf16 [rows, W]
 hipError_t residual_ln(float* x, const uint16_t* delta, int64_t stride, int write_x, const float* g, const float* b,
-                       uint16_t* out, int rows, int W, hipStream_t s);
+                       uint16_t* out, int rows, int W, hipStream_t s, uint8_t* q = nullptr, uint8_t* qs = nullptr);
 // pixels [B,3,R,R] (f32 or bf16) -> patches [B*G*G, Kp] bf16, k = c*P*P + kh*P + kw, zero pad to Kp
 hipError_t im2col(const void* pixels, int in_bf16, uint16_t* out, int B, int R, int P, int Kp,
                   hipStream_t s);
 // multi-head attention over qkv [B*S, 3W] bf16 -> out [B*S, W] bf16, head dim 64
+// q8 != nullptr: MX-fp8 output (one 64-k block per head) instead of bf16 out
 hipError_t attention(const uint16_t* qkv, uint16_t* out, int B, int S, int W, int causal,
-                     hipStream_t s);
+                     hipStream_t s, uint8_t* q8 = nullptr, uint8_t* qs = nullptr);
 // y [rows, D] f32 -> out (f32/bf16/f16), optional L2 normalisation
 hipError_t finalize_rows(const float* y, void* out, int out_dtype, int rows, int D, int l2,
                          hipStream_t s);

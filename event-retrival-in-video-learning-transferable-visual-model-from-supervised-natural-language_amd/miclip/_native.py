@@ -16,7 +16,7 @@ from .config import CLIPConfig
 LIB_NAME = "libmiclip.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 
-MI_F32, MI_BF16, MI_F16 = 0, 1, 2
+MI_F32, MI_BF16, MI_F16, MI_FP8 = 0, 1, 2, 3
 MI_NAN_FIRST, MI_NAN_LAST = 0, 1
 MI_NORM_L2, MI_NORM_L2_GUARD, MI_NORM_NONE = 0, 1, 2
 MI_PREP_CLIP, MI_PREP_SQUASH = 0, 1

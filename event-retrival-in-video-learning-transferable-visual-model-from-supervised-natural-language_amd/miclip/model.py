@@ -35,8 +35,16 @@ class _Visual:
 class CLIP:
     """MI355X-native CLIP (ViT image tower + causal text tower)."""
 
-    def __init__(self, cfg: CLIPConfig, state_dict: dict, device="cuda", image_chunk=None, text_chunk=64):
+    def __init__(self, cfg: CLIPConfig, state_dict: dict, device="cuda", image_chunk=None, text_chunk=64,
+                 weights: str = "bf16"):
+        """``weights``: "bf16" (the parity mode) or "fp8" — the vision tower's
+        GEMMs on the block-scaled fp8 MFMA with MX-fp8 weights and activations
+        (BASELINE.json configs[4], "fp8 MFMA weights")."""
         import torch
+
+        if weights not in ("bf16", "fp8"):
+            raise N.MiClipError(f"weights must be 'bf16' or 'fp8', got {weights!r}")
+        self.weights = weights
 
         self.cfg = cfg
         self._sd = {k: np.ascontiguousarray(v, dtype=np.float32) for k, v in state_dict.items()}
@@ -66,7 +74,8 @@ class CLIP:
         blob = N.pack_weights(self._sd, self.cfg)
         arch = N.Arch.from_config(self.cfg)
         ctx = ctypes.c_void_p()
-        N.check(L.mi_clip_create(ctypes.byref(arch), blob.ctypes.data, blob.size, self.device.index, N.MI_BF16,
+        wdt = N.MI_FP8 if self.weights == "fp8" else N.MI_BF16
+        N.check(L.mi_clip_create(ctypes.byref(arch), blob.ctypes.data, blob.size, self.device.index, wdt,
                                  ctypes.byref(ctx)), "mi_clip_create")
         self._ctx = ctx
         N.check(L.mi_clip_reserve(self._ctx, self._chunks[0], self._chunks[1]), "mi_clip_reserve")

@@ -37,7 +37,7 @@ extern "C" {
 
 #define MICLIP_ABI_VERSION 1
 
-enum mi_dtype { MI_F32 = 0, MI_BF16 = 1, MI_F16 = 2 };
+enum mi_dtype { MI_F32 = 0, MI_BF16 = 1, MI_F16 = 2, MI_FP8 = 3 /* weights only: MX-fp8 vision GEMMs */ };
 enum mi_status { MI_OK = 0, MI_ERR_ARG = -1, MI_ERR_HIP = -2, MI_ERR_UNSUPPORTED = -3, MI_ERR_STATE = -4 };
 enum mi_nan_policy { MI_NAN_FIRST = 0, MI_NAN_LAST = 1 };
 /* corpus row normalisation inside the rank/score kernels */
@@ -82,8 +82,11 @@ int64_t mi_clip_weights_numel(const mi_clip_arch* arch);
  * (call sites Backend/embedding.py:22, Backend/services/embedding_service.py:86,106,
  * compare_models.py:316).  `weights` is a HOST float32 blob of
  * mi_clip_weights_numel(arch) elements; weights are converted to `weight_dtype`
- * (MI_BF16; MI_F32 is rejected until the fp32 parity GEMM lands) and uploaded to
- * `device`. */
+ * and uploaded to `device`: MI_BF16 (the parity mode), or MI_FP8 — the vision
+ * tower's four GEMMs per block run on the block-scaled fp8 MFMA with MX-fp8
+ * weights (e4m3 + e8m0 per 64 k) and MX-fp8 activations produced by the
+ * LayerNorm / attention / QuickGELU kernels (BASELINE.json configs[4]).
+ * MI_F32 is rejected. */
 int mi_clip_create(const mi_clip_arch* arch, const float* weights, int64_t numel,
                    int device, int weight_dtype, mi_clip** out);
 int mi_clip_destroy(mi_clip* ctx);

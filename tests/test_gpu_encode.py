@@ -78,6 +78,44 @@ def test_encode_l14_golden(gpu, name, fname):
     _check(txt, g["text"], f"{name} text")
 
 
+# weights="fp8": e4m3 (3 mantissa bits) weights AND activations with one e8m0
+# scale per 64 k.  Looser than the bf16 parity mode's COS_TOL by design; bf16
+# stays the parity mode, fp8 is BASELINE.json configs[4]'s throughput mode.
+FP8_COS = 2e-2
+
+
+@pytest.mark.parametrize("name,fname", [("test-small", None), ("ViT-B/32", "vit_b32.npz"),
+                                        ("ViT-L/14@336px", "vit_l14_336px.npz")])
+def test_encode_fp8_weights(gpu, name, fname):
+    """The vision tower on the block-scaled fp8 MFMA (MX-fp8 weights quantised
+    on the device at create, fp8 producers fused into LN / attention / c_fc)
+    vs the fp64 oracle / HF golden; the text tower stays bf16 and exact."""
+    import torch
+    from miclip import config, weights
+    from oracle import clip_ref
+    from oracle.clip_ref import cosine
+    cfg = config.get_config(name)
+    m = _model(name, gpu, image_chunk=3, text_chunk=2, weights="fp8")
+    if fname is None:
+        px = weights.synthetic_pixels(5, cfg.image_resolution)
+        ref = clip_ref.encode_image(px, state_dict(name), cfg, np.float64)
+    else:
+        g = golden(fname)
+        px = weights.synthetic_pixels(int(g["n_images"]), cfg.image_resolution)
+        ref = g["image"]
+        _check(m.encode_text(torch.from_numpy(g["tokens"])).cpu().numpy(), g["text"], f"{name} text (bf16 tower)")
+    img = m.encode_image(torch.from_numpy(px)).cpu().numpy()
+    cos = cosine(img, ref)
+    print(f"{name} fp8 image 1-cos max {1 - cos.min():.3e}")
+    assert np.all(cos > 1 - FP8_COS), cos
+
+
+def test_fp8_rejects_narrow_width(gpu):
+    from miclip import _native as N
+    with pytest.raises(N.MiClipError):
+        _model("test-tiny", gpu, weights="fp8")      # vision_width 128: MX GEMM N tiles are 256
+
+
 def test_encode_chunking_and_dtypes(gpu):
     """Batches larger than the internal chunk, bf16 input, fp16/bf16 output,
     in-kernel L2 normalisation: all consistent with the fp32 single-chunk run."""
