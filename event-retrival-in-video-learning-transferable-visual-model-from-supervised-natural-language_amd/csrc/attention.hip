@@ -1,0 +1,380 @@
+// Multi-head attention core of openai/CLIP's nn.MultiheadAttention
+// (softmax(q k^T / sqrt(64)) v per 64-wide head, causal mask for the text
+// tower), restated in oracle/clip_ref.py::_mha.  Built with -fno-honor-nans
+// (Makefile): the softmax max/sum chains then compile to v_max3 without NaN
+// canonicalisation; -inf masking is unaffected.
+#include "common.hpp"
+#include "internal.hpp"
+
+namespace miclip {
+
+namespace {
+// --------------------------------------------------------------- attention
+// One wave per (sequence, head), head dim 64, whole padded sequence (SP rows,
+// multiple of 32) per wave; no workgroup barriers.
+//   S = Q K^T : Q (A operand) and K (B operand) fragments are loaded straight
+//     from the packed qkv rows as 16-byte pieces (the 16x16x32 operand map
+//     wants 8 consecutive head dims of one row per lane), rows past S clamped;
+//   softmax over keys in f32 registers (scale 1/8, key >= S and causal masks),
+//     rows reduced across the 16 lanes that hold them; P normalised, to bf16,
+//     through a per-wave LDS tile (C layout -> operand layout);
+//   O^T = V^T P^T with V^T (A operand) from a per-wave transposed LDS image
+//     and P (B operand), so each lane holds 4 consecutive head dims of one
+//     query row -> one 8-byte store.
+// LDS rows are padded to an odd number of 16-byte slots.
+template <int SP>
+__global__ __launch_bounds__(64) void attention_kernel(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ out,
+                                                       int S, int W, int H, int causal, int items) {
+  constexpr int TS = SP + 8;  // bf16 per V^T / P row (odd number of 16-byte slots)
+  __shared__ __attribute__((aligned(16))) uint16_t lds[64 * TS + 16 * TS];
+  uint16_t* Vt = lds;
+  uint16_t* Pw = lds + 64 * TS;
+  const int item = blockIdx.x;
+  if (item >= items) return;
+  const int bseq = item / H, h = item % H;
+  const int lane = threadIdx.x;
+  const int64_t ld = 3 * (int64_t)W;
+  const uint16_t* qb = qkv + (int64_t)bseq * S * ld + h * 64;
+  const uint16_t* kb = qb + W;
+  const uint16_t* vb = qb + 2 * W;
+
+  // V^T image: lane (ch = lane>>3, r8 = lane&7) loads 8 head dims of key
+  // row r and scatters them down column r of V^T (consecutive lanes ->
+  // consecutive keys, so the 2-byte writes of an instruction are contiguous).
+  for (int r0 = 0; r0 < SP; r0 += 8) {
+    const int r = r0 + (lane & 7), ch = lane >> 3;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (r < S) v = *(const uint4*)(vb + (int64_t)r * ld + ch * 8);
+    const uint16_t* vv = (const uint16_t*)&v;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) Vt[(ch * 8 + e) * TS + r] = vv[e];
+  }
+
+  constexpr int NKT = SP / 16;
+  const float scale = 0.125f;  // 64 ** -0.5
+  const int fr = lane & 15, fk = 8 * (lane >> 4);
+  const int nqt = (S + 15) / 16;
+  for (int qt = 0; qt < nqt; ++qt) {
+    const int64_t qrow = min(qt * 16 + fr, S - 1);
+    bf16x8 qa[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) qa[s] = *(const bf16x8*)(qb + qrow * ld + 32 * s + fk);
+    f32x4 sc[NKT];
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+      const int64_t krow = min(kt * 16 + fr, S - 1);
+      f32x4 c = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 kf = *(const bf16x8*)(kb + krow * ld + 32 * s + fk);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa[s], kf, c, 0, 0, 0);
+      }
+      sc[kt] = c;
+    }
+    // sc[kt][j]: query row qt*16 + 4*(lane>>4) + j, key kt*16 + (lane&15)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = qt * 16 + 4 * (lane >> 4) + j;
+      float m = -INFINITY;
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt) {
+        const int key = kt * 16 + fr;
+        float v = sc[kt][j] * scale;
+        if (key >= S || (causal && key > row)) v = -INFINITY;
+        sc[kt][j] = v;
+        m = fmaxf(m, v);
+      }
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+      float sum = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt) {
+        const float p = __expf(sc[kt][j] - m);
+        sc[kt][j] = p;
+        sum += p;
+      }
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) sum += __shfl_xor(sum, o, 64);
+      const float inv = 1.0f / sum;
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt) Pw[(4 * (lane >> 4) + j) * TS + kt * 16 + fr] = f2bf_hw(sc[kt][j] * inv);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    // O^T[d][q] = sum_key V^T[d][key] P[q][key]
+    uint2 ov[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      f32x4 o = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < SP / 32; ++s) {
+        const bf16x8 va = *(const bf16x8*)(Vt + (dt * 16 + fr) * TS + 32 * s + fk);
+        const bf16x8 pb = *(const bf16x8*)(Pw + fr * TS + 32 * s + fk);
+        o = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pb, o, 0, 0, 0);
+      }
+      ov[dt] = make_uint2(pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3]));
+    }
+    // lane: query row qt*16 + (lane&15), head dims dt*16 + 4*(lane>>4) + 0..3
+    const int row = qt * 16 + fr;
+    if (row < S) {
+      uint16_t* dst = out + ((int64_t)bseq * S + row) * W + h * 64 + 4 * (lane >> 4);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) *(uint2*)(dst + dt * 16) = ov[dt];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// ------------------------------------ attention, long sequences, K/V in LDS
+// One workgroup of NW waves per (sequence, head); wave w owns the NT query
+// tiles w, w + NW, ... (16 rows each) for the whole key sweep, so every 64-key
+// chunk of K and V is fetched from HBM/L2 ONCE per (sequence, head) and shared
+// by all waves through a two-slot LDS ring (a wave-per-query-tile design
+// re-reads K per tile: 37 x the K bytes at 577 tokens, 1.8x slower).  Per chunk:
+//   stage   : each thread register-loads 16 B of K and of V of chunk c + 1
+//             (issued before chunk c's math, written to the other ring slot
+//             after it; one barrier per chunk).  K lands row-major (144-byte
+//             rows: the 16 rows of an A-operand read hit disjoint banks), V
+//             transposed (V^T rows of 64 keys, 136-byte rows).
+//   frags   : the chunk's K (A operand of S^T = K Q^T) and V^T (A operand of
+//             O^T = V^T P^T) fragments are read from LDS once per chunk into
+//             registers and reused by the wave's NT tiles.
+//   softmax : scores in the log2 domain u = s * log2(e)/8 (one FMA per score
+//             with the reference max folded in); the running max is only
+//             moved (and O, l rescaled) when the chunk max exceeds it by more
+//             than 2^8 - lazy rescaling: P <= 256, exact after the final 1/l;
+//             row max across the 4 lane groups by permlane16/32 swaps.
+// Keys >= S are masked (only in the last chunk, and 16-key tiles past S skip
+// their MFMAs; skipping their exponentials too measured 10% slower - the extra
+// uniform branches split the softmax block); V^T columns >= S are 0.
+template <int NT, int NW>
+__global__ __launch_bounds__(64 * NW) void attention_flash_kernel(const uint16_t* __restrict__ qkv,
+                                                                uint16_t* __restrict__ out, int S, int W, int H,
+                                                                int causal, uint8_t* __restrict__ q8,
+                                                                uint8_t* __restrict__ qs, int64_t rows_pad) {
+  constexpr int KS = 72, VS = 68;  // LDS row strides (bf16)
+  constexpr int PP = 512 / (64 * NW);  // 16-byte pieces of K (and of V) per thread per chunk
+  static_assert(PP * 64 * NW == 512, "NW must divide 8");
+  __shared__ __attribute__((aligned(16))) uint16_t Ks[2][64 * KS];
+  __shared__ __attribute__((aligned(16))) uint16_t Vs[2][64 * VS];
+  const int item = blockIdx.x;
+  const int bseq = item / H, h = item % H;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t ld = 3 * (int64_t)W;
+  const uint16_t* qb = qkv + (int64_t)bseq * S * ld + h * 64;
+  const uint16_t* kb = qb + W;
+  const uint16_t* vb = qb + 2 * W;
+  const int nch = (S + 63) / 64, nqt = (S + 15) / 16;
+  const int fr = lane & 15, g = lane >> 4, fk = 8 * g;
+  const float sl2 = 0.125f * 1.4426950408889634f;  // head_dim^-0.5 * log2(e)
+  constexpr float RESCALE = 8.0f;                  // lazy-rescale threshold (log2 units)
+
+  uint4 kr[PP], vr[PP];
+#define FA_STAGE_LOAD(c)                                                                  \
+  _Pragma("unroll") for (int i = 0; i < PP; ++i) {                                        \
+    const int p_ = tid + i * 64 * NW, r_ = (c) * 64 + (p_ >> 3), ch_ = p_ & 7;            \
+    kr[i] = make_uint4(0, 0, 0, 0);                                                       \
+    vr[i] = make_uint4(0, 0, 0, 0);                                                       \
+    if (r_ < S) {                                                                         \
+      kr[i] = *(const uint4*)(kb + (int64_t)r_ * ld + ch_ * 8);                           \
+      vr[i] = *(const uint4*)(vb + (int64_t)r_ * ld + ch_ * 8);                           \
+    }                                                                                     \
+  }
+#define FA_STAGE_WRITE(slot)                                                              \
+  _Pragma("unroll") for (int i = 0; i < PP; ++i) {                                        \
+    const int p_ = tid + i * 64 * NW, r_ = p_ >> 3, ch_ = p_ & 7;                         \
+    *(uint4*)(&Ks[slot][r_ * KS + ch_ * 8]) = kr[i];                                      \
+    const uint16_t* vv_ = (const uint16_t*)&vr[i];                                        \
+    _Pragma("unroll") for (int e = 0; e < 8; ++e) Vs[slot][(ch_ * 8 + e) * VS + r_] = vv_[e]; \
+  }
+
+  bf16x8 qf[NT][2];
+  float m[NT], l[NT];
+  f32x4 o[NT][4];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int qrow = min((wave + NW * t) * 16 + fr, S - 1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) qf[t][s] = *(const bf16x8*)(qb + (int64_t)qrow * ld + 32 * s + fk);
+    m[t] = -INFINITY;
+    l[t] = 0.f;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[t][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  FA_STAGE_LOAD(0);
+  FA_STAGE_WRITE(0);
+  __syncthreads();
+
+  for (int c = 0; c < nch; ++c) {
+    const int slot = c & 1;
+    if (c + 1 < nch) FA_STAGE_LOAD(c + 1);
+    const int kvalid = min(64, S - c * 64);  // keys of this chunk < S
+    bf16x8 kf[4][2], vf[4][2];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) kf[kt][s] = *(const bf16x8*)(&Ks[slot][(kt * 16 + fr) * KS + 32 * s + fk]);
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const uint16_t* vrow = &Vs[slot][(dt * 16 + fr) * VS + 32 * s + 4 * g];
+        const uint2 lo = *(const uint2*)vrow;
+        const uint2 hi = *(const uint2*)(vrow + 16);
+        vf[dt][s] = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+      }
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int qt = wave + NW * t;
+      if (qt >= nqt || (causal && c * 64 > qt * 16 + 15)) continue;  // wave-uniform
+      const int qrow = qt * 16 + fr;
+      f32x4 sc[4];
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        if (kt * 16 < kvalid) {
+#pragma unroll
+          for (int s = 0; s < 2; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kt][s], qf[t][s], acc, 0, 0, 0);
+        }
+        sc[kt] = acc;
+      }
+      // sc[kt][j]: query qrow, key c*64 + kt*16 + 4g + j
+      if (kvalid < 64 || (causal && (c + 1) * 64 > qt * 16)) {
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int key = c * 64 + kt * 16 + 4 * g + j;
+            if (key >= S || (causal && key > qrow)) sc[kt][j] = -INFINITY;
+          }
+      }
+      float cm = fmaxf(fmaxf(fmaxf(sc[0][0], sc[0][1]), fmaxf(sc[0][2], sc[0][3])),
+                       fmaxf(fmaxf(sc[1][0], sc[1][1]), fmaxf(sc[1][2], sc[1][3])));
+      cm = fmaxf(cm, fmaxf(fmaxf(fmaxf(sc[2][0], sc[2][1]), fmaxf(sc[2][2], sc[2][3])),
+                           fmaxf(fmaxf(sc[3][0], sc[3][1]), fmaxf(sc[3][2], sc[3][3]))));
+      {
+        const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(cm), __float_as_uint(cm), false, false);
+        cm = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+        const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(cm), __float_as_uint(cm), false, false);
+        cm = fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+      }
+      const float cmu = cm * sl2;  // finite: chunk 0 holds key 0 <= every row
+      if (cmu > m[t] + RESCALE) {
+        const float alpha = __builtin_amdgcn_exp2f(m[t] - cmu);
+        l[t] *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) o[t][dt] *= alpha;
+        m[t] = cmu;
+      }
+      const float mu = m[t];
+      float ps[4];
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sc[kt][j] = __builtin_amdgcn_exp2f(fmaf(sc[kt][j], sl2, -mu));
+        ps[kt] = (sc[kt][0] + sc[kt][1]) + (sc[kt][2] + sc[kt][3]);
+      }
+      l[t] += (ps[0] + ps[1]) + (ps[2] + ps[3]);
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        if (s == 1 && kvalid <= 32) break;  // keys past round32(S): P = 0, V^T = 0
+        bf16x8 pb;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          pb[j] = (__bf16)sc[2 * s][j];
+          pb[4 + j] = (__bf16)sc[2 * s + 1][j];
+        }
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) o[t][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[dt][s], pb, o[t][dt], 0, 0, 0);
+      }
+    }
+    if (c + 1 < nch) FA_STAGE_WRITE(slot ^ 1);
+    __syncthreads();
+  }
+#undef FA_STAGE_LOAD
+#undef FA_STAGE_WRITE
+
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int qt = wave + NW * t;
+    if (qt >= nqt) continue;
+    const int qrow = qt * 16 + fr;
+    float lt = l[t];
+    {
+      const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(lt), __float_as_uint(lt), false, false);
+      lt = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+      const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(lt), __float_as_uint(lt), false, false);
+      lt = __uint_as_float(b[0]) + __uint_as_float(b[1]);
+    }
+    const float inv = 1.0f / lt;
+    // o[t][dt][j]: query qrow, head dim dt*16 + 4g + j
+    if (q8) {  // MX-fp8 output: this head's 64 dims are one 64-k block of out_proj
+      float amax = 0.f;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) amax = fmaxf(amax, fabsf(o[t][dt][j] * inv));
+      amax = fmaxf(amax, __shfl_xor(amax, 16, 64));
+      amax = fmaxf(amax, __shfl_xor(amax, 32, 64));
+      const int X = mx_block_exp(amax);
+      const float scl = ldexpf(1.0f, -X);
+      if (qrow < S) {
+        const int64_t row = (int64_t)bseq * S + qrow;
+        uint8_t* dst = q8 + row * W + h * 64 + 4 * g;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+          *(uint32_t*)(dst + dt * 16) =
+              mx_pack4(o[t][dt][0] * inv, o[t][dt][1] * inv, o[t][dt][2] * inv, o[t][dt][3] * inv, scl);
+        if (g == 0) qs[mx_scale_index(row, h, rows_pad)] = (uint8_t)(X + 127);
+      }
+      continue;
+    }
+    if (qrow < S) {
+      uint16_t* dst = out + ((int64_t)bseq * S + qrow) * W + h * 64 + 4 * g;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+        *(uint2*)(dst + dt * 16) = make_uint2(pack_bf16x2(o[t][dt][0] * inv, o[t][dt][1] * inv),
+                                              pack_bf16x2(o[t][dt][2] * inv, o[t][dt][3] * inv));
+    }
+  }
+}
+
+}  // namespace
+
+hipError_t attention(const uint16_t* qkv, uint16_t* out, int B, int S, int W, int causal, hipStream_t s, uint8_t* q8,
+                     uint8_t* qs) {
+  const int H = W / 64;
+  const int items = B * H;
+  if (items <= 0) return hipSuccess;
+  if (S > 640) return hipErrorInvalidValue;
+  // Every length runs attention_flash_kernel (scripts/attn_micro.py, this
+  // round: B/32 S=50 177 vs 181 us for the one-wave kernel, text S=77 25.9 vs
+  // 30.0, L/14 408 vs 572 and L/14@336 547 vs 1004 for the per-query-tile-K
+  // kernel it replaced).  Causal bit 8 selects the one-wave kernel for S <= 96
+  // (A/B and parity tests of both paths; it has no fp8 output).
+  const bool one_wave = ((causal >> 8) & 1) && S <= 96 && !q8;
+  causal &= 1;
+  const dim3 grid(items);
+  if (one_wave) {
+    if (S <= 32) hipLaunchKernelGGL(attention_kernel<32>, grid, dim3(64), 0, s, qkv, out, S, W, H, causal, items);
+    else if (S <= 64) hipLaunchKernelGGL(attention_kernel<64>, grid, dim3(64), 0, s, qkv, out, S, W, H, causal, items);
+    else hipLaunchKernelGGL(attention_kernel<96>, grid, dim3(64), 0, s, qkv, out, S, W, H, causal, items);
+    return hipGetLastError();
+  }
+  // NT query tiles per wave x NW waves >= ceil(S / 16)
+  const int nqt = (S + 15) / 16;
+  const int64_t rp = ((int64_t)B * S + 1) & ~1;
+#define FLASH(NT, NW) \
+  hipLaunchKernelGGL((attention_flash_kernel<NT, NW>), grid, dim3(64 * NW), 0, s, qkv, out, S, W, H, causal, q8, qs, rp)
+  if (nqt <= 4) FLASH(1, 4);
+  else if (nqt <= 8) FLASH(1, 8);
+  else if (nqt <= 16) FLASH(2, 8);
+  else if (nqt <= 24) FLASH(3, 8);
+  else if (nqt <= 32) FLASH(4, 8);
+  else FLASH(5, 8);
+#undef FLASH
+  return hipGetLastError();
+}
+
+}  // namespace miclip

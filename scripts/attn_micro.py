@@ -1,6 +1,6 @@
 """Attention microbenchmark through mi_op_attention (random bf16 qkv, HIP events).
-Shapes: the bench chunk of each tower.  S <= 96 runs the one-wave LDS-P kernel by default and the
-flash kernel with causal bit 8.  usage: python scripts/attn_micro.py [reps]"""
+Shapes: the bench chunk of each tower.  Every S runs the flash kernel (K/V chunks in LDS) by default;
+causal bit 8 selects the one-wave LDS-P kernel for S <= 96.  usage: python scripts/attn_micro.py [reps] [shape,shape...]"""
 import os
 import sys
 
@@ -20,7 +20,10 @@ def main():
     L = N.lib()
     dev = torch.device("cuda:0")
     sp = torch.cuda.current_stream().cuda_stream
+    only = sys.argv[2].split(",") if len(sys.argv) > 2 else None
     for name, B, S, W, causal in SHAPES:
+        if only and name not in only:
+            continue
         qkv = (torch.randn(B * S, 3 * W, device=dev) * 1.5).bfloat16()
         outs = {}
         for mode in ([0, 0x100] if S <= 96 else [0]):
@@ -39,7 +42,8 @@ def main():
             fl = 4.0 * B * S * S * W * (0.5 if causal else 1.0)
             by = B * S * 4 * W * 2
             d = (out.float() - outs[0].float()).abs().max().item()
-            print(f"{name:9s} {'one-wave' if (S <= 96 and not mode) else 'flash'} B={B} S={S} W={W}: {us:8.1f} us "
+            kind = {0: "flash", 0x100: "one-wave"}[mode]
+            print(f"{name:9s} {kind:16s} B={B} S={S} W={W}: {us:8.1f} us "
                   f"{fl / us / 1e6:6.1f} TFLOP/s {by / us / 1e3:7.1f} GB/s  maxdiff {d:.3g}", flush=True)
 
 

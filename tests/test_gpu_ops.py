@@ -81,7 +81,7 @@ def test_layernorm(gpu, rows, W):
                                           # causal, chunk boundaries
                                           (2, 577, 1024, 0), (1, 300, 256, 1), (3, 130, 128, 0), (1, 640, 128, 1),
                                           (2, 97, 256, 0), (1, 128, 192, 1), (2, 385, 128, 0)])
-@pytest.mark.parametrize("flash", [0, 0x100])
+@pytest.mark.parametrize("flash", [0, 0x100])   # flash kernel (default) / one-wave kernel (S <= 96)
 def test_attention(gpu, B, S, W, causal, flash):
     import torch
     N_ = _lib()
@@ -109,3 +109,28 @@ def test_errors_are_raised(gpu):
     assert rc != 0 and b"N" in N_.lib().mi_last_error()
     with pytest.raises(N_.MiClipError):
         N_.check(rc, "gemm")
+
+
+@pytest.mark.parametrize("S", [577, 257, 130])
+def test_attention_growing_max(gpu, S):
+    """Scores whose row max keeps growing along the keys: every 64-key chunk
+    moves the running max by more than the lazy-rescale threshold (2^8), so
+    the rescale branch of attention_flash_kernel runs on each chunk."""
+    import torch
+    N_ = _lib()
+    B, W = 2, 256
+    g = torch.Generator(device="cpu").manual_seed(S)
+    qkv = torch.randn(B, S, 3, W // 64, 64, generator=g)
+    qkv[:, :, 0] = qkv[:, :, 0].abs() * 0.5 + 0.5                      # q > 0
+    ramp = torch.linspace(0.05, 4.0, S).reshape(1, S, 1, 1)
+    qkv[:, :, 1] = qkv[:, :, 1].abs() * ramp                           # k grows with the key index
+    qkv = qkv.reshape(B * S, 3 * W).bfloat16().to(gpu)
+    out = torch.empty(B * S, W, dtype=torch.bfloat16, device=gpu)
+    N_.check(N_.lib().mi_op_attention(qkv.data_ptr(), out.data_ptr(), B, S, W, 0, _stream()), "attention")
+    torch.cuda.synchronize()
+    H = W // 64
+    x = qkv.double().reshape(B, S, 3, H, 64)
+    q, k, v = (x[:, :, i].transpose(1, 2) for i in range(3))
+    ref = (torch.softmax(q @ k.transpose(-1, -2) * 0.125, -1) @ v).transpose(1, 2).reshape(B * S, W)
+    err = (out.double() - ref).abs().max().item()
+    assert err < 3e-2, err
