@@ -214,6 +214,249 @@ __global__ __launch_bounds__(512) void gemm_mx_kernel(GemmArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Ping-pong MX-fp8 GEMM (the default for K >= 192): gemm.hip's gemm_pp_kernel
+// schedule on the 32x32x64 block-scaled MFMA.  A stage is 64 k = 64 bytes per
+// row, so the LDS geometry is byte-for-byte the bf16 kernel's (512 rows x 64 B
+// = 32 KB per stage, 4-deep ring, LDS-DMA three stages ahead with counted
+// vmcnt, the {0,2,3,1} chunk XOR), and a stage's 8 MFMAs per wave (4 M x 2 N
+// blocks of 32x32, 2x the cycles of a bf16 32x32x16) fill the same 512
+// cycles as the bf16 kernel's 32 16x16x32 MFMAs: twice the FLOPs per staged
+// byte.  The two wave groups (waves 0-3 / 4-7, one of each per SIMD) run one
+// barrier apart, so one wave per SIMD issues MFMAs while its partner issues
+// its DMA share and fragment reads.
+//   operands (scripts/probes/mx32_layout.hip, .out.txt): lane l holds row
+//     (l & 31), k = 32 (l >> 5) .. +31 of the stage (chunks 2h, 2h+1 of the
+//     64-byte row); C element j of lane l is C[8 (j >> 2) + 4 (l >> 5) + (j & 3)][l & 31];
+//   scales: byte 0 of lane l < 32 scales row l over the whole 64 k -> the
+//     e8m0 of (row, stage) straight from the stage-major scale tensor.  The
+//     stage pair's 1 KB scale block (256 A + 256 W rows x 2 B) rides in a
+//     4-slot ring, one dword LDS-DMA per stage from waves 0-3.
+// The MFMA computes C^T (A operand = W fragment) so lane l holds output row
+// m = l & 31 and columns 8i + 4h .. +3 (h = l >> 5) of each 32-column block:
+// permlane32_swap pairs give 16-byte bf16 row stores (T21).
+__device__ __forceinline__ int pp_swz(int x) { return (0x1320 >> (4 * x)) & 0xF; }  // {0,2,3,1}
+
+// LDS reads the compiler does not see (gemm.hip lds_read_f4): with plain
+// loads from the shared array hipcc drains every in-flight LDS-DMA
+// (s_waitcnt vmcnt(0)) before the section's first read, serialising the
+// stage pipeline.  The section's lgkmcnt(0) + barrier covers the reads.
+__device__ __forceinline__ int lds_u8(const uint8_t* p) {
+  int v;
+  const uint32_t addr = (uint32_t)(uintptr_t)(const LDS_AS uint8_t*)p;
+  asm volatile("ds_read_u8 %0, %1" : "=v"(v) : "v"(addr));
+  return v;
+}
+
+// 32-byte operand fragment (two 16-byte chunks of one LDS row), read with
+// the same invisible-to-the-waitcnt-pass asm for the same reason
+__device__ __forceinline__ v8i lds_frag32(const char* p, int rd0, int rd1) {
+  typedef int v4i __attribute__((ext_vector_type(4)));
+  v4i lo, hi;
+  const uint32_t a0 = (uint32_t)(uintptr_t)(const LDS_AS char*)(p + rd0);
+  const uint32_t a1 = (uint32_t)(uintptr_t)(const LDS_AS char*)(p + rd1);
+  asm volatile("ds_read_b128 %0, %1" : "=v"(lo) : "v"(a0));
+  asm volatile("ds_read_b128 %0, %1" : "=v"(hi) : "v"(a1));
+  return v8i{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+template <int EPI>
+__global__ __launch_bounds__(512) void gemm_mxpp_kernel(GemmArgs a) {
+  typedef float f32x16 __attribute__((ext_vector_type(16)));
+  constexpr int BM = 256, BN = 256, WTM = 128, WTN = 64;
+  constexpr int SB = 64;                               // k bytes per stage
+  constexpr int RING = 4, LEAD = 3;
+  constexpr int A_BYTES = BM * SB, STAGE = (BM + BN) * SB;
+  constexpr int SC = 1024;                             // scale ring slot
+  __shared__ __attribute__((aligned(16))) char smem[RING * STAGE + RING * SC];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int grp = __builtin_amdgcn_readfirstlane(wave >> 2), wc = wave & 3;
+  const int tiles_n = a.N / BN;
+  const int tiles_m = (a.M + BM - 1) / BM;
+  const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
+  const int nk = a.K / SB;
+  const int m_pad = (a.M + 1) & ~1;
+  const uint8_t* A = (const uint8_t*)a.A;
+  const uint8_t* Wt = (const uint8_t*)a.W;
+
+  // DMA: instruction j (0, 1) of wave w moves rows (w*2 + j)*16 + (lane >> 2), 4 lanes x 16 B per row
+  const int lrow = lane >> 2;
+  const int lchunk = ((lane & 3) ^ pp_swz(lane >> 4)) * 16;
+  const uint8_t* asrc[2];
+  const uint8_t* wsrc[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    asrc[j] = A + (int64_t)min(m0 + (wave * 2 + j) * 16 + lrow, a.M - 1) * a.lda + lchunk;
+    wsrc[j] = Wt + (int64_t)(n0 + (wave * 2 + j) * 16 + lrow) * a.ldw + lchunk;
+  }
+  // scales (waves 0-3): waves 0-1 move A row pairs, 2-3 W row pairs (one dword = 2 rows x {kb even, odd})
+  const int spair = (wave & 1) * 64 + lane;
+  const uint8_t* ssrc = (wave & 2) ? a.w_scale + (int64_t)(n0 + 2 * spair) * 2
+                                   : a.a_scale + (int64_t)min(m0 + 2 * spair, m_pad - 2) * 2;
+  const int64_t sstage = (wave & 2) ? (int64_t)a.N * 2 : (int64_t)m_pad * 2;
+  auto issue = [&](int st) {
+    char* base = smem + (st % RING) * STAGE;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) glds16(asrc[j] + st * SB, base + (wave * 2 + j) * 1024);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) glds16(wsrc[j] + st * SB, base + A_BYTES + (wave * 2 + j) * 1024);
+    if (grp == 0) glds4(ssrc + (st >> 1) * sstage, smem + RING * STAGE + (st % RING) * SC + (wave & 3) * 256);
+  };
+  auto wait_stage = [&](int g1) {  // retire this wave's DMA for stage g1 (5 ops per stage in group 0, 4 in group 1)
+    const int younger = min(LEAD - 1, nk - 1 - g1);
+    if (grp == 0) {
+      if (younger >= 2) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+      else if (younger == 1) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      if (younger >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else if (younger == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  };
+  auto barrier = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto lgkm_barrier = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+#pragma unroll
+  for (int st = 0; st < LEAD; ++st)
+    if (st < nk) issue(st);
+  wait_stage(0);
+  barrier();
+  if (grp == 1) barrier();
+
+  const int lr = lane & 31, h = lane >> 5;
+  const int rd0 = lr * SB + (((2 * h) ^ pp_swz((lr >> 2) & 3)) * 16);
+  const int rd1 = lr * SB + (((2 * h + 1) ^ pp_swz((lr >> 2) & 3)) * 16);
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
+  v8i wf[2], af[4];
+  int sw[2], sa[4];
+  for (int g = 0; g < nk; ++g) {
+    const char* As = smem + (g % RING) * STAGE + (grp * WTM) * SB;
+    const char* Ws = smem + (g % RING) * STAGE + A_BYTES + (wc * WTN) * SB;
+    const uint8_t* Sc = (const uint8_t*)(smem + RING * STAGE + (g % RING) * SC) + (g & 1);
+    // ---- L: DMA share of stage g+3, this stage's fragments and scales
+    if (g + LEAD < nk) issue(g + LEAD);
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni) {
+      wf[ni] = lds_frag32(Ws + ni * 32 * SB, rd0, rd1);
+      sw[ni] = lds_u8(Sc + 512 + (wc * WTN + ni * 32 + lr) * 2);
+    }
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) {
+      af[mi] = lds_frag32(As + mi * 32 * SB, rd0, rd1);
+      sa[mi] = lds_u8(Sc + (grp * WTM + mi * 32 + lr) * 2);
+    }
+    if (grp == 1 && g + 1 < nk) wait_stage(g + 1);
+    lgkm_barrier();
+    // ---- C: 8 MFMAs (4 M x 2 N blocks of 32x32x64)
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni)
+        acc[mi][ni] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(wf[ni], af[mi], acc[mi][ni], 0, 0, 0, sw[ni], 0,
+                                                                      sa[mi]);
+    if (grp == 0 && g + 1 < nk) wait_stage(g + 1);
+    barrier();
+  }
+  if (grp == 0) barrier();
+
+  // ------------------------------------------------ epilogue (no LDS, no barrier)
+  // lane: output row m0 + grp*128 + mi*32 + lr; element j of block (mi, ni) is
+  // column n0 + wc*64 + ni*32 + 8 (j >> 2) + 4h + (j & 3)
+  float4 bias[2][4];
+#pragma unroll
+  for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int n = n0 + wc * WTN + ni * 32 + 8 * i + 4 * h;
+      bias[ni][i] = a.bias ? *(const float4*)(a.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  auto val = [&](int mi, int ni, int j) -> float {
+    const float4 b = bias[ni][j >> 2];
+    const float bb = (j & 3) == 0 ? b.x : (j & 3) == 1 ? b.y : (j & 3) == 2 ? b.z : b.w;
+    const float v = acc[mi][ni][j] + bb;
+    return (EPI == EPI_GELU_BF16 || EPI == EPI_GELU_MX) ? mx_gelu(v) : v;
+  };
+  if (EPI == EPI_GELU_MX) {
+    // fp8 output for the next MX GEMM: the wave's 64 columns of a row are one
+    // 64-k block of the consumer; this lane holds 32 of them, its partner
+    // (lane ^ 32) the other 32
+    const int blk = (n0 + wc * WTN) >> 6;
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) {
+      const int m = m0 + grp * WTM + mi * 32 + lr;
+      float v[2][16];
+      float amax = 0.f;
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          v[ni][j] = val(mi, ni, j);
+          amax = fmaxf(amax, fabsf(v[ni][j]));
+        }
+      const auto sx = __builtin_amdgcn_permlane32_swap(__float_as_uint(amax), __float_as_uint(amax), false, false);
+      amax = fmaxf(__uint_as_float(sx[0]), __uint_as_float(sx[1]));
+      const int X = mx_block_exp(amax);
+      const float inv = ldexpf(1.0f, -X);
+      if (m < a.M) {
+        uint8_t* o = (uint8_t*)a.out + (int64_t)m * a.ldo + n0 + wc * WTN + 4 * h;
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            *(uint32_t*)(o + ni * 32 + 8 * i) =
+                mx_pack4(v[ni][4 * i], v[ni][4 * i + 1], v[ni][4 * i + 2], v[ni][4 * i + 3], inv);
+        if (h == 0) a.o_scale[mx_scale_index(m, blk, m_pad)] = (uint8_t)(X + 127);
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi) {
+    const int m = m0 + grp * WTM + mi * 32 + lr;
+    if (EPI == EPI_F32) {
+      if (m < a.M)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            *(float4*)((float*)a.out + (int64_t)m * a.ldo + n0 + wc * WTN + ni * 32 + 8 * i + 4 * h) =
+                make_float4(val(mi, ni, 4 * i), val(mi, ni, 4 * i + 1), val(mi, ni, 4 * i + 2), val(mi, ni, 4 * i + 3));
+      continue;
+    }
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+      for (int ip = 0; ip < 2; ++ip) {
+        // groups 2ip (cols 16ip + 4h ..) and 2ip+1 (cols 16ip + 8 + 4h ..): after the
+        // half swap lanes 0-31 hold cols 16ip .. +7, lanes 32-63 cols 16ip + 8 .. +15
+        const int j0 = 8 * ip, j1 = 8 * ip + 4;
+        const uint32_t ax = pack_bf16x2(val(mi, ni, j0), val(mi, ni, j0 + 1));
+        const uint32_t ay = pack_bf16x2(val(mi, ni, j0 + 2), val(mi, ni, j0 + 3));
+        const uint32_t bx = pack_bf16x2(val(mi, ni, j1), val(mi, ni, j1 + 1));
+        const uint32_t by = pack_bf16x2(val(mi, ni, j1 + 2), val(mi, ni, j1 + 3));
+        const auto sx = __builtin_amdgcn_permlane32_swap(ax, bx, false, false);
+        const auto sy = __builtin_amdgcn_permlane32_swap(ay, by, false, false);
+        if (m < a.M)
+          *(uint4*)((uint16_t*)a.out + (int64_t)m * a.ldo + n0 + wc * WTN + ni * 32 + 16 * ip + 8 * h) =
+              make_uint4(sx[0], sy[0], sx[1], sy[1]);
+      }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // bf16 -> MX-fp8 (OCP e4m3 + one e8m0 scale per 64 consecutive k): one lane
 // per 64-element block.  Shared exponent X = floor(log2(amax)) - 8 (e4m3's
 // largest exponent), element = RNE e4m3 of v * 2^-X, saturated to +-448;
@@ -260,6 +503,21 @@ hipError_t gemm_mx(const GemmArgs& a, int epi, hipStream_t s) {
   if (a.K % MX_BK || a.N % 256 || a.K <= 0 || !a.a_scale || !a.w_scale) return hipErrorInvalidValue;
   if ((a.lda % 16) || (a.ldw % 16) || (a.ldo % 8) || ((uintptr_t)a.out & 15)) return hipErrorInvalidValue;
   const int nt = ((a.M + 255) / 256) * (a.N / 256);
+  // default: the ping-pong 32x32x64 kernel (needs K / 64 >= 3 stages);
+  // MICLIP_GEMM_VARIANT=1: the double-buffered 16x16x128 kernel (A/B)
+  if (a.variant != 1 && a.K / 64 >= 3) {
+    switch (epi) {
+      case EPI_BF16: hipLaunchKernelGGL(gemm_mxpp_kernel<EPI_BF16>, dim3(nt), dim3(512), 0, s, a); break;
+      case EPI_GELU_BF16: hipLaunchKernelGGL(gemm_mxpp_kernel<EPI_GELU_BF16>, dim3(nt), dim3(512), 0, s, a); break;
+      case EPI_F32: hipLaunchKernelGGL(gemm_mxpp_kernel<EPI_F32>, dim3(nt), dim3(512), 0, s, a); break;
+      case EPI_GELU_MX:
+        if (!a.o_scale) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(gemm_mxpp_kernel<EPI_GELU_MX>, dim3(nt), dim3(512), 0, s, a);
+        break;
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
   switch (epi) {
     case EPI_BF16: hipLaunchKernelGGL(gemm_mx_kernel<EPI_BF16>, dim3(nt), dim3(512), 0, s, a); break;
     case EPI_GELU_BF16: hipLaunchKernelGGL(gemm_mx_kernel<EPI_GELU_BF16>, dim3(nt), dim3(512), 0, s, a); break;

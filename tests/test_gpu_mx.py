@@ -84,3 +84,29 @@ def test_gemm_mx_asymmetric_identity(gpu):
                                     out.data_ptr(), M, N, K, 3, _stream()), "gemm_mx")
     torch.cuda.synchronize()
     assert torch.equal(out.cpu(), w.float().t().contiguous())
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 256, 512), (517, 768, 1024)])
+def test_gemm_mx_block_scales(gpu, M, N, K):
+    """Magnitudes spanning 2^-12..2^12 across rows AND 64-k blocks: every
+    (row, k-block) scale byte must reach the MFMA lane that owns it."""
+    import torch
+    N_ = _lib()
+    g = torch.Generator(device="cpu").manual_seed(M * 7 + K)
+    rs = 2.0 ** torch.randint(-6, 7, (M, 1), generator=g).float()
+    ks = 2.0 ** torch.randint(-6, 7, (1, K // 64), generator=g).float().repeat_interleave(64, 1)
+    a = (torch.randn(M, K, generator=g) * rs * ks).bfloat16()
+    ws = 2.0 ** torch.randint(-6, 7, (N, K // 64), generator=g).float().repeat_interleave(64, 1)
+    w = (torch.randn(N, K, generator=g) * ws * K ** -0.5).bfloat16()
+    qa, sa = _quant_gpu(a.to(gpu))
+    qw, sw = _quant_gpu(w.to(gpu))
+    out = torch.empty(M, N, device=gpu)
+    N_.check(N_.lib().mi_op_gemm_mx(qa.data_ptr(), sa.data_ptr(), qw.data_ptr(), sw.data_ptr(), None,
+                                    out.data_ptr(), M, N, K, 3, _stream()), "gemm_mx")
+    torch.cuda.synchronize()
+    sa_, sw_ = (mx_ref.from_stage_major(x.cpu().numpy(), r, K) for x, r in ((sa, M), (sw, N)))
+    ref = mx_ref.gemm(qa.cpu().numpy(), sa_, qw.cpu().numpy(), sw_)
+    got = out.double().cpu().numpy()
+    # per-row tolerance: rows differ by 2^12 in scale
+    err = np.abs(got - ref).max(1) / np.maximum(np.abs(ref).max(1), 1e-30)
+    assert err.max() < 1e-4, err.max()
