@@ -234,7 +234,7 @@ def main():
     chunk = args.image_chunk
     if chunk is None:  # equal-size passes (so every GEMM launch has one shape)
         from miclip.config import get_config
-        base = max(8, 100_000 // get_config(args.model).vision_tokens)
+        base = max(8, 250_000 // get_config(args.model).vision_tokens)
         chunk = -(-args.frames // -(-args.frames // base))
     model, _ = api.load(args.model, device=dev, image_chunk=chunk, weights=args.weights)
     cfg = model.cfg

@@ -148,7 +148,10 @@ __global__ __launch_bounds__(64) void attention_kernel(const uint16_t* __restric
 // Keys >= S are masked (only in the last chunk, and 16-key tiles past S skip
 // their MFMAs; skipping their exponentials too measured 10% slower - the extra
 // uniform branches split the softmax block); V^T columns >= S are 0.
-template <int NT, int NW>
+// SLOTS = 1: S <= 64 (one chunk; B/32's 50 tokens): a single LDS slot and no
+// look-ahead staging, which halves the LDS footprint and frees the staging
+// registers, so more workgroups fit per CU for this latency-bound case.
+template <int NT, int NW, int SLOTS = 2>
 __global__ __launch_bounds__(64 * NW) void attention_flash_kernel(const uint16_t* __restrict__ qkv,
                                                                 uint16_t* __restrict__ out, int S, int W, int H,
                                                                 int causal, uint8_t* __restrict__ q8,
@@ -156,8 +159,8 @@ __global__ __launch_bounds__(64 * NW) void attention_flash_kernel(const uint16_t
   constexpr int KS = 72, VS = 68;  // LDS row strides (bf16)
   constexpr int PP = 512 / (64 * NW);  // 16-byte pieces of K (and of V) per thread per chunk
   static_assert(PP * 64 * NW == 512, "NW must divide 8");
-  __shared__ __attribute__((aligned(16))) uint16_t Ks[2][64 * KS];
-  __shared__ __attribute__((aligned(16))) uint16_t Vs[2][64 * VS];
+  __shared__ __attribute__((aligned(16))) uint16_t Ks[SLOTS][64 * KS];
+  __shared__ __attribute__((aligned(16))) uint16_t Vs[SLOTS][64 * VS];
   const int item = blockIdx.x;
   const int bseq = item / H, h = item % H;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -207,8 +210,8 @@ __global__ __launch_bounds__(64 * NW) void attention_flash_kernel(const uint16_t
   __syncthreads();
 
   for (int c = 0; c < nch; ++c) {
-    const int slot = c & 1;
-    if (c + 1 < nch) FA_STAGE_LOAD(c + 1);
+    const int slot = SLOTS == 1 ? 0 : (c & 1);
+    if (SLOTS > 1 && c + 1 < nch) FA_STAGE_LOAD(c + 1);
     const int kvalid = min(64, S - c * 64);  // keys of this chunk < S
     bf16x8 kf[4][2], vf[4][2];
 #pragma unroll
@@ -289,7 +292,7 @@ __global__ __launch_bounds__(64 * NW) void attention_flash_kernel(const uint16_t
         for (int dt = 0; dt < 4; ++dt) o[t][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[dt][s], pb, o[t][dt], 0, 0, 0);
       }
     }
-    if (c + 1 < nch) FA_STAGE_WRITE(slot ^ 1);
+    if (SLOTS > 1 && c + 1 < nch) FA_STAGE_WRITE(slot ^ 1);
     __syncthreads();
   }
 #undef FA_STAGE_LOAD
@@ -367,7 +370,8 @@ hipError_t attention(const uint16_t* qkv, uint16_t* out, int B, int S, int W, in
   const int64_t rp = ((int64_t)B * S + 1) & ~1;
 #define FLASH(NT, NW) \
   hipLaunchKernelGGL((attention_flash_kernel<NT, NW>), grid, dim3(64 * NW), 0, s, qkv, out, S, W, H, causal, q8, qs, rp)
-  if (nqt <= 4) FLASH(1, 4);
+  if (nqt <= 4)
+    hipLaunchKernelGGL((attention_flash_kernel<1, 4, 1>), grid, dim3(256), 0, s, qkv, out, S, W, H, causal, q8, qs, rp);
   else if (nqt <= 8) FLASH(1, 8);
   else if (nqt <= 16) FLASH(2, 8);
   else if (nqt <= 24) FLASH(3, 8);

@@ -61,9 +61,11 @@ class CLIP:
         self._out_dtype = torch.float32
         self._lock = threading.Lock()
         if image_chunk is None:
-            # ~100k token rows per pass: enough 256x256 GEMM tiles for 256 CUs
-            # even at N = 768 (391 x 3), measured best with 20k-100k rows
-            image_chunk = max(8, 100_000 // cfg.vision_tokens)
+            # ~250k token rows per pass: the GEMMs' last wave of 256x256 tiles
+            # is a small fraction of the launch (at 100k rows the N = 768
+            # GEMMs ran 1173 tiles = 4.6 rounds of 256 CUs); B/32 measured
+            # +1.9 % at 5000-10000 frames per pass against 2000
+            image_chunk = max(8, 250_000 // cfg.vision_tokens)
         self._chunks = (int(image_chunk), int(text_chunk))
         self._ctx = None
         self._build()

@@ -21,6 +21,11 @@ SHAPES = {
     "out": (100000, 768, 768, 0),
     "fc": (100000, 3072, 768, 1),
     "proj": (100000, 768, 3072, 0),
+    # the bench's default pass since round 1's chunk change: 5000 frames = 250k rows
+    "qkv250": (250000, 2304, 768, 0),
+    "out250": (250000, 768, 768, 0),
+    "fc250": (250000, 3072, 768, 1),
+    "proj250": (250000, 768, 3072, 0),
     "long": (16384, 4096, 4096, 0),
     "qkv20k": (20000, 2304, 768, 0),
     "fc20k": (20000, 3072, 768, 1),
