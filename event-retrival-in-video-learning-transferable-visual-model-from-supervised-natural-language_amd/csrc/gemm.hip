@@ -494,6 +494,189 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Persistent ping-pong (variant 18, bf16 outputs): gemm_pp_kernel's schedule
+// (CL = 1) with one workgroup per CU walking its tiles, so a tile's epilogue
+// overlaps the next tile's prologue and store drain:
+//   end of tile: realign the wave groups, issue the NEXT tile's first LEAD
+//   stages (all reads of the ring are done), then the direct-store epilogue of
+//   this tile.  The 16 stores per wave are younger than those three stages and
+//   older than every later one, so the counted waits of the next tile add the
+//   stores only while waiting for stages < LEAD; the first wait that has to
+//   cover them is stage LEAD's, three stages (~3k cycles) after they issued.
+//   A partial last m-tile (lanes with m >= M skip their stores) drains with
+//   vmcnt(0) instead, since its store count is not the fixed 16.
+//   A tile's bias is loaded (inline asm, so hipcc inserts no wait for it)
+//   just before that tile's first stages are issued: older than all of them,
+//   it has landed once the tile's first stage wait returns, and the epilogue
+//   issues no vector-memory load behind the prefetch (a plain load made hipcc
+//   drain the prefetch with vmcnt(0) before the epilogue).
+__device__ __forceinline__ void vm_wait_n(int n) {  // n wave-uniform; unlisted values wait for everything
+  switch (n) {
+    case 24: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
+    case 20: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
+    case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+__device__ __forceinline__ float4 bias_load_async(const float* p) {
+  float4 v;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+
+template <int EPI>
+__global__ __launch_bounds__(512) void gemm_ppp_kernel(GemmArgs a) {
+  constexpr int BM = 256, BN = 256;
+  constexpr int WTM = 128, WTN = 64;
+  constexpr int A_BYTES = BM * BK * 2, STAGE_BYTES = (BM + BN) * BK * 2;
+  constexpr int NSTORE = 16;  // epilogue store instructions per wave of a full tile
+  __shared__ __attribute__((aligned(16))) char smem[RING * STAGE_BYTES];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int grp = __builtin_amdgcn_readfirstlane(wave >> 2), wc = wave & 3;
+  const int tiles_n = a.N / BN;
+  const int tiles_m = (a.M + BM - 1) / BM;
+  const int ntiles = tiles_m * tiles_n;
+  const int nk = a.K / BK;
+  int vb = blockIdx.x;
+  int m0, n0;
+  auto coords = [&](int v, int& mm, int& nn) {
+    const int t = xcd_remap(v, ntiles);  // grid % 8 == 0 keeps a WG's tiles on its XCD's contiguous run
+    mm = (t / tiles_n) * BM;
+    nn = (t % tiles_n) * BN;
+  };
+  coords(vb, m0, n0);
+
+  const int lrow = lane >> 2;
+  const int lchunk = ((lane & 3) ^ swz(lane >> 4)) * 8;
+  const uint16_t* asrc[2];
+  const uint16_t* wsrc[2];
+  auto set_src = [&](int mm, int nn) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      asrc[j] = a.A + (int64_t)min(mm + (wave * 2 + j) * 16 + lrow, a.M - 1) * a.lda + lchunk;
+      wsrc[j] = a.W + (int64_t)(nn + (wave * 2 + j) * 16 + lrow) * a.ldw + lchunk;
+    }
+  };
+  auto issue = [&](int st) {
+    char* base = smem + (st % RING) * STAGE_BYTES;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      glds16(asrc[j] + st * BK, base + (wave * 2 + j) * 1024);
+      glds16(wsrc[j] + st * BK, base + A_BYTES + (wave * 2 + j) * 1024);
+    }
+  };
+  int pend = 0;  // the previous tile's stores are in flight, younger than stages 0..LEAD-1
+  auto wait_stage = [&](int g1) {
+    const int younger = min(LEAD - 1, nk - 1 - g1);
+    vm_wait_n(4 * younger + (g1 < LEAD ? pend : 0));
+  };
+  auto barrier = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto lgkm_barrier = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  const int g = lane >> 4;
+  float4 bias[4];
+  auto load_bias = [&](float4 (&b)[4], int nn) {
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni)
+      b[ni] = a.bias ? bias_load_async(a.bias + nn + wc * WTN + ni * 16 + 4 * g) : make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  load_bias(bias, n0);
+  set_src(m0, n0);
+#pragma unroll
+  for (int st = 0; st < LEAD; ++st)
+    if (st < nk) issue(st);
+  const int rd = (lane & 15) * 64 + (((lane >> 4) ^ swz((lane >> 2) & 3)) * 16);
+  while (true) {
+    wait_stage(0);
+    barrier();
+    if (grp == 1) barrier();
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 bfr[4], af[8];
+    for (int gs = 0; gs < nk; ++gs) {
+      const char* As = smem + (gs % RING) * STAGE_BYTES + (grp * WTM) * 64;
+      const char* Ws = smem + (gs % RING) * STAGE_BYTES + A_BYTES + (wc * WTN) * 64;
+      if (gs + LEAD < nk) issue(gs + LEAD);
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) bfr[ni] = *(const bf16x8*)(Ws + ni * 16 * 64 + rd);
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi) af[mi] = *(const bf16x8*)(As + mi * 16 * 64 + rd);
+      if (grp == 1 && gs + 1 < nk) wait_stage(gs + 1);
+      lgkm_barrier();
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[ni], af[mi], acc[mi][ni], 0, 0, 0);
+      if (grp == 0 && gs + 1 < nk) wait_stage(gs + 1);
+      barrier();
+    }
+    if (grp == 0) barrier();  // groups realigned; every ring read of this tile is done
+
+    // next tile's first stages go out before this tile's stores
+    const int cm0 = m0, cn0 = n0;
+    vb += gridDim.x;
+    const bool has_next = vb < ntiles;
+    float4 nbias[4];
+    if (has_next) {
+      coords(vb, m0, n0);
+      load_bias(nbias, n0);
+      set_src(m0, n0);
+#pragma unroll
+      for (int st = 0; st < LEAD; ++st)
+        if (st < nk) issue(st);
+    }
+    // ---- epilogue of tile (cm0, cn0): direct permlane-swapped row stores (gemm_pp_kernel DIRECT)
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi) {
+      const int m = cm0 + grp * WTM + mi * 16 + (lane & 15);
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        uint2 pk[2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int ni = 2 * p + q;
+          float v0 = acc[mi][ni][0] + bias[ni].x, v1 = acc[mi][ni][1] + bias[ni].y;
+          float v2 = acc[mi][ni][2] + bias[ni].z, v3 = acc[mi][ni][3] + bias[ni].w;
+          if (EPI == EPI_GELU_BF16) {
+            v0 = quick_gelu(v0); v1 = quick_gelu(v1); v2 = quick_gelu(v2); v3 = quick_gelu(v3);
+          }
+          pk[q] = make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
+        }
+        const auto sx = __builtin_amdgcn_permlane16_swap(pk[0].x, pk[1].x, false, false);
+        const auto sy = __builtin_amdgcn_permlane16_swap(pk[0].y, pk[1].y, false, false);
+        const int col = cn0 + wc * WTN + (2 * p + (g & 1)) * 16 + (g >> 1) * 8;
+        if (m < a.M) *(uint4*)((uint16_t*)a.out + (int64_t)m * a.ldo + col) = make_uint4(sx[0], sy[0], sx[1], sy[1]);
+      }
+    }
+    if (!has_next) break;
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) bias[ni] = nbias[ni];
+    if (cm0 + BM <= a.M) {
+      pend = NSTORE;
+    } else {  // partial tile: an unknown number of stores issued
+      pend = 0;
+      vm_wait_all();
+    }
+  }
+}
+
 int cu_count() {
   static int n = 0;
   if (!n) {
@@ -520,15 +703,25 @@ template <int EPI>
 hipError_t launch(const GemmArgs& a, hipStream_t s) {
   const bool big = a.N % 256 == 0 && a.M >= 1024;
   // variant 0 (default): ping-pong, one 32-MFMA cluster per stage, direct
-  // permlane-swapped row stores for bf16 outputs (16) / LDS-staged rows for f32
-  // (3) — the fastest on every tower shape measured (scripts/gemm_micro.py);
+  // permlane-swapped row stores for bf16 outputs (16, or its persistent form
+  // 18 on wide N) / LDS-staged rows for f32 (3) (scripts/gemm_micro.py);
   // 1 = persistent ring; 8 = main-loop-only timing probe (no epilogue).
   const bool bf16_out = EPI == EPI_BF16 || EPI == EPI_GELU_BF16;
-  int v = a.variant == 0 ? (bf16_out ? 16 : 3) : a.variant;
+  // default for bf16 outputs: the persistent ping-pong (18) on wide GEMMs (N >= 2048:
+  // qkv, c_fc; +1.7-3 % in scripts/gemm_micro.py), the one-tile-per-workgroup
+  // ping-pong (16) on N = 768 (the persistent kernel's static tile split lost
+  // 1-3.5 % there against the dispatcher's dynamic one)
+  int v = a.variant == 0 ? (bf16_out ? (a.N >= 2048 && !a.group ? 18 : 16) : 3) : a.variant;
   if (v == 16 && !bf16_out) v = 3;
   if (big && v == 16 && a.K / BK >= LEAD) {
     const int nt = ((a.M + 255) / 256) * (a.N / 256);
     hipLaunchKernelGGL((gemm_pp_kernel<EPI, 1, false, true>), dim3(nt), dim3(512), 0, s, a);
+    return hipGetLastError();
+  }
+  if (big && v == 18 && bf16_out && a.K / BK >= LEAD && !a.group) {  // persistent ping-pong
+    const int nt = ((a.M + 255) / 256) * (a.N / 256);
+    const int grid = nt < cu_count() ? nt : cu_count();
+    hipLaunchKernelGGL((gemm_ppp_kernel<EPI>), dim3(grid), dim3(512), 0, s, a);
     return hipGetLastError();
   }
   if (big && v == 17 && bf16_out && a.K / BK >= LEAD) {  // experiment: non-temporal output stores
