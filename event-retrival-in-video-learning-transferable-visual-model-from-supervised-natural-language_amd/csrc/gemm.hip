@@ -253,6 +253,15 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_kernel(GemmArgs a
 // the end of L_b(g).  WAR: stage g+3 is issued in L sections of stage g, after
 // every read of the buffer it overwrites (stage g-1, last read by group 1 in
 // L_b(g-1), which ends with lgkmcnt(0) + barrier).
+// Bias load the compiler does not see: issued before a tile's first LDS-DMA it
+// has landed once the first stage wait returns, so the epilogue does not wait
+// on a fresh global load (hipcc would insert vmcnt(0) there).
+__device__ __forceinline__ float4 bias_load_async(const float* p) {
+  float4 v;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+
 template <int EPI, int CL, bool PRIO, bool DIRECT = false, bool NTS = false>
 __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs a) {
   constexpr int BM = 256, BN = 256, NT = 512;
@@ -306,6 +315,12 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs a) {
     __builtin_amdgcn_sched_barrier(0);
   };
 
+  float4 bias[4];
+#pragma unroll
+  for (int ni = 0; ni < 4; ++ni) {
+    const int n = n0 + wc * WTN + ni * 16 + 4 * (lane >> 4);
+    bias[ni] = a.bias ? bias_load_async(a.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
 #pragma unroll
   for (int s = 0; s < LEAD; ++s)
     if (s < nk) { issue_half(s, 0); issue_half(s, 1); }
@@ -385,12 +400,6 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs a) {
 
   // ------------------------------------------------ epilogue
   const int wr = grp;
-  float4 bias[4];
-#pragma unroll
-  for (int ni = 0; ni < 4; ++ni) {
-    const int n = n0 + wc * WTN + ni * 16 + 4 * (lane >> 4);
-    bias[ni] = a.bias ? *(const float4*)(a.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
-  }
   auto out_row = [&](int m) -> int64_t {
     return a.group ? (int64_t)(m / a.group) * a.gstride + a.goffset + m % a.group : (int64_t)m;
   };
@@ -520,12 +529,6 @@ __device__ __forceinline__ void vm_wait_n(int n) {  // n wave-uniform; unlisted 
     case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
     default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
   }
-}
-
-__device__ __forceinline__ float4 bias_load_async(const float* p) {
-  float4 v;
-  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
-  return v;
 }
 
 template <int EPI>
