@@ -218,15 +218,21 @@ __global__ __launch_bounds__(64 * NW) void attention_flash_kernel(const uint16_t
     for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
       for (int s = 0; s < 2; ++s) kf[kt][s] = *(const bf16x8*)(&Ks[slot][(kt * 16 + fr) * KS + 32 * s + fk]);
+    auto read_vf = [&]() {
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
+      for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const uint16_t* vrow = &Vs[slot][(dt * 16 + fr) * VS + 32 * s + 4 * g];
-        const uint2 lo = *(const uint2*)vrow;
-        const uint2 hi = *(const uint2*)(vrow + 16);
-        vf[dt][s] = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
-      }
+        for (int s = 0; s < 2; ++s) {
+          const uint16_t* vrow = &Vs[slot][(dt * 16 + fr) * VS + 32 * s + 4 * g];
+          const uint2 lo = *(const uint2*)vrow;
+          const uint2 hi = *(const uint2*)(vrow + 16);
+          vf[dt][s] = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+        }
+    };
+    // NT > 1: V^T fragments read once per chunk for all tiles; single-tile
+    // (S <= 64) instance: read after the softmax, so K and V^T fragments are
+    // never live together (fewer VGPRs -> more resident workgroups)
+    if (SLOTS > 1) read_vf();
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const int qt = wave + NW * t;
@@ -279,6 +285,10 @@ __global__ __launch_bounds__(64 * NW) void attention_flash_kernel(const uint16_t
         ps[kt] = (sc[kt][0] + sc[kt][1]) + (sc[kt][2] + sc[kt][3]);
       }
       l[t] += (ps[0] + ps[1]) + (ps[2] + ps[3]);
+      if (SLOTS == 1) {
+        __builtin_amdgcn_sched_barrier(0);
+        read_vf();
+      }
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         if (s == 1 && kvalid <= 32) break;  // keys past round32(S): P = 0, V^T = 0
