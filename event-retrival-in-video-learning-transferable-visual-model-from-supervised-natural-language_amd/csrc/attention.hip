@@ -151,14 +151,16 @@ __global__ __launch_bounds__(64) void attention_kernel(const uint16_t* __restric
 // SLOTS = 1: S <= 64 (one chunk; B/32's 50 tokens): a single LDS slot and no
 // look-ahead staging, which halves the LDS footprint and frees the staging
 // registers, so more workgroups fit per CU for this latency-bound case.
-template <int NT, int NW, int SLOTS = 2>
-__global__ __launch_bounds__(64 * NW) void attention_flash_kernel(const uint16_t* __restrict__ qkv,
+// NW = blockDim / 64 waves (8, or 4 for the single-slot S <= 64 instance);
+// PP = 16-byte staging pieces of K (and of V) per thread per chunk (1 for 8
+// waves, 2 for 4).
+template <int NT, int PP, int SLOTS = 2>
+__global__ __launch_bounds__(512) void attention_flash_kernel(const uint16_t* __restrict__ qkv,
                                                                 uint16_t* __restrict__ out, int S, int W, int H,
                                                                 int causal, uint8_t* __restrict__ q8,
                                                                 uint8_t* __restrict__ qs, int64_t rows_pad) {
   constexpr int KS = 72, VS = 68;  // LDS row strides (bf16)
-  constexpr int PP = 512 / (64 * NW);  // 16-byte pieces of K (and of V) per thread per chunk
-  static_assert(PP * 64 * NW == 512, "NW must divide 8");
+  const int NW = PP == 1 ? 8 : (int)(blockDim.x >> 6);  // PP = 1 is launched with 8 waves
   __shared__ __attribute__((aligned(16))) uint16_t Ks[SLOTS][64 * KS];
   __shared__ __attribute__((aligned(16))) uint16_t Vs[SLOTS][64 * VS];
   const int item = blockIdx.x;
@@ -179,7 +181,7 @@ __global__ __launch_bounds__(64 * NW) void attention_flash_kernel(const uint16_t
     const int p_ = tid + i * 64 * NW, r_ = (c) * 64 + (p_ >> 3), ch_ = p_ & 7;            \
     kr[i] = make_uint4(0, 0, 0, 0);                                                       \
     vr[i] = make_uint4(0, 0, 0, 0);                                                       \
-    if (r_ < S) {                                                                         \
+    if ((PP == 1 || p_ < 512) && r_ < S) {                                                \
       kr[i] = *(const uint4*)(kb + (int64_t)r_ * ld + ch_ * 8);                           \
       vr[i] = *(const uint4*)(vb + (int64_t)r_ * ld + ch_ * 8);                           \
     }                                                                                     \
@@ -187,9 +189,11 @@ __global__ __launch_bounds__(64 * NW) void attention_flash_kernel(const uint16_t
 #define FA_STAGE_WRITE(slot)                                                              \
   _Pragma("unroll") for (int i = 0; i < PP; ++i) {                                        \
     const int p_ = tid + i * 64 * NW, r_ = p_ >> 3, ch_ = p_ & 7;                         \
-    *(uint4*)(&Ks[slot][r_ * KS + ch_ * 8]) = kr[i];                                      \
-    const uint16_t* vv_ = (const uint16_t*)&vr[i];                                        \
-    _Pragma("unroll") for (int e = 0; e < 8; ++e) Vs[slot][(ch_ * 8 + e) * VS + r_] = vv_[e]; \
+    if (PP == 1 || p_ < 512) {                                                            \
+      *(uint4*)(&Ks[slot][r_ * KS + ch_ * 8]) = kr[i];                                    \
+      const uint16_t* vv_ = (const uint16_t*)&vr[i];                                      \
+      _Pragma("unroll") for (int e = 0; e < 8; ++e) Vs[slot][(ch_ * 8 + e) * VS + r_] = vv_[e]; \
+    }                                                                                     \
   }
 
   bf16x8 qf[NT][2];
@@ -375,18 +379,22 @@ hipError_t attention(const uint16_t* qkv, uint16_t* out, int B, int S, int W, in
     else hipLaunchKernelGGL(attention_kernel<96>, grid, dim3(64), 0, s, qkv, out, S, W, H, causal, items);
     return hipGetLastError();
   }
-  // NT query tiles per wave x NW waves >= ceil(S / 16)
+  // NT = ceil(tiles / 8) query tiles per wave on 8 waves; S <= 64: one tile on
+  // each of 4 waves, single slot.  Fewer waves with fewer idle tile slots
+  // measured slower (L/14 257 tokens on 6 waves x 3 tiles: 470 vs 421 us; text
+  // 77 on 5 x 1: 45 vs 31 us): a workgroup lasts as long as its busiest wave
+  // either way, and 8 waves spread that wave's SIMD over fewer partners.
   const int nqt = (S + 15) / 16;
   const int64_t rp = ((int64_t)B * S + 1) & ~1;
-#define FLASH(NT, NW) \
-  hipLaunchKernelGGL((attention_flash_kernel<NT, NW>), grid, dim3(64 * NW), 0, s, qkv, out, S, W, H, causal, q8, qs, rp)
+#define FLASH(T) \
+  hipLaunchKernelGGL((attention_flash_kernel<T, 1>), grid, dim3(512), 0, s, qkv, out, S, W, H, causal, q8, qs, rp)
   if (nqt <= 4)
-    hipLaunchKernelGGL((attention_flash_kernel<1, 4, 1>), grid, dim3(256), 0, s, qkv, out, S, W, H, causal, q8, qs, rp);
-  else if (nqt <= 8) FLASH(1, 8);
-  else if (nqt <= 16) FLASH(2, 8);
-  else if (nqt <= 24) FLASH(3, 8);
-  else if (nqt <= 32) FLASH(4, 8);
-  else FLASH(5, 8);
+    hipLaunchKernelGGL((attention_flash_kernel<1, 2, 1>), grid, dim3(256), 0, s, qkv, out, S, W, H, causal, q8, qs, rp);
+  else if (nqt <= 8) FLASH(1);
+  else if (nqt <= 16) FLASH(2);
+  else if (nqt <= 24) FLASH(3);
+  else if (nqt <= 32) FLASH(4);
+  else FLASH(5);
 #undef FLASH
   return hipGetLastError();
 }
