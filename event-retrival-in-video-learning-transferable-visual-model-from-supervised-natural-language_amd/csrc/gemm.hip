@@ -253,15 +253,6 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_kernel(GemmArgs a
 // the end of L_b(g).  WAR: stage g+3 is issued in L sections of stage g, after
 // every read of the buffer it overwrites (stage g-1, last read by group 1 in
 // L_b(g-1), which ends with lgkmcnt(0) + barrier).
-// Bias load the compiler does not see: issued before a tile's first LDS-DMA it
-// has landed once the first stage wait returns, so the epilogue does not wait
-// on a fresh global load (hipcc would insert vmcnt(0) there).
-__device__ __forceinline__ float4 bias_load_async(const float* p) {
-  float4 v;
-  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
-  return v;
-}
-
 template <int EPI, int CL, bool PRIO, bool DIRECT = false, bool NTS = false>
 __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs a) {
   constexpr int BM = 256, BN = 256, NT = 512;
@@ -315,12 +306,6 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs a) {
     __builtin_amdgcn_sched_barrier(0);
   };
 
-  float4 bias[4];
-#pragma unroll
-  for (int ni = 0; ni < 4; ++ni) {
-    const int n = n0 + wc * WTN + ni * 16 + 4 * (lane >> 4);
-    bias[ni] = a.bias ? bias_load_async(a.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
-  }
 #pragma unroll
   for (int s = 0; s < LEAD; ++s)
     if (s < nk) { issue_half(s, 0); issue_half(s, 1); }
@@ -400,6 +385,12 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs a) {
 
   // ------------------------------------------------ epilogue
   const int wr = grp;
+  float4 bias[4];
+#pragma unroll
+  for (int ni = 0; ni < 4; ++ni) {
+    const int n = n0 + wc * WTN + ni * 16 + 4 * (lane >> 4);
+    bias[ni] = a.bias ? *(const float4*)(a.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
   auto out_row = [&](int m) -> int64_t {
     return a.group ? (int64_t)(m / a.group) * a.gstride + a.goffset + m % a.group : (int64_t)m;
   };
@@ -515,11 +506,11 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs a) {
 //   cover them is stage LEAD's, three stages (~3k cycles) after they issued.
 //   A partial last m-tile (lanes with m >= M skip their stores) drains with
 //   vmcnt(0) instead, since its store count is not the fixed 16.
-//   A tile's bias is loaded (inline asm, so hipcc inserts no wait for it)
-//   just before that tile's first stages are issued: older than all of them,
-//   it has landed once the tile's first stage wait returns, and the epilogue
-//   issues no vector-memory load behind the prefetch (a plain load made hipcc
-//   drain the prefetch with vmcnt(0) before the epilogue).
+//   A tile's bias (256 f32) is LDS-DMA'd by wave 0 into one of two LDS slots
+//   (tile parity) just before that tile's first stages are issued: older than
+//   them, it has landed once the tile's first stage wait + barrier return, and
+//   the epilogue reads it with an LDS read hipcc does not see.  A plain global
+//   load of the bias there made hipcc drain the prefetch with vmcnt(0).
 __device__ __forceinline__ void vm_wait_n(int n) {  // n wave-uniform; unlisted values wait for everything
   switch (n) {
     case 24: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
@@ -537,7 +528,8 @@ __global__ __launch_bounds__(512) void gemm_ppp_kernel(GemmArgs a) {
   constexpr int WTM = 128, WTN = 64;
   constexpr int A_BYTES = BM * BK * 2, STAGE_BYTES = (BM + BN) * BK * 2;
   constexpr int NSTORE = 16;  // epilogue store instructions per wave of a full tile
-  __shared__ __attribute__((aligned(16))) char smem[RING * STAGE_BYTES];
+  __shared__ __attribute__((aligned(16))) char smem[RING * STAGE_BYTES + 2 * BN * 4];
+  float* sbias = (float*)(smem + RING * STAGE_BYTES);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int grp = __builtin_amdgcn_readfirstlane(wave >> 2), wc = wave & 3;
@@ -590,13 +582,11 @@ __global__ __launch_bounds__(512) void gemm_ppp_kernel(GemmArgs a) {
   };
 
   const int g = lane >> 4;
-  float4 bias[4];
-  auto load_bias = [&](float4 (&b)[4], int nn) {
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni)
-      b[ni] = a.bias ? bias_load_async(a.bias + nn + wc * WTN + ni * 16 + 4 * g) : make_float4(0.f, 0.f, 0.f, 0.f);
+  int tpar = 0;  // tile parity: bias slot
+  auto load_bias = [&](int slot, int nn) {  // wave 0: 64 lanes x 16 B = the tile's 256 bias values
+    if (wave == 0 && a.bias) glds16(a.bias + nn + lane * 4, sbias + slot * BN);
   };
-  load_bias(bias, n0);
+  load_bias(0, n0);
   set_src(m0, n0);
 #pragma unroll
   for (int st = 0; st < LEAD; ++st)
@@ -636,16 +626,19 @@ __global__ __launch_bounds__(512) void gemm_ppp_kernel(GemmArgs a) {
     const int cm0 = m0, cn0 = n0;
     vb += gridDim.x;
     const bool has_next = vb < ntiles;
-    float4 nbias[4];
     if (has_next) {
       coords(vb, m0, n0);
-      load_bias(nbias, n0);
+      load_bias(tpar ^ 1, n0);
       set_src(m0, n0);
 #pragma unroll
       for (int st = 0; st < LEAD; ++st)
         if (st < nk) issue(st);
     }
     // ---- epilogue of tile (cm0, cn0): direct permlane-swapped row stores (gemm_pp_kernel DIRECT)
+    float4 bias[4];
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni)
+      bias[ni] = a.bias ? lds_read_f4(sbias + tpar * BN + wc * WTN + ni * 16 + 4 * g) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
     for (int mi = 0; mi < 8; ++mi) {
       const int m = cm0 + grp * WTM + mi * 16 + (lane & 15);
@@ -669,8 +662,7 @@ __global__ __launch_bounds__(512) void gemm_ppp_kernel(GemmArgs a) {
       }
     }
     if (!has_next) break;
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni) bias[ni] = nbias[ni];
+    tpar ^= 1;
     if (cm0 + BM <= a.M) {
       pend = NSTORE;
     } else {  // partial tile: an unknown number of stores issued
