@@ -240,6 +240,10 @@ __device__ __forceinline__ int pp_swz(int x) { return (0x1320 >> (4 * x)) & 0xF;
 // loads from the shared array hipcc drains every in-flight LDS-DMA
 // (s_waitcnt vmcnt(0)) before the section's first read, serialising the
 // stage pipeline.  The section's lgkmcnt(0) + barrier covers the reads.
+// Caveat of untracked reads: nothing may copy their destination registers
+// before that wait; the emitted code reads straight into the MFMA operand
+// tuples (checked in the .s: no v_mov between the ds_reads and the
+// lgkmcnt(0)), and tests/test_gpu_mx.py would catch a stale operand.
 __device__ __forceinline__ int lds_u8(const uint8_t* p) {
   int v;
   const uint32_t addr = (uint32_t)(uintptr_t)(const LDS_AS uint8_t*)p;
