@@ -119,3 +119,72 @@ def rank_of_targets(scores, pair_query, pair_target):
                                            pq.shape[0], out.data_ptr(), N.stream_ptr(s.device)),
                 "mi_rank_of_targets")
     return out
+
+
+class MirroredCorpus:
+    """HBM-resident corpus with a bf16 ranking mirror and the f32 master kept
+    for exact re-scoring.
+
+    ``topk`` ranks the bf16 mirror for ``k' = min(MAX_K, oversample * k)``
+    candidates per query (half the HBM bytes of the f32 pass), gathers the
+    union of the candidates' f32 rows (ascending corpus order) and re-ranks
+    them with the exact f32 kernel, so scores are bit-identical to
+    ``rank_topk(master, ...)``.  The result is certified per query: with the
+    mirror's score error bounded by ``delta`` (bf16 rounding of the rows,
+    2^-8 relative, on both the dot product and the norm), every row outside the
+    k' candidates scores at most ``s_bf16[k'-1] + delta`` exactly, so once the
+    exact k-th score exceeds that bound no row outside can enter the top-k.
+    Queries that fail the certificate (near-ties across the candidate edge)
+    fall back to the exact f32 pass over the master.
+
+    Reference semantics: ``EmbeddingService.search_top_frames`` ranks
+    ``get_embeddings`` rows (embedding_service.py:209-210, 314-320); the stored
+    ``.npy`` rows stay the f32 master (embedding_service.py:505).
+    """
+
+    def __init__(self, master, oversample: int = 4):
+        import torch
+        if not master.is_cuda:
+            raise N.MiClipError("MirroredCorpus lives in HBM: move the master rows to the device first")
+        self.master = _corpus(master).float().contiguous()
+        self.mirror = self.master.to(torch.bfloat16).contiguous()
+        self.oversample = int(oversample)
+        self.fallbacks = 0
+
+    def __len__(self):
+        return self.master.shape[0]
+
+    def topk(self, queries, k, norm="l2", nan_policy="first"):
+        import torch
+        q = _queries(queries, self.master.device)
+        n = self.master.shape[0]
+        kk = min(k, n)
+        kc = min(MAX_K, max(kk, self.oversample * kk), n)
+        if kk <= 0:
+            return rank_topk(self.master, q, k, norm=norm, nan_policy=nan_policy)
+        s1, i1 = rank_topk(self.mirror, q, kc, norm=norm, nan_policy=nan_policy)
+        if kc >= n:      # every row is a candidate: the exact pass is the answer
+            return rank_topk(self.master, q, k, norm=norm, nan_policy=nan_policy)
+        union = torch.unique(i1.flatten())                    # sorted ascending: index ties keep corpus order
+        s2, j2 = rank_topk(self.master.index_select(0, union), q, kk, norm=norm, nan_policy=nan_policy)
+        i2 = union[j2]
+        # certificate: bf16 rows carry a relative error <= 2^-8 per element, so
+        # |s_bf16 - s_exact| <= delta = 2^-7 |q| (dot and norm) for "l2";
+        # un-normalised scores scale with the row norm, so certify only "l2"
+        if norm != "l2":
+            self.fallbacks += q.shape[0]
+            return rank_topk(self.master, q, k, norm=norm, nan_policy=nan_policy)
+        delta = q.norm(dim=1) * 2.0 ** -7
+        edge = s1[:, kc - 1]
+        ok = (s2[:, kk - 1] > edge + 2 * delta) & torch.isfinite(s2).all(1) & torch.isfinite(s1).all(1)
+        if bool(ok.all()):
+            return s2, i2
+        bad = torch.nonzero(~ok).flatten()
+        self.fallbacks += int(bad.numel())
+        sf, jf = rank_topk(self.master, q.index_select(0, bad), k, norm=norm, nan_policy=nan_policy)
+        s2 = s2.clone()
+        i2 = i2.clone()
+        s2[bad] = sf
+        i2[bad] = jf
+        return s2, i2
+

@@ -135,3 +135,32 @@ def test_reference_flow_rk_fixture(gpu):
     assert np.array_equal(res["i2t_ranks"], g["i2t_ranks"])
     for d, arr in (("t2i", g["t2i_r"]), ("i2t", g["i2t_r"])):
         assert [res[d]["R@1"], res[d]["R@5"], res[d]["R@10"]] == list(arr)
+
+
+@pytest.mark.parametrize("N,D,Q,k", [(20000, 512, 32, 10), (4097, 768, 7, 16), (500, 512, 3, 60)])
+def test_mirrored_corpus_matches_f32(gpu, N, D, Q, k):
+    """bf16 mirror + exact f32 re-scoring == the f32 pass, bit for bit (§8(f) item 2)."""
+    from miclip import retrieval, weights
+    corpus = _t(weights.normal(21, f"m{N}", (N, D)), gpu)
+    q = _t(weights.synthetic_corpus(Q, D, seed=22), gpu)
+    mc = retrieval.MirroredCorpus(corpus)
+    s, i = mc.topk(q, k)
+    s0, i0 = retrieval.rank_topk(corpus, q, k)
+    assert (i.cpu() == i0.cpu()).all()
+    assert (s.cpu() == s0.cpu()).all()
+
+
+def test_mirrored_corpus_near_ties_fall_back(gpu):
+    """Rows that tie in bf16 across the candidate edge fail the certificate and
+    take the exact path; the answer is still the f32 one."""
+    import torch
+    from miclip import retrieval, weights
+    base = weights.normal(23, "tie", (1, 256))
+    rows = np.repeat(base, 400, axis=0) + weights.normal(24, "eps", (400, 256)) * 1e-4   # near-duplicates
+    corpus = _t(rows, gpu)
+    q = torch.from_numpy(base / np.linalg.norm(base)).to(gpu)
+    mc = retrieval.MirroredCorpus(corpus)
+    s, i = mc.topk(q, 10)
+    s0, i0 = retrieval.rank_topk(corpus, q, 10)
+    assert (i.cpu() == i0.cpu()).all() and (s.cpu() == s0.cpu()).all()
+    assert mc.fallbacks == 1
