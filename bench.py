@@ -45,7 +45,8 @@ def parse():
     ap.add_argument("--image-chunk", type=int, default=None)
     ap.add_argument("--weights", choices=["bf16", "fp8"], default="bf16",
                     help="fp8: vision GEMMs on the MX-fp8 block-scaled MFMA (BASELINE configs[4])")
-    ap.add_argument("--cpu-frames", type=int, default=64, help="CPU baseline sample (BASELINE configs[0])")
+    ap.add_argument("--cpu-frames", type=int, default=768,
+                    help="CPU baseline sample: frames encoded at batch 64 (BASELINE configs[0]), ~10-20 s of CPU work")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
     return ap.parse_args()
