@@ -404,6 +404,20 @@ static GemmArgs gargs(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t
   return g;
 }
 
+// Vision residual stream storage: fp16 after the first residual add (2 B
+// instead of 4 per element on each of the 24 residual LayerNorms' read and
+// write); MICLIP_RESID16=0 keeps it f32 (A/B, parity comparisons).
+static int resid16() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("MICLIP_RESID16");
+    v = e ? atoi(e) != 0 : 1;
+  }
+  return v;
+}
+// xmode of a layer's first residual_ln: the f32 stream from ln_pre is converted at layer 0
+static int xmode_at(int r16, size_t l) { return r16 ? (l == 0 ? 1 : 2) : 0; }
+
 // One tower.  On return x + delta is the final residual stream (the last
 // c_proj output is left in delta; the caller's final LayerNorm adds it).
 // Per block (openai/CLIP ResidualAttentionBlock):
@@ -411,7 +425,8 @@ static GemmArgs gargs(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t
 //   x += delta ; h = ln_2(x)                      (residual_ln)
 //   m = QuickGELU(h W_fc^T + b_fc) ; delta = m W_pr^T + b_pr
 //   x += delta ; h = ln_1'(x)  (next block)       (residual_ln)
-static int run_tower(mi_clip* c, const std::vector<Layer>& layers, int B, int S, int W, int causal, hipStream_t s) {
+static int run_tower(mi_clip* c, const std::vector<Layer>& layers, int B, int S, int W, int causal, hipStream_t s,
+                     int r16 = 0) {
   const int M = B * S;
   HIP_TRY(layernorm_bf16(c->x, W, layers[0].ln1_g, layers[0].ln1_b, c->h, W, M, W, s));
   for (size_t l = 0; l < layers.size(); ++l) {
@@ -419,11 +434,12 @@ static int run_tower(mi_clip* c, const std::vector<Layer>& layers, int B, int S,
     HIP_TRY(gemm_bf16(gargs(c->h, W, L.w_qkv, W, L.b_qkv, c->qkv, 3 * W, M, 3 * W, W), EPI_BF16, s));
     HIP_TRY(attention(c->qkv, c->att, B, S, W, causal, s));
     HIP_TRY(gemm_bf16(gargs(c->att, W, L.w_out, W, L.b_out, c->delta, W, M, W, W), EPI_BF16, s));
-    HIP_TRY(residual_ln(c->x, c->delta, W, 1, L.ln2_g, L.ln2_b, c->h, M, W, s));
+    HIP_TRY(residual_ln(c->x, c->delta, W, 1, L.ln2_g, L.ln2_b, c->h, M, W, s, nullptr, nullptr, xmode_at(r16, l)));
     HIP_TRY(gemm_bf16(gargs(c->h, W, L.w_fc, W, L.b_fc, c->mlp, 4 * W, M, 4 * W, W), EPI_GELU_BF16, s));
     HIP_TRY(gemm_bf16(gargs(c->mlp, 4 * W, L.w_proj, 4 * W, L.b_proj, c->delta, W, M, W, 4 * W), EPI_BF16, s));
     if (l + 1 < layers.size())
-      HIP_TRY(residual_ln(c->x, c->delta, W, 1, layers[l + 1].ln1_g, layers[l + 1].ln1_b, c->h, M, W, s));
+      HIP_TRY(residual_ln(c->x, c->delta, W, 1, layers[l + 1].ln1_g, layers[l + 1].ln1_b, c->h, M, W, s, nullptr, nullptr,
+                          r16 ? 2 : 0));
   }
   return MI_OK;
 }
@@ -441,7 +457,7 @@ static GemmArgs margs(const uint8_t* A, const uint8_t* as, const uint8_t* W, con
 // run_tower, every GEMM on the block-scaled MFMA; the producers of GEMM A
 // operands (the LayerNorms, attention, c_fc's QuickGELU epilogue) emit MX-fp8
 // directly, so no separate quantisation pass runs.
-static int run_tower_mx(mi_clip* c, const std::vector<Layer>& layers, int B, int S, int W, hipStream_t s) {
+static int run_tower_mx(mi_clip* c, const std::vector<Layer>& layers, int B, int S, int W, hipStream_t s, int r16) {
   const int M = B * S;
   HIP_TRY(layernorm_bf16(c->x, W, layers[0].ln1_g, layers[0].ln1_b, c->h, W, M, W, s, c->hq, c->hqs));
   for (size_t l = 0; l < layers.size(); ++l) {
@@ -449,14 +465,14 @@ static int run_tower_mx(mi_clip* c, const std::vector<Layer>& layers, int B, int
     HIP_TRY(gemm_mx(margs(c->hq, c->hqs, L.q_qkv, L.s_qkv, L.b_qkv, c->qkv, 3 * W, M, 3 * W, W), EPI_BF16, s));
     HIP_TRY(attention(c->qkv, c->att, B, S, W, 0, s, c->attq, c->attqs));
     HIP_TRY(gemm_mx(margs(c->attq, c->attqs, L.q_out, L.s_out, L.b_out, c->delta, W, M, W, W), EPI_BF16, s));
-    HIP_TRY(residual_ln(c->x, c->delta, W, 1, L.ln2_g, L.ln2_b, c->h, M, W, s, c->hq, c->hqs));
+    HIP_TRY(residual_ln(c->x, c->delta, W, 1, L.ln2_g, L.ln2_b, c->h, M, W, s, c->hq, c->hqs, xmode_at(r16, l)));
     GemmArgs fc = margs(c->hq, c->hqs, L.q_fc, L.s_fc, L.b_fc, c->mlpq, 4 * W, M, 4 * W, W);
     fc.o_scale = c->mlpqs;
     HIP_TRY(gemm_mx(fc, EPI_GELU_MX, s));
     HIP_TRY(gemm_mx(margs(c->mlpq, c->mlpqs, L.q_proj, L.s_proj, L.b_proj, c->delta, W, M, W, 4 * W), EPI_BF16, s));
     if (l + 1 < layers.size())
       HIP_TRY(residual_ln(c->x, c->delta, W, 1, layers[l + 1].ln1_g, layers[l + 1].ln1_b, c->h, M, W, s, c->hq,
-                          c->hqs));
+                          c->hqs, r16 ? 2 : 0));
   }
   return MI_OK;
 }
@@ -488,10 +504,12 @@ int mi_clip_encode_image(mi_clip* c, const void* pixels, int64_t B, int in_dtype
     pg.goffset = 1;
     HIP_TRY(gemm_bf16(pg, EPI_F32, s));
     HIP_TRY(vision_embed_ln(c->x, c->cls, c->vpos, c->ln_pre_g, c->ln_pre_b, nb, S, W, s));
-    int r = c->fp8 ? run_tower_mx(c, c->vl, nb, S, W, s) : run_tower(c, c->vl, nb, S, W, 0, s);
+    const int r16 = resid16() && !c->vl.empty();
+    int r = c->fp8 ? run_tower_mx(c, c->vl, nb, S, W, s, r16) : run_tower(c, c->vl, nb, S, W, 0, s, r16);
     if (r) return r;
     // ln_post(x[:, 0] + last c_proj delta) over the CLS rows only
-    HIP_TRY(residual_ln(c->x, c->delta, (int64_t)S * W, 0, c->ln_post_g, c->ln_post_b, c->cls_ln, nb, W, s));
+    HIP_TRY(residual_ln(c->x, c->delta, (int64_t)S * W, 0, c->ln_post_g, c->ln_post_b, c->cls_ln, nb, W, s, nullptr,
+                        nullptr, r16 ? 2 : 0));
     HIP_TRY(gemm_bf16(gargs(c->cls_ln, W, c->vproj_t, W, nullptr, c->y, E, nb, E, W), EPI_F32, s));
     HIP_TRY(finalize_rows(c->y, (char*)out + c0 * E * dtype_size(out_dtype), out_dtype, nb, E, l2_normalize, s));
   }
@@ -610,6 +628,16 @@ int mi_op_layernorm(const float* x, const float* g, const float* b, void* out, i
   if (!x || !g || !b || !out || rows < 0) return fail(MI_ERR_ARG, "mi_op_layernorm: bad arguments");
   if (W % 4 || W > 1024) return fail(MI_ERR_UNSUPPORTED, "mi_op_layernorm: W must be a multiple of 4, <= 1024");
   HIP_TRY(layernorm_bf16(x, W, g, b, (uint16_t*)out, W, rows, W, (hipStream_t)stream));
+  return MI_OK;
+}
+
+int mi_op_residual_ln(void* x, const void* delta, const float* g, const float* b, void* out, int32_t rows, int32_t W,
+                      int32_t xmode, void* stream) {
+  if (!x || !delta || !g || !b || !out || rows < 0) return fail(MI_ERR_ARG, "mi_op_residual_ln: bad arguments");
+  if (W % 4 || W > 1024) return fail(MI_ERR_UNSUPPORTED, "mi_op_residual_ln: W must be a multiple of 4, <= 1024");
+  if (xmode < 0 || xmode > 2) return fail(MI_ERR_ARG, "mi_op_residual_ln: xmode must be 0, 1 or 2");
+  HIP_TRY(residual_ln((float*)x, (const uint16_t*)delta, W, 1, g, b, (uint16_t*)out, rows, W, (hipStream_t)stream,
+                      nullptr, nullptr, xmode));
   return MI_OK;
 }
 

@@ -8,7 +8,8 @@
 //   text embeddings: token_embedding[t] + positional_embedding          T1
 //   attention: softmax(q k^T / sqrt(64) [+ causal mask]) v per head     V4/T2 (:280-335)
 //   text pooling at argmax(tokens) then ln_final                        T3 (:559-571)
-// The residual stream stays f32 in HBM; GEMM operands are bf16.
+// The residual stream is f32 (text tower) or fp16 (vision tower, after its
+// first residual add; residual_ln_kernel) in HBM; GEMM operands are bf16.
 #include <cstdlib>
 
 #include "common.hpp"
@@ -98,46 +99,66 @@ __global__ __launch_bounds__(256) void ln_bf16_kernel(const float* __restrict__ 
 
 // Residual add + LayerNorm: xr = x[r*stride] + delta[r*stride] (delta = the
 // bf16 out_proj / c_proj GEMM output, bias included); optionally x is
-// written back (f32 residual stream), and out[r] = LN(xr) in bf16.
-// This is `x = x + attn(ln_1(x)); h = ln_2(x)` (and `x = x + mlp(..);
+// written back, and out[r] = LN(xr) in bf16.
+// This is `x = x + attn(ln_1(x)); h = ln_1'(x)` (and `x = x + mlp(..);
 // h = ln_1'(x)` / `ln_post(x[:, 0])`) of openai/CLIP ResidualAttentionBlock.
-template <bool NTS>
+// Residual storage (XM): RES_F32 f32 in/out; RES_F32_TO_F16 reads f32 and
+// writes the row back as fp16 into the first half of its own f32 slot (the
+// wave has read the whole row before it stores); RES_F16 fp16 in/out in that
+// half-row layout (element (r, j) at ((half*)x)[2 * r * stride + j]).  The
+// add and the LayerNorm are f32 either way; fp16 storage is the precision the
+// reference's GPU path keeps its whole residual stream in (clip.load on cuda
+// converts the model to fp16, openai/CLIP model.py convert_weights).
+constexpr int RES_F32 = 0, RES_F32_TO_F16 = 1, RES_F16 = 2;
+template <bool NTS, int XM>
 __global__ __launch_bounds__(256) void residual_ln_kernel(float* __restrict__ x, const uint16_t* __restrict__ delta,
                                                           int64_t stride, int write_x, const float* __restrict__ g,
                                                           const float* __restrict__ b, uint16_t* __restrict__ out,
                                                           int rows, int W, uint8_t* __restrict__ q,
                                                           uint8_t* __restrict__ qs) {
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  typedef _Float16 h4v __attribute__((ext_vector_type(4)));
+  typedef uint32_t u2v __attribute__((ext_vector_type(2)));
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= rows) return;
   const int n4 = W >> 2;
-  float4* xr = (float4*)(x + (int64_t)row * stride);
-  const uint2* dr = (const uint2*)(delta + (int64_t)row * stride);
+  f4v* xr = (f4v*)(x + (int64_t)row * stride);
+  h4v* xh = (h4v*)((_Float16*)x + (int64_t)row * stride * 2);
+  const u2v* dr = (const u2v*)(delta + (int64_t)row * stride);
   RowVals r;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int idx = lane + 64 * i;
     if (idx < n4) {
-      typedef float f4v __attribute__((ext_vector_type(4)));
-      typedef uint32_t u2v __attribute__((ext_vector_type(2)));
-      float4 v;
-      uint2 d;
-      if (NTS) {  // non-temporal residual stream (read once per LN, next read ~ms later)
-        const f4v vv = __builtin_nontemporal_load((const f4v*)&xr[idx]);
-        const u2v dd = __builtin_nontemporal_load((const u2v*)&dr[idx]);
-        v = make_float4(vv[0], vv[1], vv[2], vv[3]);
-        d = make_uint2(dd[0], dd[1]);
+      f4v v;
+      u2v d;
+      if (XM == RES_F16) {
+        const h4v vh = NTS ? __builtin_nontemporal_load(&xh[idx]) : xh[idx];
+        v = f4v{(float)vh[0], (float)vh[1], (float)vh[2], (float)vh[3]};
       } else {
-        v = xr[idx];
-        d = dr[idx];
+        v = NTS ? __builtin_nontemporal_load(&xr[idx]) : xr[idx];
       }
-      r.v[i] = make_float4(v.x + bf2f((uint16_t)(d.x & 0xffff)), v.y + bf2f((uint16_t)(d.x >> 16)),
-                           v.z + bf2f((uint16_t)(d.y & 0xffff)), v.w + bf2f((uint16_t)(d.y >> 16)));
-      if (write_x) {
-        if (NTS) __builtin_nontemporal_store(f4v{r.v[i].x, r.v[i].y, r.v[i].z, r.v[i].w}, (f4v*)&xr[idx]);
-        else xr[idx] = r.v[i];
+      d = NTS ? __builtin_nontemporal_load(&dr[idx]) : dr[idx];  // non-temporal: read once, next read ~ms later
+      r.v[i] = make_float4(v[0] + bf2f((uint16_t)(d[0] & 0xffff)), v[1] + bf2f((uint16_t)(d[0] >> 16)),
+                           v[2] + bf2f((uint16_t)(d[1] & 0xffff)), v[3] + bf2f((uint16_t)(d[1] >> 16)));
+      if (write_x && XM == RES_F32) {
+        const f4v o{r.v[i].x, r.v[i].y, r.v[i].z, r.v[i].w};
+        if (NTS) __builtin_nontemporal_store(o, &xr[idx]);
+        else xr[idx] = o;
       }
     } else {
       r.v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  if (write_x && XM != RES_F32) {  // after every load of the row (RES_F32_TO_F16 overwrites its first half)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int idx = lane + 64 * i;
+      if (idx < n4) {
+        const h4v o{(_Float16)r.v[i].x, (_Float16)r.v[i].y, (_Float16)r.v[i].z, (_Float16)r.v[i].w};
+        if (NTS) __builtin_nontemporal_store(o, &xh[idx]);
+        else xh[idx] = o;
+      }
     }
   }
   float mean, rstd;
@@ -373,9 +394,9 @@ hipError_t eot_gather_ln(const int32_t* tokens, const float* x, const uint16_t* 
 }
 
 hipError_t residual_ln(float* x, const uint16_t* delta, int64_t stride, int write_x, const float* g, const float* b,
-                       uint16_t* out, int rows, int W, hipStream_t s, uint8_t* q, uint8_t* qs) {
+                       uint16_t* out, int rows, int W, hipStream_t s, uint8_t* q, uint8_t* qs, int xmode) {
   if (rows <= 0) return hipSuccess;
-  if (W % 4 || W > 1024 || (q && W % 128)) return hipErrorInvalidValue;
+  if (W % 4 || W > 1024 || (q && W % 128) || xmode < RES_F32 || xmode > RES_F16) return hipErrorInvalidValue;
   // default: non-temporal x / delta accesses (the residual stream is read once
   // per LN and next touched milliseconds later; keeping it out of the Infinity
   // Cache leaves that to the GEMM/attention operands): +1.8 % end to end on
@@ -385,12 +406,18 @@ hipError_t residual_ln(float* x, const uint16_t* delta, int64_t stride, int writ
     const char* e = getenv("MICLIP_LN_NT");
     nts = e ? atoi(e) : 1;
   }
-  if (nts)
-    hipLaunchKernelGGL(residual_ln_kernel<true>, dim3((rows + 3) / 4), dim3(256), 0, s, x, delta, stride, write_x, g, b,
-                       out, rows, W, q, qs);
-  else
-    hipLaunchKernelGGL(residual_ln_kernel<false>, dim3((rows + 3) / 4), dim3(256), 0, s, x, delta, stride, write_x, g, b,
-                       out, rows, W, q, qs);
+  const dim3 grid((rows + 3) / 4), block(256);
+#define RLN(NT, XM) hipLaunchKernelGGL((residual_ln_kernel<NT, XM>), grid, block, 0, s, x, delta, stride, write_x, g, b, out, rows, W, q, qs)
+  if (nts) {
+    if (xmode == RES_F32) RLN(true, RES_F32);
+    else if (xmode == RES_F32_TO_F16) RLN(true, RES_F32_TO_F16);
+    else RLN(true, RES_F16);
+  } else {
+    if (xmode == RES_F32) RLN(false, RES_F32);
+    else if (xmode == RES_F32_TO_F16) RLN(false, RES_F32_TO_F16);
+    else RLN(false, RES_F16);
+  }
+#undef RLN
   return hipGetLastError();
 }
 

@@ -73,9 +73,11 @@ hipError_t text_embed(const int32_t* tokens, const float* tok_emb, const float* 
 // out[q] = LN(x[r] (+ delta[r])), r = q*S + argmax_t tokens[q*S + t]; bf16
 hipError_t eot_gather_ln(const int32_t* tokens, const float* x, const uint16_t* delta, const float* g,
                          const float* b, uint16_t* out, int Q, int S, int W, hipStream_t s);
-// row r = i*stride: xr = x[r] + delta[r] (bf16); if write_x: x[r] = xr; out[i] = LN(xr) bf16 [rows, W]
+// row r = i*stride: xr = x[r] + delta[r] (bf16); if write_x: x[r] = xr; out[i] = LN(xr) bf16 [rows, W].
+// xmode: 0 residual f32; 1 f32 in, fp16 out (half-row layout); 2 fp16 in/out (encoder.hip)
 hipError_t residual_ln(float* x, const uint16_t* delta, int64_t stride, int write_x, const float* g, const float* b,
-                       uint16_t* out, int rows, int W, hipStream_t s, uint8_t* q = nullptr, uint8_t* qs = nullptr);
+                       uint16_t* out, int rows, int W, hipStream_t s, uint8_t* q = nullptr, uint8_t* qs = nullptr,
+                       int xmode = 0);
 // pixels [B,3,R,R] (f32 or bf16) -> patches [B*G*G, Kp] bf16, k = c*P*P + kh*P + kw, zero pad to Kp
 hipError_t im2col(const void* pixels, int in_bf16, uint16_t* out, int B, int R, int P, int Kp,
                   hipStream_t s);

@@ -181,6 +181,13 @@ int mi_op_gemm(const void* A, const void* W, const float* bias, void* out, int32
 int mi_op_layernorm(const float* x, const float* gamma, const float* beta, void* out, int32_t rows, int32_t W,
                     void* stream);
 int mi_op_attention(const void* qkv, void* out, int32_t B, int32_t S, int32_t W, int32_t causal, void* stream);
+/* mi_op_residual_ln: x += delta (bf16 [rows,W]); out bf16 = LN(x) — the residual add +
+ *   ln_2 / next ln_1 of openai/CLIP ResidualAttentionBlock (x = x + attn(ln_1(x));
+ *   x = x + mlp(ln_2(x))).  xmode 0: x f32 [rows,W]; 1: x read f32, written back fp16
+ *   into the first half of each f32 row slot; 2: x fp16 in that half-row layout
+ *   (the vision tower's residual stream after its first add). */
+int mi_op_residual_ln(void* x, const void* delta, const float* gamma, const float* beta, void* out, int32_t rows,
+                      int32_t W, int32_t xmode, void* stream);
 
 /* MX-fp8 operator entry points (the "fp8 MFMA weights" configuration,
  * BASELINE.json configs[4]; OCP e4m3 elements with one e8m0 scale per 64

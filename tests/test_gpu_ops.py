@@ -75,6 +75,41 @@ def test_layernorm(gpu, rows, W):
     assert err < 2e-2, err
 
 
+@pytest.mark.parametrize("rows,W", [(1, 128), (1000, 768), (50, 1024), (33, 512)])
+@pytest.mark.parametrize("xmode", [0, 1, 2])
+def test_residual_ln(gpu, rows, W, xmode):
+    """x += delta; out = LN(x) for the three residual storage modes (f32, f32 -> fp16, fp16 half-row).
+    The written-back residual is bit-exact: the f32 sum x + bf16(delta), rounded to fp16 when stored as fp16."""
+    import torch
+    N_ = _lib()
+    g = torch.Generator(device="cpu").manual_seed(rows * 3 + W + xmode)
+    x32 = torch.randn(rows, W, generator=g) * 3 + 1
+    delta = torch.randn(rows, W, generator=g).bfloat16()
+    gamma = (1 + 0.1 * torch.randn(W, generator=g))
+    beta = 0.1 * torch.randn(W, generator=g)
+    slot = torch.zeros(rows, W, dtype=torch.float32)  # f32 row slots; fp16 modes use their first halves
+    if xmode == 2:
+        x32 = x32.half().float()  # the fp16 stream holds fp16 values
+        slot.view(torch.float16).view(rows, 2 * W)[:, :W] = x32.half()
+    else:
+        slot.copy_(x32)
+    xd = slot.to(gpu)
+    out = torch.empty(rows, W, dtype=torch.bfloat16, device=gpu)
+    dd, gd, bd = delta.to(gpu), gamma.to(gpu), beta.to(gpu)  # held: a freed temporary's block is reused
+    N_.check(N_.lib().mi_op_residual_ln(xd.data_ptr(), dd.data_ptr(), gd.data_ptr(), bd.data_ptr(), out.data_ptr(),
+                                        rows, W, xmode, _stream()), "residual_ln")
+    torch.cuda.synchronize()
+    s = x32 + delta.float()  # f32 add, as the kernel
+    if xmode == 0:
+        assert torch.equal(xd.cpu(), s)
+    else:
+        got = xd.cpu().view(torch.float16).view(rows, 2 * W)[:, :W]
+        assert torch.equal(got, s.half())
+    ref = torch.nn.functional.layer_norm(s.double(), (W,), gamma.double(), beta.double(), 1e-5)
+    err = (out.cpu().double() - ref).abs().max().item()
+    assert err < 2e-2, err
+
+
 @pytest.mark.parametrize("B,S,W,causal", [(1, 50, 768, 0), (7, 50, 768, 0), (3, 77, 512, 1), (2, 17, 128, 0),
                                           (2, 10, 256, 1), (1, 257, 1024, 0), (4, 197, 768, 0),
                                           # long-sequence (flash) kernel: L/14@336 = 577 tokens, ragged tails,
