@@ -400,6 +400,7 @@ static GemmArgs gargs(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t
   GemmArgs g;
   g.A = A; g.lda = lda; g.W = W; g.ldw = ldw; g.bias = bias; g.out = out; g.ldo = ldo;
   g.M = M; g.N = N; g.K = K; g.group = 0; g.gstride = 0; g.goffset = 0; g.ngroup = 0; g.a_scale = nullptr; g.w_scale = nullptr; g.o_scale = nullptr;
+  g.patch_R = 0;
   g.variant = gemm_variant();
   return g;
 }
@@ -411,6 +412,17 @@ static int resid16() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("MICLIP_RESID16");
+    v = e ? atoi(e) != 0 : 1;
+  }
+  return v;
+}
+// Patch embedding reads the bf16 pixels straight from the GEMM's A-operand DMA
+// (B/32: one 32-pixel row segment per k stage) instead of through an im2col
+// buffer; MICLIP_PATCH_FUSED=0 keeps the im2col pass (A/B).
+static int patch_fused() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("MICLIP_PATCH_FUSED");
     v = e ? atoi(e) != 0 : 1;
   }
   return v;
@@ -497,8 +509,17 @@ int mi_clip_encode_image(mi_clip* c, const void* pixels, int64_t B, int in_dtype
   const size_t in_img = (size_t)3 * R * R * dtype_size(in_dtype);
   for (int64_t c0 = 0; c0 < B; c0 += c->img_chunk) {
     const int nb = (int)((B - c0) < c->img_chunk ? (B - c0) : c->img_chunk);
-    HIP_TRY(im2col((const char*)pixels + c0 * in_img, in_dtype == MI_BF16, c->patches, nb, R, P, c->Kp, s));
-    GemmArgs pg = gargs(c->patches, c->Kp, c->conv_w, c->Kp, nullptr, c->x, W, nb * G2, W, c->Kp);
+    const char* px = (const char*)pixels + c0 * in_img;
+    const bool fused = patch_fused() && in_dtype == MI_BF16 && P == 32 && c->Kp == 3 * P * P && R % 8 == 0 &&
+                       ((uintptr_t)px & 15) == 0 && (int64_t)nb * G2 >= 1024;
+    GemmArgs pg;
+    if (fused) {
+      pg = gargs((const uint16_t*)px, 0, c->conv_w, c->Kp, nullptr, c->x, W, nb * G2, W, c->Kp);
+      pg.patch_R = R;
+    } else {
+      HIP_TRY(im2col(px, in_dtype == MI_BF16, c->patches, nb, R, P, c->Kp, s));
+      pg = gargs(c->patches, c->Kp, c->conv_w, c->Kp, nullptr, c->x, W, nb * G2, W, c->Kp);
+    }
     pg.group = G2;
     pg.gstride = S;
     pg.goffset = 1;

@@ -253,7 +253,14 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_kernel(GemmArgs a
 // the end of L_b(g).  WAR: stage g+3 is issued in L sections of stage g, after
 // every read of the buffer it overwrites (stage g-1, last read by group 1 in
 // L_b(g-1), which ends with lgkmcnt(0) + barrier).
-template <int EPI, int CL, bool PRIO, bool DIRECT = false, bool NTS = false>
+//
+// PATCH (patch embedding, a.patch_R = R > 0): A is the bf16 NCHW pixel tensor
+// and output row m is patch m % G^2 of frame m / G^2 (G = R / 32).  With
+// P = 32 a BK = 32 stage st is one contiguous 32-pixel segment of an image
+// row (channel st / 32, patch row st % 32), so the DMA source of row m at
+// stage st is pix(m) + (st >> 5) * R^2 + (st & 31) * R: the im2col gather
+// rides on the LDS-DMA address and no patch matrix is written or read.
+template <int EPI, int CL, bool PRIO, bool DIRECT = false, bool NTS = false, bool PATCH = false>
 __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs a) {
   constexpr int BM = 256, BN = 256, NT = 512;
   constexpr int WTM = 128, WTN = 64;
@@ -281,12 +288,22 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs a) {
   const uint16_t* wsrc[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
-    asrc[j] = a.A + (int64_t)min(m0 + (wave * 2 + j) * 16 + lrow, a.M - 1) * a.lda + lchunk;
+    const int m = min(m0 + (wave * 2 + j) * 16 + lrow, a.M - 1);
+    if (PATCH) {
+      const int R = a.patch_R, G = R >> 5, p = m % (G * G);
+      asrc[j] = a.A + ((int64_t)(m / (G * G)) * 3 * R + (p / G) * 32) * R + (p % G) * 32 + lchunk;
+    } else {
+      asrc[j] = a.A + (int64_t)m * a.lda + lchunk;
+    }
     wsrc[j] = a.W + (int64_t)(n0 + (wave * 2 + j) * 16 + lrow) * a.ldw + lchunk;
   }
+  auto a_off = [&](int st) -> int64_t {
+    if (PATCH) return (int64_t)(st >> 5) * a.patch_R * a.patch_R + (st & 31) * a.patch_R;
+    return (int64_t)st * BK;
+  };
   auto issue_half = [&](int st, int j) {
     char* base = smem + (st % RING) * STAGE_BYTES;
-    glds16(asrc[j] + st * BK, base + (wave * 2 + j) * 1024);
+    glds16(asrc[j] + a_off(st), base + (wave * 2 + j) * 1024);
     glds16(wsrc[j] + st * BK, base + A_BYTES + (wave * 2 + j) * 1024);
   };
   auto wait_stage = [&](int g1) {  // retire this wave's DMA for stage g1
@@ -706,6 +723,12 @@ hipError_t launch(const GemmArgs& a, hipStream_t s) {
   // qkv, c_fc; +1.7-3 % in scripts/gemm_micro.py), the one-tile-per-workgroup
   // ping-pong (16) on N = 768 (the persistent kernel's static tile split lost
   // 1-3.5 % there against the dispatcher's dynamic one)
+  if (a.patch_R) {  // fused patch gather: f32 output rows, ping-pong only
+    if (!big || a.K != 3 * 32 * 32 || (a.patch_R & 31)) return hipErrorInvalidValue;
+    const int nt = ((a.M + 255) / 256) * (a.N / 256);
+    hipLaunchKernelGGL((gemm_pp_kernel<EPI, 1, false, false, false, true>), dim3(nt), dim3(512), 0, s, a);
+    return hipGetLastError();
+  }
   int v = a.variant == 0 ? (bf16_out ? (a.N >= 2048 && !a.group ? 18 : 16) : 3) : a.variant;
   if (v == 16 && !bf16_out) v = 3;
   if (big && v == 16 && a.K / BK >= LEAD) {

@@ -49,6 +49,11 @@ struct GemmArgs {
   const uint8_t *a_scale, *w_scale;  // MX-fp8 GEMM: e8m0 per 64 k, stage-major [K/128][rows_pad][2] (gemm_mx.hip)
   uint8_t* o_scale;                  // EPI_GELU_MX: scales of the fp8 output (same layout, rows = M)
   int ngroup;   // tile order: n-blocks per group (0 = m-major raster; gemm.hip tile_coords)
+  // Fused patch gather (gemm.hip, bf16 A only): patch_R > 0 makes A the bf16
+  // NCHW pixels [B,3,R,R] and row m the patch (m / G^2, m % G^2) of a P = 32
+  // grid (K = 3*32*32, one 32-pixel image-row segment per BK = 32 stage), so
+  // no im2col buffer is written or read.  0 = plain row-major A.
+  int patch_R = 0;
 };
 
 // Requirements: K % 64 == 0, N % 128 == 0, A/W 16-byte aligned rows.

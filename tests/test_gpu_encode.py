@@ -141,6 +141,23 @@ def test_encode_chunking_and_dtypes(gpu):
     assert np.allclose(t1, t2, atol=1e-5)
 
 
+def test_patch_gather_fused_matches_im2col(gpu):
+    """B/32 bf16 pixels take the fused patch-gather GEMM (the A-operand DMA
+    reads 32-pixel row segments straight from NCHW, no im2col buffer) when a
+    chunk has >= 1024 patch rows; f32 pixels of the same values go through
+    im2col + the plain GEMM.  Same products in the same k order: the outputs
+    must be bit-identical.  Chunks of 30 then 18 frames cover a partial last
+    M tile (1470 rows) and the small-chunk im2col fallback (882 rows)."""
+    import torch
+    from miclip import config, weights
+    cfg = config.get_config("ViT-B/32")
+    m = _model("ViT-B/32", gpu, image_chunk=30)
+    px = torch.from_numpy(weights.synthetic_pixels(48, cfg.image_resolution)).to(gpu).bfloat16()
+    fused = m.encode_image(px).cpu().numpy()
+    ref = m.encode_image(px.float()).cpu().numpy()
+    assert np.array_equal(fused, ref), np.abs(fused - ref).max()
+
+
 def test_encode_empty_and_shape_errors(gpu):
     import torch
     from miclip import _native
