@@ -235,7 +235,10 @@ def main():
     chunk = args.image_chunk
     if chunk is None:  # equal-size passes (so every GEMM launch has one shape)
         from miclip.config import get_config
-        base = max(8, 250_000 // get_config(args.model).vision_tokens)
+        # up to ~500k token rows per pass: B/32's 10k frames in one pass (one
+        # tile round fewer on the N = 768 / qkv GEMMs than two 5000-frame
+        # passes; +0.4 % measured, scripts/gpu_ab_args.sh)
+        base = max(8, 500_000 // get_config(args.model).vision_tokens)
         chunk = -(-args.frames // -(-args.frames // base))
     model, _ = api.load(args.model, device=dev, image_chunk=chunk, weights=args.weights)
     cfg = model.cfg

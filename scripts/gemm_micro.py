@@ -26,6 +26,11 @@ SHAPES = {
     "out250": (250000, 768, 768, 0),
     "fc250": (250000, 3072, 768, 1),
     "proj250": (250000, 768, 3072, 0),
+    # bench default since the single-pass change: 10000 frames = 500k rows
+    "qkv500": (500000, 2304, 768, 0),
+    "out500": (500000, 768, 768, 0),
+    "fc500": (500000, 3072, 768, 1),
+    "proj500": (500000, 768, 3072, 0),
     "long": (16384, 4096, 4096, 0),
     "qkv20k": (20000, 2304, 768, 0),
     "fc20k": (20000, 3072, 768, 1),
