@@ -427,6 +427,16 @@ static int patch_fused() {
   }
   return v;
 }
+// The first block's ln_1 fused into the vision embedding kernel (bf16 tower);
+// MICLIP_EMBED_LN1=0 keeps the separate LayerNorm pass (A/B).
+static int embed_ln1() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("MICLIP_EMBED_LN1");
+    v = e ? atoi(e) != 0 : 1;
+  }
+  return v;
+}
 // xmode of a layer's first residual_ln: the f32 stream from ln_pre is converted at layer 0
 static int xmode_at(int r16, size_t l) { return r16 ? (l == 0 ? 1 : 2) : 0; }
 
@@ -437,10 +447,12 @@ static int xmode_at(int r16, size_t l) { return r16 ? (l == 0 ? 1 : 2) : 0; }
 //   x += delta ; h = ln_2(x)                      (residual_ln)
 //   m = QuickGELU(h W_fc^T + b_fc) ; delta = m W_pr^T + b_pr
 //   x += delta ; h = ln_1'(x)  (next block)       (residual_ln)
+// h_ready: the caller already wrote h = ln_1(x) of the first block (the
+// vision embedding kernel fuses it).
 static int run_tower(mi_clip* c, const std::vector<Layer>& layers, int B, int S, int W, int causal, hipStream_t s,
-                     int r16 = 0) {
+                     int r16 = 0, bool h_ready = false) {
   const int M = B * S;
-  HIP_TRY(layernorm_bf16(c->x, W, layers[0].ln1_g, layers[0].ln1_b, c->h, W, M, W, s));
+  if (!h_ready) HIP_TRY(layernorm_bf16(c->x, W, layers[0].ln1_g, layers[0].ln1_b, c->h, W, M, W, s));
   for (size_t l = 0; l < layers.size(); ++l) {
     const Layer& L = layers[l];
     HIP_TRY(gemm_bf16(gargs(c->h, W, L.w_qkv, W, L.b_qkv, c->qkv, 3 * W, M, 3 * W, W), EPI_BF16, s));
@@ -524,9 +536,12 @@ int mi_clip_encode_image(mi_clip* c, const void* pixels, int64_t B, int in_dtype
     pg.gstride = S;
     pg.goffset = 1;
     HIP_TRY(gemm_bf16(pg, EPI_F32, s));
-    HIP_TRY(vision_embed_ln(c->x, c->cls, c->vpos, c->ln_pre_g, c->ln_pre_b, nb, S, W, s));
+    const bool fuse_ln1 = !c->fp8 && !c->vl.empty() && embed_ln1();  // the MX tower's first LN writes fp8 itself
+    HIP_TRY(vision_embed_ln(c->x, c->cls, c->vpos, c->ln_pre_g, c->ln_pre_b, nb, S, W, s,
+                            fuse_ln1 ? c->vl[0].ln1_g : nullptr, fuse_ln1 ? c->vl[0].ln1_b : nullptr,
+                            fuse_ln1 ? c->h : nullptr));
     const int r16 = resid16() && !c->vl.empty();
-    int r = c->fp8 ? run_tower_mx(c, c->vl, nb, S, W, s, r16) : run_tower(c, c->vl, nb, S, W, 0, s, r16);
+    int r = c->fp8 ? run_tower_mx(c, c->vl, nb, S, W, s, r16) : run_tower(c, c->vl, nb, S, W, 0, s, r16, fuse_ln1);
     if (r) return r;
     // ln_post(x[:, 0] + last c_proj delta) over the CLS rows only
     HIP_TRY(residual_ln(c->x, c->delta, (int64_t)S * W, 0, c->ln_post_g, c->ln_post_b, c->cls_ln, nb, W, s, nullptr,

@@ -166,9 +166,15 @@ __global__ __launch_bounds__(256) void residual_ln_kernel(float* __restrict__ x,
   ln_store(r, mean, rstd, g, b, out + (int64_t)row * W, q, qs, row, (rows + 1) & ~1, lane, n4);
 }
 
+// x = ln_pre([CLS | patches] + pos) in place (f32).  With h != nullptr the
+// first block's ln_1 runs on the same registers (h = ln_1(x) in bf16: the
+// values the stored f32 x holds, so bit-identical to a separate LayerNorm
+// pass over x) and the tower skips that pass's 4 B/element re-read of x.
 __global__ __launch_bounds__(256) void vision_embed_ln_kernel(float* __restrict__ x, const float* __restrict__ cls,
                                                               const float* __restrict__ pos, const float* __restrict__ g,
-                                                              const float* __restrict__ b, int rows, int S, int W) {
+                                                              const float* __restrict__ b, int rows, int S, int W,
+                                                              const float* __restrict__ g1,
+                                                              const float* __restrict__ b1, uint16_t* __restrict__ h) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= rows) return;
   const int t = row % S, n4 = W >> 2;
@@ -195,9 +201,14 @@ __global__ __launch_bounds__(256) void vision_embed_ln_kernel(float* __restrict_
     const int idx = lane + 64 * i;
     if (idx < n4) {
       const float4 gg = g4[idx], bb = b4[idx];
-      xr[idx] = make_float4((r.v[i].x - mean) * rstd * gg.x + bb.x, (r.v[i].y - mean) * rstd * gg.y + bb.y,
-                            (r.v[i].z - mean) * rstd * gg.z + bb.z, (r.v[i].w - mean) * rstd * gg.w + bb.w);
+      r.v[i] = make_float4((r.v[i].x - mean) * rstd * gg.x + bb.x, (r.v[i].y - mean) * rstd * gg.y + bb.y,
+                           (r.v[i].z - mean) * rstd * gg.z + bb.z, (r.v[i].w - mean) * rstd * gg.w + bb.w);
+      xr[idx] = r.v[i];
     }
+  }
+  if (h) {  // wave-uniform
+    ln_stats(r, n4, lane, W, mean, rstd);
+    ln_store(r, mean, rstd, g1, b1, h + (int64_t)row * W, nullptr, nullptr, row, 0, lane, n4);
   }
 }
 
@@ -368,11 +379,12 @@ hipError_t layernorm_bf16(const float* x, int64_t in_stride, const float* g, con
 }
 
 hipError_t vision_embed_ln(float* x, const float* cls, const float* pos, const float* g, const float* b, int B,
-                           int S, int W, hipStream_t s) {
+                           int S, int W, hipStream_t s, const float* g1, const float* b1, uint16_t* h) {
   const int rows = B * S;
   if (rows <= 0) return hipSuccess;
   if (W % 4 || W > 1024) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(vision_embed_ln_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, x, cls, pos, g, b, rows, S, W);
+  hipLaunchKernelGGL(vision_embed_ln_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, x, cls, pos, g, b, rows, S, W,
+                     g1, b1, h);
   return hipGetLastError();
 }
 

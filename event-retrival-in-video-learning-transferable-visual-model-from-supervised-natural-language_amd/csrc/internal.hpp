@@ -69,9 +69,11 @@ hipError_t quantize_mx(const uint16_t* in, int64_t ld_in, uint8_t* q, int64_t ld
 hipError_t layernorm_bf16(const float* x, int64_t in_stride, const float* g, const float* b,
                           uint16_t* out, int64_t out_stride, int rows, int W, hipStream_t s,
                           uint8_t* q = nullptr, uint8_t* qs = nullptr);
-// x[b*S + t] = LN((t == 0 ? cls : x[b*S + t]) + pos[t]) in place (f32)
+// x[b*S + t] = LN((t == 0 ? cls : x[b*S + t]) + pos[t]) in place (f32); with
+// h != nullptr also h = LN_{g1,b1}(x) in bf16 (the first block's ln_1, fused)
 hipError_t vision_embed_ln(float* x, const float* cls, const float* pos, const float* g,
-                           const float* b, int B, int S, int W, hipStream_t s);
+                           const float* b, int B, int S, int W, hipStream_t s, const float* g1 = nullptr,
+                           const float* b1 = nullptr, uint16_t* h = nullptr);
 // x[q*S + t] = tok_emb[tokens[q*S + t]] + pos[t]
 hipError_t text_embed(const int32_t* tokens, const float* tok_emb, const float* pos, float* x,
                       int Q, int S, int W, int vocab, hipStream_t s);
