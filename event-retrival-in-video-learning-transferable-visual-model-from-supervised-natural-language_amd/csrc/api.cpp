@@ -659,6 +659,14 @@ int mi_op_gemm(const void* A, const void* W, const float* bias, void* out, int32
   return MI_OK;
 }
 
+// Diagnostics: timestamps of the GEMM timing-probe variant (19), 4 per
+// workgroup (not part of include/miclip.h; scripts/gemm_micro.py only).
+extern "C" int mi_debug_gemm_probe(unsigned long long* host, int32_t n) {
+  if (!host || n < 0) return fail(MI_ERR_ARG, "mi_debug_gemm_probe: bad arguments");
+  HIP_TRY(gemm_probe_read(host, n));
+  return MI_OK;
+}
+
 int mi_op_layernorm(const float* x, const float* g, const float* b, void* out, int32_t rows, int32_t W,
                     void* stream) {
   if (!x || !g || !b || !out || rows < 0) return fail(MI_ERR_ARG, "mi_op_layernorm: bad arguments");

@@ -515,16 +515,21 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs a) {
 // Persistent ping-pong (variant 18, bf16 outputs): gemm_pp_kernel's schedule
 // (CL = 1) with one workgroup per CU walking its tiles, so a tile's epilogue
 // overlaps the next tile's prologue and store drain:
-//   end of tile: realign the wave groups, issue the NEXT tile's first LEAD
-//   stages (all reads of the ring are done), then the direct-store epilogue of
-//   this tile.  The 16 stores per wave are younger than those three stages and
-//   older than every later one, so the counted waits of the next tile add the
-//   stores only while waiting for stages < LEAD; the first wait that has to
-//   cover them is stage LEAD's, three stages (~3k cycles) after they issued.
+//   the stages of all of a workgroup's tiles are one stream through the ring:
+//   the NEXT tile's first LEAD stages (and its bias) are issued in this tile's
+//   last LEAD main-loop iterations, into the ring slots a continuous pipeline
+//   would use (same WAR rule as inside a tile), so they have landed by the end
+//   of this tile's direct-store epilogue.  The 16 stores per wave are younger
+//   than those three stages and older than every later one, so the counted
+//   waits of the next tile add the stores only while waiting for stages < LEAD;
+//   the first wait that has to cover them is stage LEAD's, three stages (~3k
+//   cycles) after they issued.  (Issuing the next tile's stages only after the
+//   main loop, the previous form, measured 0-4 % slower.)
 //   A partial last m-tile (lanes with m >= M skip their stores) drains with
 //   vmcnt(0) instead, since its store count is not the fixed 16.
 //   A tile's bias (256 f32) is LDS-DMA'd by wave 0 into one of two LDS slots
-//   (tile parity) just before that tile's first stages are issued: older than
+//   (tile parity; the previous tile's epilogue finished reading the slot
+//   before this tile started) just before that tile's first stages are issued: older than
 //   them, it has landed once the tile's first stage wait + barrier return, and
 //   the epilogue reads it with an LDS read hipcc does not see.  A plain global
 //   load of the bias there made hipcc drain the prefetch with vmcnt(0).
@@ -539,7 +544,13 @@ __device__ __forceinline__ void vm_wait_n(int n) {  // n wave-uniform; unlisted 
   }
 }
 
-template <int EPI>
+// Timing probe (variant 19, scripts/gemm_micro.py): s_memrealtime stamps
+// (100 MHz) of each workgroup's third tile - main loop start, main loop end,
+// epilogue stores issued, next tile's main loop start - kept in SGPRs and
+// written once at kernel end (a mid-loop store would break the counted waits).
+__device__ unsigned long long g_gemm_probe[4096 * 4];
+
+template <int EPI, bool PROBE = false>
 __global__ __launch_bounds__(512) void gemm_ppp_kernel(GemmArgs a) {
   constexpr int BM = 256, BN = 256;
   constexpr int WTM = 128, WTN = 64;
@@ -574,8 +585,8 @@ __global__ __launch_bounds__(512) void gemm_ppp_kernel(GemmArgs a) {
       wsrc[j] = a.W + (int64_t)(nn + (wave * 2 + j) * 16 + lrow) * a.ldw + lchunk;
     }
   };
-  auto issue = [&](int st) {
-    char* base = smem + (st % RING) * STAGE_BYTES;
+  auto issue = [&](int st, int slot) {  // stage st of the tile set_src points at -> ring slot
+    char* base = smem + slot * STAGE_BYTES;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       glds16(asrc[j] + st * BK, base + (wave * 2 + j) * 1024);
@@ -583,8 +594,14 @@ __global__ __launch_bounds__(512) void gemm_ppp_kernel(GemmArgs a) {
     }
   };
   int pend = 0;  // the previous tile's stores are in flight, younger than stages 0..LEAD-1
+  // The stages of a workgroup's tiles form ONE stream through the ring: the
+  // next tile's first LEAD stages are issued in this tile's last LEAD main-loop
+  // iterations (where a single tile's pipeline would run dry), so they have
+  // landed before the epilogue ends.  rb = ring slot of this tile's stage 0.
+  int rb = 0, nm0 = 0, nn0 = 0;
+  bool has_next = false;
   auto wait_stage = [&](int g1) {
-    const int younger = min(LEAD - 1, nk - 1 - g1);
+    const int younger = has_next ? LEAD - 1 : min(LEAD - 1, nk - 1 - g1);
     vm_wait_n(4 * younger + (g1 < LEAD ? pend : 0));
   };
   auto barrier = [&]() {
@@ -607,12 +624,21 @@ __global__ __launch_bounds__(512) void gemm_ppp_kernel(GemmArgs a) {
   set_src(m0, n0);
 #pragma unroll
   for (int st = 0; st < LEAD; ++st)
-    if (st < nk) issue(st);
+    if (st < nk) issue(st, st);
   const int rd = (lane & 15) * 64 + (((lane >> 4) ^ swz((lane >> 2) & 3)) * 16);
+  int ti = 0;
+  unsigned long long ts0 = 0, ts1 = 0, ts2 = 0, ts3 = 0;
   while (true) {
+    const int nvb = vb + gridDim.x;
+    has_next = nvb < ntiles;
+    if (has_next) coords(nvb, nm0, nn0);
     wait_stage(0);
     barrier();
     if (grp == 1) barrier();
+    if (PROBE) {
+      if (ti == 2) ts0 = __builtin_amdgcn_s_memrealtime();
+      if (ti == 3) ts3 = __builtin_amdgcn_s_memrealtime();
+    }
     f32x4 acc[8][4];
 #pragma unroll
     for (int i = 0; i < 8; ++i)
@@ -620,9 +646,19 @@ __global__ __launch_bounds__(512) void gemm_ppp_kernel(GemmArgs a) {
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     bf16x8 bfr[4], af[8];
     for (int gs = 0; gs < nk; ++gs) {
-      const char* As = smem + (gs % RING) * STAGE_BYTES + (grp * WTM) * 64;
-      const char* Ws = smem + (gs % RING) * STAGE_BYTES + A_BYTES + (wc * WTN) * 64;
-      if (gs + LEAD < nk) issue(gs + LEAD);
+      const int slot = (rb + gs) % RING;
+      const char* As = smem + slot * STAGE_BYTES + (grp * WTM) * 64;
+      const char* Ws = smem + slot * STAGE_BYTES + A_BYTES + (wc * WTN) * 64;
+      if (gs + LEAD < nk) {
+        issue(gs + LEAD, (rb + gs + LEAD) % RING);
+      } else if (has_next) {  // the next tile's stage gs + LEAD - nk, same ring position in the stream
+        const int st = gs + LEAD - nk;
+        if (st == 0) {
+          load_bias(tpar ^ 1, nn0);
+          set_src(nm0, nn0);
+        }
+        issue(st, (rb + gs + LEAD) % RING);
+      }
 #pragma unroll
       for (int ni = 0; ni < 4; ++ni) bfr[ni] = *(const bf16x8*)(Ws + ni * 16 * 64 + rd);
 #pragma unroll
@@ -638,19 +674,10 @@ __global__ __launch_bounds__(512) void gemm_ppp_kernel(GemmArgs a) {
       barrier();
     }
     if (grp == 0) barrier();  // groups realigned; every ring read of this tile is done
+    if (PROBE && ti == 2) ts1 = __builtin_amdgcn_s_memrealtime();
 
-    // next tile's first stages go out before this tile's stores
+    // the next tile's first stages are already in flight (issued in the main loop)
     const int cm0 = m0, cn0 = n0;
-    vb += gridDim.x;
-    const bool has_next = vb < ntiles;
-    if (has_next) {
-      coords(vb, m0, n0);
-      load_bias(tpar ^ 1, n0);
-      set_src(m0, n0);
-#pragma unroll
-      for (int st = 0; st < LEAD; ++st)
-        if (st < nk) issue(st);
-    }
     // ---- epilogue of tile (cm0, cn0): direct permlane-swapped row stores (gemm_pp_kernel DIRECT)
     float4 bias[4];
 #pragma unroll
@@ -678,7 +705,13 @@ __global__ __launch_bounds__(512) void gemm_ppp_kernel(GemmArgs a) {
         if (m < a.M) *(uint4*)((uint16_t*)a.out + (int64_t)m * a.ldo + col) = make_uint4(sx[0], sy[0], sx[1], sy[1]);
       }
     }
+    if (PROBE && ti == 2) ts2 = __builtin_amdgcn_s_memrealtime();
+    ++ti;
     if (!has_next) break;
+    vb = nvb;
+    m0 = nm0;
+    n0 = nn0;
+    rb = (rb + nk) % RING;
     tpar ^= 1;
     if (cm0 + BM <= a.M) {
       pend = NSTORE;
@@ -686,6 +719,10 @@ __global__ __launch_bounds__(512) void gemm_ppp_kernel(GemmArgs a) {
       pend = 0;
       vm_wait_all();
     }
+  }
+  if (PROBE && wave == 0 && lane == 0 && blockIdx.x < 4096) {
+    unsigned long long* d = g_gemm_probe + blockIdx.x * 4;
+    d[0] = ts0; d[1] = ts1; d[2] = ts2; d[3] = ts3;
   }
 }
 
@@ -742,6 +779,12 @@ hipError_t launch(const GemmArgs& a, hipStream_t s) {
     hipLaunchKernelGGL((gemm_ppp_kernel<EPI>), dim3(grid), dim3(512), 0, s, a);
     return hipGetLastError();
   }
+  if (big && v == 19 && bf16_out && a.K / BK >= LEAD && !a.group) {  // persistent + timing probe
+    const int nt = ((a.M + 255) / 256) * (a.N / 256);
+    const int grid = nt < cu_count() ? nt : cu_count();
+    hipLaunchKernelGGL((gemm_ppp_kernel<EPI, true>), dim3(grid), dim3(512), 0, s, a);
+    return hipGetLastError();
+  }
   if (big && v == 17 && bf16_out && a.K / BK >= LEAD) {  // experiment: non-temporal output stores
     const int nt = ((a.M + 255) / 256) * (a.N / 256);
     hipLaunchKernelGGL((gemm_pp_kernel<EPI, 1, false, true, true>), dim3(nt), dim3(512), 0, s, a);
@@ -778,6 +821,11 @@ hipError_t launch(const GemmArgs& a, hipStream_t s) {
 }
 
 }  // namespace
+
+hipError_t gemm_probe_read(unsigned long long* host, int n) {
+  if (n > 4096 * 4) n = 4096 * 4;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_gemm_probe), n * sizeof(unsigned long long), 0, hipMemcpyDeviceToHost);
+}
 
 hipError_t gemm_bf16(const GemmArgs& a, int epi, hipStream_t s) {
   if (a.M <= 0) return hipSuccess;

@@ -58,6 +58,8 @@ struct GemmArgs {
 
 // Requirements: K % 64 == 0, N % 128 == 0, A/W 16-byte aligned rows.
 hipError_t gemm_bf16(const GemmArgs& a, int epi, hipStream_t s);
+// variant 19's per-workgroup timestamps (gemm.hip g_gemm_probe) -> host
+hipError_t gemm_probe_read(unsigned long long* host, int n);
 // MX-fp8: A, W e4m3 bytes (row strides lda/ldw in BYTES), a_scale/w_scale e8m0; K % 128 == 0, N % 256 == 0
 hipError_t gemm_mx(const GemmArgs& a, int epi, hipStream_t s);
 // bf16 [rows][K] -> e4m3 [rows][K] + e8m0 scales [K/128][rows_pad][2] (one per 64 k; K % 128 == 0)
