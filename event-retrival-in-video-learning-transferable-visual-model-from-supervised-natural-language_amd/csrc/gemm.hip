@@ -757,16 +757,19 @@ hipError_t launch(const GemmArgs& a, hipStream_t s) {
   // 1 = persistent ring; 8 = main-loop-only timing probe (no epilogue).
   const bool bf16_out = EPI == EPI_BF16 || EPI == EPI_GELU_BF16;
   // default for bf16 outputs: the persistent ping-pong (18) on wide GEMMs (N >= 2048:
-  // qkv, c_fc; +1.7-3 % in scripts/gemm_micro.py), the one-tile-per-workgroup
-  // ping-pong (16) on N = 768 (the persistent kernel's static tile split lost
-  // 1-3.5 % there against the dispatcher's dynamic one)
+  // qkv, c_fc; +1.7-3 % in scripts/gemm_micro.py) and on K <= 1024 (out_proj),
+  // the one-tile-per-workgroup ping-pong (16) on N = 768 with long K (c_proj:
+  // the persistent kernel's static tile split loses 3.8 % there against the
+  // dispatcher's dynamic one)
   if (a.patch_R) {  // fused patch gather: f32 output rows, ping-pong only
     if (!big || a.K != 3 * 32 * 32 || (a.patch_R & 31)) return hipErrorInvalidValue;
     const int nt = ((a.M + 255) / 256) * (a.N / 256);
     hipLaunchKernelGGL((gemm_pp_kernel<EPI, 1, false, false, false, true>), dim3(nt), dim3(512), 0, s, a);
     return hipGetLastError();
   }
-  int v = a.variant == 0 ? (bf16_out ? (a.N >= 2048 && !a.group ? 18 : 16) : 3) : a.variant;
+  // (N = 768: persistent on K = 768 since the stage streaming, +5 % on out500;
+  // c_proj, K = 3072, stays one tile per workgroup: -3.8 % persistent)
+  int v = a.variant == 0 ? (bf16_out ? ((a.N >= 2048 || a.K <= 1024) && !a.group ? 18 : 16) : 3) : a.variant;
   if (v == 16 && !bf16_out) v = 3;
   if (big && v == 16 && a.K / BK >= LEAD) {
     const int nt = ((a.M + 255) / 256) * (a.N / 256);
