@@ -550,7 +550,9 @@ __device__ __forceinline__ void vm_wait_n(int n) {  // n wave-uniform; unlisted 
 // written once at kernel end (a mid-loop store would break the counted waits).
 __device__ unsigned long long g_gemm_probe[4096 * 4];
 
-template <int EPI, bool PROBE = false>
+// EARLY (variant 20): group 0, one section ahead, issues its epilogue during
+// group 1's last MFMA section and realigns afterwards (same barrier count).
+template <int EPI, bool PROBE = false, bool EARLY = false>
 __global__ __launch_bounds__(512) void gemm_ppp_kernel(GemmArgs a) {
   constexpr int BM = 256, BN = 256;
   constexpr int WTM = 128, WTN = 64;
@@ -673,7 +675,7 @@ __global__ __launch_bounds__(512) void gemm_ppp_kernel(GemmArgs a) {
       if (grp == 0 && gs + 1 < nk) wait_stage(gs + 1);
       barrier();
     }
-    if (grp == 0) barrier();  // groups realigned; every ring read of this tile is done
+    if (!EARLY && grp == 0) barrier();  // groups realigned; every ring read of this tile is done
     if (PROBE && ti == 2) ts1 = __builtin_amdgcn_s_memrealtime();
 
     // the next tile's first stages are already in flight (issued in the main loop)
@@ -705,6 +707,7 @@ __global__ __launch_bounds__(512) void gemm_ppp_kernel(GemmArgs a) {
         if (m < a.M) *(uint4*)((uint16_t*)a.out + (int64_t)m * a.ldo + col) = make_uint4(sx[0], sy[0], sx[1], sy[1]);
       }
     }
+    if (EARLY && grp == 0) barrier();
     if (PROBE && ti == 2) ts2 = __builtin_amdgcn_s_memrealtime();
     ++ti;
     if (!has_next) break;
@@ -780,6 +783,12 @@ hipError_t launch(const GemmArgs& a, hipStream_t s) {
     const int nt = ((a.M + 255) / 256) * (a.N / 256);
     const int grid = nt < cu_count() ? nt : cu_count();
     hipLaunchKernelGGL((gemm_ppp_kernel<EPI>), dim3(grid), dim3(512), 0, s, a);
+    return hipGetLastError();
+  }
+  if (big && v == 20 && bf16_out && a.K / BK >= LEAD && !a.group) {  // persistent, early group-0 epilogue
+    const int nt = ((a.M + 255) / 256) * (a.N / 256);
+    const int grid = nt < cu_count() ? nt : cu_count();
+    hipLaunchKernelGGL((gemm_ppp_kernel<EPI, false, true>), dim3(grid), dim3(512), 0, s, a);
     return hipGetLastError();
   }
   if (big && v == 19 && bf16_out && a.K / BK >= LEAD && !a.group) {  // persistent + timing probe
