@@ -8,10 +8,14 @@ the GPU, inputs resident in HBM before the timed region:
   (N>1) RCCL all-gather of the per-shard top-k + merge kernel
 Workload at N=1 is BASELINE.json configs[1] (ViT-B/32 bf16, 10k frames x 32
 queries, top-10); with --gpus N each rank embeds its own 10k-frame shard
-(weak scaling, configs[3]'s design).
+(weak scaling), or with --global-frames G one G-frame corpus is split into N
+contiguous shards (strong scaling; configs[3] = --global-frames 1000000 on 8).
 
-Launch: python bench.py [--gpus N --steps K --warmup W]; for N>1 under
-torch.distributed.run (RCCL backend "nccl").  Rank 0 prints ONE JSON line.
+Launch: python bench.py [--gpus N --steps K --warmup W].  With N > 1 and no
+WORLD_SIZE in the environment this process starts torch.distributed.run with
+N workers (one per GPU, RCCL backend "nccl") as a child, before touching the
+GPU; under torch.distributed.run directly it is one of the N ranks.  Rank 0
+prints ONE JSON line.
 """
 from __future__ import annotations
 
@@ -39,14 +43,22 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--model", default="ViT-B/32")
-    ap.add_argument("--frames", type=int, default=10_000, help="frames per GPU (corpus shard)")
+    ap.add_argument("--frames", type=int, default=10_000, help="frames per GPU (weak scaling: each rank's shard)")
+    ap.add_argument("--global-frames", type=int, default=None,
+                    help="strong scaling: one corpus of this many frames split into contiguous shards "
+                         "(configs[3]: 1000000 over 8 GPUs = 125k per rank)")
     ap.add_argument("--queries", type=int, default=32)
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--image-chunk", type=int, default=None)
     ap.add_argument("--weights", choices=["bf16", "fp8"], default="bf16",
                     help="fp8: vision GEMMs on the MX-fp8 block-scaled MFMA (BASELINE configs[4])")
-    ap.add_argument("--cpu-frames", type=int, default=768,
-                    help="CPU baseline sample: frames encoded at batch 64 (BASELINE configs[0]), ~10-20 s of CPU work")
+    ap.add_argument("--cpu-frames", type=int, default=256,
+                    help="CPU baseline sample: frames encoded at batch 64 (secondary figure)")
+    ap.add_argument("--cpu-frames-b1", type=int, default=64,
+                    help="CPU baseline sample: frames encoded one per call (Backend/embedding.py; configs[0]'s 64)")
+    ap.add_argument("--no-rank-roofline", action="store_true")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher rehearsal on CPU/gloo: rendezvous + all-gather, no GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
     return ap.parse_args()
@@ -179,51 +191,176 @@ def rank_timing(corpus, txt, k, reps=50):
             "tflops_f32": round(2.0 * corpus.shape[0] * txt.shape[0] * corpus.shape[1] / us / 1e6, 2)}
 
 
-def cpu_baseline(cfg, n_frames_metric, Q, k, sample_frames):
-    """Oracle (numpy fp32 restatement of the reference CPU path) on a bounded
-    sample: `sample_frames` frames encoded at batch 64 (configs[0]) + 1 text
-    query + np.dot/np.argsort ranking over an N-row corpus
-    (embedding_service.py:314-320); extrapolated to the metric's workload."""
-    import numpy as np
-    from miclip import weights
-    from oracle import clip_ref, rank_ref
+def _cpu_model():
     try:
-        from threadpoolctl import threadpool_info
-        cores = max(i.get("num_threads", 1) for i in threadpool_info()) if threadpool_info() else os.cpu_count()
-    except Exception:
-        cores = os.cpu_count()
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(cfg, n_frames_metric, Q, k, b1_frames, b64_frames):
+    """The reference CPU path timed on this box's host cores (BASELINE.md
+    CPU-baseline plan): the torch-CPU fp32 restatement of openai/CLIP
+    (oracle/clip_torch.py) run as Backend/embedding.py does on a CPU host,
+    one image per call (embedding.py:39-52, `b1_frames` frames = configs[0]'s
+    64) and, secondarily, at batch 64 (`b64_frames` frames); one encode_text;
+    np.dot + np.argsort(s)[::-1][:k] over an N-row corpus
+    (embedding_service.py:314-320).  Extrapolated to the metric's workload
+    (N frames embedded + Q queries ranked).  The numpy restatement
+    (oracle/clip_ref.py) at batch 64 is reported beside it."""
+    import numpy as np
+    import torch
+    from miclip import weights
+    from oracle import clip_ref, clip_torch, rank_ref
+    threads = int(os.environ.get("OMP_NUM_THREADS") or 0) or os.cpu_count()
+    torch.set_num_threads(threads)
     sd = weights.make_state_dict(cfg)
-    px = weights.synthetic_pixels(sample_frames, cfg.image_resolution)
+    m = clip_torch.TorchCLIP(sd, cfg)
+    n_px = max(b1_frames, b64_frames, 64)
+    px = weights.synthetic_pixels(n_px, cfg.image_resolution)
     tk = weights.synthetic_tokens(1, cfg.context_length, cfg.vocab_size)
+    m.encode_image(px[:1])                                  # warm-up (allocator, thread pool)
     t0 = time.perf_counter()
-    emb = np.concatenate([clip_ref.encode_image(px[i:i + 64], sd, cfg) for i in range(0, sample_frames, 64)])
-    t_img = (time.perf_counter() - t0) / sample_frames
+    emb = np.concatenate([m.encode_image(px[i:i + 1]) for i in range(b1_frames)])
+    t_b1 = (time.perf_counter() - t0) / b1_frames
     t0 = time.perf_counter()
-    txt = clip_ref.encode_text(tk, sd, cfg)
+    for i in range(0, b64_frames, 64):
+        m.encode_image(px[i:i + 64])
+    t_b64 = (time.perf_counter() - t0) / b64_frames
+    t0 = time.perf_counter()
+    np.concatenate([clip_ref.encode_image(px[i:i + 64], sd, cfg) for i in range(0, 64, 64)])
+    t_np = (time.perf_counter() - t0) / 64
+    t0 = time.perf_counter()
+    txt = m.encode_text(tk)
     t_txt = time.perf_counter() - t0
-    corpus = np.tile(emb, (n_frames_metric // sample_frames + 1, 1))[:n_frames_metric]
+    corpus = np.tile(emb, (n_frames_metric // emb.shape[0] + 1, 1))[:n_frames_metric]
     frames = list(range(n_frames_metric))
     t0 = time.perf_counter()
     rank_ref.search_top_frames_ref(corpus, txt, k, frames)
     t_rank = time.perf_counter() - t0
-    total = n_frames_metric * t_img + Q * t_txt + Q * t_rank
-    return {"value": round(n_frames_metric / total, 2), "unit": "frames/s", "cores": int(cores), "kind": "port",
-            "sample": f"oracle numpy fp32 (reference CPU path restated): {sample_frames} frames at batch 64 "
-                      f"({t_img * 1e3:.1f} ms/frame) + 1 encode_text ({t_txt * 1e3:.1f} ms) + np.dot/argsort over "
-                      f"{n_frames_metric} rows ({t_rank * 1e3:.2f} ms/query); extrapolated to "
-                      f"{n_frames_metric} frames x {Q} queries"}
+
+    def rate(t_img):
+        return n_frames_metric / (n_frames_metric * t_img + Q * t_txt + Q * t_rank)
+
+    return {"value": round(rate(t_b1), 2), "unit": "frames/s", "cores": int(threads), "kind": "port",
+            "nproc": os.cpu_count(), "cpu_model": _cpu_model(),
+            "batch64_value": round(rate(t_b64), 2), "numpy_batch64_value": round(rate(t_np), 2),
+            "sample": f"torch-CPU fp32 restatement of openai/CLIP (oracle/clip_torch.py), {threads} threads: "
+                      f"{b1_frames} frames one per call as Backend/embedding.py:39-52 ({t_b1 * 1e3:.1f} ms/frame; "
+                      f"batch 64 over {b64_frames} frames: {t_b64 * 1e3:.1f} ms/frame; numpy oracle batch 64: "
+                      f"{t_np * 1e3:.1f} ms/frame) + 1 encode_text ({t_txt * 1e3:.1f} ms) + np.dot/argsort over "
+                      f"{n_frames_metric} rows ({t_rank * 1e3:.2f} ms/query); extrapolated to {n_frames_metric} "
+                      f"frames x {Q} queries"}
+
+
+def rank_roofline(dev, reps=20):
+    """The fused normalise + cosine + top-k kernel (mi_rank_topk) at sizes where
+    it is HBM-bound (N*D*elt bytes per launch against the HBM
+    roofline), HIP events on the launch stream: configs[3]'s 125k-row shard
+    and a 1M-row corpus, D = 512 / 768, Q = 32 / 1000, f32 and bf16 rows."""
+    import torch
+    from miclip import retrieval
+    out = {}
+    g = torch.Generator(device=dev).manual_seed(3)
+    for (N, D, Q, dt) in [(125_000, 512, 32, torch.float32), (1_000_000, 512, 32, torch.float32),
+                          (1_000_000, 512, 32, torch.bfloat16), (1_000_000, 768, 32, torch.float32),
+                          (1_000_000, 768, 1000, torch.float32)]:
+        corpus = torch.randn(N, D, device=dev, generator=g).to(dt)
+        q = torch.nn.functional.normalize(torch.randn(Q, D, device=dev, generator=g), dim=1)
+        retrieval.rank_topk(corpus, q, 10)
+        torch.cuda.synchronize(dev)
+        stream = torch.cuda.current_stream(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        n = reps if Q <= 32 else 3
+        e0.record(stream)
+        for _ in range(n):
+            retrieval.rank_topk(corpus, q, 10)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        us = e0.elapsed_time(e1) * 1e3 / n
+        nbytes = corpus.numel() * corpus.element_size()
+        name = f"N{N // 1000}k_D{D}_Q{Q}_{'f32' if dt == torch.float32 else 'bf16'}"
+        out[name] = {"us": round(us, 1), "gbs": round(nbytes / us / 1e3, 1),
+                     "hbm_frac": round(nbytes / us / 1e3 / HBM_PEAK_GBS, 4),
+                     "tflops_f32_mfma": round(2.0 * N * Q * D / us / 1e6, 2)}
+        del corpus
+    return out
+
+
+def launch_workers(args):
+    """`bench.py --gpus N` without torch.distributed.run: start N worker
+    processes (one per GPU) through torch.distributed.run as a CHILD process,
+    before this process touches the GPU, and return its exit code."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    return subprocess.call(cmd, env=env)
+
+
+def dry_run(args, world, rank):
+    """Launcher rehearsal on CPU (gloo): the same rendezvous, barrier,
+    max-over-ranks timing and top-k all-gather + merge shape as the GPU run,
+    with no GPU and no kernels (tests/test_bench_launcher.py)."""
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+    Q, k = args.queries, args.k
+    t0 = time.perf_counter()
+    s = torch.full((Q, k), float(rank))
+    i = torch.arange(Q * k, dtype=torch.int64).reshape(Q, k) + rank * 1_000_000
+    if world > 1:
+        gs = [torch.empty_like(s) for _ in range(world)]
+        gi = [torch.empty_like(i) for _ in range(world)]
+        dist.all_gather(gs, s)
+        dist.all_gather(gi, i)
+        ok = all(bool((gs[r] == r).all()) and bool((gi[r] // 1_000_000 == r).all()) for r in range(world))
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        seen = dist.get_world_size()
+    else:
+        ok, seen = True, 1
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": args.gpus, "world_size_seen": seen, "gather_ok": ok}),
+              flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 def main():
     args = parse()
+    world_env = int(os.environ.get("WORLD_SIZE", "0"))
+    if world_env == 0 and args.gpus > 1:
+        sys.exit(launch_workers(args))         # the parent never touches the GPU
+    world = world_env or 1
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch with `python -m torch.distributed.run "
+              f"--nnodes=1 --nproc-per-node {args.gpus} --master-addr 127.0.0.1 --master-port P bench.py --gpus "
+              f"{args.gpus} ...` or plain `python bench.py --gpus {args.gpus}`", file=sys.stderr)
+        sys.exit(2)
+    if args.dry_run:
+        return dry_run(args, world, rank)
+
     import numpy as np
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    os.environ.setdefault("MICLIP_SYNTHETIC_WEIGHTS", "1")     # random-init weights of the architecture (data: synthetic)
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -232,24 +369,28 @@ def main():
 
     from miclip import api, distributed, retrieval, weights
 
+    strong = args.global_frames is not None
+    if strong:     # configs[3]/[4]: a fixed corpus split into contiguous shards
+        lo, hi = distributed.shard_range(args.global_frames, world, rank)
+        Nf, base = hi - lo, lo
+    else:          # weak scaling: every rank embeds its own --frames shard
+        Nf, base = args.frames, rank * args.frames
     chunk = args.image_chunk
     if chunk is None:  # equal-size passes (so every GEMM launch has one shape)
         from miclip.config import get_config
         # up to ~500k token rows per pass: B/32's 10k frames in one pass (one
         # tile round fewer on the N = 768 / qkv GEMMs than two 5000-frame
         # passes; +0.4 % measured, scripts/gpu_ab_args.sh)
-        base = max(8, 500_000 // get_config(args.model).vision_tokens)
-        chunk = -(-args.frames // -(-args.frames // base))
+        cap = max(8, 500_000 // get_config(args.model).vision_tokens)
+        chunk = -(-Nf // -(-Nf // cap))
     model, _ = api.load(args.model, device=dev, image_chunk=chunk, weights=args.weights)
     cfg = model.cfg
     chunk = model._chunks[0]
-    Nf, Q, k = args.frames, args.queries, args.k
+    Q, k = args.queries, args.k
     R = cfg.image_resolution
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     pixels = torch.randn(Nf, 3, R, R, device=dev, generator=g, dtype=torch.float32).bfloat16()
     tokens = torch.from_numpy(weights.synthetic_tokens(Q, cfg.context_length, cfg.vocab_size)).to(dev)
-    corpus = torch.empty(Nf, cfg.embed_dim, device=dev)
-    base = rank * Nf
 
     def step():
         emb = model.encode_image(pixels, out_dtype=torch.float32)
@@ -272,15 +413,16 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
+    seen = 1
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
+        seen = dist.get_world_size()
     assert torch.isfinite(top_s[:, 0]).all() and (top_i[:, 0] >= 0).all()
-    del corpus
 
     ms = elapsed / args.steps * 1e3
-    total_frames = Nf * world * args.steps
+    total_frames = (args.global_frames if strong else Nf * world) * args.steps
     value = total_frames / elapsed
     result = None
     if rank == 0:
@@ -288,9 +430,10 @@ def main():
         txt = model.encode_text(tokens, normalize=True, out_dtype=torch.float32)
         kern["rank_topk"] = rank_timing(emb, txt, k)
         kern["preprocess_720p"] = preprocess_timing(dev, cfg.image_resolution)
+        rank_roof = None if args.no_rank_roofline else rank_roofline(dev)
         F_frame, F_text = cfg.image_flops(), cfg.text_flops()
-        step_flops = Nf * F_frame + Q * F_text + 2.0 * Nf * Q * cfg.embed_dim
-        mfma_frac = step_flops / (ms / 1e3) / (BF16_PEAK_TFLOPS * 1e12)
+        step_flops = Nf * world * F_frame + Q * world * F_text + 2.0 * Nf * world * Q * cfg.embed_dim
+        mfma_frac = step_flops / (ms / 1e3) / (BF16_PEAK_TFLOPS * 1e12) / world
         dom = kern.get("gemm_fc")
         M = chunk * cfg.vision_tokens
         roof = None
@@ -314,20 +457,28 @@ def main():
                     "avg_launch_us": dom["us"]}
         cpu = None
         if not args.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline(cfg, Nf, Q, k, args.cpu_frames)
+            cpu = cpu_baseline(cfg, Nf, Q, k, args.cpu_frames_b1, args.cpu_frames)
+        workload = f"{cfg.name} {args.weights}, "
+        if strong:
+            workload += f"{args.global_frames} frames over {world} shards x {Q} text queries, top-{k}"
+        else:
+            workload += f"{Nf} frames/GPU x {Q} text queries, top-{k}"
+        if world > 1:
+            workload += " (RCCL all-gather top-k)"
+        elif (cfg.name, Nf, Q, k) == ("ViT-B/32", 10_000, 32, 10):
+            workload += " (BASELINE configs[1])"
         result = {
             "metric": "frames/sec embedded+ranked, ViT-B/32 224², 1/2/4/8 MI355X; R@1/5/10 parity",
-            "value": round(value, 1), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "bf16" if args.weights == "bf16" else "fp8-e4m3(MX) vision GEMMs, bf16 rest", "data": "synthetic (random pixels/tokens, deterministic "
-                                                          "random-init weights of the real architecture)",
-            "config": {"workload": f"{cfg.name} {args.weights}, {Nf} frames/GPU x {Q} text queries, top-{k}"
-                                   + (f" ({world} shards, RCCL all-gather top-k)" if world > 1 else
-                                      " (BASELINE configs[1])" if (cfg.name, Nf, Q, k) == ("ViT-B/32", 10_000, 32, 10)
-                                      else ""),
-                       "frames_per_gpu": Nf, "global_frames": Nf * world, "queries": Q, "k": k,
+            "value": round(value, 1), "unit": "frames/s", "n_gpus": world, "world_size_seen": seen,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
+            "scaling": "strong" if strong else "weak", "vs_baseline": None,
+            "dtype": "bf16" if args.weights == "bf16" else "fp8-e4m3(MX) vision GEMMs, bf16 rest",
+            "data": "synthetic (random pixels/tokens, deterministic random-init weights of the real architecture)",
+            "config": {"workload": workload, "frames_per_gpu": Nf,
+                       "global_frames": args.global_frames if strong else Nf * world, "queries": Q, "k": k,
                        "image_chunk": chunk, "parallelism": f"dp{world}"},
             "roofline": roof,
+            "rank_roofline": rank_roof,
             "mfma_frac_end_to_end": round(mfma_frac, 4),
             "kernels": kern,
             "cpu_baseline": cpu,

@@ -585,8 +585,9 @@ size_t mi_rank_workspace_bytes(int64_t N, int64_t Q, int32_t k) {
 
 static int check_rank_args(int64_t N, int64_t D, int dt, int64_t Q, int32_t k, int norm_mode, int nan_policy) {
   if (N < 0 || Q < 0) return fail(MI_ERR_ARG, "negative size");
-  if (k < 1 || k > 64) return fail(MI_ERR_UNSUPPORTED, "k must be in [1, 64] (got %d)", k);
-  if (D < 32 || D % 32 || D > 4096) return fail(MI_ERR_UNSUPPORTED, "D must be a multiple of 32 in [32, 4096]");
+  if (k < 1 || k > RANK_MAX_K) return fail(MI_ERR_UNSUPPORTED, "k must be in [1, %d] (got %d)", RANK_MAX_K, k);
+  if (D < 32 || D % 32 || D > RANK_MAX_D)
+    return fail(MI_ERR_UNSUPPORTED, "D must be a multiple of 32 in [32, %d] (queries are staged in LDS)", RANK_MAX_D);
   if (dt != MI_F32 && dt != MI_BF16 && dt != MI_F16) return fail(MI_ERR_ARG, "bad corpus dtype");
   if (norm_mode < 0 || norm_mode > 2) return fail(MI_ERR_ARG, "bad norm_mode");
   if (nan_policy != MI_NAN_FIRST && nan_policy != MI_NAN_LAST) return fail(MI_ERR_ARG, "bad nan_policy");
@@ -605,7 +606,7 @@ int mi_rank_topk(const void* corpus, int64_t N, int64_t D, int corpus_dtype, con
   hipStream_t s = (hipStream_t)stream;
   const int nf = nan_policy == MI_NAN_FIRST;
   if (N == 0) {
-    HIP_TRY(rank_merge(nullptr, nullptr, Q, 0, k, nf, out_scores, out_index, s));
+    HIP_TRY(rank_fill_empty(Q, k, out_scores, out_index, s));
     return MI_OK;
   }
   const size_t need = rank_workspace_bytes(N, Q, k);
@@ -619,7 +620,7 @@ int mi_rank_topk(const void* corpus, int64_t N, int64_t D, int corpus_dtype, con
 int mi_rank_merge(const float* cs, const int64_t* ci, int64_t Q, int64_t C, int32_t k, int nan_policy, float* out_s,
                   int64_t* out_i, void* stream) {
   if (Q < 0 || C < 0) return fail(MI_ERR_ARG, "negative size");
-  if (k < 1 || k > 64) return fail(MI_ERR_UNSUPPORTED, "k must be in [1, 64] (got %d)", k);
+  if (k < 1 || k > RANK_REG_K) return fail(MI_ERR_UNSUPPORTED, "k must be in [1, %d] (got %d)", RANK_REG_K, k);
   if (nan_policy != MI_NAN_FIRST && nan_policy != MI_NAN_LAST) return fail(MI_ERR_ARG, "bad nan_policy");
   if (Q == 0) return MI_OK;
   if ((C > 0 && (!cs || !ci)) || !out_s || !out_i) return fail(MI_ERR_ARG, "mi_rank_merge: null pointer");

@@ -101,12 +101,17 @@ hipError_t finalize_rows(const float* y, void* out, int out_dtype, int rows, int
 }  // namespace miclip
 
 namespace miclip {
+constexpr int RANK_REG_K = 64;          // register top-k lists (rank_stage1) up to this k
+constexpr int RANK_MAX_K = 1 << 24;     // select + sort path above it (rank.hip)
+constexpr int RANK_MAX_D = 1024;        // 32 queries x (D + 4) f32 staged in LDS
 size_t rank_workspace_bytes(int64_t N, int64_t Q, int k);
 hipError_t rank_topk(const void* corpus, int64_t N, int64_t D, int dt, const float* q, int64_t Q, int k,
                      int64_t base, int norm_mode, int nan_first, float* out_s, int64_t* out_i, void* ws,
                      hipStream_t s);
 hipError_t rank_merge(const float* cs, const int64_t* ci, int64_t Q, int64_t C, int k, int nan_first, float* out_s,
                       int64_t* out_i, hipStream_t s);
+// out_s = -inf, out_i = -1 for all Q x k slots (empty corpus)
+hipError_t rank_fill_empty(int64_t Q, int k, float* out_s, int64_t* out_i, hipStream_t s);
 hipError_t score_matrix(const void* corpus, int64_t N, int64_t D, int dt, const float* q, int64_t Q, int norm_mode,
                         float* out, hipStream_t s);
 hipError_t rank_of_targets(const float* S, int64_t Q, int64_t N, const int64_t* pq, const int64_t* pt, int64_t T,

@@ -338,10 +338,256 @@ __global__ __launch_bounds__(256) void rank_of_targets_kernel(const float* __res
   if (lane == 0) out[t] = total + 1;
 }
 
+// ---------------------------------------------------------------------------
+// Large k (k > 64: the register top-k lists stop there).  The reference's
+// np.argsort(s)[::-1][:top_k] with top_k = 3 x the UI request (query_strategies.py:55)
+// exceeds 64 from a request of 22 results on; top_k >= N is a full sort
+// (embedding_service.py:317-318).  Path: the exact-f32 score matrix
+// (score_matrix_kernel, the same score_tile arithmetic as rank_stage1), then
+// per query
+//   select_kernel   radix select of the k-th best key (4 passes of 8-bit
+//                   digit histograms over the row's keys), then a compaction of
+//                   every key above it plus the lowest-index ties equal to it
+//                   (waves own contiguous index ranges, so ballot prefixes
+//                   number the ties in index order) -> k candidates;
+//   sort_chunks     bitonic sort of chunks of <= SORT_CHUNK candidates in LDS
+//                   by (key desc, index asc);
+//   merge_pass      merge-path merges of sorted runs (k > SORT_CHUNK);
+//   finalize        decode keys -> scores, global indices.
+constexpr int SEL_NT = 1024;
+constexpr int SORT_CHUNK = 8192;
+constexpr int MERGE_ITEMS = 16;
+
+__device__ __forceinline__ float decode_key(uint32_t bk, int nan_first) {
+  if ((bk == 0xFFFFFFFFu && nan_first) || (bk == 0u && !nan_first)) return __uint_as_float(0x7fc00000u);
+  return __uint_as_float((bk & 0x80000000u) ? (bk & 0x7fffffffu) : ~bk);
+}
+
+__global__ __launch_bounds__(SEL_NT) void select_kernel(const float* __restrict__ S, int64_t N, int k, int nan_first,
+                                                        uint32_t* __restrict__ ck, int32_t* __restrict__ ci,
+                                                        int64_t kp) {
+  __shared__ uint32_t hist[256];
+  __shared__ uint32_t sh[4];          // prefix, krem, gt counter
+  __shared__ uint32_t wcnt[SEL_NT / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t q = blockIdx.x;
+  const float* s = S + q * N;
+  uint32_t* okey = ck + q * kp;
+  int32_t* oidx = ci + q * kp;
+  uint32_t prefix = 0, mask = 0, krem = (uint32_t)k;
+  for (int shift = 24; shift >= 0; shift -= 8) {
+    for (int i = tid; i < 256; i += SEL_NT) hist[i] = 0;
+    __syncthreads();
+    for (int64_t i = tid; i < N; i += SEL_NT) {
+      const uint32_t key = score_key(s[i], nan_first);
+      if ((key & mask) == prefix) atomicAdd(&hist[(key >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      uint32_t acc = 0;
+      int d = 255;
+      for (; d > 0; --d) {
+        if (acc + hist[d] >= krem) break;
+        acc += hist[d];
+      }
+      sh[0] = prefix | ((uint32_t)d << shift);
+      sh[1] = krem - acc;
+    }
+    __syncthreads();
+    prefix = sh[0];
+    krem = sh[1];
+    mask |= 255u << shift;
+    __syncthreads();
+  }
+  // prefix = T, the k-th best key; k - krem keys are above it, krem ties at T
+  // are taken in index order.  Wave w owns indices [w*per, (w+1)*per).
+  const uint32_t T = prefix, n_gt = (uint32_t)k - krem;
+  const int64_t per = ((N + SEL_NT / 64 - 1) / (SEL_NT / 64) + 63) / 64 * 64;
+  const int64_t b0 = wave * per, b1 = min(N, b0 + per);
+  const uint64_t lt = (1ull << lane) - 1ull;
+  uint32_t neq = 0;
+  for (int64_t i = b0; i < b1; i += 64) {
+    const bool eq = i + lane < b1 && score_key(s[i + lane], nan_first) == T;
+    neq += (uint32_t)__popcll(__ballot(eq));
+  }
+  if (lane == 0) wcnt[wave] = neq;
+  if (tid == 0) sh[2] = 0;
+  __syncthreads();
+  uint32_t run = 0;
+  for (int w = 0; w < wave; ++w) run += wcnt[w];
+  for (int64_t i = b0; i < b1; i += 64) {
+    const bool valid = i + lane < b1;
+    const uint32_t key = valid ? score_key(s[i + lane], nan_first) : 0u;
+    const bool gt = valid && key > T, eq = valid && key == T;
+    const uint64_t bg = __ballot(gt), be = __ballot(eq);
+    if (bg) {
+      const int lead = __ffsll((unsigned long long)bg) - 1;
+      uint32_t base = 0;
+      if (lane == lead) base = atomicAdd(&sh[2], (uint32_t)__popcll(bg));
+      base = __shfl(base, lead, 64);
+      if (gt) {
+        const uint32_t p = base + (uint32_t)__popcll(bg & lt);
+        okey[p] = key;
+        oidx[p] = (int32_t)(i + lane);
+      }
+    }
+    if (eq) {
+      const uint32_t r = run + (uint32_t)__popcll(be & lt);
+      if (r < krem) {
+        okey[n_gt + r] = key;
+        oidx[n_gt + r] = (int32_t)(i + lane);
+      }
+    }
+    run += (uint32_t)__popcll(be);
+  }
+  for (int64_t p = k + tid; p < kp; p += SEL_NT) {  // padding sorts after every real candidate
+    okey[p] = 0u;
+    oidx[p] = INT_MAX;
+  }
+}
+
+// Bitonic sort of one chunk of `n` (power of two, <= SORT_CHUNK) candidates in
+// LDS into "best first" order.
+__global__ __launch_bounds__(1024) void sort_chunks_kernel(uint32_t* __restrict__ ck, int32_t* __restrict__ ci,
+                                                           int64_t kp, int n) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint32_t* K = (uint32_t*)smem;
+  int32_t* I = (int32_t*)(smem + SORT_CHUNK * 4);
+  const int tid = threadIdx.x;
+  const int64_t base = (int64_t)blockIdx.y * kp + (int64_t)blockIdx.x * n;
+  for (int i = tid; i < n; i += 1024) {
+    K[i] = ck[base + i];
+    I[i] = ci[base + i];
+  }
+  __syncthreads();
+  for (int size = 2; size <= n; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int t = tid; t < n / 2; t += 1024) {
+        const int i = 2 * t - (t & (stride - 1)), j = i + stride;
+        const bool up = (i & size) == 0;
+        const uint32_t ki = K[i], kj = K[j];
+        const int32_t ii = I[i], ij = I[j];
+        if (up ? better(kj, ij, ki, ii) : better(ki, ii, kj, ij)) {
+          K[i] = kj; K[j] = ki;
+          I[i] = ij; I[j] = ii;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = tid; i < n; i += 1024) {
+    ck[base + i] = K[i];
+    ci[base + i] = I[i];
+  }
+}
+
+// One merge-path pass: sorted runs of `run` elements -> runs of 2*run.
+__global__ __launch_bounds__(256) void merge_pass_kernel(const uint32_t* __restrict__ sk, const int32_t* __restrict__ si,
+                                                         uint32_t* __restrict__ dk, int32_t* __restrict__ di,
+                                                         int64_t kp, int64_t run) {
+  const int64_t o0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * MERGE_ITEMS;
+  if (o0 >= kp) return;
+  const int64_t qb = (int64_t)blockIdx.y * kp;
+  const int64_t a0 = o0 / (2 * run) * (2 * run);
+  const int64_t la = min(run, kp - a0);
+  const int64_t b0 = a0 + la;
+  const int64_t lb = max((int64_t)0, min(run, kp - b0));
+  const int64_t d = o0 - a0;
+  const uint32_t* AK = sk + qb + a0;
+  const int32_t* AI = si + qb + a0;
+  const uint32_t* BK = sk + qb + b0;
+  const int32_t* BI = si + qb + b0;
+  int64_t lo = max((int64_t)0, d - lb), hi = min(d, la);
+  while (lo < hi) {  // i = number of the first d outputs taken from A (A first on equal elements)
+    const int64_t mid = (lo + hi) >> 1;
+    if (!better(BK[d - 1 - mid], BI[d - 1 - mid], AK[mid], AI[mid])) lo = mid + 1;
+    else hi = mid;
+  }
+  int64_t ia = lo, ib = d - lo;
+  for (int t = 0; t < MERGE_ITEMS && o0 + t < kp; ++t) {
+    const bool takeA = ib >= lb || (ia < la && !better(BK[ib], BI[ib], AK[ia], AI[ia]));
+    dk[qb + o0 + t] = takeA ? AK[ia] : BK[ib];
+    di[qb + o0 + t] = takeA ? AI[ia] : BI[ib];
+    ia += takeA ? 1 : 0;
+    ib += takeA ? 0 : 1;
+  }
+}
+
+__global__ __launch_bounds__(256) void finalize_large_kernel(const uint32_t* __restrict__ ck,
+                                                             const int32_t* __restrict__ ci, int64_t kp, int k, int kk,
+                                                             int nan_first, int64_t base, float* __restrict__ out_s,
+                                                             int64_t* __restrict__ out_i) {
+  const int64_t q = blockIdx.y;
+  for (int o = blockIdx.x * 256 + threadIdx.x; o < k; o += gridDim.x * 256) {
+    if (o < kk) {
+      out_s[q * k + o] = decode_key(ck[q * kp + o], nan_first);
+      out_i[q * k + o] = base + ci[q * kp + o];
+    } else {
+      out_s[q * k + o] = -INFINITY;
+      out_i[q * k + o] = -1;
+    }
+  }
+}
+
 }  // namespace
 
 // ------------------------------------------------------------ host helpers
 static int kc_for(int k) { return k <= 16 ? 16 : 64; }
+
+static int64_t large_kp(int64_t kk) {  // padded candidate count per query
+  if (kk <= SORT_CHUNK) {
+    int64_t p = 2;
+    while (p < kk) p <<= 1;
+    return p;
+  }
+  return (kk + SORT_CHUNK - 1) / SORT_CHUNK * SORT_CHUNK;
+}
+
+static size_t large_ws_bytes(int64_t N, int64_t Q, int k) {
+  const int64_t kk = k < N ? k : N;
+  const size_t sbytes = ((size_t)(Q * N) * 4 + 255) / 256 * 256;
+  return sbytes + (size_t)(2 * Q * large_kp(kk)) * 8;
+}
+
+hipError_t rank_fill_empty(int64_t Q, int k, float* out_s, int64_t* out_i, hipStream_t s) {
+  if (Q <= 0) return hipSuccess;
+  const unsigned fb = (unsigned)((k + 255) / 256 < 64 ? (k + 255) / 256 : 64);
+  hipLaunchKernelGGL(finalize_large_kernel, dim3(fb, (unsigned)Q), dim3(256), 0, s, nullptr, nullptr, (int64_t)0, k,
+                     0, 0, (int64_t)0, out_s, out_i);
+  return hipGetLastError();
+}
+
+static hipError_t rank_topk_large(const void* corpus, int64_t N, int64_t D, int dt, const float* q, int64_t Q, int k,
+                                  int64_t base, int norm_mode, int nan_first, float* out_s, int64_t* out_i, void* ws,
+                                  hipStream_t s) {
+  const int kk = (int)(k < N ? k : N);
+  const int64_t kp = large_kp(kk);
+  float* S = (float*)ws;
+  char* p = (char*)ws + ((size_t)(Q * N) * 4 + 255) / 256 * 256;
+  uint32_t* k0 = (uint32_t*)p;
+  int32_t* i0 = (int32_t*)(p + (size_t)(Q * kp) * 4);
+  uint32_t* k1 = (uint32_t*)(p + (size_t)(Q * kp) * 8);
+  int32_t* i1 = (int32_t*)(p + (size_t)(Q * kp) * 12);
+  hipError_t e = score_matrix(corpus, N, D, dt, q, Q, norm_mode, S, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(select_kernel, dim3((unsigned)Q), dim3(SEL_NT), 0, s, S, N, kk, nan_first, k0, i0, kp);
+  const int chunk = (int)(kp < SORT_CHUNK ? kp : SORT_CHUNK);
+  const size_t lds = (size_t)SORT_CHUNK * 8;
+  e = hipFuncSetAttribute((const void*)sort_chunks_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(sort_chunks_kernel, dim3((unsigned)(kp / chunk), (unsigned)Q), dim3(1024), lds, s, k0, i0, kp,
+                     chunk);
+  for (int64_t run = chunk; run < kp; run *= 2) {
+    const unsigned nb = (unsigned)((kp + 256 * MERGE_ITEMS - 1) / (256 * MERGE_ITEMS));
+    hipLaunchKernelGGL(merge_pass_kernel, dim3(nb, (unsigned)Q), dim3(256), 0, s, k0, i0, k1, i1, kp, run);
+    uint32_t* tk = k0; k0 = k1; k1 = tk;
+    int32_t* ti = i0; i0 = i1; i1 = ti;
+  }
+  const unsigned fb = (unsigned)((k + 255) / 256 < 64 ? (k + 255) / 256 : 64);
+  hipLaunchKernelGGL(finalize_large_kernel, dim3(fb, (unsigned)Q), dim3(256), 0, s, k0, i0, kp, k, kk, nan_first,
+                     base, out_s, out_i);
+  return hipGetLastError();
+}
 
 int64_t rank_chunks(int64_t N) {
   // rows per workgroup: multiples of 128, enough workgroups to fill 256 CUs
@@ -350,6 +596,7 @@ int64_t rank_chunks(int64_t N) {
 }
 
 size_t rank_workspace_bytes(int64_t N, int64_t Q, int k) {
+  if (k > RANK_REG_K) return large_ws_bytes(N, Q, k);
   const int64_t nch = N > 0 ? rank_chunks(N) : 1;
   return (size_t)(Q * nch * k) * (sizeof(float) + sizeof(int64_t));
 }
@@ -386,6 +633,7 @@ hipError_t rank_merge(const float* cs, const int64_t* ci, int64_t Q, int64_t C, 
 hipError_t rank_topk(const void* corpus, int64_t N, int64_t D, int dt, const float* q, int64_t Q, int k,
                      int64_t base, int norm_mode, int nan_first, float* out_s, int64_t* out_i, void* ws,
                      hipStream_t s) {
+  if (k > RANK_REG_K) return rank_topk_large(corpus, N, D, dt, q, Q, k, base, norm_mode, nan_first, out_s, out_i, ws, s);
   const int64_t nch = rank_chunks(N);
   const int64_t rpw = ((N + nch - 1) / nch + 127) / 128 * 128;
   const int64_t nwg = (N + rpw - 1) / rpw;

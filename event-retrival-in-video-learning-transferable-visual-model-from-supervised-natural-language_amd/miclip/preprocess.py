@@ -93,12 +93,15 @@ def preprocess_frames(frames, n_px: int = 224, squash: bool = False, out_dtype=N
     return out
 
 
-def load_frames(paths, n_px: int = 224, device="cuda", squash: bool = False, out_dtype=None, threads: int = 8):
+def load_frames(paths, n_px: int = 224, device="cuda", squash: bool = False, out_dtype=None, threads: int = 8,
+                strict: bool = False):
     """Decode frame files on host threads (PIL; decoding releases the GIL),
     upload each same-size group once as uint8, preprocess it on the GPU.
     Returns ([len(paths), 3, n_px, n_px] tensor in path order, list of failed
     indices).  A frame that cannot be read is left as zeros, as the
-    reference's ingest does (Backend/services/embedding_service.py:476-480)."""
+    reference's ingest does (Backend/services/embedding_service.py:476-480);
+    with ``strict`` the decode error propagates instead (Backend/embedding.py:45
+    has no handler)."""
     import torch
     from concurrent.futures import ThreadPoolExecutor
     from PIL import Image
@@ -108,6 +111,8 @@ def load_frames(paths, n_px: int = 224, device="cuda", squash: bool = False, out
             with Image.open(p) as im:
                 return np.asarray(im.convert("RGB"), dtype=np.uint8)
         except Exception as e:  # reference: print and substitute a zero frame
+            if strict:
+                raise
             print(f"Error preprocessing image {p}: {e}")
             return None
 

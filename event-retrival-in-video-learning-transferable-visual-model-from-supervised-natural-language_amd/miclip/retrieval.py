@@ -20,19 +20,25 @@ from . import _native as N
 
 _NORMS = {"l2": N.MI_NORM_L2, "l2_guard": N.MI_NORM_L2_GUARD, "none": N.MI_NORM_NONE}
 _NANS = {"first": N.MI_NAN_FIRST, "last": N.MI_NAN_LAST}
-MAX_K = 64
+REG_K = 64          # fused single-pass top-k (register lists) up to this k
+MAX_K = 1 << 24     # above REG_K: exact scores + radix select + sort (rank.hip)
+MAX_D = 1024
 
 _ws_lock = threading.Lock()
 _ws = {}
 
 
 def _workspace(device, nbytes):
+    """Scratch for mi_rank_topk, one buffer per (device, stream): kernels of
+    two threads on different streams never share it (same-stream callers are
+    ordered by the stream)."""
     import torch
+    key = (device, N.stream_ptr(device))
     with _ws_lock:
-        buf = _ws.get(device)
+        buf = _ws.get(key)
         if buf is None or buf.numel() < nbytes:
             buf = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
-            _ws[device] = buf
+            _ws[key] = buf
         return buf
 
 
@@ -67,6 +73,8 @@ def rank_topk(corpus, queries, k, index_base=0, norm="l2", nan_policy="first"):
     Q = q.shape[0]
     if not 1 <= k <= MAX_K:
         raise N.MiClipError(f"k must be in [1, {MAX_K}]")
+    if not (32 <= D <= MAX_D and D % 32 == 0):
+        raise N.MiClipError(f"D must be a multiple of 32 in [32, {MAX_D}], got {D}")
     out_s = torch.empty((Q, k), dtype=torch.float32, device=c.device)
     out_i = torch.empty((Q, k), dtype=torch.int64, device=c.device)
     L = N.lib()
@@ -125,7 +133,7 @@ class MirroredCorpus:
     """HBM-resident corpus with a bf16 ranking mirror and the f32 master kept
     for exact re-scoring.
 
-    ``topk`` ranks the bf16 mirror for ``k' = min(MAX_K, oversample * k)``
+    ``topk`` ranks the bf16 mirror for ``k' = min(REG_K, oversample * k)``
     candidates per query (half the HBM bytes of the f32 pass), gathers the
     union of the candidates' f32 rows (ascending corpus order) and re-ranks
     them with the exact f32 kernel, so scores are bit-identical to
@@ -159,7 +167,7 @@ class MirroredCorpus:
         q = _queries(queries, self.master.device)
         n = self.master.shape[0]
         kk = min(k, n)
-        kc = min(MAX_K, max(kk, self.oversample * kk), n)
+        kc = min(max(REG_K, kk), max(kk, self.oversample * kk), n)
         if kk <= 0:
             return rank_topk(self.master, q, k, norm=norm, nan_policy=nan_policy)
         s1, i1 = rank_topk(self.mirror, q, kc, norm=norm, nan_policy=nan_policy)

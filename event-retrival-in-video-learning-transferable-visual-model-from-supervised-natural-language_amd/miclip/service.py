@@ -27,7 +27,7 @@ import numpy as np
 
 from . import api
 from .preprocess import load_frames
-from .retrieval import MAX_K, rank_topk, score_matrix
+from .retrieval import rank_topk
 from .weights import load_state_dict
 
 
@@ -155,20 +155,16 @@ class EmbeddingService:
         return frames
 
     def _rank(self, corpus, query_vec, top_k):
-        """Top-k (score desc, index asc; NaN first as argsort(s)[::-1])."""
+        """Top-k (score desc, index asc; NaN first as argsort(s)[::-1]); any
+        k up to the corpus size (a full sort when top_k >= N, as the reference's
+        np.argsort(s)[::-1] at embedding_service.py:317-318)."""
         import torch
         k = min(int(top_k), corpus.shape[0])
         if k <= 0:
             return np.zeros(0, np.float32), np.zeros(0, np.int64)
         q = torch.as_tensor(np.asarray(query_vec, dtype=np.float32).reshape(1, -1), device=corpus.device)
-        if k <= MAX_K:
-            s, i = rank_topk(corpus, q, k, norm="l2", nan_policy="first")
-            return s[0].cpu().numpy(), i[0].cpu().numpy()
-        # large k: fused score kernel, then a stable device sort (descending,
-        # ties by index; torch sorts NaN as largest -> first)
-        s = score_matrix(corpus, q, norm="l2")[0]
-        order = torch.sort(s, descending=True, stable=True).indices[:k]
-        return s[order].cpu().numpy(), order.cpu().numpy()
+        s, i = rank_topk(corpus, q, k, norm="l2", nan_policy="first")
+        return s[0].cpu().numpy(), i[0].cpu().numpy()
 
     # --------------------------------------------------------------- search
     def extract_query_confidence(self, frame_path, query, video_name=None):

@@ -164,28 +164,144 @@ def synthetic_corpus(n: int, d: int, seed: int = CORPUS_SEED) -> np.ndarray:
     return x / np.linalg.norm(x, axis=-1, keepdims=True)
 
 
+_STORAGE_DTYPES = {
+    "FloatStorage": np.float32, "HalfStorage": np.float16, "DoubleStorage": np.float64,
+    "BFloat16Storage": "bf16", "LongStorage": np.int64, "IntStorage": np.int32, "ShortStorage": np.int16,
+    "CharStorage": np.int8, "ByteStorage": np.uint8, "BoolStorage": np.bool_,
+}
+
+
+def _is_torchscript_archive(path: str) -> bool:
+    import zipfile
+    if not zipfile.is_zipfile(path):
+        return False
+    with zipfile.ZipFile(path) as zf:
+        return any(n.split("/", 1)[-1].startswith("code/") for n in zf.namelist())
+
+
+def read_torchscript_tensors(path: str) -> dict:
+    """Tensors of a TorchScript archive (openai/CLIP's ``ViT-B-32.pt`` form)
+    WITHOUT executing anything from the file.
+
+    The archive's ``data.pkl`` describes the module tree; it is read by a
+    restricted unpickler that resolves only tensor-rebuild functions, storage
+    type markers and ``OrderedDict``; every ``__torch__.*`` module class becomes
+    an inert record of its attribute dict.  No TorchScript code is loaded or run
+    (``torch.jit.load`` would compile and run the archive's ``code/``).  The
+    attribute paths of the tensors are the OpenAI state-dict keys, as
+    ``model.state_dict()`` after ``torch.jit.load`` would name them (openai/CLIP
+    ``clip.load(jit=False)`` builds its model from exactly that dict)."""
+    import collections
+    import io
+    import pickle
+    import zipfile
+
+    class _Module:                       # inert stand-in for a __torch__.* class
+        def __init__(self, *a, **k):
+            self._state = {}
+
+        def __setstate__(self, state):
+            self._state = state if isinstance(state, dict) else {"__state__": state}
+
+    class _StorageType:
+        def __init__(self, name):
+            self.name = name
+
+    def rebuild_tensor(storage, offset, size, stride, *rest):
+        base = storage
+        return np.lib.stride_tricks.as_strided(
+            base[offset:], shape=tuple(size), strides=tuple(s * base.itemsize for s in stride)).copy()
+
+    def rebuild_parameter(data, *rest):
+        return data
+
+    with zipfile.ZipFile(path) as zf:
+        names = zf.namelist()
+        pkl = next(n for n in names if n.endswith("/data.pkl") or n == "data.pkl")
+        root = pkl[: -len("data.pkl")]
+        storages = {}
+
+        def storage(key, typ):
+            if key not in storages:
+                raw = zf.read(f"{root}data/{key}")
+                dt = _STORAGE_DTYPES.get(typ.name if isinstance(typ, _StorageType) else str(typ))
+                if dt is None:
+                    raise pickle.UnpicklingError(f"unsupported storage type {typ}")
+                if dt == "bf16":
+                    u = np.frombuffer(raw, dtype=np.uint16).astype(np.uint32) << np.uint32(16)
+                    storages[key] = u.view(np.float32)
+                else:
+                    storages[key] = np.frombuffer(raw, dtype=dt)
+            return storages[key]
+
+        class _Restricted(pickle.Unpickler):
+            def find_class(self, module, name):
+                if module == "torch._utils" and name in ("_rebuild_tensor_v2", "_rebuild_tensor"):
+                    return rebuild_tensor
+                if module == "torch._utils" and name == "_rebuild_parameter":
+                    return rebuild_parameter
+                if module == "collections" and name == "OrderedDict":
+                    return collections.OrderedDict
+                if module == "torch" and name.endswith("Storage"):
+                    return _StorageType(name)
+                if module == "torch.jit._pickle":          # TorchScript's typed-list markers: plain data
+                    if name in ("build_intlist", "build_doublelist", "build_boollist", "build_tensorlist",
+                                "build_complexlist"):
+                        return list
+                    if name == "restore_type_tag":
+                        return lambda value, type_str: value
+                if module.startswith("__torch__"):
+                    return type(name, (_Module,), {})
+                raise pickle.UnpicklingError(f"refusing to resolve {module}.{name} from a TorchScript archive")
+
+            def persistent_load(self, pid):
+                # ('storage', storage_type, key, location, numel)
+                if not (isinstance(pid, tuple) and pid and pid[0] == "storage"):
+                    raise pickle.UnpicklingError(f"unexpected persistent id {pid!r}")
+                return storage(str(pid[2]), pid[1])
+
+        obj = _Restricted(io.BytesIO(zf.read(pkl))).load()
+
+    out = {}
+
+    def walk(o, prefix):
+        if isinstance(o, np.ndarray):
+            out[prefix[:-1]] = o
+        elif isinstance(o, _Module):
+            for k, v in o._state.items():
+                walk(v, f"{prefix}{k}.")
+        elif isinstance(o, dict):
+            for k, v in o.items():
+                walk(v, f"{prefix}{k}.")
+
+    walk(obj, "")
+    return out
+
+
 def load_state_dict(path: str) -> dict:
     """Load an OpenAI-layout state dict from a LOCAL file (``$CLIP_WEIGHTS``).
 
     Accepted: ``.safetensors``, a plain ``torch.save`` state dict
-    (``weights_only=True``), or an OpenAI TorchScript archive (its
-    ``state_dict()`` is read, as openai/CLIP ``clip.load(jit=False)`` does).
+    (``weights_only=True``), or an OpenAI TorchScript archive (its tensors are
+    read by ``read_torchscript_tensors``, which executes nothing from the file).
     A fine-tuned ``CLIPWithClassifier`` checkpoint
     (``{'model_state_dict': {'clip_model.*', 'classifier.*'}}``,
     ``Backend/services/embedding_service.py:112-113``) is unwrapped to its
-    ``clip_model.*`` part."""
+    ``clip_model.*`` part.  Any other file is refused with the loader's own
+    error (no second, less restricted deserializer is tried)."""
     import torch
 
     if path.endswith(".safetensors"):
         from safetensors.numpy import load_file
         sd = load_file(path)
+    elif _is_torchscript_archive(path):
+        sd = read_torchscript_tensors(path)
     else:
-        try:
-            obj = torch.load(path, map_location="cpu", weights_only=True)
-        except Exception:
-            obj = torch.jit.load(path, map_location="cpu").state_dict()
+        obj = torch.load(path, map_location="cpu", weights_only=True)
         if isinstance(obj, dict) and "model_state_dict" in obj:
             obj = obj["model_state_dict"]
+        if not isinstance(obj, dict):
+            raise RuntimeError(f"{path}: expected a state dict, got {type(obj).__name__}")
         sd = {k: (v.float().numpy() if hasattr(v, "numpy") else np.asarray(v)) for k, v in obj.items()}
     if any(k.startswith("clip_model.") for k in sd):
         sd = {k[len("clip_model."):]: v for k, v in sd.items() if k.startswith("clip_model.")}
@@ -194,21 +310,47 @@ def load_state_dict(path: str) -> dict:
     return {k: np.ascontiguousarray(v, dtype=np.float32) for k, v in sd.items()}
 
 
+SYNTHETIC_ENV = "MICLIP_SYNTHETIC_WEIGHTS"
+SYNTHETIC_PREFIX = "synthetic:"
+
+
 def resolve(name_or_path: str):
     """(cfg, state_dict) for a model name or a local checkpoint path.
 
-    ``$CLIP_WEIGHTS`` (a local file) supplies real weights for a named model;
-    otherwise the deterministic generator is used (no network)."""
+    * a path to a local checkpoint: its weights (architecture inferred);
+    * a published name ("ViT-B/32", ...): the weights of the LOCAL file
+      ``$CLIP_WEIGHTS`` (there is no download); a file of another
+      architecture is an error;
+    * deterministic random-init weights of the architecture only when asked
+      for: the ``synthetic:`` name prefix, ``$MICLIP_SYNTHETIC_WEIGHTS=1``
+      (tests, bench), or the ``test-*`` parity configurations, which exist only
+      with synthetic weights.  Otherwise loading raises, so the drop-in never
+      ranks frames with a meaningless model by accident."""
+    import warnings
+    from ._native import MiClipError
     from .config import get_config
 
     if os.path.isfile(name_or_path):
         sd = load_state_dict(name_or_path)
         return from_state_dict(sd), sd
-    cfg = get_config(name_or_path)
+    synthetic = name_or_path.startswith(SYNTHETIC_PREFIX)
+    name = name_or_path[len(SYNTHETIC_PREFIX):] if synthetic else name_or_path
+    cfg = get_config(name)
+    test_cfg = cfg.name.startswith("test-")
     env = os.environ.get("CLIP_WEIGHTS")
-    if env and os.path.isfile(env):
+    if env and not synthetic and not test_cfg:
+        if not os.path.isfile(env):
+            raise MiClipError(f"$CLIP_WEIGHTS={env!r} is not a file")
         sd = load_state_dict(env)
         real = from_state_dict(sd)
-        if real.name == cfg.name:
-            return real, sd
-    return cfg, make_state_dict(cfg)
+        if real.name != cfg.name:
+            raise MiClipError(f"$CLIP_WEIGHTS={env!r} holds a {real.name} checkpoint, but {cfg.name} was requested")
+        return real, sd
+    if synthetic or test_cfg or os.environ.get(SYNTHETIC_ENV) == "1":
+        if not test_cfg and not synthetic:
+            warnings.warn(f"{cfg.name}: deterministic random-init weights (${SYNTHETIC_ENV}=1); embeddings and "
+                          f"rankings are meaningless outside tests and benchmarks", RuntimeWarning, stacklevel=3)
+        return cfg, make_state_dict(cfg)
+    raise MiClipError(f"no weights for {cfg.name}: set $CLIP_WEIGHTS to a local OpenAI checkpoint "
+                      f"(.pt TorchScript archive, state-dict .pt or .safetensors) or pass its path to clip.load; "
+                      f"random-init weights need '{SYNTHETIC_PREFIX}{cfg.name}' or ${SYNTHETIC_ENV}=1")

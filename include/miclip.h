@@ -120,7 +120,13 @@ size_t mi_rank_workspace_bytes(int64_t N, int64_t Q, int32_t k);
  * L2 norm (norm_mode) + fp32-exact dot with every query + top-k.
  * corpus: device [N,D] (MI_F32/MI_BF16/MI_F16, row stride D); queries: device
  * f32 [Q,D]; out_scores f32 [Q,k], out_index int64 [Q,k] (global index =
- * index_base + row; slots past N are index -1, score -inf).  1 <= k <= 64. */
+ * index_base + row; slots past N are index -1, score -inf).  32 <= D <= 1024,
+ * D % 32 == 0 (32 queries x D f32 are staged in LDS).  1 <= k <= 2^24:
+ * k <= 64 is the single fused pass (register top-k lists); larger k (the
+ * reference's top_k*3 candidates for UI requests above 21, query_strategies.py:55,
+ * and full sorts, embedding_service.py:317-318) runs the exact score matrix +
+ * radix select + sort kernels over the same scores, with the workspace
+ * mi_rank_workspace_bytes reports for that k (it includes Q*N f32 scores). */
 int mi_rank_topk(const void* corpus, int64_t N, int64_t D, int corpus_dtype,
                  const float* queries, int64_t Q, int32_t k, int64_t index_base,
                  int norm_mode, int nan_policy, float* out_scores, int64_t* out_index,
@@ -128,7 +134,7 @@ int mi_rank_topk(const void* corpus, int64_t N, int64_t D, int corpus_dtype,
 
 /* Merge per-query candidate lists (e.g. the RCCL all-gather of per-shard
  * top-k) into the global top-k with the same order rule.
- * cand_scores f32 [Q,C], cand_index int64 [Q,C] (index -1 = empty slot). */
+ * cand_scores f32 [Q,C], cand_index int64 [Q,C] (index -1 = empty slot); 1 <= k <= 64. */
 int mi_rank_merge(const float* cand_scores, const int64_t* cand_index, int64_t Q, int64_t C,
                   int32_t k, int nan_policy, float* out_scores, int64_t* out_index, void* stream);
 

@@ -11,6 +11,10 @@ for p in (PKG, ROOT):
     if p not in sys.path:
         sys.path.insert(0, p)
 
+# the parity tests run on deterministic random-init weights of the real
+# architectures (no checkpoints offline); the product refuses them unless asked
+os.environ.setdefault("MICLIP_SYNTHETIC_WEIGHTS", "1")
+
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 

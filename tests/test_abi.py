@@ -44,10 +44,19 @@ def test_weights_numel_matches_packer():
 def test_argument_errors_without_gpu():
     from miclip import _native
     L = _native.lib()
-    rc = L.mi_rank_topk(None, 10, 512, 0, None, 1, 100, 0, 0, 0, None, None, None, 0, None)
+    rc = L.mi_rank_topk(None, 10, 512, 0, None, 1, (1 << 24) + 1, 0, 0, 0, None, None, None, 0, None)
+    assert rc == -3 and b"k must be" in L.mi_last_error()
+    rc = L.mi_rank_topk(None, 10, 512, 0, None, 1, 0, 0, 0, 0, None, None, None, 0, None)
     assert rc == -3 and b"k must be" in L.mi_last_error()
     rc = L.mi_rank_topk(None, 10, 500, 0, None, 1, 10, 0, 0, 0, None, None, None, 0, None)
     assert rc == -3 and b"multiple of 32" in L.mi_last_error()
+    # the query block is staged in LDS: D is capped where it still fits
+    rc = L.mi_rank_topk(None, 10, 1056, 0, None, 1, 10, 0, 0, 0, None, None, None, 0, None)
+    assert rc == -3 and b"1024" in L.mi_last_error()
+    rc = L.mi_rank_topk(None, 10, 1024, 0, None, 1, 10, 0, 0, 0, None, None, None, 0, None)
+    assert rc == -1                                              # D = 1024 accepted; fails on the null pointers
+    # large k (select + sort path) needs the score matrix in the workspace
+    assert L.mi_rank_workspace_bytes(3000, 2, 200) >= 2 * 3000 * 4 + 2 * 2 * 256 * 8
     rc = L.mi_rank_merge(None, None, 1, 4, 0, 0, None, None, None)
     assert rc == -3
     arch = _native.Arch(512, 224, 12, 768, 32, 77, 49408, 512, 8, 12)

@@ -164,3 +164,44 @@ def test_mirrored_corpus_near_ties_fall_back(gpu):
     s0, i0 = retrieval.rank_topk(corpus, q, 10)
     assert (i.cpu() == i0.cpu()).all() and (s.cpu() == s0.cpu()).all()
     assert mc.fallbacks == 1
+
+
+@pytest.mark.parametrize("N,k,pol", [(3000, 65, "first"), (3000, 3000, "last"), (20000, 1000, "first"),
+                                     (20000, 8192, "last"), (20000, 9000, "first"), (20000, 20000, "first"),
+                                     (20000, 25000, "last"), (1, 100, "first")])
+def test_topk_large_k_select_path(gpu, N, k, pol):
+    """k > 64: exact scores + radix select + bitonic chunks + merge-path passes
+    (rank.hip).  Zero rows (NaN), groups of duplicated rows (exact ties at
+    every position, index ascending) and k >= N (a full sort, the reference's
+    argsort(s)[::-1] when top_k >= N, embedding_service.py:317-318)."""
+    from miclip import retrieval, weights
+    from oracle import rank_ref
+    corpus = weights.normal(21, f"large{N}", (N, 256))
+    if N > 10:
+        corpus[[5, N // 2, N - 1]] = 0.0
+        for a in range(0, N - 20, max(1, N // 37)):
+            corpus[a + 7] = corpus[a]                      # exact ties
+    q = weights.synthetic_corpus(3, 256, seed=22)
+    s, i = retrieval.rank_topk(_t(corpus, gpu), _t(q, gpu), k, nan_policy=pol)
+    kk = min(k, N)
+    assert s.shape == (3, kk)
+    S = rank_ref.scores_ref(corpus, q)
+    s, i = s.cpu().numpy(), i.cpu().numpy()
+    for r in range(3):
+        rank_ref.assert_topk_equivalent(s[r], i[r], S[r], kk, nan_policy=pol)
+        # ties and NaNs: where float64 scores are EQUAL the order is index ascending, exactly
+        for p in range(kk - 1):
+            a, b = S[r][i[r][p]], S[r][i[r][p + 1]]
+            if a == b or (np.isnan(a) and np.isnan(b)):
+                assert i[r][p] < i[r][p + 1]
+
+
+def test_topk_large_k_matches_fused_path_prefix(gpu):
+    """The select path and the fused single pass agree on the first 64."""
+    from miclip import retrieval, weights
+    corpus = _t(weights.normal(23, "pref", (50000, 512)), gpu)
+    q = _t(weights.synthetic_corpus(32, 512, seed=24), gpu)
+    s1, i1 = retrieval.rank_topk(corpus, q, 64)
+    s2, i2 = retrieval.rank_topk(corpus, q, 500)
+    assert np.array_equal(i1.cpu().numpy(), i2[:, :64].cpu().numpy())
+    assert np.array_equal(s1.cpu().numpy(), s2[:, :64].cpu().numpy())

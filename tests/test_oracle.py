@@ -94,3 +94,20 @@ def test_topk_ref_edge_cases():
     assert i.shape == (1, 20) and i[0, -1] == 4
     s, i = rank_ref.topk_ref(C, q, 3, index_base=100)
     assert (i >= 100).all()
+
+
+@pytest.mark.parametrize("name,fname", [("test-small", "test_small.npz"), ("ViT-B/32", "vit_b32.npz")])
+def test_torch_cpu_restatement_matches_golden(name, fname):
+    """oracle/clip_torch.py (the torch-CPU fp32 form the CPU baseline times,
+    BASELINE.md) against the same HF-pinned goldens."""
+    from miclip import config, weights
+    from oracle import clip_ref, clip_torch
+    cfg = config.get_config(name)
+    g = golden(fname)
+    m = clip_torch.TorchCLIP(state_dict(name), cfg)
+    px = weights.synthetic_pixels(int(g["n_images"]), cfg.image_resolution)
+    img = np.concatenate([m.encode_image(px[i:i + 1]) for i in range(px.shape[0])])   # batch 1, embedding.py:46-50
+    txt = m.encode_text(g["tokens"])
+    np.testing.assert_allclose(img, g["image"], rtol=0, atol=5e-5 * np.abs(g["image"]).max())
+    np.testing.assert_allclose(txt, g["text"], rtol=0, atol=5e-5 * np.abs(g["text"]).max())
+    assert 1 - clip_ref.cosine(img, g["image"]).min() < 1e-8
