@@ -512,6 +512,116 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Main-loop ablation probes (variants 31-33, scripts/gemm_micro.py; no
+// epilogue, like variant 8): gemm_pp_kernel<EPI_NONE, 1>'s schedule with one
+// component removed, to see which one sets the stage time.
+//   31: no LDS-DMA (the MFMAs read whatever the ring holds)
+//   32: no fragment ds_reads (the MFMAs reuse the first stage's fragments)
+//   33: no MFMAs (the fragments are kept live by an empty asm)
+template <int ABL>
+__global__ __launch_bounds__(512) void gemm_abl_kernel(GemmArgs a) {
+  constexpr int BM = 256, BN = 256;
+  constexpr int WTM = 128, WTN = 64;
+  constexpr int A_BYTES = BM * BK * 2, STAGE_BYTES = (BM + BN) * BK * 2;
+  __shared__ __attribute__((aligned(16))) char smem[RING * STAGE_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int grp = __builtin_amdgcn_readfirstlane(wave >> 2), wc = wave & 3;
+  const int tiles_n = a.N / BN;
+  const int tiles_m = (a.M + BM - 1) / BM;
+  int m0, n0;
+  tile_coords(xcd_remap(blockIdx.x, tiles_m * tiles_n), tiles_m, tiles_n, 0, m0, n0);
+  m0 *= BM;
+  n0 *= BN;
+  const int nk = a.K / BK;
+  const int lrow = lane >> 2;
+  const int lchunk = ((lane & 3) ^ swz(lane >> 4)) * 8;
+  const uint16_t* asrc[2];
+  const uint16_t* wsrc[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    asrc[j] = a.A + (int64_t)min(m0 + (wave * 2 + j) * 16 + lrow, a.M - 1) * a.lda + lchunk;
+    wsrc[j] = a.W + (int64_t)(n0 + (wave * 2 + j) * 16 + lrow) * a.ldw + lchunk;
+  }
+  auto issue_half = [&](int st, int j) {
+    if (ABL == 1) return;
+    char* base = smem + (st % RING) * STAGE_BYTES;
+    glds16(asrc[j] + (int64_t)st * BK, base + (wave * 2 + j) * 1024);
+    glds16(wsrc[j] + st * BK, base + A_BYTES + (wave * 2 + j) * 1024);
+  };
+  auto wait_stage = [&](int g1) {
+    const int younger = min(LEAD - 1, nk - 1 - g1);
+    if (younger >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (younger == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+  auto barrier = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto lgkm_barrier = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+#pragma unroll
+  for (int s = 0; s < LEAD; ++s)
+    if (s < nk) { issue_half(s, 0); issue_half(s, 1); }
+  wait_stage(0);
+  barrier();
+  if (grp == 1) barrier();
+  const int rd = (lane & 15) * 64 + (((lane >> 4) ^ swz((lane >> 2) & 3)) * 16);
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 bfr[4], af[8];
+  {
+    const char* As = smem + (grp * WTM) * 64;
+    const char* Ws = smem + A_BYTES + (wc * WTN) * 64;
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) bfr[ni] = *(const bf16x8*)(Ws + ni * 16 * 64 + rd);
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi) af[mi] = *(const bf16x8*)(As + mi * 16 * 64 + rd);
+  }
+  for (int g = 0; g < nk; ++g) {
+    const char* As = smem + (g % RING) * STAGE_BYTES + (grp * WTM) * 64;
+    const char* Ws = smem + (g % RING) * STAGE_BYTES + A_BYTES + (wc * WTN) * 64;
+    if (g + LEAD < nk) { issue_half(g + LEAD, 0); issue_half(g + LEAD, 1); }
+    if (ABL != 2) {
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) bfr[ni] = *(const bf16x8*)(Ws + ni * 16 * 64 + rd);
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi) af[mi] = *(const bf16x8*)(As + mi * 16 * 64 + rd);
+    }
+    if (grp == 1 && g + 1 < nk) wait_stage(g + 1);
+    lgkm_barrier();
+    if (ABL == 3) {
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) asm volatile("" ::"v"(bfr[ni]));
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi) asm volatile("" ::"v"(af[mi]));
+    } else {
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[ni], af[mi], acc[mi][ni], 0, 0, 0);
+    }
+    if (grp == 0 && g + 1 < nk) wait_stage(g + 1);
+    barrier();
+  }
+  if (grp == 0) barrier();
+  float t = 0.f;
+#pragma unroll
+  for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) t += acc[mi][ni][0] + acc[mi][ni][1] + acc[mi][ni][2] + acc[mi][ni][3];
+  if (t == 12345.f && a.M < 0) *(float*)a.out = t;
+}
+
+// ---------------------------------------------------------------------------
 // Persistent ping-pong (variant 18, bf16 outputs): gemm_pp_kernel's schedule
 // (CL = 1) with one workgroup per CU walking its tiles, so a tile's epilogue
 // overlaps the next tile's prologue and store drain:
@@ -800,6 +910,13 @@ hipError_t launch(const GemmArgs& a, hipStream_t s) {
   if (big && v == 17 && bf16_out && a.K / BK >= LEAD) {  // experiment: non-temporal output stores
     const int nt = ((a.M + 255) / 256) * (a.N / 256);
     hipLaunchKernelGGL((gemm_pp_kernel<EPI, 1, false, true, true>), dim3(nt), dim3(512), 0, s, a);
+    return hipGetLastError();
+  }
+  if (big && v >= 31 && v <= 33 && a.K / BK >= LEAD) {  // main-loop ablation probes
+    const int nt = ((a.M + 255) / 256) * (a.N / 256);
+    if (v == 31) hipLaunchKernelGGL(gemm_abl_kernel<1>, dim3(nt), dim3(512), 0, s, a);
+    else if (v == 32) hipLaunchKernelGGL(gemm_abl_kernel<2>, dim3(nt), dim3(512), 0, s, a);
+    else hipLaunchKernelGGL(gemm_abl_kernel<3>, dim3(nt), dim3(512), 0, s, a);
     return hipGetLastError();
   }
   if (big && v == 8 && a.K / BK >= LEAD) {

@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 
 #include <climits>
+#include <cstdlib>
 
 #include "common.hpp"
 #include "internal.hpp"
@@ -36,6 +37,11 @@ __device__ __forceinline__ uint32_t score_key(float s, int nan_first) {
   if (s == 0.0f) s = 0.0f;  // -0 == +0
   const uint32_t u = __float_as_uint(s);
   return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+__device__ __forceinline__ float decode_key(uint32_t bk, int nan_first) {
+  if ((bk == 0xFFFFFFFFu && nan_first) || (bk == 0u && !nan_first)) return __uint_as_float(0x7fc00000u);
+  return __uint_as_float((bk & 0x80000000u) ? (bk & 0x7fffffffu) : ~bk);
 }
 
 template <typename I>
@@ -88,11 +94,20 @@ __device__ __forceinline__ void load_chunk(const void* corpus, int64_t row, int6
   }
 }
 
-__device__ __forceinline__ float apply_norm(float dot, float ss, int norm_mode) {
-  if (norm_mode == 2) return dot;
+// Row normalisation as a reciprocal computed once per row (score = dot * inv):
+// MI_NORM_L2 inv = 1/||e|| (a zero row gives 0 * inf = NaN, as E/||E|| does at
+// embedding_service.py:210); MI_NORM_L2_GUARD inv = 1 when ||e|| <= 1e-8
+// (compare_models.py:1168-1171); MI_NORM_NONE inv = 1.  Every kernel that
+// scores rows uses these two helpers, so all paths give identical scores.
+__device__ __forceinline__ float inv_norm(float ss, int norm_mode) {
+  if (norm_mode == 2) return 1.f;
   const float n = sqrtf(ss);
-  if (norm_mode == 1) return n > 1e-8f ? dot / n : dot;
-  return dot / n;
+  if (norm_mode == 1) return n > 1e-8f ? 1.f / n : 1.f;
+  return 1.f / n;
+}
+
+__device__ __forceinline__ float apply_norm(float dot, float ss, int norm_mode) {
+  return norm_mode == 2 ? dot : dot * inv_norm(ss, norm_mode);
 }
 
 // Computes the 32x32 f32 score tile of (rows row0.., queries of this block)
@@ -130,6 +145,228 @@ __device__ __forceinline__ void score_tile(const void* corpus, int64_t N, int64_
   if (h == 0) nrm[r] = ss;
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_wave_barrier();
+}
+
+// Streaming stage 1 (the default for k <= 16, rank_stream): the same
+// 32-row x 32-query wave tiles and exact-f32 MFMA arithmetic as rank_stage1,
+// rebuilt around the memory stream and a data-independent top-k update:
+//  * a wave's tiles are ONE continuous stream of 32-k chunks (tile after
+//    tile), loaded two chunks ahead into three register buffers used in place
+//    (the chunk loop is unrolled by 3, so no buffer is copied: a copy of a
+//    freshly loaded register waits for its load and caps the lookahead at one
+//    chunk); the next tile's first chunks are in flight while a tile finishes;
+//  * NW waves per workgroup share one LDS copy of the 32 queries;
+//  * top-k: a candidate is one u64, (score key << 32) | ~row, so "better"
+//    (key desc, row asc) is a single unsigned compare.  After each tile a
+//    lane sorts its 16 new candidates with a bitonic network and merges them
+//    into its sorted list of 16 (max of the list and the reversed candidates,
+//    then a bitonic clean-up): ~112 compare-exchanges per tile whatever the
+//    data.  rank_stage1 inserted candidate by candidate under a wave vote,
+//    which fires on nearly every row of the first tiles (64 independent lists)
+//    and cost 3x the MFMA issue in VALU (PMC: 126M VALU vs 8M MFMA at 1M
+//    rows);
+//  * the tile is skipped when no lane has a candidate above
+//    max(its list's 16th key, tau[q]), tau[q] (LDS) = max over the workgroup's
+//    lists of their k-th key: a score below it cannot reach the workgroup's
+//    top-k (that list already holds k better rows).
+// LDS: queries [32][D+4] f32, row norms [NW][32], tau [32]; the lists
+// [64*NW lanes][16] (key u32, idx i32) reuse the query area after a barrier.
+__device__ __forceinline__ void ce_desc(uint64_t& a, uint64_t& b) {  // a >= b afterwards
+  const uint64_t x = a > b ? a : b, y = a > b ? b : a;
+  a = x;
+  b = y;
+}
+
+__device__ __forceinline__ void bitonic_sort16_desc(uint64_t (&c)[16]) {
+#pragma unroll
+  for (int size = 2; size <= 16; size <<= 1)
+#pragma unroll
+    for (int stride = size >> 1; stride > 0; stride >>= 1)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int j = i ^ stride;
+        if (j > i) {
+          if ((i & size) == 0) ce_desc(c[i], c[j]);
+          else ce_desc(c[j], c[i]);
+        }
+      }
+}
+
+// L sorted desc, c sorted desc -> L = the 16 best of both, sorted desc
+__device__ __forceinline__ void merge16_desc(uint64_t (&L)[16], const uint64_t (&c)[16]) {
+#pragma unroll
+  for (int i = 0; i < 16; ++i) L[i] = L[i] > c[15 - i] ? L[i] : c[15 - i];   // bitonic (max of desc, asc)
+#pragma unroll
+  for (int stride = 8; stride > 0; stride >>= 1)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int j = i ^ stride;
+      if (j > i) ce_desc(L[i], L[j]);
+    }
+}
+
+template <int DT, int NW>
+__global__ __launch_bounds__(64 * NW) void rank_stream(const void* __restrict__ corpus, int64_t N, int64_t D,
+                                                       const float* __restrict__ queries, int64_t Q, int k,
+                                                       int64_t rows_per_wg, int norm_mode, int nan_first,
+                                                       int64_t index_base, float* __restrict__ ws_s,
+                                                       int64_t* __restrict__ ws_i, int64_t C) {
+  constexpr int NT = 64 * NW, KC = 16;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int ts_stride = (int)D + 4;
+  float* Ts = (float*)smem;
+  float* nrm_all = Ts + RQ * ts_stride;
+  uint32_t* tau = (uint32_t*)(nrm_all + NW * 32);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int64_t q0 = (int64_t)blockIdx.y * RQ;
+
+  for (int64_t e = tid; e < RQ * D; e += NT) {
+    const int qq = (int)(e / D);
+    const int64_t d = e % D;
+    Ts[qq * ts_stride + d] = (q0 + qq < Q) ? queries[(q0 + qq) * D + d] : 0.f;
+  }
+  if (tid < RQ) tau[tid] = 0u;
+  __syncthreads();
+
+  const int64_t r_begin = (int64_t)blockIdx.x * rows_per_wg;
+  const int64_t r_end = min(N, r_begin + rows_per_wg);
+  float* nrm = nrm_all + wave * 32;
+  const int64_t ntw = (r_end - r_begin + 31) / 32;
+  const int my_tiles = ntw > wave ? (int)((ntw - 1 - wave) / NW + 1) : 0;
+  const int nch = (int)(D / 32);
+  const int64_t total = (int64_t)my_tiles * nch;
+  const int nrows = (int)(r_end - r_begin);
+
+  uint64_t L[KC];
+#pragma unroll
+  for (int p = 0; p < KC; ++p) L[p] = 0ull;      // (key 0, row ~0): below every real candidate
+  const bool qvalid = q0 + r < Q;
+  const float* tq = Ts + r * ts_stride + 16 * h;
+
+  int lt = 0, lj = 0;  // load cursor (tile ordinal, chunk); loads past the end re-read a valid row
+  auto next_load = [&](float (&buf)[16]) {
+    const int64_t row = min(r_begin + (int64_t)(wave + NW * lt) * 32 + r, N - 1);
+    load_chunk<DT>(corpus, row, D, 32 * lj + 16 * h, buf);
+    if (++lj == nch) { lj = 0; ++lt; }
+  };
+  int ct = 0, cj = 0;  // compute cursor
+  f32x16 acc = f32x16{};
+  float ss = 0.f;
+  auto finalize = [&]() {
+    ss += __shfl_xor(ss, 32, 64);
+    if (h == 0) nrm[r] = inv_norm(ss, norm_mode);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    const int tr0 = (wave + NW * ct) * 32;           // tile's first row, relative to r_begin
+    const uint32_t tq_thr = tau[r];
+    const uint32_t own = (uint32_t)(L[KC - 1] >> 32);
+    const uint32_t thr = own > tq_thr ? own : tq_thr;
+    uint64_t c[16];
+    bool any = false;
+#pragma unroll
+    for (int rg = 0; rg < 16; ++rg) {
+      const int rr = (rg & 3) + 8 * (rg >> 2) + 4 * h;
+      const int lr = tr0 + rr;
+      const float sc = norm_mode == 2 ? acc[rg] : acc[rg] * nrm[rr];
+      const uint32_t key = score_key(sc, nan_first);
+      const bool ok = qvalid && lr < nrows && key >= thr;
+      c[rg] = ok ? (((uint64_t)key << 32) | (uint32_t)~(uint32_t)lr) : 0ull;
+      any |= ok;
+    }
+    if (__any(any)) {
+      bitonic_sort16_desc(c);
+      merge16_desc(L, c);
+      // publish this list's k-th key (a lower bound of the query's k-th best)
+      uint32_t kth = (uint32_t)(L[0] >> 32);
+#pragma unroll
+      for (int p = 1; p < KC; ++p) kth = (p == k - 1) ? (uint32_t)(L[p] >> 32) : kth;
+      const uint32_t other = (uint32_t)__shfl_xor((int)kth, 32, 64);
+      kth = kth > other ? kth : other;
+      if (h == 0 && qvalid && kth > tq_thr) atomicMax(&tau[r], kth);
+    }
+    __builtin_amdgcn_wave_barrier();
+    acc = f32x16{};
+    ss = 0.f;
+    ++ct;
+    cj = 0;
+  };
+  auto consume = [&](const float (&buf)[16]) {
+    float tb[16];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float4 t = *(const float4*)(tq + 32 * cj + 4 * i);
+      tb[4 * i] = t.x; tb[4 * i + 1] = t.y; tb[4 * i + 2] = t.z; tb[4 * i + 3] = t.w;
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(buf[i], tb[i], acc, 0, 0, 0);
+      ss = fmaf(buf[i], buf[i], ss);
+    }
+    if (++cj == nch) finalize();
+  };
+
+  // Three register buffers used in place, loaded two chunks ahead (hipcc's
+  // own counted waits; measured 3.8-4.0 TB/s at 1M rows).  Tried and
+  // rejected: a padded exit-free body with sched_barriers (hipcc then drained
+  // the ring at the back-edge) and inline-asm loads with hand-counted waits
+  // (hipcc copies the in-flight registers).
+  if (total > 0) {
+    float b0[16], b1[16], b2[16];
+    next_load(b0);
+    next_load(b1);
+    for (int64_t c = 0; c < total; c += 3) {
+      next_load(b2);
+      consume(b0);
+      if (c + 1 >= total) break;
+      next_load(b0);
+      consume(b1);
+      if (c + 2 >= total) break;
+      next_load(b1);
+      consume(b2);
+    }
+  }
+  __syncthreads();  // query area free -> lists
+  uint32_t* Lk = (uint32_t*)smem;
+  int32_t* Li = (int32_t*)(smem + NT * KC * 4);
+#pragma unroll
+  for (int p = 0; p < KC; ++p) {
+    const bool real = L[p] != 0ull;
+    Lk[tid * KC + p] = real ? (uint32_t)(L[p] >> 32) : 0u;
+    Li[tid * KC + p] = real ? (int32_t)~(uint32_t)L[p] : INT_MAX;
+  }
+  __syncthreads();
+  if (tid < RQ && q0 + tid < Q) {
+    // 2*NW sorted lists for query tid: lanes {w*64 + tid, w*64 + 32 + tid}
+    int pos[2 * NW];
+#pragma unroll
+    for (int l = 0; l < 2 * NW; ++l) pos[l] = 0;
+    float* os = ws_s + (q0 + tid) * C + (int64_t)blockIdx.x * k;
+    int64_t* oi = ws_i + (q0 + tid) * C + (int64_t)blockIdx.x * k;
+    for (int o = 0; o < k; ++o) {
+      uint32_t bk = 0u;
+      int32_t bi = INT_MAX;
+      int bl = 0;
+#pragma unroll
+      for (int l = 0; l < 2 * NW; ++l) {
+        const int src = (l >> 1) * 64 + (l & 1) * 32 + tid;
+        if (pos[l] < KC) {
+          const uint32_t kk = Lk[src * KC + pos[l]];
+          const int32_t ii = Li[src * KC + pos[l]];
+          if (better(kk, ii, bk, bi)) { bk = kk; bi = ii; bl = l; }
+        }
+      }
+#pragma unroll
+      for (int l = 0; l < 2 * NW; ++l) pos[l] += (l == bl) ? 1 : 0;
+      if (bi == INT_MAX) {
+        os[o] = -INFINITY;
+        oi[o] = -1;
+      } else {
+        os[o] = decode_key(bk, nan_first);
+        oi[o] = index_base + r_begin + bi;
+      }
+    }
+  }
 }
 
 // stage-1 LDS: queries [32][D+4] f32, per-wave norms [4][32]; the lists
@@ -358,11 +595,6 @@ constexpr int SEL_NT = 1024;
 constexpr int SORT_CHUNK = 8192;
 constexpr int MERGE_ITEMS = 16;
 
-__device__ __forceinline__ float decode_key(uint32_t bk, int nan_first) {
-  if ((bk == 0xFFFFFFFFu && nan_first) || (bk == 0u && !nan_first)) return __uint_as_float(0x7fc00000u);
-  return __uint_as_float((bk & 0x80000000u) ? (bk & 0x7fffffffu) : ~bk);
-}
-
 __global__ __launch_bounds__(SEL_NT) void select_kernel(const float* __restrict__ S, int64_t N, int k, int nan_first,
                                                         uint32_t* __restrict__ ck, int32_t* __restrict__ ci,
                                                         int64_t kp) {
@@ -590,9 +822,11 @@ static hipError_t rank_topk_large(const void* corpus, int64_t N, int64_t D, int 
 }
 
 int64_t rank_chunks(int64_t N) {
-  // rows per workgroup: multiples of 128, enough workgroups to fill 256 CUs
-  const int64_t tiles = (N + 127) / 128;
-  return tiles < 1024 ? tiles : 1024;
+  // one workgroup per CU-slot pair (512) once the corpus is large, so each
+  // wave streams several 32-row tiles; rows per workgroup are multiples of 384
+  // (one tile round of 12 waves)
+  const int64_t tiles = (N + 383) / 384;
+  return tiles < 512 ? tiles : 512;
 }
 
 size_t rank_workspace_bytes(int64_t N, int64_t Q, int k) {
@@ -630,25 +864,54 @@ hipError_t rank_merge(const float* cs, const int64_t* ci, int64_t Q, int64_t C, 
   return hipGetLastError();
 }
 
+template <int DT, int NW>
+static hipError_t launch_stream(dim3 grid, size_t lds, hipStream_t s, const void* corpus, int64_t N, int64_t D,
+                                const float* q, int64_t Q, int k, int64_t rpw, int nm, int nf, int64_t base,
+                                float* ws_s, int64_t* ws_i, int64_t C) {
+  auto fn = rank_stream<DT, NW>;
+  hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(fn, grid, dim3(64 * NW), lds, s, corpus, N, D, q, Q, k, rpw, nm, nf, base, ws_s, ws_i, C);
+  return hipGetLastError();
+}
+
 hipError_t rank_topk(const void* corpus, int64_t N, int64_t D, int dt, const float* q, int64_t Q, int k,
                      int64_t base, int norm_mode, int nan_first, float* out_s, int64_t* out_i, void* ws,
                      hipStream_t s) {
   if (k > RANK_REG_K) return rank_topk_large(corpus, N, D, dt, q, Q, k, base, norm_mode, nan_first, out_s, out_i, ws, s);
   const int64_t nch = rank_chunks(N);
-  const int64_t rpw = ((N + nch - 1) / nch + 127) / 128 * 128;
+  const int64_t rpw = ((N + nch - 1) / nch + 383) / 384 * 384;
   const int64_t nwg = (N + rpw - 1) / rpw;
   const int64_t C = nwg * k;
   float* ws_s = (float*)ws;
   int64_t* ws_i = (int64_t*)((char*)ws + (size_t)(Q * nch * k) * sizeof(float));
   const dim3 grid((unsigned)nwg, (unsigned)((Q + RQ - 1) / RQ));
   const int KC = kc_for(k);
-  const size_t lds = stage1_lds(D, KC);
+  // streaming kernel for k <= 16 (KC = 16 lists stay in registers); 8 or 12
+  // waves per workgroup (MICLIP_RANK_NW A/B), one workgroup per CU either way
+  // (~150 VGPRs, LDS = the list area).  KC = 64 keeps rank_stage1 (its 64-deep
+  // lists would go to scratch in the streaming kernel).
+  const char* nwenv = getenv("MICLIP_RANK_NW");
+  const int NW = nwenv && atoi(nwenv) == 8 ? 8 : 12;
+  const size_t qa = (size_t)RQ * (D + 4) * 4 + (size_t)NW * 32 * 4 + RQ * 4;
+  const size_t la = (size_t)64 * NW * KC * 8;
+  const size_t lds = qa > la ? qa : la;
   hipError_t e;
+  const char* legacy = getenv("MICLIP_RANK_STAGE1");   // A/B: the previous one-tile-at-a-time kernel
+  if (KC == 64 || (legacy && legacy[0] == '1')) {
 #define MI_S1(KCV, DTV) \
-  launch_stage1<KCV, DTV>(grid, lds, s, corpus, N, D, q, Q, k, rpw, norm_mode, nan_first, base, ws_s, ws_i, C)
-  if (KC == 16) e = dt == 0 ? MI_S1(16, 0) : dt == 1 ? MI_S1(16, 1) : MI_S1(16, 2);
-  else e = dt == 0 ? MI_S1(64, 0) : dt == 1 ? MI_S1(64, 1) : MI_S1(64, 2);
+  launch_stage1<KCV, DTV>(grid, stage1_lds(D, KCV), s, corpus, N, D, q, Q, k, rpw, norm_mode, nan_first, base, ws_s, \
+                          ws_i, C)
+    if (KC == 16) e = dt == 0 ? MI_S1(16, 0) : dt == 1 ? MI_S1(16, 1) : MI_S1(16, 2);
+    else e = dt == 0 ? MI_S1(64, 0) : dt == 1 ? MI_S1(64, 1) : MI_S1(64, 2);
 #undef MI_S1
+  } else {
+#define MI_RS(DTV, NWV) \
+  launch_stream<DTV, NWV>(grid, lds, s, corpus, N, D, q, Q, k, rpw, norm_mode, nan_first, base, ws_s, ws_i, C)
+    if (NW == 8) e = dt == 0 ? MI_RS(0, 8) : dt == 1 ? MI_RS(1, 8) : MI_RS(2, 8);
+    else e = dt == 0 ? MI_RS(0, 12) : dt == 1 ? MI_RS(1, 12) : MI_RS(2, 12);
+#undef MI_RS
+  }
   if (e != hipSuccess) return e;
   return rank_merge(ws_s, ws_i, Q, C, k, nan_first, out_s, out_i, s);
 }

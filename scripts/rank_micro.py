@@ -1,0 +1,67 @@
+"""A/B of the fused rank kernel variants in ONE process, interleaved rounds
+(MICLIP_RANK_STAGE1=1: the one-tile-at-a-time kernel; MICLIP_RANK_NW=8/12:
+the streaming kernel's waves per workgroup), HIP events on the launch stream.
+
+  python scripts/rank_micro.py [rounds]
+"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "event-retrival-in-video-learning-transferable-visual-model-from-supervised-natural-language_amd"))
+
+import torch  # noqa: E402
+from miclip import retrieval  # noqa: E402
+
+VARIANTS = {"stage1": {"MICLIP_RANK_STAGE1": "1"}, "nw8": {"MICLIP_RANK_NW": "8"}, "nw12": {"MICLIP_RANK_NW": "12"}}
+SHAPES = [(125_000, 512, 32, torch.float32), (1_000_000, 512, 32, torch.float32),
+          (1_000_000, 512, 32, torch.bfloat16), (1_000_000, 768, 32, torch.float32), (10_000, 512, 32, torch.float32)]
+
+
+def setenv(v):
+    for k in ("MICLIP_RANK_STAGE1", "MICLIP_RANK_NW"):
+        os.environ.pop(k, None)
+    os.environ.update(VARIANTS[v])
+
+
+def main():
+    rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev).manual_seed(3)
+    res = {}
+    for (N, D, Q, dt) in SHAPES:
+        corpus = torch.randn(N, D, device=dev, generator=g).to(dt)
+        q = torch.nn.functional.normalize(torch.randn(Q, D, device=dev, generator=g), dim=1)
+        name = f"N{N // 1000}k_D{D}_{'f32' if dt == torch.float32 else 'bf16'}"
+        ref = None
+        for v in VARIANTS:           # parity across variants: identical indices and scores
+            setenv(v)
+            s, i = retrieval.rank_topk(corpus, q, 10)
+            if ref is None:
+                ref = (s.clone(), i.clone())
+            else:
+                assert torch.equal(i, ref[1]) and torch.equal(s, ref[0]), (name, v)
+        times = {v: [] for v in VARIANTS}
+        stream = torch.cuda.current_stream(dev)
+        for _ in range(rounds):
+            for v in VARIANTS:
+                setenv(v)
+                retrieval.rank_topk(corpus, q, 10)
+                torch.cuda.synchronize(dev)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                for _ in range(10):
+                    retrieval.rank_topk(corpus, q, 10)
+                e1.record(stream)
+                torch.cuda.synchronize(dev)
+                times[v].append(e0.elapsed_time(e1) * 100)
+        nb = corpus.numel() * corpus.element_size()
+        res[name] = {v: {"us": round(min(t), 1), "gbs": round(nb / min(t) / 1e3, 1)} for v, t in times.items()}
+        print(name, json.dumps(res[name]), flush=True)
+        del corpus
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
