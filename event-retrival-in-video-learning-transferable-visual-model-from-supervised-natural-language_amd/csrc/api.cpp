@@ -395,6 +395,26 @@ static int gemm_variant() {
   return v;
 }
 
+// Per-GEMM schedule overrides for A/B runs of the whole encoder
+// (MICLIP_GEMM_VARIANT_{QKV,OUT,FC,PROJ}; 0 = MICLIP_GEMM_VARIANT / default).
+enum { GV_QKV = 0, GV_OUT = 1, GV_FC = 2, GV_PROJ = 3 };
+static int gemm_variant_for(int which) {
+  static int v[4] = {-1, -1, -1, -1};
+  static const char* names[4] = {"MICLIP_GEMM_VARIANT_QKV", "MICLIP_GEMM_VARIANT_OUT", "MICLIP_GEMM_VARIANT_FC",
+                                 "MICLIP_GEMM_VARIANT_PROJ"};
+  if (v[which] < 0) {
+    const char* e = getenv(names[which]);
+    v[which] = e ? atoi(e) : 0;
+  }
+  return v[which];
+}
+
+static GemmArgs with_variant(GemmArgs g, int which) {
+  const int v = gemm_variant_for(which);
+  if (v) g.variant = v;
+  return g;
+}
+
 static GemmArgs gargs(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, const float* bias, void* out,
                       int64_t ldo, int M, int N, int K) {
   GemmArgs g;
@@ -455,12 +475,15 @@ static int run_tower(mi_clip* c, const std::vector<Layer>& layers, int B, int S,
   if (!h_ready) HIP_TRY(layernorm_bf16(c->x, W, layers[0].ln1_g, layers[0].ln1_b, c->h, W, M, W, s));
   for (size_t l = 0; l < layers.size(); ++l) {
     const Layer& L = layers[l];
-    HIP_TRY(gemm_bf16(gargs(c->h, W, L.w_qkv, W, L.b_qkv, c->qkv, 3 * W, M, 3 * W, W), EPI_BF16, s));
+    HIP_TRY(gemm_bf16(with_variant(gargs(c->h, W, L.w_qkv, W, L.b_qkv, c->qkv, 3 * W, M, 3 * W, W), GV_QKV), EPI_BF16,
+                      s));
     HIP_TRY(attention(c->qkv, c->att, B, S, W, causal, s));
-    HIP_TRY(gemm_bf16(gargs(c->att, W, L.w_out, W, L.b_out, c->delta, W, M, W, W), EPI_BF16, s));
+    HIP_TRY(gemm_bf16(with_variant(gargs(c->att, W, L.w_out, W, L.b_out, c->delta, W, M, W, W), GV_OUT), EPI_BF16, s));
     HIP_TRY(residual_ln(c->x, c->delta, W, 1, L.ln2_g, L.ln2_b, c->h, M, W, s, nullptr, nullptr, xmode_at(r16, l)));
-    HIP_TRY(gemm_bf16(gargs(c->h, W, L.w_fc, W, L.b_fc, c->mlp, 4 * W, M, 4 * W, W), EPI_GELU_BF16, s));
-    HIP_TRY(gemm_bf16(gargs(c->mlp, 4 * W, L.w_proj, 4 * W, L.b_proj, c->delta, W, M, W, 4 * W), EPI_BF16, s));
+    HIP_TRY(gemm_bf16(with_variant(gargs(c->h, W, L.w_fc, W, L.b_fc, c->mlp, 4 * W, M, 4 * W, W), GV_FC),
+                      EPI_GELU_BF16, s));
+    HIP_TRY(gemm_bf16(with_variant(gargs(c->mlp, 4 * W, L.w_proj, 4 * W, L.b_proj, c->delta, W, M, W, 4 * W), GV_PROJ),
+                      EPI_BF16, s));
     if (l + 1 < layers.size())
       HIP_TRY(residual_ln(c->x, c->delta, W, 1, layers[l + 1].ln1_g, layers[l + 1].ln1_b, c->h, M, W, s, nullptr, nullptr,
                           r16 ? 2 : 0));

@@ -542,9 +542,21 @@ __global__ __launch_bounds__(512) void gemm_abl_kernel(GemmArgs a) {
     asrc[j] = a.A + (int64_t)min(m0 + (wave * 2 + j) * 16 + lrow, a.M - 1) * a.lda + lchunk;
     wsrc[j] = a.W + (int64_t)(n0 + (wave * 2 + j) * 16 + lrow) * a.ldw + lchunk;
   }
+  // ABL 4/5: the same bytes per stage, fetched as full 128-byte row lines
+  // (8 rows x 128 B per instruction: rows of half (st & 1), k in [64*(st>>1), +64))
+  // instead of 16 rows x 64 B; the data is wrong, the timing shows the cost of
+  // half-line pieces.
+  const int frow = lane >> 3, fcol = (lane & 7) * 8;
   auto issue_half = [&](int st, int j) {
     if (ABL == 1) return;
     char* base = smem + (st % RING) * STAGE_BYTES;
+    if (ABL == 4 || ABL == 5) {
+      const int r0 = (st & 1) * 128 + (wave * 2 + j) * 8 + frow;
+      const int64_t k0 = (int64_t)(st >> 1) * 64 + fcol;
+      glds16(a.A + (int64_t)min(m0 + r0, a.M - 1) * a.lda + k0, base + (wave * 2 + j) * 1024);
+      glds16(a.W + (int64_t)(n0 + r0) * a.ldw + k0, base + A_BYTES + (wave * 2 + j) * 1024);
+      return;
+    }
     glds16(asrc[j] + (int64_t)st * BK, base + (wave * 2 + j) * 1024);
     glds16(wsrc[j] + st * BK, base + A_BYTES + (wave * 2 + j) * 1024);
   };
@@ -597,7 +609,7 @@ __global__ __launch_bounds__(512) void gemm_abl_kernel(GemmArgs a) {
     }
     if (grp == 1 && g + 1 < nk) wait_stage(g + 1);
     lgkm_barrier();
-    if (ABL == 3) {
+    if (ABL == 3 || ABL == 4) {
 #pragma unroll
       for (int ni = 0; ni < 4; ++ni) asm volatile("" ::"v"(bfr[ni]));
 #pragma unroll
@@ -662,7 +674,7 @@ __device__ unsigned long long g_gemm_probe[4096 * 4];
 
 // EARLY (variant 20): group 0, one section ahead, issues its epilogue during
 // group 1's last MFMA section and realigns afterwards (same barrier count).
-template <int EPI, bool PROBE = false, bool EARLY = false>
+template <int EPI, bool PROBE = false, bool EARLY = false, bool NTS = false>
 __global__ __launch_bounds__(512) void gemm_ppp_kernel(GemmArgs a) {
   constexpr int BM = 256, BN = 256;
   constexpr int WTM = 128, WTN = 64;
@@ -681,8 +693,10 @@ __global__ __launch_bounds__(512) void gemm_ppp_kernel(GemmArgs a) {
   int m0, n0;
   auto coords = [&](int v, int& mm, int& nn) {
     const int t = xcd_remap(v, ntiles);  // grid % 8 == 0 keeps a WG's tiles on its XCD's contiguous run
-    mm = (t / tiles_n) * BM;
-    nn = (t % tiles_n) * BN;
+    int mb, nb;
+    tile_coords(t, tiles_m, tiles_n, a.ngroup, mb, nb);   // ngroup 0: m-major raster
+    mm = mb * BM;
+    nn = nb * BN;
   };
   coords(vb, m0, n0);
 
@@ -814,7 +828,13 @@ __global__ __launch_bounds__(512) void gemm_ppp_kernel(GemmArgs a) {
         const auto sx = __builtin_amdgcn_permlane16_swap(pk[0].x, pk[1].x, false, false);
         const auto sy = __builtin_amdgcn_permlane16_swap(pk[0].y, pk[1].y, false, false);
         const int col = cn0 + wc * WTN + (2 * p + (g & 1)) * 16 + (g >> 1) * 8;
-        if (m < a.M) *(uint4*)((uint16_t*)a.out + (int64_t)m * a.ldo + col) = make_uint4(sx[0], sy[0], sx[1], sy[1]);
+        if (m < a.M) {
+          typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+          u32x4* dst = (u32x4*)((uint16_t*)a.out + (int64_t)m * a.ldo + col);
+          const u32x4 val = {sx[0], sy[0], sx[1], sy[1]};
+          if (NTS) __builtin_nontemporal_store(val, dst);
+          else *dst = val;
+        }
       }
     }
     if (EARLY && grp == 0) barrier();
@@ -889,6 +909,24 @@ hipError_t launch(const GemmArgs& a, hipStream_t s) {
     hipLaunchKernelGGL((gemm_pp_kernel<EPI, 1, false, true>), dim3(nt), dim3(512), 0, s, a);
     return hipGetLastError();
   }
+  if (big && v >= 60 && v < 80 && bf16_out && a.K / BK >= LEAD && !a.group) {
+    // persistent kernel, non-temporal output stores, n-blocks in groups of (v - 60)
+    GemmArgs ga = a;
+    ga.ngroup = v - 60;
+    const int nt = ((a.M + 255) / 256) * (a.N / 256);
+    const int grid = nt < cu_count() ? nt : cu_count();
+    hipLaunchKernelGGL((gemm_ppp_kernel<EPI, false, false, true>), dim3(grid), dim3(512), 0, s, ga);
+    return hipGetLastError();
+  }
+  if (big && v >= 40 && v < 60 && bf16_out && a.K / BK >= LEAD && !a.group) {
+    // tile-order probe: the persistent kernel with n-blocks walked in groups of (v - 40)
+    GemmArgs ga = a;
+    ga.ngroup = v - 40;
+    const int nt = ((a.M + 255) / 256) * (a.N / 256);
+    const int grid = nt < cu_count() ? nt : cu_count();
+    hipLaunchKernelGGL((gemm_ppp_kernel<EPI>), dim3(grid), dim3(512), 0, s, ga);
+    return hipGetLastError();
+  }
   if (big && v == 18 && bf16_out && a.K / BK >= LEAD && !a.group) {  // persistent ping-pong
     const int nt = ((a.M + 255) / 256) * (a.N / 256);
     const int grid = nt < cu_count() ? nt : cu_count();
@@ -917,6 +955,12 @@ hipError_t launch(const GemmArgs& a, hipStream_t s) {
     if (v == 31) hipLaunchKernelGGL(gemm_abl_kernel<1>, dim3(nt), dim3(512), 0, s, a);
     else if (v == 32) hipLaunchKernelGGL(gemm_abl_kernel<2>, dim3(nt), dim3(512), 0, s, a);
     else hipLaunchKernelGGL(gemm_abl_kernel<3>, dim3(nt), dim3(512), 0, s, a);
+    return hipGetLastError();
+  }
+  if (big && (v == 34 || v == 35) && a.K / BK >= LEAD && (a.K / BK) % 2 == 0) {  // full-line fetch probes
+    const int nt = ((a.M + 255) / 256) * (a.N / 256);
+    if (v == 34) hipLaunchKernelGGL(gemm_abl_kernel<4>, dim3(nt), dim3(512), 0, s, a);
+    else hipLaunchKernelGGL(gemm_abl_kernel<5>, dim3(nt), dim3(512), 0, s, a);
     return hipGetLastError();
   }
   if (big && v == 8 && a.K / BK >= LEAD) {
