@@ -909,7 +909,8 @@ hipError_t launch(const GemmArgs& a, hipStream_t s) {
     hipLaunchKernelGGL((gemm_pp_kernel<EPI, 1, false, true>), dim3(nt), dim3(512), 0, s, a);
     return hipGetLastError();
   }
-  if (big && v >= 60 && v < 80 && bf16_out && a.K / BK >= LEAD && !a.group) {
+  if (v == 70 && bf16_out && gemm_w4_ok(a)) return gemm_w4(a, EPI, s, cu_count());   // one wave per SIMD, BK 64
+  if (big && v >= 60 && v < 70 && bf16_out && a.K / BK >= LEAD && !a.group) {
     // persistent kernel, non-temporal output stores, n-blocks in groups of (v - 60)
     GemmArgs ga = a;
     ga.ngroup = v - 60;
