@@ -903,6 +903,9 @@ hipError_t launch(const GemmArgs& a, hipStream_t s) {
   // (N = 768: persistent on K = 768 since the stage streaming, +5 % on out500;
   // c_proj, K = 3072, stays one tile per workgroup: -3.8 % persistent)
   int v = a.variant == 0 ? (bf16_out ? ((a.N >= 2048 || a.K <= 1024) && !a.group ? 18 : 16) : 3) : a.variant;
+  // default for bf16 outputs since the 8-phase kernel (gemm_8p.hip): +12-18 % over 16/18 on all four
+  // B/32 tower shapes at M = 500k, bit-identical (scripts/gemm_micro.py); 16/18 stay for K % 128 != 0 / grouped rows
+  if (a.variant == 0 && bf16_out && gemm_8p_ok(a)) v = 80;
   if (v == 16 && !bf16_out) v = 3;
   if (big && v == 16 && a.K / BK >= LEAD) {
     const int nt = ((a.M + 255) / 256) * (a.N / 256);
@@ -910,6 +913,11 @@ hipError_t launch(const GemmArgs& a, hipStream_t s) {
     return hipGetLastError();
   }
   if (v == 70 && bf16_out && gemm_w4_ok(a)) return gemm_w4(a, EPI, s, cu_count());   // one wave per SIMD, BK 64
+  if (v >= 80 && v < 90 && bf16_out && gemm_8p_ok(a)) {   // 8-phase interleave; n-groups of (v - 80)
+    GemmArgs ga = a;
+    ga.ngroup = v - 80;
+    return gemm_8p(ga, EPI, s, cu_count());
+  }
   if (big && v >= 60 && v < 70 && bf16_out && a.K / BK >= LEAD && !a.group) {
     // persistent kernel, non-temporal output stores, n-blocks in groups of (v - 60)
     GemmArgs ga = a;
