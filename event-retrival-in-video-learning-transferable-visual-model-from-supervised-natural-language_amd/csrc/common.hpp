@@ -23,8 +23,14 @@ __device__ __host__ __forceinline__ u16 f2bf(float f) {
 
 // Hardware RNE conversion (v_cvt_pk_bf16_f32; keeps NaN a NaN).
 __device__ __forceinline__ u16 f2bf_hw(float f) { return __builtin_bit_cast(u16, (__bf16)f); }
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+// one v_cvt_pk_bf16_f32 for the pair (two scalar conversions + shift/or otherwise)
 __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
-  return (uint32_t)f2bf_hw(lo) | ((uint32_t)f2bf_hw(hi) << 16);
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){lo, hi}, bf16x2_t));
+}
+__device__ __forceinline__ uint32_t pack_bf16x2(f32x2 v) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
 }
 
 __device__ __host__ __forceinline__ float bf2f(u16 h) {

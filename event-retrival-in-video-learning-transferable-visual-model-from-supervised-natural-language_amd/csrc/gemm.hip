@@ -905,7 +905,7 @@ hipError_t launch(const GemmArgs& a, hipStream_t s) {
   int v = a.variant == 0 ? (bf16_out ? ((a.N >= 2048 || a.K <= 1024) && !a.group ? 18 : 16) : 3) : a.variant;
   // default for bf16 outputs since the 8-phase kernel (gemm_8p.hip): +12-18 % over 16/18 on all four
   // B/32 tower shapes at M = 500k, bit-identical (scripts/gemm_micro.py); 16/18 stay for K % 128 != 0 / grouped rows
-  if (a.variant == 0 && bf16_out && gemm_8p_ok(a)) v = 80;
+  if (a.variant == 0 && bf16_out && gemm_8p_ok(a)) v = 98;   // (+ early phase-1 DMAs: 0-3 % over 80)
   if (v == 16 && !bf16_out) v = 3;
   if (big && v == 16 && a.K / BK >= LEAD) {
     const int nt = ((a.M + 255) / 256) * (a.N / 256);
@@ -913,6 +913,10 @@ hipError_t launch(const GemmArgs& a, hipStream_t s) {
     return hipGetLastError();
   }
   if (v == 70 && bf16_out && gemm_w4_ok(a)) return gemm_w4(a, EPI, s, cu_count());   // one wave per SIMD, BK 64
+  if (((v >= 91 && v <= 96 && v != 95) || v == 87 || v == 88) && bf16_out && gemm_8p_ok(a)) return gemm_8p(a, EPI, s, cu_count(), v < 90 ? v - 80 : v - 90);   // 8-phase probes
+  if (v == 97 && bf16_out && gemm_8p_ok(a)) return gemm_8p(a, EPI, s, cu_count(), 100);   // 8-phase, aligned epilogue
+  if (v == 98 && bf16_out && gemm_8p_ok(a)) return gemm_8p(a, EPI, s, cu_count(), 101);   // 8-phase, early phase-1 DMAs
+  if (v == 99 && bf16_out && gemm_8p_ok(a)) return gemm_8p(a, EPI, s, cu_count(), 102);   // both
   if (v >= 80 && v < 90 && bf16_out && gemm_8p_ok(a)) {   // 8-phase interleave; n-groups of (v - 80)
     GemmArgs ga = a;
     ga.ngroup = v - 80;

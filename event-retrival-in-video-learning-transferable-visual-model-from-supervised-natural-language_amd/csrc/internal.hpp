@@ -63,7 +63,7 @@ int gemm_w4_ok(const GemmArgs& a);
 hipError_t gemm_w4(const GemmArgs& a, int epi, hipStream_t s, int cus);
 // 8-phase interleaved ping-pong, 256x256x64 persistent (gemm_8p.hip); bf16 epilogues, K % 128 == 0
 int gemm_8p_ok(const GemmArgs& a);
-hipError_t gemm_8p(const GemmArgs& a, int epi, hipStream_t s, int cus);
+hipError_t gemm_8p(const GemmArgs& a, int epi, hipStream_t s, int cus, int abl = 0);
 // variant 19's per-workgroup timestamps (gemm.hip g_gemm_probe) -> host
 hipError_t gemm_probe_read(unsigned long long* host, int n);
 // MX-fp8: A, W e4m3 bytes (row strides lda/ldw in BYTES), a_scale/w_scale e8m0; K % 128 == 0, N % 256 == 0
