@@ -711,7 +711,7 @@ int mi_op_residual_ln(void* x, const void* delta, const float* g, const float* b
 
 int mi_op_attention(const void* qkv, void* out, int32_t B, int32_t S, int32_t W, int32_t causal, void* stream) {
   if (!qkv || !out || B < 0 || S < 1) return fail(MI_ERR_ARG, "mi_op_attention: bad arguments");
-  if (W % 64 || S > 640 || (causal & ~0x101)) return fail(MI_ERR_UNSUPPORTED, "mi_op_attention: W %% 64 == 0 and S <= 640");
+  if (W % 64 || S > 640 || (causal & ~0x301)) return fail(MI_ERR_UNSUPPORTED, "mi_op_attention: W %% 64 == 0 and S <= 640");
   HIP_TRY(attention((const uint16_t*)qkv, (uint16_t*)out, B, S, W, causal, (hipStream_t)stream));
   return MI_OK;
 }

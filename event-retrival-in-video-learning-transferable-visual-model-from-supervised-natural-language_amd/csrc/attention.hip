@@ -3,6 +3,8 @@
 // tower), restated in oracle/clip_ref.py::_mha.  Built with -fno-honor-nans
 // (Makefile): the softmax max/sum chains then compile to v_max3 without NaN
 // canonicalisation; -inf masking is unaffected.
+#include <type_traits>
+
 #include "common.hpp"
 #include "internal.hpp"
 
@@ -357,6 +359,207 @@ __global__ __launch_bounds__(512) void attention_flash_kernel(const uint16_t* __
   }
 }
 
+
+// ----------------------------- attention, vision towers: K/V resident in LDS
+// 64 < S <= 640, non-causal (ViT-L/14 257 tokens, L/14@336 577).  One
+// workgroup of NW waves per (sequence, head).  The whole head's K and V
+// (rows padded to 32, rows >= S clamped copies: masked / multiplied by P = 0)
+// are DMA'd into LDS ONCE (global_load_lds, 8 rows x 128 B per instruction),
+// then every wave runs its query tiles (16 rows: w, w + NW, ...) over all keys
+// with no further workgroup barrier — a straggler wave no longer parks the
+// other seven at a per-chunk barrier, and a second workgroup on the CU
+// (S = 257: 72 KB of LDS each) fills the SIMDs meanwhile.
+//   K image : 16-byte chunk c of key row r at slot c ^ ((r >> 1) & 7) (the 16
+//             rows of a ds_read_b128 A-operand read hit all 16 slots);
+//   V image : row-major [key][64 dims], 8-byte unit u at u ^ (((r >> 1) & 3) << 2),
+//             read transposed by ds_read_b64_tr_b16 into the V^T A operand of
+//             O^T = V^T P^T (a 32-lane half = 8 consecutive keys x 4 units:
+//             all 32 8-byte bank pairs once) — no transposing LDS writes;
+//   per 64-key chunk: S^T = K Q^T (8 MFMA), online softmax in the log2
+//   domain with lazy rescale (flash kernel above), P to bf16, 8 PV MFMAs;
+//   the partial last chunk runs only its valid 16-key tiles (NKT template).
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void attention_res_kernel(const uint16_t* __restrict__ qkv,
+                                                                uint16_t* __restrict__ out, int S, int W, int H,
+                                                                uint8_t* __restrict__ q8, uint8_t* __restrict__ qs,
+                                                                int64_t rows_pad) {
+  extern __shared__ __attribute__((aligned(16))) char res_lds[];
+  const int spad = (S + 31) & ~31;
+  char* Kimg = res_lds;
+  char* Vimg = res_lds + spad * 128;
+  const int item = blockIdx.x;
+  const int bseq = item / H, h = item % H;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t ld = 3 * (int64_t)W;
+  const uint16_t* qb = qkv + (int64_t)bseq * S * ld + h * 64;
+  const uint16_t* kb = qb + W;
+  const uint16_t* vb = qb + 2 * W;
+
+  // ---- K, V -> LDS (one DMA instruction = 8 rows)
+  {
+    const int nr8 = spad >> 3;
+    const int slot = lane & 7;
+    for (int i = wave; i < 2 * nr8; i += NW) {
+      const bool isv = i >= nr8;
+      const int i8 = isv ? i - nr8 : i;
+      const int r = i8 * 8 + (lane >> 3);
+      const int c = isv ? (slot ^ (((r >> 1) & 3) << 1)) : (slot ^ ((r >> 1) & 7));
+      glds16((isv ? vb : kb) + (int64_t)min(r, S - 1) * ld + c * 8, (isv ? Vimg : Kimg) + i8 * 1024);
+    }
+  }
+
+  const int nqt = (S + 15) / 16, nch = (S + 63) / 64;
+  const int last_kvalid = S - (nch - 1) * 64;   // 1..64
+  const int fr = lane & 15, g = lane >> 4;
+  const float sl2 = 0.125f * 1.4426950408889634f;  // head_dim^-0.5 * log2(e)
+  constexpr float RESCALE = 8.0f;
+  const int rk0 = fr * 128 + (((0 + g) ^ (fr >> 1)) << 4);
+  const int rk1 = fr * 128 + (((4 + g) ^ (fr >> 1)) << 4);
+  const int vq = (lane & 15) >> 2, vp = lane & 3;
+  const int vx = (2 * g + (vq >> 1)) & 3;
+  const int rvb = (4 * g + vq) * 128 + vp * 8;
+  typedef short s16x4 __attribute__((ext_vector_type(4)));
+  auto tr_read = [&](const char* p) -> s16x4 {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(LDS_AS char*)(uintptr_t)(const LDS_AS char*)p);
+  };
+
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  for (int t = wave; t < nqt; t += NW) {
+    bf16x8 qf[2];
+    {
+      const int qrow = min(t * 16 + fr, S - 1);
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) qf[s2] = *(const bf16x8*)(qb + (int64_t)qrow * ld + 32 * s2 + 8 * g);
+    }
+    float m = -INFINITY, l = 0.f;
+    f32x4 o[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // one 64-key chunk; NKT valid 16-key tiles, MASK: keys >= S inside them
+    auto chunk = [&](auto nkt_c, auto mask_c, int c) {
+      constexpr int NKT = decltype(nkt_c)::value;
+      constexpr bool MASK = decltype(mask_c)::value;
+      const char* kc = Kimg + c * 64 * 128;
+      f32x4 sc[NKT];
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt) {
+        const bf16x8 k0 = *(const bf16x8*)(kc + kt * 16 * 128 + rk0);
+        const bf16x8 k1 = *(const bf16x8*)(kc + kt * 16 * 128 + rk1);
+        f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k0, qf[0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        sc[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k1, qf[1], acc, 0, 0, 0);
+      }
+      // sc[kt][j]: query t*16 + fr, key c*64 + kt*16 + 4g + j
+      if (MASK) {
+#pragma unroll
+        for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (c * 64 + kt * 16 + 4 * g + j >= S) sc[kt][j] = -INFINITY;
+      }
+      float cm = fmaxf(fmaxf(sc[0][0], sc[0][1]), fmaxf(sc[0][2], sc[0][3]));
+#pragma unroll
+      for (int kt = 1; kt < NKT; ++kt) cm = fmaxf(cm, fmaxf(fmaxf(sc[kt][0], sc[kt][1]), fmaxf(sc[kt][2], sc[kt][3])));
+      {
+        const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(cm), __float_as_uint(cm), false, false);
+        cm = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+        const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(cm), __float_as_uint(cm), false, false);
+        cm = fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+      }
+      const float cmu = cm * sl2;   // finite: chunk 0 holds key 0 for every row
+      if (cmu > m + RESCALE) {
+        const float alpha = __builtin_amdgcn_exp2f(m - cmu);
+        l *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
+        m = cmu;
+      }
+      float ps = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sc[kt][j] = __builtin_amdgcn_exp2f(fmaf(sc[kt][j], sl2, -m));
+        ps += (sc[kt][0] + sc[kt][1]) + (sc[kt][2] + sc[kt][3]);
+      }
+      l += ps;
+#pragma unroll
+      for (int s2 = 0; s2 < (NKT + 1) / 2; ++s2) {
+        bf16x8 pb;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          pb[j] = (__bf16)sc[2 * s2][j];
+          pb[4 + j] = 2 * s2 + 1 < NKT ? (__bf16)sc[(2 * s2 + 1) < NKT ? 2 * s2 + 1 : 0][j] : (__bf16)0.f;
+        }
+        const char* vc = Vimg + (c * 64 + 32 * s2) * 128 + rvb;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          const s16x4 lo = tr_read(vc + ((dt ^ vx) << 5));
+          const s16x4 hi = tr_read(vc + 16 * 128 + ((dt ^ vx) << 5));
+          typedef short s16x8 __attribute__((ext_vector_type(8)));
+          const s16x8 v8 = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+          const bf16x8 vf = __builtin_bit_cast(bf16x8, v8);
+          o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pb, o[dt], 0, 0, 0);
+        }
+      }
+    };
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, 3>;
+    using I4 = std::integral_constant<int, 4>;
+    using BF = std::integral_constant<bool, false>;
+    using BT = std::integral_constant<bool, true>;
+    for (int c = 0; c < nch - 1; ++c) chunk(I4{}, BF{}, c);
+    {
+      const int c = nch - 1;
+      if (last_kvalid > 48) chunk(I4{}, BT{}, c);
+      else if (last_kvalid > 32) chunk(I3{}, BT{}, c);
+      else if (last_kvalid > 16) chunk(I2{}, BT{}, c);
+      else chunk(I1{}, BT{}, c);
+    }
+
+    float lt = l;
+    {
+      const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(lt), __float_as_uint(lt), false, false);
+      lt = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+      const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(lt), __float_as_uint(lt), false, false);
+      lt = __uint_as_float(b[0]) + __uint_as_float(b[1]);
+    }
+    const float inv = 1.0f / lt;
+    const int qrow = t * 16 + fr;
+    // o[dt][j]: query qrow, head dim dt*16 + 4g + j
+    if (q8) {  // MX-fp8 output: this head's 64 dims are one 64-k block of out_proj
+      float amax = 0.f;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) amax = fmaxf(amax, fabsf(o[dt][j] * inv));
+      amax = fmaxf(amax, __shfl_xor(amax, 16, 64));
+      amax = fmaxf(amax, __shfl_xor(amax, 32, 64));
+      const int X = mx_block_exp(amax);
+      const float scl = ldexpf(1.0f, -X);
+      if (qrow < S) {
+        const int64_t row = (int64_t)bseq * S + qrow;
+        uint8_t* dst = q8 + row * W + h * 64 + 4 * g;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+          *(uint32_t*)(dst + dt * 16) = mx_pack4(o[dt][0] * inv, o[dt][1] * inv, o[dt][2] * inv, o[dt][3] * inv, scl);
+        if (g == 0) qs[mx_scale_index(row, h, rows_pad)] = (uint8_t)(X + 127);
+      }
+      continue;
+    }
+    if (qrow < S) {
+      uint16_t* dst = out + ((int64_t)bseq * S + qrow) * W + h * 64 + 4 * g;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+        *(uint2*)(dst + dt * 16) = make_uint2(pack_bf16x2(o[dt][0] * inv, o[dt][1] * inv),
+                                              pack_bf16x2(o[dt][2] * inv, o[dt][3] * inv));
+    }
+  }
+}
+
 }  // namespace
 
 hipError_t attention(const uint16_t* qkv, uint16_t* out, int B, int S, int W, int causal, hipStream_t s, uint8_t* q8,
@@ -371,8 +574,24 @@ hipError_t attention(const uint16_t* qkv, uint16_t* out, int B, int S, int W, in
   // kernel it replaced).  Causal bit 8 selects the one-wave kernel for S <= 96
   // (A/B and parity tests of both paths; it has no fp8 output).
   const bool one_wave = ((causal >> 8) & 1) && S <= 96 && !q8;
+  const bool old_flash = (causal >> 9) & 1;   // A/B: the chunk-streaming flash kernel for S > 64
   causal &= 1;
   const dim3 grid(items);
+  if (!one_wave && !old_flash && !causal && S > 64) {
+    // vision towers (257 / 577 tokens): K/V resident in LDS, no per-chunk barriers
+    const int spad = (S + 31) & ~31;
+    const size_t lds = 2 * (size_t)spad * 128;
+    static bool attr_set = false;
+    if (!attr_set) {
+      hipError_t e = hipFuncSetAttribute((const void*)attention_res_kernel<8>,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      if (e != hipSuccess) return e;
+      attr_set = true;
+    }
+    const int64_t rp = ((int64_t)B * S + 1) & ~1;
+    hipLaunchKernelGGL(attention_res_kernel<8>, grid, dim3(512), lds, s, qkv, out, S, W, H, q8, qs, rp);
+    return hipGetLastError();
+  }
   if (one_wave) {
     if (S <= 32) hipLaunchKernelGGL(attention_kernel<32>, grid, dim3(64), 0, s, qkv, out, S, W, H, causal, items);
     else if (S <= 64) hipLaunchKernelGGL(attention_kernel<64>, grid, dim3(64), 0, s, qkv, out, S, W, H, causal, items);

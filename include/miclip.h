@@ -181,7 +181,9 @@ int mi_preprocess_frames(const uint8_t* frames, int64_t B, int32_t H, int32_t W,
  *   (nn.Linear of attn.in_proj / out_proj / mlp.c_fc / c_proj, conv1 as GEMM)
  * mi_op_layernorm: bf16 out = LN(x f32 [rows,W]) (openai/CLIP LayerNorm, fp32)
  * mi_op_attention: bf16 [B*S, W] = MHA core over packed qkv bf16 [B*S, 3W]
- *   (nn.MultiheadAttention softmax(qk^T/8)v per 64-wide head; causal for text) */
+ *   (nn.MultiheadAttention softmax(qk^T/8)v per 64-wide head; causal for text).
+ *   causal bit 0: causal mask; bits 8 / 9 select the alternative kernels for
+ *   A/B and parity tests (one-wave S <= 96 / chunk-streaming flash S > 64) */
 int mi_op_gemm(const void* A, const void* W, const float* bias, void* out, int32_t M, int32_t N, int32_t K,
                int32_t epilogue, void* stream);
 int mi_op_layernorm(const float* x, const float* gamma, const float* beta, void* out, int32_t rows, int32_t W,

@@ -1,6 +1,6 @@
 """Attention microbenchmark through mi_op_attention (random bf16 qkv, HIP events).
 Shapes: the bench chunk of each tower.  Every S runs the flash kernel (K/V chunks in LDS) by default;
-causal bit 8 selects the one-wave LDS-P kernel for S <= 96.  usage: python scripts/attn_micro.py [reps] [shape,shape...]"""
+causal bit 8 selects the one-wave LDS-P kernel for S <= 96, bit 9 the chunk-streaming flash kernel for S > 64 (default there: K/V resident in LDS).  usage: python scripts/attn_micro.py [reps] [shape,shape...]"""
 import os
 import sys
 
@@ -12,7 +12,9 @@ import torch  # noqa: E402
 from miclip import _native as N  # noqa: E402
 
 SHAPES = [("B/32", 2000, 50, 768, 0), ("text", 256, 77, 512, 1), ("L/14", 385, 257, 1024, 0),
-          ("L/14@336", 173, 577, 1024, 0)]
+          ("L/14@336", 173, 577, 1024, 0),
+          # the bench chunks of configs[2] (L/14, 1667 frames) and configs[4] (L/14@336)
+          ("L/14c", 1667, 257, 1024, 0), ("L/14@336c", 1000, 577, 1024, 0)]
 
 
 def main():
@@ -26,7 +28,7 @@ def main():
             continue
         qkv = (torch.randn(B * S, 3 * W, device=dev) * 1.5).bfloat16()
         outs = {}
-        for mode in ([0, 0x100] if S <= 96 else [0]):
+        for mode in ([0, 0x100] if S <= 96 else [0, 0x200]):
             out = torch.empty(B * S, W, dtype=torch.bfloat16, device=dev)
             run = lambda: N.check(L.mi_op_attention(qkv.data_ptr(), out.data_ptr(), B, S, W, causal | mode, sp), "attn")
             run()
@@ -42,7 +44,7 @@ def main():
             fl = 4.0 * B * S * S * W * (0.5 if causal else 1.0)
             by = B * S * 4 * W * 2
             d = (out.float() - outs[0].float()).abs().max().item()
-            kind = {0: "flash", 0x100: "one-wave"}[mode]
+            kind = {0: "default", 0x100: "one-wave", 0x200: "flash(chunked)"}[mode]
             print(f"{name:9s} {kind:16s} B={B} S={S} W={W}: {us:8.1f} us "
                   f"{fl / us / 1e6:6.1f} TFLOP/s {by / us / 1e3:7.1f} GB/s  maxdiff {d:.3g}", flush=True)
 

@@ -116,7 +116,9 @@ def test_residual_ln(gpu, rows, W, xmode):
                                           # causal, chunk boundaries
                                           (2, 577, 1024, 0), (1, 300, 256, 1), (3, 130, 128, 0), (1, 640, 128, 1),
                                           (2, 97, 256, 0), (1, 128, 192, 1), (2, 385, 128, 0)])
-@pytest.mark.parametrize("flash", [0, 0x100])   # flash kernel (default) / one-wave kernel (S <= 96)
+# default (S > 64 non-causal: K/V resident in LDS; else the flash kernel) / one-wave kernel (S <= 96) /
+# chunk-streaming flash kernel (S > 64)
+@pytest.mark.parametrize("flash", [0, 0x100, 0x200])
 def test_attention(gpu, B, S, W, causal, flash):
     import torch
     N_ = _lib()
@@ -147,10 +149,12 @@ def test_errors_are_raised(gpu):
 
 
 @pytest.mark.parametrize("S", [577, 257, 130])
-def test_attention_growing_max(gpu, S):
+@pytest.mark.parametrize("mode", [0, 0x200])
+def test_attention_growing_max(gpu, S, mode):
     """Scores whose row max keeps growing along the keys: every 64-key chunk
     moves the running max by more than the lazy-rescale threshold (2^8), so
-    the rescale branch of attention_flash_kernel runs on each chunk."""
+    the rescale branch runs on each chunk (attention_res_kernel by default,
+    attention_flash_kernel with bit 9)."""
     import torch
     N_ = _lib()
     B, W = 2, 256
@@ -161,7 +165,7 @@ def test_attention_growing_max(gpu, S):
     qkv[:, :, 1] = qkv[:, :, 1].abs() * ramp                           # k grows with the key index
     qkv = qkv.reshape(B * S, 3 * W).bfloat16().to(gpu)
     out = torch.empty(B * S, W, dtype=torch.bfloat16, device=gpu)
-    N_.check(N_.lib().mi_op_attention(qkv.data_ptr(), out.data_ptr(), B, S, W, 0, _stream()), "attention")
+    N_.check(N_.lib().mi_op_attention(qkv.data_ptr(), out.data_ptr(), B, S, W, mode, _stream()), "attention")
     torch.cuda.synchronize()
     H = W // 64
     x = qkv.double().reshape(B, S, 3, H, 64)
