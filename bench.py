@@ -447,7 +447,7 @@ def main():
             eb = 1 if fp8 else 2            # operand element bytes (fp8 adds 1/64 B of scales per element)
             roof = {"bound": "mfma",
                     "kernel": ("gemm_mx_kernel<EPI_GELU_BF16> (mlp.c_fc + QuickGELU, MX-fp8 operands)" if fp8
-                               else "gemm_8p_kernel<EPI_GELU_BF16> (8-phase interleaved persistent, 256x256x64; mlp.c_fc + QuickGELU)"),
+                               else "gemm_8q_kernel<EPI_GELU_BF16> (8-phase interleaved persistent, 256x256x64, descriptor DMAs; mlp.c_fc + QuickGELU)"),
                     "achieved": round(ach, 1), "peak": peak, "unit": "TFLOP/s",
                     "frac": round(ach / peak, 4), "traffic": None if fp8 else traffic,
                     "traffic_source": None if fp8 else tsrc,

@@ -691,6 +691,12 @@ extern "C" int mi_debug_gemm_probe(unsigned long long* host, int32_t n) {
   return MI_OK;
 }
 
+extern "C" int mi_debug_gemm8q_probe(unsigned long long* host, int32_t n) {
+  if (!host || n < 0) return fail(MI_ERR_ARG, "mi_debug_gemm8q_probe: bad arguments");
+  HIP_TRY(gemm8q_probe_read(host, n));
+  return MI_OK;
+}
+
 int mi_op_layernorm(const float* x, const float* g, const float* b, void* out, int32_t rows, int32_t W,
                     void* stream) {
   if (!x || !g || !b || !out || rows < 0) return fail(MI_ERR_ARG, "mi_op_layernorm: bad arguments");

@@ -906,11 +906,22 @@ hipError_t launch(const GemmArgs& a, hipStream_t s) {
   // default for bf16 outputs since the 8-phase kernel (gemm_8p.hip): +12-18 % over 16/18 on all four
   // B/32 tower shapes at M = 500k, bit-identical (scripts/gemm_micro.py); 16/18 stay for K % 128 != 0 / grouped rows
   if (a.variant == 0 && bf16_out && gemm_8p_ok(a)) v = 98;   // (+ early phase-1 DMAs: 0-3 % over 80)
+  // default since gemm_8q.hip (descriptor DMAs, template-form waits, descriptor-store epilogue):
+  // fc500 -4..-7 %, qkv500 -3..-4 %, proj500 -6 %, out500 +-3 % against v98, bit-identical
+  if (a.variant == 0 && bf16_out && gemm_8q_ok(a)) v = 110;
   if (v == 16 && !bf16_out) v = 3;
   if (big && v == 16 && a.K / BK >= LEAD) {
     const int nt = ((a.M + 255) / 256) * (a.N / 256);
     hipLaunchKernelGGL((gemm_pp_kernel<EPI, 1, false, true>), dim3(nt), dim3(512), 0, s, a);
     return hipGetLastError();
+  }
+  if (v >= 120 && v <= 124 && bf16_out) {   // 256 x 128 tiles, deferred epilogue (v98 where it does not apply)
+    if (gemm_8r_ok(a)) return gemm_8r(a, EPI, s, cu_count(), v - 120);
+    v = 98;
+  }
+  if (v >= 110 && v <= 119 && bf16_out) {   // 8-phase, second schedule (gemm_8p's v98 where it does not apply)
+    if (gemm_8q_ok(a)) return gemm_8q(a, EPI, s, cu_count(), v - 110);
+    v = 98;
   }
   if (v == 70 && bf16_out && gemm_w4_ok(a)) return gemm_w4(a, EPI, s, cu_count());   // one wave per SIMD, BK 64
   if (((v >= 91 && v <= 96 && v != 95) || v == 87 || v == 88) && bf16_out && gemm_8p_ok(a)) return gemm_8p(a, EPI, s, cu_count(), v < 90 ? v - 80 : v - 90);   // 8-phase probes

@@ -1,0 +1,488 @@
+// bf16 MFMA GEMM, 8-phase interleaved ping-pong, second schedule (gfx950):
+// C[M,N] = A[M,K] . W[N,K]^T (+ bias, QuickGELU), bf16 out — the tower GEMMs
+// of openai/CLIP's encode_image / encode_text.
+//
+// Same tile geometry, LDS image and quadrant order as gemm_8p.hip (256 x 256
+// tile, K staged 64 wide, 8 waves as 2 (M) x 4 (N), each wave 128 x 64 in
+// four 64 x 32 quadrants, one quadrant x 64 k = 16 MFMAs per phase, two
+// K-tile buffers, one iteration = 8 phases = 2 K-tiles).  Three changes,
+// each measured against gemm_8p (scripts/gpu_8p_abl.sh ablations: there the
+// no-MFMA build ran at 90 % of the full kernel's time, i.e. the memory
+// sections, not the MFMAs, set the phase length):
+//
+// 1. Buffer-descriptor DMAs (buffer_load_dwordx4 ... lds).  Each lane's row
+//    offsets inside a tile are fixed for the kernel's lifetime (6 VGPRs);
+//    the tile origin lives in the descriptor base (rebuilt by scalar code
+//    when the restage cursor changes tiles) and the k offset in soffset, so
+//    a DMA costs one M0 write and the load — gemm_8p spends ~8 VALU (64-bit
+//    multiply-adds) per DMA on the address.  Rows past M are out of the
+//    descriptor's range (num_records = the tile's valid rows x row bytes)
+//    and load zeros instead of a clamped row.
+// 2. Template-form waits (cdna_hip_programming.md §5 "The 256² 8-phase
+//    template"): a phase's fragment reads are waited for AFTER its first
+//    barrier (lgkmcnt(0) at the head of the MFMA section), so their latency
+//    overlaps the barrier instead of lengthening the memory section.  That
+//    needs every half-tile restaged two phases after its last read (WAR),
+//    so the issue table shifts by one phase and each K-tile is waited for
+//    with vmcnt(4) (two phases of DMAs younger than it):
+//      phase  reads (buffer)      restages
+//      1      even A_m0 + B_n0    odd  A_m1   (current pair)
+//      2      even B_n1           odd  B_n0   (current pair)
+//      3      even A_m1           even A_m0   (next pair; the cursor advances here)
+//      4      even B_n0           even B_n1   + vmcnt(4): odd buffer landed
+//      5      odd  A_m0 + B_n0    even A_m1
+//      6      odd  B_n1           even B_n0
+//      7      odd  A_m1           odd  A_m0   (next pair)
+//      8      odd  B_n0           odd  B_n1   + vmcnt(4): even buffer landed
+//    RAW: a buffer is read one phase after the wait that retires it (one
+//    barrier more than the stagger needs).  WAR: a half-tile's last reader
+//    (either M-group) has passed its lgkmcnt(0) before the barrier that
+//    precedes the restaging section of both groups.
+// 3. Epilogue: the previous tile's (bias, QuickGELU, bf16, permlane16-swapped
+//    16-byte row stores) opens the next tile's first phase, behind that
+//    phase's DMAs — which on a tile's first pair are BOTH odd half-tiles
+//    (A_m1 and B_n0): the last pair does not re-read B_n0 in phase 8 (it keeps
+//    phase 5's fragments), so B_n0's last read is three phases back.  The 16
+//    stores are then younger than every DMA the first pair's phase-4 wait
+//    needs (vmcnt(20)) and have until phase 8 to complete.  Stores go through
+//    a descriptor whose range is the tile's valid rows (no per-store branch or
+//    64-bit address math), the four bias reads share one wait, and a tile's
+//    first MFMA into each accumulator takes C = 0 (no zeroing pass).
+//    Measured alternatives: the epilogue split by quadrant over phases 1-4
+//    (+12 % on fc500: each quadrant's VALU lengthens a memory section the
+//    partner's 16 MFMAs cannot cover); a start stagger of half the workgroups
+//    (+-1 %: the store cost is per CU, ~48 cycles per 1-KB store instruction,
+//    not a chip-wide write burst; scripts/gemm_probe8q.py stamps).
+// Result (scripts/gemm_micro.py, M = 500k, interleaved with v98 in one process):
+// fc -4..-7 %, qkv -3..-4 %, proj -6 %, out +-3 %; bit-identical to gemm_8p.
+#include "common.hpp"
+#include "internal.hpp"
+
+namespace miclip {
+namespace {
+
+constexpr int BM = 256, BN = 256, BK8 = 64;
+constexpr int HALF = 128 * BK8 * 2;   // 16 KB half-tile
+constexpr int BUF = 4 * HALF;         // 64 KB K-tile buffer
+constexpr int H_A0 = 0, H_B0 = 1, H_B1 = 2, H_A1 = 3;
+// flags
+constexpr int F_GLDS = 1;   // flat global_load_lds with per-DMA address math (gemm_8p's) instead of descriptors
+
+__device__ __forceinline__ f32x2 quick_gelu2_8q(f32x2 v) {
+  const f32x2 t = v * (f32x2){-2.45546696f, -2.45546696f};   // -1.702 * log2(e)
+  f32x2 e = {__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)};
+  e = e + 1.0f;
+  return v * (f32x2){__builtin_amdgcn_rcpf(e.x), __builtin_amdgcn_rcpf(e.y)};
+}
+
+__device__ __forceinline__ void tile_coords_8q(int t, int tiles_m, int tiles_n, int ng, int& mb, int& nb) {
+  if (ng <= 0 || ng >= tiles_n) {
+    mb = t / tiles_n;
+    nb = t % tiles_n;
+    return;
+  }
+  const int per = tiles_m * ng;
+  const int gg = t / per, r = t - gg * per;
+  const int ngg = min(ng, tiles_n - gg * ng);
+  mb = r / ngg;
+  nb = gg * ng + r % ngg;
+}
+
+// timing probe (ABL 9, scripts/gemm_probe.py 8q): per workgroup and M-group, s_memtime stamps
+// of its third tile (see the S* comments) + two s_memrealtime stamps for the clock
+__device__ unsigned long long g_probe8q[1024 * 2 * 9];
+
+template <int P>
+struct Ph8q {
+  static constexpr int value = P;
+};
+template <bool V>
+struct BoolC {
+  static constexpr bool value = V;
+};
+
+// ABL (timing probes): 2 = no MFMAs, 4 = no epilogue work (accumulators kept live), 9 = stamps
+template <int EPI, int ABL = 0, int F = 0>
+__global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF + 2 * BN * 4];
+  float* sbias = (float*)(smem + 2 * BUF);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int tiles_n = a.N / BN;
+  const int tiles_m = (a.M + BM - 1) / BM;
+  const int ntiles = tiles_m * tiles_n;
+  const int npairs = a.K / (2 * BK8);
+  const int G = gridDim.x;
+  if ((int)blockIdx.x >= ntiles) return;
+
+  auto coords = [&](int v, int& mm, int& nn) {
+    const int t = xcd_remap(v, ntiles);
+    int mb, nb;
+    tile_coords_8q(t, tiles_m, tiles_n, a.ngroup, mb, nb);
+    mm = mb * BM;
+    nn = nb * BN;
+  };
+
+  // ---- restage cursor: K-tile pair rpp of tile rv (origin rm0, rn0)
+  int rv = blockIdx.x, rpp = 0, rm0, rn0;
+  coords(rv, rm0, rn0);
+  const int drow = lane >> 3;
+  const int c0 = (lane & 7) ^ (lane >> 4), c1 = (lane & 7) ^ (4 + (lane >> 4));
+  // per-lane byte offsets of this thread's two DMA rows in each half-tile
+  // (image row ir = (2 * wave + j) * 8 + drow, 16-byte slot c permuted on the source)
+  uint32_t voA0[2], voA1[2], voB[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int ir = (2 * wave + j) * 8 + drow;
+    const int c = j ? c1 : c0;
+    const int ra = (ir >> 6) * 128 + (ir & 63);
+    voA0[j] = (uint32_t)(ra * a.lda * 2 + c * 16);
+    voA1[j] = (uint32_t)((ra + 64) * a.lda * 2 + c * 16);
+    voB[j] = (uint32_t)(((ir >> 5) * 64 + (ir & 31)) * a.ldw * 2 + c * 16);
+  }
+  const int b1_sofs = 32 * (int)a.ldw * 2;   // B_n1 rows sit 32 rows below B_n0's
+  __amdgpu_buffer_rsrc_t rsA, rsW;
+  auto make_rs = [&]() {
+    const int rows = min(a.M - rm0, BM);
+    rsA = __builtin_amdgcn_make_buffer_rsrc((void*)(a.A + (int64_t)rm0 * a.lda), (short)0, rows * (int)a.lda * 2, 0x00020000);
+    rsW = __builtin_amdgcn_make_buffer_rsrc((void*)(a.W + (int64_t)rn0 * a.ldw), (short)0, BN * (int)a.ldw * 2, 0x00020000);
+  };
+  if (!(F & F_GLDS)) make_rs();
+  auto advance = [&]() {
+    if (++rpp == npairs) {
+      rpp = 0;
+      rv += G;
+      if (rv < ntiles) {   // past the end: keep re-loading the last tile's valid rows
+        coords(rv, rm0, rn0);
+        if (!(F & F_GLDS)) make_rs();
+      }
+    }
+  };
+  // one half-tile h of K-tile (2 * rpp + b) into buffer b: two 1-KB DMAs per thread
+  auto issue = [&](int h, int b) {
+    const int kofs = (2 * rpp + b) * BK8;
+    char* dst = smem + b * BUF + h * HALF + (2 * wave) * 1024;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      if (F & F_GLDS) {
+        const int ir = (2 * wave + j) * 8 + drow;
+        const int c = j ? c1 : c0;
+        const uint16_t* src;
+        if (h == H_A0 || h == H_A1) {
+          const int row = (ir >> 6) * 128 + (h == H_A1 ? 64 : 0) + (ir & 63);
+          src = a.A + (int64_t)min(rm0 + row, a.M - 1) * a.lda + kofs + c * 8;
+        } else {
+          const int row = (ir >> 5) * 64 + (h == H_B1 ? 32 : 0) + (ir & 31);
+          src = a.W + (int64_t)(rn0 + row) * a.ldw + kofs + c * 8;
+        }
+        glds16(src, dst + j * 1024);
+      } else if (h == H_A0 || h == H_A1) {
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (LDS_AS void*)(dst + j * 1024), 16, h == H_A1 ? voA1[j] : voA0[j],
+                                                 kofs * 2, 0, 0);
+      } else {
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsW, (LDS_AS void*)(dst + j * 1024), 16, voB[j],
+                                                 kofs * 2 + (h == H_B1 ? b1_sofs : 0), 0, 0);
+      }
+    }
+  };
+
+  // ---- fragment side
+  const int fr = lane & 15, fq = lane >> 4, g = fq;
+  const int rd0 = fr * 128 + (((0 + fq) ^ (fr >> 1)) << 4);   // k 0..31 of the K-tile
+  const int rd1 = fr * 128 + (((4 + fq) ^ (fr >> 1)) << 4);   // k 32..63
+  bf16x8 fa[4][2], fb0[2][2], fb1[2][2];
+  auto read_a = [&](const char* half) {
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) {
+      const char* p = half + (wr * 64 + mi * 16) * 128;
+      fa[mi][0] = *(const bf16x8*)(p + rd0);
+      fa[mi][1] = *(const bf16x8*)(p + rd1);
+    }
+  };
+  auto read_b = [&](const char* half, bf16x8 (&fb)[2][2]) {
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni) {
+      const char* p = half + (wc * 32 + ni * 16) * 128;
+      fb[ni][0] = *(const bf16x8*)(p + rd0);
+      fb[ni][1] = *(const bf16x8*)(p + rd1);
+    }
+  };
+  f32x4 acc[8][4];
+  auto barrier = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  unsigned long long st[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  int ti = 0;   // this workgroup's tile index
+  auto stamp = [&](int i) {
+    if ((ABL == 9 || ABL == 10) && ti == 2) {
+      __builtin_amdgcn_sched_barrier(0);
+      st[i] = __builtin_amdgcn_s_memtime();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  // previous tile (its epilogue runs in this tile's phases 1-4)
+  int pm0 = 0, pn0 = 0, ppar = 0;
+  bool has_prev = false;
+  int nxt_n0 = 0, cpar = 0;
+  bool has_next = false;
+
+  // the previous tile's epilogue: bias (+ QuickGELU), bf16, permlane16-swapped
+  // 16-byte row stores through a descriptor whose range is the tile's valid
+  // rows (rows past M are dropped by the range check: no per-store branch),
+  // each lane's row/column offset fixed for the kernel, the 16-row block in a
+  // scalar multiple, the column half in the instruction offset
+  typedef unsigned int u32x4_8q __attribute__((ext_vector_type(4)));
+  const uint32_t voO = (uint32_t)(((wr * 128 + fr) * a.ldo + wc * 64 + (g & 1) * 16 + (g >> 1) * 8) * 2);
+  const uint32_t blkO = (uint32_t)(16 * a.ldo * 2);
+  auto epilogue = [&]() {
+    if (ABL == 4) {
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) asm volatile("" ::"v"(acc[mi][ni]));
+      return;
+    }
+    float4 bias[4];
+    if (a.bias) {   // four reads under one wait, invisible to the compiler (gemm.hip lds_read_f4)
+      const uint32_t ba = (uint32_t)(uintptr_t)(const LDS_AS float*)(sbias + ppar * BN + wc * 64 + 4 * g);
+      asm volatile("ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:64\n\tds_read_b128 %2, %4 offset:128\n\t"
+                   "ds_read_b128 %3, %4 offset:192\n\ts_waitcnt lgkmcnt(0)"
+                   : "=&v"(bias[0]), "=&v"(bias[1]), "=&v"(bias[2]), "=&v"(bias[3]) : "v"(ba) : "memory");
+    } else {
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) bias[ni] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    const int rows = min(a.M - pm0, BM);
+    const __amdgpu_buffer_rsrc_t rsO = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)((uint16_t*)a.out + (int64_t)pm0 * a.ldo + pn0), (short)0, rows * (int)a.ldo * 2, 0x00020000);
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi) {
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        uint2 pk[2];
+#pragma unroll
+        for (int qq = 0; qq < 2; ++qq) {
+          const int ni = 2 * p + qq;
+          f32x2 lo = (f32x2){acc[mi][ni][0], acc[mi][ni][1]} + (f32x2){bias[ni].x, bias[ni].y};
+          f32x2 hi = (f32x2){acc[mi][ni][2], acc[mi][ni][3]} + (f32x2){bias[ni].z, bias[ni].w};
+          if (EPI == EPI_GELU_BF16) {
+            lo = quick_gelu2_8q(lo);
+            hi = quick_gelu2_8q(hi);
+          }
+          pk[qq] = make_uint2(pack_bf16x2(lo), pack_bf16x2(hi));
+        }
+        const auto sx = __builtin_amdgcn_permlane16_swap(pk[0].x, pk[1].x, false, false);
+        const auto sy = __builtin_amdgcn_permlane16_swap(pk[0].y, pk[1].y, false, false);
+        const u32x4_8q d = {sx[0], sy[0], sx[1], sy[1]};
+        if (ABL == 10) asm volatile("" ::"v"(d));   // stamp probe without the stores
+        else if (p == 0) __builtin_amdgcn_raw_buffer_store_b128(d, rsO, voO + mi * blkO, 0, 0);
+        else __builtin_amdgcn_raw_buffer_store_b128(d, rsO, voO + mi * blkO + 64, 0, 0);
+      }
+    }
+  };
+
+  // FIRST / LAST: the tile's first / last K-tile pair (compile-time: separate code paths)
+  auto phase = [&](auto pc, auto firstc, auto lastc) {
+    constexpr int P = decltype(pc)::value;
+    constexpr bool FIRST = decltype(firstc)::value, LAST = decltype(lastc)::value;
+    constexpr int b = P <= 4 ? 0 : 1;
+    constexpr int q = (P - 1) & 3;
+    const char* rbuf = smem + b * BUF;
+    if (P == 1 && FIRST) {
+      stamp(0);   // S0: tile start
+      if ((ABL == 9 || ABL == 10) && ti == 2) st[7] = __builtin_amdgcn_s_memrealtime();
+    }
+    if (P == 1) {
+      issue(H_A1, 1);
+      // a tile's first pair restages the odd B_n0 here too, ahead of the
+      // previous tile's stores: the last pair did not re-read it in phase 8
+      if (FIRST) issue(H_B0, 1);
+      __builtin_amdgcn_sched_barrier(0);
+      if (FIRST && has_prev) {
+        // the previous tile's whole epilogue, ahead of this phase's fragment
+        // reads (its bias reads wait lgkmcnt(0)), behind the phase's DMAs
+        epilogue();
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (FIRST) stamp(1);   // S1: epilogue issued
+    }
+    if (q == 0) {
+      read_a(rbuf + H_A0 * HALF);
+      read_b(rbuf + H_B0 * HALF, fb0);
+    } else if (q == 1) {
+      read_b(rbuf + H_B1 * HALF, fb1);
+    } else if (q == 2) {
+      read_a(rbuf + H_A1 * HALF);
+    } else if (!(LAST && P == 8)) {
+      read_b(rbuf + H_B0 * HALF, fb0);   // re-read (16 fewer live VGPRs than keeping it from the q = 0 phase)
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (P == 2 && !FIRST) issue(H_B0, 1);
+    if (P == 3) { advance(); issue(H_A0, 0); }
+    if (P == 4) issue(H_B1, 0);
+    if (P == 5) issue(H_A1, 0);
+    if (P == 6) issue(H_B0, 0);
+    if (P == 7) issue(H_A0, 1);
+    if (P == 8) issue(H_B1, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    // the awaited K-tile has two phases of DMAs younger than it; on a tile's
+    // first pair the previous tile's 16 epilogue stores are younger as well
+    // (they then have until phase 8 to complete)
+    if (P == 4) {
+      if (FIRST && has_prev && ABL != 10) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      if (FIRST) stamp(3);   // S3: first pair's phase-4 wait passed
+    }
+    if (P == 8 && FIRST) stamp(4);   // S4: before the first pair's phase-8 wait (the stores must be done)
+    if (P == 8) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    if (P == 8 && FIRST) stamp(5);   // S5: after it
+    if (P == 8 && LAST && has_next && wave == 0 && a.bias)   // next tile's bias, older than phase 1's DMAs
+      glds16(a.bias + nxt_n0 + lane * 4, sbias + (cpar ^ 1) * BN);
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (P == 1 && FIRST) stamp(2);   // S2: phase 1's MFMA section starts
+    __builtin_amdgcn_s_setprio(1);
+    constexpr int mh = q >= 2 ? 1 : 0, nh = (q == 1 || q == 2) ? 1 : 0;
+    auto& fb = nh ? fb1 : fb0;
+    if (ABL == 2) {
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) asm volatile("" ::"v"(fa[mi][0]), "v"(fa[mi][1]));
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) asm volatile("" ::"v"(fb[ni][0]), "v"(fb[ni][1]));
+    } else
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < 2; ++ni)
+            // a tile's first MFMA into each accumulator (first pair, phases 1-4, k-step 0)
+            // takes C = 0 as an inline constant: no zeroing pass between tiles
+            acc[mh * 4 + mi][nh * 2 + ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                fb[ni][ks], fa[mi][ks], (FIRST && P <= 4 && ks == 0) ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[mh * 4 + mi][nh * 2 + ni],
+                0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    barrier();
+  };
+  auto pair = [&](auto firstc, auto lastc) {
+    phase(Ph8q<1>{}, firstc, lastc);
+    phase(Ph8q<2>{}, firstc, lastc);
+    phase(Ph8q<3>{}, firstc, lastc);
+    phase(Ph8q<4>{}, firstc, lastc);
+    phase(Ph8q<5>{}, firstc, lastc);
+    phase(Ph8q<6>{}, firstc, lastc);
+    phase(Ph8q<7>{}, firstc, lastc);
+    phase(Ph8q<8>{}, firstc, lastc);
+  };
+
+  if (a.stagger_phases > 1) {   // start stagger (see GemmArgs)
+    const int ph = (blockIdx.x >> 3) % a.stagger_phases;
+    if (ph) {
+      const uint64_t until = __builtin_amdgcn_s_memrealtime() + (uint64_t)ph * a.stagger_ticks;
+      while (__builtin_amdgcn_s_memrealtime() < until) __builtin_amdgcn_s_sleep(8);
+    }
+  }
+  // ---- prologue: tile 0's bias, the whole even K-tile and the odd A_m0 / B_n1 of pair 0
+  {
+    int m0, n0;
+    coords(blockIdx.x, m0, n0);
+    if (wave == 0 && a.bias) glds16(a.bias + n0 + lane * 4, sbias);
+  }
+  issue(H_A0, 0);
+  issue(H_B1, 0);
+  issue(H_A1, 0);
+  issue(H_B0, 0);
+  issue(H_A0, 1);
+  issue(H_B1, 1);
+  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  barrier();
+  if (wr == 1) barrier();   // stagger the two M-groups by one barrier
+
+  for (int v = blockIdx.x; v < ntiles; v += G) {
+    int cm0, cn0;
+    coords(v, cm0, cn0);
+    has_next = v + G < ntiles;
+    if (has_next) {
+      int nm0;
+      coords(v + G, nm0, nxt_n0);
+    }
+    // (npairs >= 2, gemm_8q_ok: a one-pair instance beside these made hipcc spill ~200 VGPRs)
+    pair(BoolC<true>{}, BoolC<false>{});
+    for (int pp = 1; pp < npairs - 1; ++pp) pair(BoolC<false>{}, BoolC<false>{});
+    pair(BoolC<false>{}, BoolC<true>{});
+    stamp(6);   // S6: tile end
+    if ((ABL == 9 || ABL == 10) && ti == 2) st[8] = __builtin_amdgcn_s_memrealtime();
+    ++ti;
+    pm0 = cm0;
+    pn0 = cn0;
+    ppar = cpar;
+    has_prev = true;
+    cpar ^= 1;
+  }
+  // the last tile's epilogue
+  if (wr == 0) barrier();   // the M-groups' barrier counts meet
+  epilogue();
+  if ((ABL == 9 || ABL == 10) && lane == 0 && (wave & 3) == 0 && blockIdx.x < 1024) {
+#pragma unroll
+    for (int i = 0; i < 9; ++i) g_probe8q[(blockIdx.x * 2 + wr) * 9 + i] = st[i];
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // trailing (dummy) DMAs land before the workgroup's LDS is released
+}
+
+}  // namespace
+
+int gemm_8q_ok(const GemmArgs& a) {
+  // descriptors: a tile's rows x row bytes must fit num_records (int)
+  return a.N % BN == 0 && a.K % (2 * BK8) == 0 && a.K >= 4 * BK8 && a.M >= BM && !a.group && !a.patch_R &&
+         (int64_t)BM * a.lda * 2 < (1LL << 31) && (int64_t)BN * a.ldw * 2 < (1LL << 31) &&
+         (int64_t)(BM + 64) * a.lda * 2 < (1LL << 32);
+}
+
+// mode: 0 = default (descriptors), 2 = no-MFMA probe,
+// 3 = flat global_load_lds addressing, 4 = no-epilogue probe
+hipError_t gemm_8q(const GemmArgs& a0, int epi, hipStream_t s, int cus, int mode) {
+  GemmArgs a = a0;
+  if (mode == 5 || mode == 6 || mode == 7 || mode == 8) {   // start-stagger probes: 2 / 4 / 2 phases of ~1/2, 1/4, 1/4 tile
+    const int tile_ticks = (int)(2200LL * a.K / 768);   // ~22 us per 256 x 256 tile at K = 768
+    a.stagger_phases = mode == 6 ? 4 : 2;
+    a.stagger_ticks = (mode == 5 || mode == 8) ? tile_ticks / 2 : tile_ticks / 4;
+    mode = mode == 8 ? 9 : 0;   // 8: the stamp probe, staggered
+  }
+  const int nt = ((a.M + BM - 1) / BM) * (a.N / BN);
+  const int grid = nt < cus ? nt : cus;
+#define L8Q(E, ABL_, F_) hipLaunchKernelGGL((gemm_8q_kernel<E, ABL_, F_>), dim3(grid), dim3(512), 0, s, a)
+#define L8Q_ALL(E)                   \
+  if (mode == 0) L8Q(E, 0, 0);       \
+  else if (mode == 2) L8Q(E, 2, 0);  \
+  else if (mode == 3) L8Q(E, 0, F_GLDS); \
+  else if (mode == 4) L8Q(E, 4, 0);  \
+  else if (mode == 9) L8Q(E, 9, 0);  \
+  else if (mode == 1) L8Q(E, 10, 0);  \
+  else return hipErrorInvalidValue;
+  if (epi == EPI_GELU_BF16) {
+    L8Q_ALL(EPI_GELU_BF16)
+  } else if (epi == EPI_BF16) {
+    L8Q_ALL(EPI_BF16)
+  } else {
+    return hipErrorInvalidValue;
+  }
+#undef L8Q_ALL
+#undef L8Q
+  return hipGetLastError();
+}
+
+}  // namespace miclip
+
+namespace miclip {
+hipError_t gemm8q_probe_read(unsigned long long* host, int n) {
+  if (n > 1024 * 2 * 9) n = 1024 * 2 * 9;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_probe8q), n * sizeof(unsigned long long), 0, hipMemcpyDeviceToHost);
+}
+}  // namespace miclip

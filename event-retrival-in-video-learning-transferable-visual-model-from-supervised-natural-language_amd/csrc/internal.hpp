@@ -54,6 +54,9 @@ struct GemmArgs {
   // grid (K = 3*32*32, one 32-pixel image-row segment per BK = 32 stage), so
   // no im2col buffer is written or read.  0 = plain row-major A.
   int patch_R = 0;
+  // persistent 8-phase kernels (gemm_8q.hip): workgroups start (blockIdx / 8) % stagger_phases x
+  // stagger_ticks (100 MHz) late, so the CUs' tile epilogues (all 16 stores) do not coincide
+  int stagger_phases = 0, stagger_ticks = 0;
 };
 
 // Requirements: K % 64 == 0, N % 128 == 0, A/W 16-byte aligned rows.
@@ -64,6 +67,13 @@ hipError_t gemm_w4(const GemmArgs& a, int epi, hipStream_t s, int cus);
 // 8-phase interleaved ping-pong, 256x256x64 persistent (gemm_8p.hip); bf16 epilogues, K % 128 == 0
 int gemm_8p_ok(const GemmArgs& a);
 hipError_t gemm_8p(const GemmArgs& a, int epi, hipStream_t s, int cus, int abl = 0);
+// 8-phase, second schedule: descriptor DMAs, template-form waits, quadrant-split epilogue (gemm_8q.hip)
+int gemm_8q_ok(const GemmArgs& a);
+hipError_t gemm_8q(const GemmArgs& a, int epi, hipStream_t s, int cus, int mode = 0);
+hipError_t gemm8q_probe_read(unsigned long long* host, int n);   // ABL 9 stamps (gemm_8q.hip)
+// 256 x 128 tiles, deferred (drained) epilogue, three-slot ring (gemm_8r.hip)
+int gemm_8r_ok(const GemmArgs& a);
+hipError_t gemm_8r(const GemmArgs& a, int epi, hipStream_t s, int cus, int mode = 0);
 // variant 19's per-workgroup timestamps (gemm.hip g_gemm_probe) -> host
 hipError_t gemm_probe_read(unsigned long long* host, int n);
 // MX-fp8: A, W e4m3 bytes (row strides lda/ldw in BYTES), a_scale/w_scale e8m0; K % 128 == 0, N % 256 == 0

@@ -45,6 +45,35 @@ def test_gemm(gpu, M, N, K, epi):
     assert err < tol, f"max err {err} (tol {tol})"
 
 
+@pytest.mark.parametrize("M,N,K,epi", [(20000, 3072, 768, 1), (5000, 2304, 768, 0), (3000, 768, 3072, 0),
+                                       (777, 768, 128, 1), (256, 256, 256, 0), (70001, 768, 768, 0)])
+def test_gemm_8phase_schedules_bit_identical(gpu, M, N, K, epi):
+    """The 8-phase kernels (gemm_8p v98, gemm_8q v110 block epilogue / v113 flat DMAs; gemm_8r v120 256 x 128 deferred epilogue
+    DMAs) run the same MFMA order and epilogue arithmetic, so their outputs
+    must match bit for bit, over multi-tile persistent walks, partial last
+    M-tiles and one-pair K; v98 is also checked against torch fp32."""
+    import torch
+    N_ = _lib()
+    g = torch.Generator(device="cpu").manual_seed(M + N + K)
+    A = (torch.rand(M, K, generator=g) * 2 - 1).bfloat16().to(gpu)
+    W = ((torch.rand(N, K, generator=g) * 2 - 1) * K ** -0.5).bfloat16().to(gpu)
+    bias = torch.randn(N, generator=g).float().to(gpu)
+    outs = {}
+    for v in (98, 110, 113, 120):
+        out = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=gpu)
+        N_.check(N_.lib().mi_op_gemm(A.data_ptr(), W.data_ptr(), bias.data_ptr(), out.data_ptr(), M, N, K,
+                                     epi | (v << 8), _stream()), f"gemm v{v}")
+        outs[v] = out
+    torch.cuda.synchronize()
+    ref = A.float() @ W.float().t() + bias
+    if epi == 1:
+        ref = ref * torch.sigmoid(1.702 * ref)
+    err = (outs[98].float() - ref).abs().max().item()
+    assert err < 2e-2 * max(1.0, ref.abs().max().item()), err
+    for v in (110, 113, 120):
+        assert torch.equal(outs[v], outs[98]), f"v{v} differs from v98"
+
+
 def test_gemm_asymmetric_identity(gpu):
     """A = I with an asymmetric W catches a transposed C write (guide §3)."""
     import torch
