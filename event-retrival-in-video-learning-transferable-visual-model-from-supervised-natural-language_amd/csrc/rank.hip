@@ -369,6 +369,218 @@ __global__ __launch_bounds__(64 * NW) void rank_stream(const void* __restrict__ 
   }
 }
 
+// Register-query streaming stage 1 (f32 corpus, D = 512, k <= 16:
+// rank_reg; rank_stream otherwise).  PMC of rank_stream at 1M x 512, Q = 32
+// (profiles/r02_rank_pmc.json): FETCH = 1.02x the corpus bytes but MFMA busy
+// 44 %, 8.75 VALU per MFMA, and hipcc compiled its register ring into a
+// vmcnt(0) per chunk plus 32 buffer copies per chunk.  Here:
+//  * one wave per SIMD (4 per workgroup, one workgroup per CU), the 32
+//    queries of the block held in registers as MFMA B operands for the whole
+//    kernel (lane l: query l & 31, k = 32j + 16h + i: D / 2 VGPRs), so no LDS
+//    query reads at all;
+//  * the corpus streams through a per-wave LDS ring (NB slots of one 32-row x
+//    32-k chunk, 4 KB) by buffer-descriptor DMA, PF chunks ahead, with counted
+//    vmcnt waits and no barriers (each wave fills and reads only its own
+//    slots).  The descriptor base is the 32-row tile's first row and its range
+//    the tile's valid rows, so rows past the workgroup's range read zeros.
+//    Image row r at r * 128 B, 16-byte slot s at s ^ ((r >> 1) & 7) (the
+//    GEMM's conflict-free image; the DMA permutes its source pieces);
+//  * the same arithmetic as rank_stream (k order within and across the
+//    v_mfma_f32_32x32x2_f32 chain, the fmaf sum of squares, inv_norm, keys,
+//    bitonic list update, tau threshold, workgroup list merge), so the
+//    candidates are bit-identical.
+template <int D, int NB = 8, int PF = 6>
+__global__ __launch_bounds__(256) void rank_reg(const float* __restrict__ corpus, int64_t N,
+                                                const float* __restrict__ queries, int64_t Q, int k,
+                                                int64_t rows_per_wg, int norm_mode, int nan_first, int64_t index_base,
+                                                float* __restrict__ ws_s, int64_t* __restrict__ ws_i, int64_t C) {
+  constexpr int NW = 4, NT = 64 * NW, KC = 16, NCH = D / 32;
+  // NB ring slots per wave, PF chunks in flight (NB >= PF + 2: a refilled slot was read two chunks ago)
+  constexpr int SLOT = 32 * 128;           // 4 KB
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* ring = smem;                       // [NW][NB][SLOT]
+  float* nrm_all = (float*)(smem + NW * NB * SLOT);
+  uint32_t* tau = (uint32_t*)(nrm_all + NW * 32);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, h = lane >> 5;
+  const int64_t q0 = (int64_t)blockIdx.y * RQ;
+  const bool qvalid = q0 + r < Q;
+
+  // queries -> registers (zeros past Q)
+  float qv[NCH][16];
+  {
+    const float* qp = queries + (qvalid ? (q0 + r) : 0) * D + 16 * h;
+#pragma unroll
+    for (int j = 0; j < NCH; ++j)
+#pragma unroll
+      for (int i4 = 0; i4 < 4; ++i4) {
+        const float4 t = *(const float4*)(qp + 32 * j + 4 * i4);
+        qv[j][4 * i4] = qvalid ? t.x : 0.f;
+        qv[j][4 * i4 + 1] = qvalid ? t.y : 0.f;
+        qv[j][4 * i4 + 2] = qvalid ? t.z : 0.f;
+        qv[j][4 * i4 + 3] = qvalid ? t.w : 0.f;
+      }
+  }
+  if (tid < RQ) tau[tid] = 0u;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  const int64_t r_begin = (int64_t)blockIdx.x * rows_per_wg;
+  const int64_t r_end = min(N, r_begin + rows_per_wg);
+  const int nrows = (int)(r_end - r_begin);
+  const int ntw = (nrows + 31) / 32;
+  const int my_tiles = ntw > wave ? (ntw - 1 - wave) / NW + 1 : 0;
+  float* nrm = nrm_all + wave * 32;
+  char* wring = ring + wave * NB * SLOT;
+
+  // DMA: 4 x 1 KB per chunk; instruction m covers image rows 8m .. 8m + 7,
+  // lane l row 8m + (l >> 3), LDS slot (l & 7), source piece (l & 7) ^ ((row >> 1) & 7)
+  uint32_t voff[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const int row = 8 * m + (lane >> 3);
+    const int c = (lane & 7) ^ ((row >> 1) & 7);
+    voff[m] = (uint32_t)(row * D * 4 + c * 16);
+  }
+  int lt = 0, lj = 0, lslot = 0;           // load cursor: tile ordinal, chunk, ring slot
+  __amdgpu_buffer_rsrc_t rs;
+  auto make_rs = [&]() {
+    const int trow = (wave + NW * lt) * 32;   // relative to r_begin
+    const int rows = max(0, min(32, nrows - trow));
+    // wave-uniform by construction; readfirstlane makes it provable (no waterfall loop per load, guide T20)
+    const uint64_t base = (uint64_t)(uintptr_t)(corpus + (r_begin + (rows ? trow : 0)) * (int64_t)D);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)base);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
+    const int nrec = __builtin_amdgcn_readfirstlane(rows * D * 4);
+    rs = __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)(((uint64_t)hi << 32) | lo), (short)0, nrec, 0x00020000);
+  };
+  make_rs();
+  auto issue = [&]() {   // chunk (lt, lj) -> slot lslot; past this wave's tiles: range 0, zeros
+    char* dst = wring + lslot * SLOT;
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (LDS_AS void*)(dst + m * 1024), 16, voff[m], lj * 128, 0, 0);
+    lslot = lslot == NB - 1 ? 0 : lslot + 1;
+    if (++lj == NCH) {
+      lj = 0;
+      ++lt;
+      make_rs();
+    }
+  };
+  // fragment read: row r, k 16h .. 16h + 15 = slots 4h .. 4h + 3 (permuted)
+  const int rbase = r * 128;
+  const int sw = (r >> 1) & 7;
+  uint64_t L[KC];
+#pragma unroll
+  for (int p = 0; p < KC; ++p) L[p] = 0ull;
+
+  if (my_tiles > 0) {
+#pragma unroll
+    for (int p = 0; p < PF; ++p) issue();
+    int cslot = 0;
+    for (int ct = 0; ct < my_tiles; ++ct) {
+      f32x16 acc = f32x16{};
+      float ss = 0.f;
+#pragma unroll
+      for (int j = 0; j < NCH; ++j) {
+        issue();   // chunk PF ahead (the ring slot it fills was read NB - PF chunks ago)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * PF) : "memory");   // this chunk landed
+        const char* src = wring + cslot * SLOT + rbase;
+        float4 v[4];
+#pragma unroll
+        for (int i4 = 0; i4 < 4; ++i4) {
+          const uint32_t a = (uint32_t)(uintptr_t)(const LDS_AS char*)(src + (((4 * h + i4) ^ sw) << 4));
+          asm volatile("ds_read_b128 %0, %1" : "=v"(v[i4]) : "v"(a) : "memory");
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        const float cur[16] = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w,
+                               v[2].x, v[2].y, v[2].z, v[2].w, v[3].x, v[3].y, v[3].z, v[3].w};
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[i], qv[j][i], acc, 0, 0, 0);
+          ss = fmaf(cur[i], cur[i], ss);
+        }
+        cslot = cslot == NB - 1 ? 0 : cslot + 1;
+      }
+      // ---- tile finished: scores, threshold test, list update (rank_stream's finalize)
+      ss += __shfl_xor(ss, 32, 64);
+      if (h == 0) nrm[r] = inv_norm(ss, norm_mode);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+      const int tr0 = (wave + NW * ct) * 32;
+      const uint32_t tq_thr = tau[r];
+      const uint32_t own = (uint32_t)(L[KC - 1] >> 32);
+      const uint32_t thr = own > tq_thr ? own : tq_thr;
+      uint64_t c[16];
+      bool any = false;
+#pragma unroll
+      for (int rg = 0; rg < 16; ++rg) {
+        const int rr = (rg & 3) + 8 * (rg >> 2) + 4 * h;
+        const int lr = tr0 + rr;
+        const float sc = norm_mode == 2 ? acc[rg] : acc[rg] * nrm[rr];
+        const uint32_t key = score_key(sc, nan_first);
+        const bool ok = qvalid && lr < nrows && key >= thr;
+        c[rg] = ok ? (((uint64_t)key << 32) | (uint32_t)~(uint32_t)lr) : 0ull;
+        any |= ok;
+      }
+      if (__any(any)) {
+        bitonic_sort16_desc(c);
+        merge16_desc(L, c);
+        uint32_t kth = (uint32_t)(L[0] >> 32);
+#pragma unroll
+        for (int p = 1; p < KC; ++p) kth = (p == k - 1) ? (uint32_t)(L[p] >> 32) : kth;
+        const uint32_t other = (uint32_t)__shfl_xor((int)kth, 32, 64);
+        kth = kth > other ? kth : other;
+        if (h == 0 && qvalid && kth > tq_thr) atomicMax(&tau[r], kth);
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // trailing (zero-range) DMAs land before the ring is reused
+  __syncthreads();   // ring free -> lists
+  uint32_t* Lk = (uint32_t*)smem;
+  int32_t* Li = (int32_t*)(smem + NT * KC * 4);
+#pragma unroll
+  for (int p = 0; p < KC; ++p) {
+    const bool real = L[p] != 0ull;
+    Lk[tid * KC + p] = real ? (uint32_t)(L[p] >> 32) : 0u;
+    Li[tid * KC + p] = real ? (int32_t)~(uint32_t)L[p] : INT_MAX;
+  }
+  __syncthreads();
+  if (tid < RQ && q0 + tid < Q) {
+    int pos[2 * NW];
+#pragma unroll
+    for (int l = 0; l < 2 * NW; ++l) pos[l] = 0;
+    float* os = ws_s + (q0 + tid) * C + (int64_t)blockIdx.x * k;
+    int64_t* oi = ws_i + (q0 + tid) * C + (int64_t)blockIdx.x * k;
+    for (int o = 0; o < k; ++o) {
+      uint32_t bk = 0u;
+      int32_t bi = INT_MAX;
+      int bl = 0;
+#pragma unroll
+      for (int l = 0; l < 2 * NW; ++l) {
+        const int src = (l >> 1) * 64 + (l & 1) * 32 + tid;
+        if (pos[l] < KC) {
+          const uint32_t kk = Lk[src * KC + pos[l]];
+          const int32_t ii = Li[src * KC + pos[l]];
+          if (better(kk, ii, bk, bi)) { bk = kk; bi = ii; bl = l; }
+        }
+      }
+#pragma unroll
+      for (int l = 0; l < 2 * NW; ++l) pos[l] += (l == bl) ? 1 : 0;
+      if (bi == INT_MAX) {
+        os[o] = -INFINITY;
+        oi[o] = -1;
+      } else {
+        os[o] = decode_key(bk, nan_first);
+        oi[o] = index_base + r_begin + bi;
+      }
+    }
+  }
+}
+
 // stage-1 LDS: queries [32][D+4] f32, per-wave norms [4][32]; the lists
 // [256 lanes][KC] (key u32, idx i32) reuse the query area after a barrier.
 template <int KC, int DT>
@@ -864,6 +1076,28 @@ hipError_t rank_merge(const float* cs, const int64_t* ci, int64_t Q, int64_t C, 
   return hipGetLastError();
 }
 
+template <int D>
+static hipError_t launch_reg(int64_t N, const float* corpus, const float* q, int64_t Q, int k, int nm, int nf,
+                             int64_t base, float* ws_s, int64_t* ws_i, int64_t& C, hipStream_t s) {
+  // one workgroup per CU (LDS ring 128 KB), rows per workgroup a multiple of 128
+  // (one 32-row tile per wave); never more workgroups than rank_chunks (workspace)
+  int64_t nwg = rank_chunks(N);
+  if (nwg > 256) nwg = 256;
+  if (nwg > (N + 127) / 128) nwg = (N + 127) / 128;
+  const int64_t rpw = ((N + nwg - 1) / nwg + 127) / 128 * 128;
+  nwg = (N + rpw - 1) / rpw;
+  C = nwg * k;
+  const size_t lds = (size_t)4 * 8 * 4096 + 4 * 32 * 4 + RQ * 4;
+  // (a 9-slot ring with 7 chunks in flight, 147 KB of LDS, failed every rank test, N = 1
+  // included, for a reason not yet found; the 8-slot ring is bit-identical to rank_stream)
+  auto fn = rank_reg<D, 8, 6>;
+  hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  const dim3 grid((unsigned)nwg, (unsigned)((Q + RQ - 1) / RQ));
+  hipLaunchKernelGGL(fn, grid, dim3(256), lds, s, corpus, N, q, Q, k, rpw, nm, nf, base, ws_s, ws_i, C);
+  return hipGetLastError();
+}
+
 template <int DT, int NW>
 static hipError_t launch_stream(dim3 grid, size_t lds, hipStream_t s, const void* corpus, int64_t N, int64_t D,
                                 const float* q, int64_t Q, int k, int64_t rpw, int nm, int nf, int64_t base,
@@ -898,6 +1132,14 @@ hipError_t rank_topk(const void* corpus, int64_t N, int64_t D, int dt, const flo
   const size_t lds = qa > la ? qa : la;
   hipError_t e;
   const char* legacy = getenv("MICLIP_RANK_STAGE1");   // A/B: the previous one-tile-at-a-time kernel
+  const char* noreg = getenv("MICLIP_RANK_REG");        // A/B: 0 = rank_stream for f32 D = 512 too
+  if (KC == 16 && dt == 0 && D == 512 && !(legacy && legacy[0] == '1') && !(noreg && noreg[0] == '0')) {
+    int64_t Creg = 0;
+    // (D = 768 would hold 384 query VGPRs: hipcc spills ~230, so it keeps rank_stream)
+    e = launch_reg<512>(N, (const float*)corpus, q, Q, k, norm_mode, nan_first, base, ws_s, ws_i, Creg, s);
+    if (e != hipSuccess) return e;
+    return rank_merge(ws_s, ws_i, Q, Creg, k, nan_first, out_s, out_i, s);
+  }
   if (KC == 64 || (legacy && legacy[0] == '1')) {
 #define MI_S1(KCV, DTV) \
   launch_stage1<KCV, DTV>(grid, stage1_lds(D, KCV), s, corpus, N, D, q, Q, k, rpw, norm_mode, nan_first, base, ws_s, \

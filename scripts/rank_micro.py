@@ -1,6 +1,6 @@
 """A/B of the fused rank kernel variants in ONE process, interleaved rounds
-(MICLIP_RANK_STAGE1=1: the one-tile-at-a-time kernel; MICLIP_RANK_NW=8/12:
-the streaming kernel's waves per workgroup), HIP events on the launch stream.
+(default: rank_reg for f32 D = 512, else rank_stream; MICLIP_RANK_REG=0: rank_stream;
+MICLIP_RANK_STAGE1=1: the one-tile-at-a-time kernel), HIP events on the launch stream.
 
   python scripts/rank_micro.py [rounds]
 """
@@ -14,13 +14,14 @@ sys.path.insert(0, os.path.join(ROOT, "event-retrival-in-video-learning-transfer
 import torch  # noqa: E402
 from miclip import retrieval  # noqa: E402
 
-VARIANTS = {"stage1": {"MICLIP_RANK_STAGE1": "1"}, "nw8": {"MICLIP_RANK_NW": "8"}, "nw12": {"MICLIP_RANK_NW": "12"}}
+VARIANTS = {"default": {}, "stream12": {"MICLIP_RANK_REG": "0", "MICLIP_RANK_NW": "12"},
+            "stage1": {"MICLIP_RANK_STAGE1": "1"}}
 SHAPES = [(125_000, 512, 32, torch.float32), (1_000_000, 512, 32, torch.float32),
           (1_000_000, 512, 32, torch.bfloat16), (1_000_000, 768, 32, torch.float32), (10_000, 512, 32, torch.float32)]
 
 
 def setenv(v):
-    for k in ("MICLIP_RANK_STAGE1", "MICLIP_RANK_NW"):
+    for k in ("MICLIP_RANK_STAGE1", "MICLIP_RANK_NW", "MICLIP_RANK_REG"):
         os.environ.pop(k, None)
     os.environ.update(VARIANTS[v])
 
