@@ -161,3 +161,76 @@ def test_error_semantics(service):
     assert svc.extract_query_confidence("nope.png", "x", "missing_video") == 0.0  # :280-282
     svc.extract_and_save_embeddings_from_folder(str(frame_dir), video_name="vid")
     assert svc.extract_query_confidence("not_a_frame.png", "x", "vid") == 0.0
+
+
+def _ref_search_by_image(svc, image_path, thr, top_k, data, fmt, video_name):
+    """search_service.py:611-706 restated literally (local-path branch): encode
+    the query, top_k * 3 candidates, then re-encode EVERY candidate frame
+    (extract_image_embedding) for its cosine, threshold, sort, [:top_k]."""
+    import torch
+    from pathlib import Path
+    from PIL import Image
+    image = svc.preprocess(Image.open(image_path).convert("RGB")).unsqueeze(0)
+    f = svc.original_model.encode_image(image, out_dtype=torch.float32).float()
+    feats = (f / f.norm(dim=-1, keepdim=True)).cpu().numpy()
+    results = []
+    for frame_name in svc.search_top_frames_by_image(feats, top_k * 3, video_name):
+        try:
+            frame_idx = int(Path(frame_name).stem)
+            frame_data = next((item for item in data if item.get("frameidx") == frame_idx), None)
+            if frame_data:
+                emb = svc.extract_image_embedding(frame_name)
+                if emb is not None:
+                    sim = np.dot(emb, feats.T)[0][0]
+                    if sim >= thr:
+                        fd = frame_data.copy()
+                        fd["clip_similarity"] = float(sim)
+                        ev = fmt(fd)
+                        ev["clip_similarity"] = float(sim)
+                        ev["confidence"] = float(sim)
+                        results.append(ev)
+        except Exception as e:
+            print(f"Error processing frame {frame_name}: {e}")
+    results.sort(key=lambda x: x.get("clip_similarity", 0), reverse=True)
+    return results[:top_k]
+
+
+class _SearchData:
+    def __init__(self, data):
+        self.data = data
+
+    def load_json_data(self, video_name):
+        return self.data
+
+    def format_event_for_frontend(self, fd):
+        return {"frame": fd["frame"], "frameidx": fd["frameidx"]}
+
+
+@pytest.mark.parametrize("reencode", [False, True])
+def test_search_by_image_matches_reference_flow(service, monkeypatch, reencode):
+    """miclip.search.search_by_image against the literal restatement: same
+    events in the same order, similarities within 1e-5 (the stored rows are the
+    encoder's own output; the reference recomputes them by re-encoding); the
+    query frame itself ranks first at cosine ~1; an unreadable candidate frame
+    (zero row / failed re-encode) never appears; the data:image branch returns
+    [] as the reference's does (it hands undecoded base64 to PIL)."""
+    from miclip import search
+    svc, frame_dir, names, paths = service
+    svc.extract_and_save_embeddings_from_folder(str(frame_dir), video_name="vid")
+    monkeypatch.chdir(frame_dir)           # frame names are paths relative to the working directory, as there
+    data = [{"frame": n, "frameidx": int(n.split(".")[0])} for n in names if n != "broken.png"]
+    data.insert(3, {"frame": "dup", "frameidx": data[5]["frameidx"]})   # duplicate frameidx: the first wins
+    ds = _SearchData(data)
+    for qi, thr, k in ((4, 0.0, 5), (9, 0.5, 8), (17, -1.0, 10)):
+        q = str(frame_dir / names[qi])
+        ref = _ref_search_by_image(svc, q, thr, k, data, ds.format_event_for_frontend, "vid")
+        got = search.search_by_image(svc, ds, q, thr, k, "vid", reencode=reencode)
+        assert [e["frame"] for e in got] == [e["frame"] for e in ref]
+        for a, b in zip(got, ref):
+            assert abs(a["clip_similarity"] - b["clip_similarity"]) < 1e-5 and a["confidence"] == a["clip_similarity"]
+        assert got and got[0]["frame"] in (names[qi], "dup") and got[0]["clip_similarity"] > 0.999
+        assert all(e["frame"] != "broken.png" for e in got)
+    import base64
+    png = (frame_dir / names[2]).read_bytes()
+    assert search.search_by_image(svc, ds, "data:image/png;base64," + base64.b64encode(png).decode(), 0.0, 5,
+                                  "vid") == []
