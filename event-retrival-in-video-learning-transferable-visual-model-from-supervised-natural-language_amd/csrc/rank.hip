@@ -389,13 +389,15 @@ __global__ __launch_bounds__(64 * NW) void rank_stream(const void* __restrict__ 
 //    v_mfma_f32_32x32x2_f32 chain, the fmaf sum of squares, inv_norm, keys,
 //    bitonic list update, tau threshold, workgroup list merge), so the
 //    candidates are bit-identical.
-template <int D, int NB = 8, int PF = 6>
+// NOMFMA: timing probe (the stream and the fragment reads without the MFMAs; wrong scores)
+template <int D, int NB = 8, int PF = 6, bool NOMFMA = false>
 __global__ __launch_bounds__(256) void rank_reg(const float* __restrict__ corpus, int64_t N,
                                                 const float* __restrict__ queries, int64_t Q, int k,
                                                 int64_t rows_per_wg, int norm_mode, int nan_first, int64_t index_base,
                                                 float* __restrict__ ws_s, int64_t* __restrict__ ws_i, int64_t C) {
   constexpr int NW = 4, NT = 64 * NW, KC = 16, NCH = D / 32;
-  // NB ring slots per wave, PF chunks in flight (NB >= PF + 2: a refilled slot was read two chunks ago)
+  // NB ring slots per wave, PF chunks in flight (NB >= PF + 1: a refilled slot was read, and its
+  // reads waited for, in an earlier chunk iteration)
   constexpr int SLOT = 32 * 128;           // 4 KB
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* ring = smem;                       // [NW][NB][SLOT]
@@ -499,7 +501,8 @@ __global__ __launch_bounds__(256) void rank_reg(const float* __restrict__ corpus
                                v[2].x, v[2].y, v[2].z, v[2].w, v[3].x, v[3].y, v[3].z, v[3].w};
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[i], qv[j][i], acc, 0, 0, 0);
+          if (NOMFMA) asm volatile("" ::"v"(cur[i]), "v"(qv[j][i]));
+          else acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[i], qv[j][i], acc, 0, 0, 0);
           ss = fmaf(cur[i], cur[i], ss);
         }
         cslot = cslot == NB - 1 ? 0 : cslot + 1;
@@ -1090,7 +1093,9 @@ static hipError_t launch_reg(int64_t N, const float* corpus, const float* q, int
   const size_t lds = (size_t)4 * 8 * 4096 + 4 * 32 * 4 + RQ * 4;
   // (a 9-slot ring with 7 chunks in flight, 147 KB of LDS, failed every rank test, N = 1
   // included, for a reason not yet found; the 8-slot ring is bit-identical to rank_stream)
-  auto fn = rank_reg<D, 8, 6>;
+  const char* probe = getenv("MICLIP_RANK_PROBE");
+  // (7 chunks in flight measured the same: the stream alone, NOMFMA, reads 5.3 TB/s either way)
+  auto fn = (probe && probe[0] == '1') ? rank_reg<D, 8, 6, true> : rank_reg<D, 8, 6>;
   hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
   const dim3 grid((unsigned)nwg, (unsigned)((Q + RQ - 1) / RQ));
