@@ -173,6 +173,57 @@ def preprocess_timing(dev, n_px, B=256, H=720, W=1280, reps=10):
             "gbs": round(B * H * W * 3 / us / 1e3, 1), "shape": [B, H, W, 3]}
 
 
+def jpeg_ingest_timing(dev, n_px, B=512, threads=16):
+    """Frame ingest from JPEG bytes in host memory to preprocessed [B,3,n,n]
+    bf16 tensors: the reference's 16 real 1280x720
+    frames (tests/golden/ref_frames) repeated to B.  GPU path: header parse +
+    table build on the host, mi_jpeg_decode + mi_preprocess_frames on the
+    device (bit-identical to Pillow, tests/test_gpu_jpeg.py); host path: Pillow
+    decode on `threads` host threads, as the reference decodes, + the same GPU
+    preprocessing.  Wall-clock, synchronised; not part of the timed step."""
+    import glob
+    import io
+    import time
+    from concurrent.futures import ThreadPoolExecutor
+
+    import numpy as np
+    import torch
+    from PIL import Image
+    from miclip import jpeg
+    from miclip.preprocess import preprocess_frames
+    files = sorted(glob.glob(os.path.join(ROOT, "tests", "golden", "ref_frames", "*.jpg")))
+    if not files:
+        return None
+    raw = [open(f, "rb").read() for f in files]
+    bufs = [raw[i % len(raw)] for i in range(B)]
+
+    def gpu():
+        fr = jpeg.decode_batch(bufs, dev)
+        return preprocess_frames(torch.stack(fr), n_px, out_dtype=torch.bfloat16)
+
+    def pil_one(b):
+        with Image.open(io.BytesIO(b)) as im:
+            return np.asarray(im.convert("RGB"), dtype=np.uint8)
+
+    def host():
+        with ThreadPoolExecutor(threads) as ex:
+            arrs = list(ex.map(pil_one, bufs))
+        return preprocess_frames(torch.from_numpy(np.stack(arrs)).to(dev), n_px, out_dtype=torch.bfloat16)
+
+    res = {"frames": B, "source": "tests/golden/ref_frames (16 reference frames, 1280x720 4:2:0)",
+           "host_threads": threads}
+    for name, fn in (("gpu_decode", gpu), ("pil_decode", host)):
+        fn()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(2):
+            out = fn()
+        torch.cuda.synchronize(dev)
+        res[name + "_frames_per_s"] = round(2 * B / (time.perf_counter() - t0), 1)
+        del out
+    return res
+
+
 def rank_timing(corpus, txt, k, reps=50):
     import torch
     from miclip import retrieval
@@ -430,6 +481,9 @@ def main():
         txt = model.encode_text(tokens, normalize=True, out_dtype=torch.float32)
         kern["rank_topk"] = rank_timing(emb, txt, k)
         kern["preprocess_720p"] = preprocess_timing(dev, cfg.image_resolution)
+        ingest = jpeg_ingest_timing(dev, cfg.image_resolution)
+        if ingest:
+            kern["jpeg_ingest_720p"] = ingest
         rank_roof = None if args.no_rank_roofline else rank_roofline(dev)
         F_frame, F_text = cfg.image_flops(), cfg.text_flops()
         step_flops = Nf * world * F_frame + Q * world * F_text + 2.0 * Nf * world * Q * cfg.embed_dim

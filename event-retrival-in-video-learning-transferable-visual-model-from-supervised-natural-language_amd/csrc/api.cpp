@@ -772,4 +772,37 @@ int mi_preprocess_frames(const uint8_t* frames, int64_t B, int32_t H, int32_t W,
   return MI_OK;
 }
 
+size_t mi_jpeg_workspace_bytes(const int32_t* geom, int32_t B) {
+  if (!geom || B < 0) return 0;
+  return jpeg_workspace_bytes(geom, B);
+}
+
+int mi_jpeg_decode(const uint8_t* data, const int64_t* seg_off, const int64_t* seg_end, const void* huff,
+                   const uint16_t* qtab, const int32_t* geom, int32_t B, uint8_t* out_rgb, void* workspace,
+                   size_t workspace_bytes, void* stream) {
+  if (!geom || B < 0) return fail(MI_ERR_ARG, "mi_jpeg_decode: bad arguments");
+  if (B == 0) return MI_OK;
+  if (!data || !seg_off || !seg_end || !huff || !qtab || !out_rgb) return fail(MI_ERR_ARG, "mi_jpeg_decode: null pointer");
+  const int W = geom[0], H = geom[1], nc = geom[2], ri = geom[3], nseg = geom[4];
+  if (W < 1 || H < 1 || W > 65535 || H > 65535 || (nc != 1 && nc != 3) || ri < 0 || nseg < 1)
+    return fail(MI_ERR_ARG, "mi_jpeg_decode: bad geometry");
+  if (nc == 3) {
+    const int h0 = geom[5], v0 = geom[6];
+    const bool luma_ok = (h0 == 1 && v0 == 1) || (h0 == 2 && v0 == 1) || (h0 == 2 && v0 == 2);
+    for (int c = 1; c < 3; ++c)
+      if (geom[5 + 2 * c] != 1 || geom[6 + 2 * c] != 1 || !luma_ok)
+        return fail(MI_ERR_UNSUPPORTED, "mi_jpeg_decode: sampling must be luma 1x1/2x1/2x2 with chroma 1x1");
+  }
+  for (int c = 0; c < nc; ++c)
+    if (geom[11 + c] < 0 || geom[11 + c] > 3 || geom[14 + c] < 0 || geom[14 + c] > 1 || geom[17 + c] < 0 ||
+        geom[17 + c] > 1)
+      return fail(MI_ERR_ARG, "mi_jpeg_decode: bad table selector");
+  const size_t need = jpeg_workspace_bytes(geom, B);
+  if (!workspace || workspace_bytes < need)
+    return fail(MI_ERR_ARG, "mi_jpeg_decode: workspace too small (%zu < %zu)", workspace_bytes, need);
+  HIP_TRY(jpeg_decode(data, seg_off, seg_end, huff, qtab, geom, B, out_rgb, workspace, workspace_bytes,
+                      (hipStream_t)stream));
+  return MI_OK;
+}
+
 }  // extern "C"

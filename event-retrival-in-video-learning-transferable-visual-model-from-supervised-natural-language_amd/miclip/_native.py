@@ -29,6 +29,7 @@ EXPORTS = (
     "mi_rank_topk", "mi_rank_merge", "mi_score_matrix", "mi_rank_of_targets",
     "mi_op_gemm", "mi_op_layernorm", "mi_op_attention", "mi_op_residual_ln",
     "mi_resample_coeffs", "mi_preprocess_workspace_bytes", "mi_preprocess_frames",
+    "mi_jpeg_workspace_bytes", "mi_jpeg_decode",
     "mi_op_quantize_mx", "mi_op_gemm_mx",
 )
 
@@ -93,6 +94,8 @@ def lib():
         "mi_resample_coeffs": (ctypes.c_int, [I32, ctypes.c_double, ctypes.c_double, I32, ctypes.c_int, P, I64, P]),
         "mi_preprocess_workspace_bytes": (SZ, [I64, I32, I32, I32, ctypes.c_int]),
         "mi_preprocess_frames": (ctypes.c_int, [P, I64, I32, I32, I32, ctypes.c_int, P, ctypes.c_int, P, SZ, P]),
+        "mi_jpeg_workspace_bytes": (SZ, [P, I32]),
+        "mi_jpeg_decode": (ctypes.c_int, [P, P, P, P, P, P, I32, P, P, SZ, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

@@ -1,0 +1,307 @@
+"""Baseline JPEG decode on the GPU (``mi_jpeg_decode``, ``csrc/jpeg.hip``),
+bit-identical to Pillow's ``Image.open(p).convert("RGB")`` — the decode step
+of the reference's frame ingest (``Backend/services/embedding_service.py:472-480``,
+``Backend/embedding.py:46``).
+
+The host reads each file's markers (DQT, SOF0/SOF1, DHT, DRI, SOS), builds the
+Huffman decode tables in libjpeg's derived form (9-bit look-ahead + maxcode /
+value offsets per code length), de-zigzags the quantisation tables, locates
+restart markers, and hands one batch per geometry to the device: the entropy
+decode runs one lane per frame (or per restart interval), the IDCT one thread
+per block, the upsampling + colour conversion one thread per pixel.
+
+Files the device path does not cover (progressive or arithmetic coding,
+12-bit samples, CMYK / Adobe-transform or 4-component images, sampling other
+than chroma 1x1 with luma 1x1 / 2x1 / 2x2, more than two Huffman tables of a
+class, EXIF orientation is NOT applied by either path) are decoded by Pillow
+on the host, so every frame gets the reference's pixels.
+"""
+from __future__ import annotations
+
+import struct
+
+import numpy as np
+
+from . import _native as N
+
+ZIGZAG = np.array([0, 1, 8, 16, 9, 2, 3, 10, 17, 24, 32, 25, 18, 11, 4, 5, 12, 19, 26, 33, 40, 48, 41, 34, 27, 20,
+                   13, 6, 7, 14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51, 58, 59,
+                   52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63], dtype=np.int64)
+HUFF_BYTES = 1424
+_HUFF_DT = np.dtype([("look", "<u2", 512), ("maxcode", "<i4", 18), ("valoff", "<i4", 18), ("vals", "u1", 256)])
+assert _HUFF_DT.itemsize == HUFF_BYTES
+
+
+def build_huff(bits, vals):
+    """libjpeg jpeg_make_d_derived_tbl: canonical codes from the 16 length
+    counts; 9-bit look-ahead entries (length << 8) | symbol; maxcode / value
+    offsets for the longer codes."""
+    t = np.zeros((), dtype=_HUFF_DT)
+    t["maxcode"][:] = -1
+    t["maxcode"][17] = 0x7FFFFFFF
+    vals = list(vals)
+    t["vals"][:len(vals)] = vals
+    code, p = 0, 0
+    for ln in range(1, 17):
+        n = bits[ln - 1]
+        if n:
+            t["valoff"][ln] = p - code
+            for _ in range(n):
+                if ln <= 9:
+                    lo = code << (9 - ln)
+                    t["look"][lo:lo + (1 << (9 - ln))] = (ln << 8) | vals[p]
+                code += 1
+                p += 1
+            t["maxcode"][ln] = code - 1
+        code <<= 1
+    return t
+
+
+class JpegHeader:
+    __slots__ = ("width", "height", "ncomp", "samp", "qsel", "dcsel", "acsel", "ri", "qt", "huff", "scan_start",
+                 "supported", "why")
+
+
+def parse(buf: bytes) -> JpegHeader:
+    """Marker walk up to the first SOS; sets ``supported`` False (with ``why``)
+    for anything the device decoder does not restate."""
+    h = JpegHeader()
+    h.supported, h.why = False, ""
+    h.qt, h.huff, h.ri = {}, {}, 0
+    h.width = h.height = h.ncomp = 0
+    comps = []
+    if len(buf) < 4 or buf[0] != 0xFF or buf[1] != 0xD8:
+        h.why = "not a JPEG"
+        return h
+    i = 2
+    adobe_transform = None
+    while i + 4 <= len(buf):
+        if buf[i] != 0xFF:
+            h.why = "bad marker"
+            return h
+        m = buf[i + 1]
+        if m == 0xFF:          # fill byte
+            i += 1
+            continue
+        if m in (0xD8, 0x01) or 0xD0 <= m <= 0xD7:
+            i += 2
+            continue
+        ln = struct.unpack(">H", buf[i + 2:i + 4])[0]
+        seg = buf[i + 4:i + 2 + ln]
+        if m == 0xDB:                                     # DQT
+            j = 0
+            while j < len(seg):
+                pq, tq = seg[j] >> 4, seg[j] & 15
+                if pq:
+                    q = np.frombuffer(seg[j + 1:j + 129], dtype=">u2").astype(np.uint16)
+                    j += 129
+                else:
+                    q = np.frombuffer(seg[j + 1:j + 65], dtype=np.uint8).astype(np.uint16)
+                    j += 65
+                nat = np.zeros(64, np.uint16)
+                nat[ZIGZAG] = q
+                h.qt[tq] = nat
+        elif m in (0xC0, 0xC1):                           # baseline / extended sequential, Huffman
+            if seg[0] != 8:
+                h.why = "sample precision != 8"
+                return h
+            h.height, h.width = struct.unpack(">HH", seg[1:5])
+            h.ncomp = seg[5]
+            for c in range(h.ncomp):
+                cid, hv, tq = seg[6 + 3 * c], seg[7 + 3 * c], seg[8 + 3 * c]
+                comps.append((cid, hv >> 4, hv & 15, tq))
+        elif 0xC2 <= m <= 0xCF and m not in (0xC4, 0xC8, 0xCC):
+            h.why = f"SOF{m - 0xC0} (progressive / lossless / arithmetic)"
+            return h
+        elif m == 0xC4:                                   # DHT
+            j = 0
+            while j < len(seg):
+                tc, th = seg[j] >> 4, seg[j] & 15
+                bits = list(seg[j + 1:j + 17])
+                n = sum(bits)
+                h.huff[(tc, th)] = (bits, bytes(seg[j + 17:j + 17 + n]))
+                j += 17 + n
+        elif m == 0xDD:                                   # DRI
+            h.ri = struct.unpack(">H", seg[:2])[0]
+        elif m == 0xEE and seg[:5] == b"Adobe" and len(seg) >= 12:
+            adobe_transform = seg[11]
+        elif m == 0xDA:                                   # SOS
+            ns = seg[0]
+            scomp = [(seg[1 + 2 * k], seg[2 + 2 * k] >> 4, seg[2 + 2 * k] & 15) for k in range(ns)]
+            ss, se, ahal = seg[1 + 2 * ns], seg[2 + 2 * ns], seg[3 + 2 * ns]
+            h.scan_start = i + 2 + ln
+            if not comps:
+                h.why = "SOS before SOF"
+                return h
+            if ns != h.ncomp or ss != 0 or se != 63 or ahal != 0:
+                h.why = "not a single interleaved sequential scan"
+                return h
+            byid = {cid: (hs, vs, tq) for cid, hs, vs, tq in comps}
+            try:
+                h.samp = [(byid[cid][0], byid[cid][1]) for cid, _, _ in scomp]
+                h.qsel = [byid[cid][2] for cid, _, _ in scomp]
+            except KeyError:
+                h.why = "scan names an unknown component"
+                return h
+            h.dcsel = [td for _, td, _ in scomp]
+            h.acsel = [ta for _, _, ta in scomp]
+            if h.ncomp == 3:
+                if adobe_transform == 0:
+                    h.why = "Adobe RGB (no YCbCr transform)"
+                    return h
+                if h.samp[1] != (1, 1) or h.samp[2] != (1, 1) or h.samp[0] not in ((1, 1), (2, 1), (2, 2)):
+                    h.why = f"sampling {h.samp}"
+                    return h
+            elif h.ncomp != 1:
+                h.why = f"{h.ncomp} components"
+                return h
+            if any(t > 1 for t in h.dcsel + h.acsel):
+                h.why = "Huffman table id > 1"
+                return h
+            if any(q not in h.qt for q in h.qsel) or any((0, t) not in h.huff for t in h.dcsel) or \
+                    any((1, t) not in h.huff for t in h.acsel):
+                h.why = "missing table"
+                return h
+            if any(q > 3 for q in h.qsel) or h.width < 1 or h.height < 1:
+                h.why = "bad frame header"
+                return h
+            if buf.rfind(b"\xff\xd9") <= h.scan_start:   # truncated: Pillow raises; let it
+                h.why = "no EOI after the scan"
+                return h
+            h.supported = True
+            return h
+        elif m == 0xD9:
+            break
+        i += 2 + ln
+    h.why = h.why or "no scan"
+    return h
+
+
+def _geom_key(h):
+    return (h.width, h.height, h.ncomp, tuple(h.samp), h.ri)
+
+
+def _segments(buf, h):
+    """Entropy-coded byte ranges of the restart segments (one without DRI)."""
+    start = h.scan_start
+    if not h.ri:
+        return [(start, len(buf))]
+    segs, j, n = [], start, len(buf)
+    s0 = start
+    while j + 1 < n:
+        if buf[j] == 0xFF:
+            c = buf[j + 1]
+            if 0xD0 <= c <= 0xD7:
+                segs.append((s0, j))
+                j += 2
+                s0 = j
+                continue
+            if c == 0xD9:
+                break
+            j += 2 if c == 0x00 else 1
+            continue
+        j += 1
+    segs.append((s0, n))
+    return segs
+
+
+def decode_batch(bufs, device="cuda"):
+    """Decode JPEG byte strings on the GPU where the geometry allows, Pillow
+    otherwise.  Returns a list of uint8 [H, W, 3] device tensors (None for a
+    file neither path can read) in input order; frames of one geometry are
+    decoded in one launch."""
+    import torch
+    L = N.lib()
+    heads = [parse(b) for b in bufs]
+    out = [None] * len(bufs)
+    groups = {}
+    for i, h in enumerate(heads):
+        if h.supported:
+            groups.setdefault(_geom_key(h), []).append(i)
+        else:
+            out[i] = _host_decode(bufs[i], device)
+    dev = torch.device(device)
+    for key, idx in groups.items():
+        W, H, nc, samp, ri = key
+        h0 = heads[idx[0]]
+        mcux = -(-W // (8 * (max(s[0] for s in samp) if nc == 3 else 1)))
+        mcuy = -(-H // (8 * (max(s[1] for s in samp) if nc == 3 else 1)))
+        nseg = -(-(mcux * mcuy) // ri) if ri else 1
+        offs, ends, chunks, pos = [], [], [], 0
+        keep = []
+        for i in idx:
+            segs = _segments(bufs[i], heads[i])
+            if len(segs) != nseg:     # restart markers not where DRI says: leave it to the host decoder
+                out[i] = _host_decode(bufs[i], device)
+                continue
+            keep.append(i)
+            for a, b in segs:
+                offs.append(pos + a - segs[0][0])
+                ends.append(pos + b - segs[0][0])
+            seg_bytes = bufs[i][segs[0][0]:segs[-1][1]]
+            chunks.append(seg_bytes)
+            pos += len(seg_bytes)
+        if not keep:
+            continue
+        B = len(keep)
+        data = np.frombuffer(bytearray(b"".join(chunks) + b"\xff\xd9" * 4), dtype=np.uint8)
+        huff = np.zeros((B, 4), dtype=_HUFF_DT)
+        qt = np.zeros((B, 4, 64), dtype=np.uint16)
+        for r, i in enumerate(keep):
+            h = heads[i]
+            for (tc, th), (bits, vals) in h.huff.items():
+                if th <= 1:
+                    huff[r, th * 2 + tc] = build_huff(bits, vals)
+            for tq, q in h.qt.items():
+                if tq <= 3:
+                    qt[r, tq] = q
+        geom = np.zeros(20, np.int32)
+        geom[:5] = (W, H, nc, ri, nseg)
+        for c in range(nc):
+            geom[5 + 2 * c], geom[6 + 2 * c] = (samp[c] if nc == 3 else (1, 1))
+            geom[11 + c], geom[14 + c], geom[17 + c] = h0.qsel[c], h0.dcsel[c], h0.acsel[c]
+        # per-frame table selectors must agree within the group (they come from the SOS / SOF)
+        sel_ok = [heads[i].qsel == h0.qsel and heads[i].dcsel == h0.dcsel and heads[i].acsel == h0.acsel for i in keep]
+        if not all(sel_ok):
+            for i, ok in zip(keep, sel_ok):
+                out[i] = _host_decode(bufs[i], device)
+            continue
+        d_data = torch.from_numpy(data).to(dev)
+        d_off = torch.tensor(offs, dtype=torch.int64, device=dev)
+        d_end = torch.tensor(ends, dtype=torch.int64, device=dev)
+        d_huff = torch.from_numpy(huff.view(np.uint8).reshape(-1)).to(dev)
+        d_qt = torch.from_numpy(qt).to(dev)
+        rgb = torch.empty(B, H, W, 3, dtype=torch.uint8, device=dev)
+        gp = geom.ctypes.data
+        nb = L.mi_jpeg_workspace_bytes(gp, B)
+        ws = torch.empty(max(nb, 1), dtype=torch.uint8, device=dev)
+        N.check(L.mi_jpeg_decode(d_data.data_ptr(), d_off.data_ptr(), d_end.data_ptr(), d_huff.data_ptr(),
+                                 d_qt.data_ptr(), gp, B, rgb.data_ptr(), ws.data_ptr(), nb,
+                                 N.stream_ptr(dev)), "mi_jpeg_decode")
+        for r, i in enumerate(keep):
+            out[i] = rgb[r]
+    return out
+
+
+def _host_decode(buf, device):
+    import io
+
+    import torch
+    from PIL import Image
+    try:
+        with Image.open(io.BytesIO(buf)) as im:
+            return torch.from_numpy(np.asarray(im.convert("RGB"), dtype=np.uint8).copy()).to(device)
+    except Exception:
+        return None
+
+
+def decode_files(paths, device="cuda"):
+    """``decode_batch`` over files (read on the host, decoded on the GPU)."""
+    bufs = []
+    for p in paths:
+        try:
+            with open(p, "rb") as f:
+                bufs.append(f.read())
+        except OSError:
+            bufs.append(b"")
+    return decode_batch(bufs, device)

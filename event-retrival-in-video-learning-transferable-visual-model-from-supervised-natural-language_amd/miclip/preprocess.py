@@ -20,6 +20,8 @@ is no GPU JPEG decoder in this image).
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 
 MEAN = np.array([0.48145466, 0.4578275, 0.40821073], dtype=np.float32)
@@ -94,17 +96,57 @@ def preprocess_frames(frames, n_px: int = 224, squash: bool = False, out_dtype=N
 
 
 def load_frames(paths, n_px: int = 224, device="cuda", squash: bool = False, out_dtype=None, threads: int = 8,
-                strict: bool = False):
-    """Decode frame files on host threads (PIL; decoding releases the GIL),
-    upload each same-size group once as uint8, preprocess it on the GPU.
-    Returns ([len(paths), 3, n_px, n_px] tensor in path order, list of failed
-    indices).  A frame that cannot be read is left as zeros, as the
-    reference's ingest does (Backend/services/embedding_service.py:476-480);
-    with ``strict`` the decode error propagates instead (Backend/embedding.py:45
-    has no handler)."""
+                strict: bool = False, gpu_decode=None):
+    """Decode frame files and preprocess them on the GPU.  Returns
+    ([len(paths), 3, n_px, n_px] tensor in path order, list of failed indices).
+
+    Decode: baseline JPEGs on the GPU (``miclip.jpeg``, bit-identical to
+    Pillow; the default, ``$MICLIP_JPEG_GPU=0`` or ``gpu_decode=False`` turns it
+    off), everything else with Pillow on host threads (decoding releases the
+    GIL).  Each same-size group of decoded uint8 frames is preprocessed in one
+    launch.  A frame that cannot be read is left as zeros, as the reference's
+    ingest does (Backend/services/embedding_service.py:476-480); with
+    ``strict`` the decode error propagates instead (Backend/embedding.py:45 has
+    no handler)."""
     import torch
     from concurrent.futures import ThreadPoolExecutor
     from PIL import Image
+
+    if gpu_decode is None:
+        gpu_decode = os.environ.get("MICLIP_JPEG_GPU", "1") != "0"
+    if gpu_decode and str(device).startswith("cuda"):
+        from . import jpeg
+
+        def read(p):
+            try:
+                with open(p, "rb") as f:
+                    return f.read()
+            except OSError as e:
+                if strict:
+                    raise
+                print(f"Error preprocessing image {p}: {e}")
+                return b""
+
+        with ThreadPoolExecutor(max(1, threads)) as ex:
+            bufs = list(ex.map(read, paths))
+        frames = jpeg.decode_batch(bufs, device)
+        out = torch.zeros(len(paths), 3, n_px, n_px, dtype=out_dtype or torch.float32, device=device)
+        groups, failed = {}, []
+        for i, fr in enumerate(frames):
+            if fr is None:
+                if strict:      # Pillow's own error
+                    with Image.open(paths[i]) as im:
+                        im.convert("RGB")
+                if bufs[i]:
+                    print(f"Error preprocessing image {paths[i]}: cannot identify or decode image file")
+                failed.append(i)
+            else:
+                groups.setdefault(tuple(fr.shape), []).append(i)
+        for idx in groups.values():
+            batch = torch.stack([frames[i] for i in idx])
+            out[torch.tensor(idx, device=out.device)] = preprocess_frames(batch, n_px, squash=squash,
+                                                                           out_dtype=out.dtype)
+        return out, failed
 
     def load(p):
         try:

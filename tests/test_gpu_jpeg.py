@@ -1,0 +1,127 @@
+"""GPU JPEG decode (mi_jpeg_decode) against Pillow
+itself — the reference's own decoder (Image.open(p).convert("RGB"),
+Backend/services/embedding_service.py:472-480): every pixel of every frame must
+be identical.  Cases: the 16 real frames of the reference's
+Backend/static/processed_frames (1280x720 4:2:0, standard tables), Pillow-written
+JPEGs at 4:4:4 / 4:2:2 / 4:2:0, qualities 10..100, odd sizes (partial MCUs,
+1-pixel edges), restart markers, grayscale; files the device path hands back to
+the host (progressive, PNG, truncated) decode as Pillow does (or fail as it does)."""
+import glob
+import io
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+
+
+def _pil(buf):
+    from PIL import Image
+    with Image.open(io.BytesIO(buf)) as im:
+        return np.asarray(im.convert("RGB"), dtype=np.uint8)
+
+
+def _img(h, w, seed, mode="RGB"):
+    from PIL import Image
+    rng = np.random.default_rng(seed)
+    yy, xx = np.mgrid[0:h, 0:w]
+    base = 127 + 80 * np.sin(xx / 5.0 + seed) * np.cos(yy / 7.0) + rng.normal(0, 40, (h, w))
+    arr = np.stack([base, np.roll(base, 3, 1) * 0.8, 255 - base], -1)
+    arr = np.clip(arr, 0, 255).astype(np.uint8)
+    im = Image.fromarray(arr)
+    return im.convert("L") if mode == "L" else im
+
+
+def _save(im, **kw):
+    b = io.BytesIO()
+    im.save(b, "JPEG", **kw)
+    return b.getvalue()
+
+
+def _check(bufs, expect_device=None):
+    from miclip import jpeg
+    got = jpeg.decode_batch(bufs, "cuda")
+    for i, (b, g) in enumerate(zip(bufs, got)):
+        ref = _pil(b)
+        assert g is not None, i
+        g = g.cpu().numpy()
+        assert g.shape == ref.shape, (i, g.shape, ref.shape)
+        bad = np.argwhere(g != ref)
+        assert bad.size == 0, f"frame {i}: {len(bad)} bytes differ, first {bad[:3].tolist()}"
+    if expect_device is not None:
+        assert [jpeg.parse(b).supported for b in bufs] == expect_device
+
+
+def test_reference_frames_bit_exact(gpu):
+    files = sorted(glob.glob(os.path.join(ROOT, "golden", "ref_frames", "*.jpg")))
+    assert len(files) == 16
+    _check([open(f, "rb").read() for f in files], expect_device=[True] * 16)
+
+
+@pytest.mark.parametrize("subsampling", [0, 1, 2])
+@pytest.mark.parametrize("quality", [10, 75, 100])
+def test_synthetic_sampling_quality_bit_exact(gpu, subsampling, quality):
+    bufs = [_save(_img(h, w, s), quality=quality, subsampling=subsampling)
+            for s, (h, w) in enumerate([(37, 53), (64, 64), (17, 9), (1, 1), (241, 319), (16, 33)])]
+    _check(bufs, expect_device=[True] * len(bufs))
+
+
+@pytest.mark.parametrize("kw", [dict(restart_marker_blocks=1), dict(restart_marker_blocks=5),
+                                dict(restart_marker_rows=1), dict(restart_marker_rows=3)])
+def test_restart_markers_bit_exact(gpu, kw):
+    bufs = [_save(_img(h, w, 7 + s), quality=85, **kw) for s, (h, w) in enumerate([(72, 100), (131, 47), (200, 256)])]
+    for b in bufs:
+        assert b.count(b"\xff\xdd") == 1
+    _check(bufs, expect_device=[True] * len(bufs))
+
+
+def test_grayscale_and_mixed_batch(gpu):
+    bufs = [_save(_img(45, 61, 1, "L"), quality=90), _save(_img(45, 61, 2), quality=90),
+            _save(_img(45, 61, 3, "L"), quality=40), _save(_img(30, 30, 4), quality=90, subsampling=1)]
+    _check(bufs, expect_device=[True] * 4)
+
+
+def test_host_fallbacks(gpu):
+    from PIL import Image
+    from miclip import jpeg
+    prog = _save(_img(50, 70, 5), quality=80, progressive=True)
+    png = io.BytesIO()
+    _img(20, 30, 6).save(png, "PNG")
+    good = _save(_img(50, 70, 8), quality=80)
+    bufs = [prog, png.getvalue(), good]
+    assert [jpeg.parse(b).supported for b in bufs] == [False, False, True]
+    _check(bufs)
+    trunc = good[:len(good) // 2]
+    assert not jpeg.parse(trunc).supported
+    got = jpeg.decode_batch([trunc, b"not an image"], "cuda")
+    with pytest.raises(OSError):
+        with Image.open(io.BytesIO(trunc)) as im:
+            im.convert("RGB")
+    assert got == [None, None]
+
+
+def test_load_frames_gpu_decode_matches_host_path(gpu, tmp_path):
+    """miclip.preprocess.load_frames: the GPU-decode route and the Pillow route
+    give bit-identical preprocessed tensors (mixed JPEG / PNG / unreadable files,
+    two frame sizes); the unreadable file is a zero frame in both."""
+    import shutil
+    import torch
+    from miclip.preprocess import load_frames
+    files = sorted(glob.glob(os.path.join(ROOT, "golden", "ref_frames", "*.jpg")))[:5]
+    paths = []
+    for i, f in enumerate(files):
+        paths.append(str(tmp_path / f"{i}.jpg"))
+        shutil.copy(f, paths[-1])
+    _img(90, 120, 3).save(tmp_path / "a.png")
+    (tmp_path / "b.jpg").write_bytes(_save(_img(90, 120, 4), quality=70, subsampling=1))
+    (tmp_path / "bad.jpg").write_bytes(b"\xff\xd8garbage")
+    paths += [str(tmp_path / "a.png"), str(tmp_path / "b.jpg"), str(tmp_path / "bad.jpg")]
+    for squash in (False, True):
+        g, fg = load_frames(paths, 224, "cuda", squash=squash, gpu_decode=True)
+        h, fh = load_frames(paths, 224, "cuda", squash=squash, gpu_decode=False)
+        assert fg == fh == [len(paths) - 1]
+        assert torch.equal(g, h)
+        assert not g[-1].any()
