@@ -640,6 +640,41 @@ int mi_rank_topk(const void* corpus, int64_t N, int64_t D, int corpus_dtype, con
   return MI_OK;
 }
 
+int mi_mirror_build(const void* corpus, int64_t N, int64_t D, int corpus_dtype, void* mirror, void* stream) {
+  int r = check_rank_args(N, D, corpus_dtype, 1, 1, MI_NORM_L2, MI_NAN_FIRST);
+  if (r) return r;
+  if (!rank_mirror_supported(D)) return fail(MI_ERR_UNSUPPORTED, "mi_mirror_build: D must be 512 or 768 (got %lld)", (long long)D);
+  if (N == 0) return MI_OK;
+  if (!corpus || !mirror) return fail(MI_ERR_ARG, "mi_mirror_build: null pointer");
+  HIP_TRY(mirror_build(corpus, N, D, corpus_dtype, (uint16_t*)mirror, (hipStream_t)stream));
+  return MI_OK;
+}
+
+size_t mi_rank_mirror_workspace_bytes(int64_t N, int64_t Q) {
+  if (N < 0 || Q < 0) return 0;
+  return rank_mirror_workspace_bytes(N, Q);
+}
+
+int mi_rank_mirror(const void* mirror, const void* master, int64_t N, int64_t D, int master_dtype,
+                   const float* queries, int64_t Q, int32_t k, int64_t index_base, int nan_policy, float* out_scores,
+                   int64_t* out_index, int32_t* out_certified, void* workspace, size_t workspace_bytes,
+                   void* stream) {
+  int r = check_rank_args(N, D, master_dtype, Q, k, MI_NORM_L2, nan_policy);
+  if (r) return r;
+  if (!rank_mirror_supported(D)) return fail(MI_ERR_UNSUPPORTED, "mi_rank_mirror: D must be 512 or 768 (got %lld)", (long long)D);
+  if (k > MIRROR_MAX_K) return fail(MI_ERR_UNSUPPORTED, "mi_rank_mirror: k must be in [1, %d] (got %d)", MIRROR_MAX_K, k);
+  if (Q == 0) return MI_OK;
+  if (N == 0) return fail(MI_ERR_ARG, "mi_rank_mirror: empty corpus");
+  if (!mirror || !master || !queries || !out_scores || !out_index || !out_certified)
+    return fail(MI_ERR_ARG, "mi_rank_mirror: null pointer");
+  const size_t need = rank_mirror_workspace_bytes(N, Q);
+  if (!workspace || workspace_bytes < need)
+    return fail(MI_ERR_ARG, "mi_rank_mirror: workspace too small (%zu < %zu)", workspace_bytes, need);
+  HIP_TRY(rank_mirror((const uint16_t*)mirror, master, N, D, master_dtype, queries, Q, k, index_base,
+                      nan_policy == MI_NAN_FIRST, out_scores, out_index, out_certified, workspace, (hipStream_t)stream));
+  return MI_OK;
+}
+
 int mi_rank_merge(const float* cs, const int64_t* ci, int64_t Q, int64_t C, int32_t k, int nan_policy, float* out_s,
                   int64_t* out_i, void* stream) {
   if (Q < 0 || C < 0) return fail(MI_ERR_ARG, "negative size");

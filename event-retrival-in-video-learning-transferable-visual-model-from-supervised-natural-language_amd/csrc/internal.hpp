@@ -137,6 +137,14 @@ hipError_t score_matrix(const void* corpus, int64_t N, int64_t D, int dt, const 
                         float* out, hipStream_t s);
 hipError_t rank_of_targets(const float* S, int64_t Q, int64_t N, const int64_t* pq, const int64_t* pt, int64_t T,
                            int64_t* out, hipStream_t s);
+// mirrored corpus (rank_mirror.hip): fp16 unit-row mirror + certified exact re-score, k <= 16
+constexpr int MIRROR_MAX_K = 16;
+int rank_mirror_supported(int64_t D);
+size_t rank_mirror_workspace_bytes(int64_t N, int64_t Q);
+hipError_t mirror_build(const void* master, int64_t N, int64_t D, int dt, uint16_t* mirror, hipStream_t s);
+hipError_t rank_mirror(const uint16_t* mirror, const void* master, int64_t N, int64_t D, int dt, const float* q,
+                       int64_t Q, int k, int64_t base, int nan_first, float* out_s, int64_t* out_i, int32_t* cert,
+                       void* ws, hipStream_t s);
 }  // namespace miclip
 
 #include <vector>

@@ -25,90 +25,17 @@
 
 #include "common.hpp"
 #include "internal.hpp"
+#include "rank_keys.hpp"
 
 namespace miclip {
 namespace {
+using namespace rankk;
 
 constexpr int RQ = 32;          // queries per workgroup (MFMA N)
 constexpr int ROWS_WAVE = 32;   // corpus rows per wave tile (MFMA M)
 
-__device__ __forceinline__ uint32_t score_key(float s, int nan_first) {
-  if (s != s) return nan_first ? 0xFFFFFFFFu : 0u;
-  if (s == 0.0f) s = 0.0f;  // -0 == +0
-  const uint32_t u = __float_as_uint(s);
-  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-}
 
-__device__ __forceinline__ float decode_key(uint32_t bk, int nan_first) {
-  if ((bk == 0xFFFFFFFFu && nan_first) || (bk == 0u && !nan_first)) return __uint_as_float(0x7fc00000u);
-  return __uint_as_float((bk & 0x80000000u) ? (bk & 0x7fffffffu) : ~bk);
-}
 
-template <typename I>
-__device__ __forceinline__ bool better(uint32_t ka, I ia, uint32_t kb, I ib) {
-  return ka > kb || (ka == kb && ia < ib);
-}
-
-template <int KC, typename I>
-__device__ __forceinline__ void list_insert(uint32_t (&lk)[KC], I (&li)[KC], uint32_t c, I ci) {
-#pragma unroll
-  for (int p = 0; p < KC; ++p) {
-    const bool sw = better(c, ci, lk[p], li[p]);
-    const uint32_t tk = lk[p];
-    const I ti = li[p];
-    lk[p] = sw ? c : tk;
-    li[p] = sw ? ci : ti;
-    c = sw ? tk : c;
-    ci = sw ? ti : ci;
-  }
-}
-
-template <int DT>
-__device__ __forceinline__ void load_chunk(const void* corpus, int64_t row, int64_t D, int k0, float (&v)[16]) {
-  if (DT == 0) {
-    const float4* p = (const float4*)((const float*)corpus + row * D + k0);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float4 t = p[i];
-      v[4 * i] = t.x; v[4 * i + 1] = t.y; v[4 * i + 2] = t.z; v[4 * i + 3] = t.w;
-    }
-  } else {
-    const uint4* p = (const uint4*)((const uint16_t*)corpus + row * D + k0);
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const uint4 t = p[i];
-      const uint32_t w[4] = {t.x, t.y, t.z, t.w};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        if (DT == 1) {
-          v[8 * i + 2 * e] = bf2f((uint16_t)(w[e] & 0xffff));
-          v[8 * i + 2 * e + 1] = bf2f((uint16_t)(w[e] >> 16));
-        } else {
-          union { uint32_t u; _Float16 h[2]; } cv;
-          cv.u = w[e];
-          v[8 * i + 2 * e] = (float)cv.h[0];
-          v[8 * i + 2 * e + 1] = (float)cv.h[1];
-        }
-      }
-    }
-  }
-}
-
-// Row normalisation as a reciprocal computed once per row (score = dot * inv):
-// MI_NORM_L2 inv = 1/||e|| (a zero row gives 0 * inf = NaN, as E/||E|| does at
-// embedding_service.py:210); MI_NORM_L2_GUARD inv = 1 when ||e|| <= 1e-8
-// (compare_models.py:1168-1171); MI_NORM_NONE inv = 1.  Every kernel that
-// scores rows uses these two helpers, so all paths give identical scores.
-__device__ __forceinline__ float inv_norm(float ss, int norm_mode) {
-  if (norm_mode == 2) return 1.f;
-  const float n = sqrtf(ss);
-  if (norm_mode == 1) return n > 1e-8f ? 1.f / n : 1.f;
-  return 1.f / n;
-}
-
-__device__ __forceinline__ float apply_norm(float dot, float ss, int norm_mode) {
-  return norm_mode == 2 ? dot : dot * inv_norm(ss, norm_mode);
-}
 
 // Computes the 32x32 f32 score tile of (rows row0.., queries of this block)
 // for one wave.  Returns acc (C layout: col = query = lane&31,
@@ -171,39 +98,6 @@ __device__ __forceinline__ void score_tile(const void* corpus, int64_t N, int64_
 //    top-k (that list already holds k better rows).
 // LDS: queries [32][D+4] f32, row norms [NW][32], tau [32]; the lists
 // [64*NW lanes][16] (key u32, idx i32) reuse the query area after a barrier.
-__device__ __forceinline__ void ce_desc(uint64_t& a, uint64_t& b) {  // a >= b afterwards
-  const uint64_t x = a > b ? a : b, y = a > b ? b : a;
-  a = x;
-  b = y;
-}
-
-__device__ __forceinline__ void bitonic_sort16_desc(uint64_t (&c)[16]) {
-#pragma unroll
-  for (int size = 2; size <= 16; size <<= 1)
-#pragma unroll
-    for (int stride = size >> 1; stride > 0; stride >>= 1)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int j = i ^ stride;
-        if (j > i) {
-          if ((i & size) == 0) ce_desc(c[i], c[j]);
-          else ce_desc(c[j], c[i]);
-        }
-      }
-}
-
-// L sorted desc, c sorted desc -> L = the 16 best of both, sorted desc
-__device__ __forceinline__ void merge16_desc(uint64_t (&L)[16], const uint64_t (&c)[16]) {
-#pragma unroll
-  for (int i = 0; i < 16; ++i) L[i] = L[i] > c[15 - i] ? L[i] : c[15 - i];   // bitonic (max of desc, asc)
-#pragma unroll
-  for (int stride = 8; stride > 0; stride >>= 1)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int j = i ^ stride;
-      if (j > i) ce_desc(L[i], L[j]);
-    }
-}
 
 template <int DT, int NW>
 __global__ __launch_bounds__(64 * NW) void rank_stream(const void* __restrict__ corpus, int64_t N, int64_t D,
@@ -390,7 +284,15 @@ __global__ __launch_bounds__(64 * NW) void rank_stream(const void* __restrict__ 
 //    bitonic list update, tau threshold, workgroup list merge), so the
 //    candidates are bit-identical.
 // NOMFMA: timing probe (the stream and the fragment reads without the MFMAs; wrong scores)
-template <int D, int NB = 8, int PF = 6, bool NOMFMA = false>
+// ILV (A/B, slower: see launch_reg): interleaved tile order.  Tile t of wave w
+// in workgroup g is global 32-row tile (t * NW + w) * G + g, so the whole grid
+// streams one contiguous band of NW * G tiles instead of G row ranges
+// rows_per_wg apart.  Candidates then carry global rows.
+// PIPE: a chunk's fragments are read from the ring one chunk ahead (two
+// register buffers), so the LDS latency hides under the previous chunk's MFMAs
+// instead of sitting between the wait and the MFMAs; the DMA lookahead is then
+// PF - 1 chunks beyond the one being read.
+template <int D, int NB = 8, int PF = 6, bool NOMFMA = false, bool ILV = false, bool PIPE = false>
 __global__ __launch_bounds__(256) void rank_reg(const float* __restrict__ corpus, int64_t N,
                                                 const float* __restrict__ queries, int64_t Q, int k,
                                                 int64_t rows_per_wg, int norm_mode, int nan_first, int64_t index_base,
@@ -428,11 +330,15 @@ __global__ __launch_bounds__(256) void rank_reg(const float* __restrict__ corpus
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  const int64_t r_begin = (int64_t)blockIdx.x * rows_per_wg;
-  const int64_t r_end = min(N, r_begin + rows_per_wg);
+  const int G = gridDim.x;
+  const int64_t r_begin = ILV ? 0 : (int64_t)blockIdx.x * rows_per_wg;
+  const int64_t r_end = ILV ? N : min(N, r_begin + rows_per_wg);
   const int nrows = (int)(r_end - r_begin);
   const int ntw = (nrows + 31) / 32;
-  const int my_tiles = ntw > wave ? (ntw - 1 - wave) / NW + 1 : 0;
+  // ILV: tiles (t * NW + wave) * G + blockIdx.x < ntw
+  const int sid = ILV ? wave * G + (int)blockIdx.x : wave;
+  const int sstep = ILV ? NW * G : NW;
+  const int my_tiles = ntw > sid ? (ntw - 1 - sid) / sstep + 1 : 0;
   float* nrm = nrm_all + wave * 32;
   char* wring = ring + wave * NB * SLOT;
 
@@ -448,7 +354,7 @@ __global__ __launch_bounds__(256) void rank_reg(const float* __restrict__ corpus
   int lt = 0, lj = 0, lslot = 0;           // load cursor: tile ordinal, chunk, ring slot
   __amdgpu_buffer_rsrc_t rs;
   auto make_rs = [&]() {
-    const int trow = (wave + NW * lt) * 32;   // relative to r_begin
+    const int trow = (sid + sstep * lt) * 32;   // relative to r_begin
     const int rows = max(0, min(32, nrows - trow));
     // wave-uniform by construction; readfirstlane makes it provable (no waterfall loop per load, guide T20)
     const uint64_t base = (uint64_t)(uintptr_t)(corpus + (r_begin + (rows ? trow : 0)) * (int64_t)D);
@@ -477,26 +383,43 @@ __global__ __launch_bounds__(256) void rank_reg(const float* __restrict__ corpus
 #pragma unroll
   for (int p = 0; p < KC; ++p) L[p] = 0ull;
 
+  auto read_frag = [&](int slot, float4 (&v)[4]) {
+    const char* src = wring + slot * SLOT + rbase;
+#pragma unroll
+    for (int i4 = 0; i4 < 4; ++i4) {
+      const uint32_t a = (uint32_t)(uintptr_t)(const LDS_AS char*)(src + (((4 * h + i4) ^ sw) << 4));
+      asm volatile("ds_read_b128 %0, %1" : "=v"(v[i4]) : "v"(a) : "memory");
+    }
+  };
   if (my_tiles > 0) {
 #pragma unroll
     for (int p = 0; p < PF; ++p) issue();
     int cslot = 0;
+    float4 vb[2][4];
+    if (PIPE) {   // chunk 0's fragments
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (PF - 1)) : "memory");
+      read_frag(0, vb[0]);
+      cslot = 1;
+    }
     for (int ct = 0; ct < my_tiles; ++ct) {
       f32x16 acc = f32x16{};
       float ss = 0.f;
 #pragma unroll
       for (int j = 0; j < NCH; ++j) {
         issue();   // chunk PF ahead (the ring slot it fills was read NB - PF chunks ago)
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * PF) : "memory");   // this chunk landed
-        const char* src = wring + cslot * SLOT + rbase;
-        float4 v[4];
-#pragma unroll
-        for (int i4 = 0; i4 < 4; ++i4) {
-          const uint32_t a = (uint32_t)(uintptr_t)(const LDS_AS char*)(src + (((4 * h + i4) ^ sw) << 4));
-          asm volatile("ds_read_b128 %0, %1" : "=v"(v[i4]) : "v"(a) : "memory");
+        float4 (&v)[4] = vb[PIPE ? (j & 1) : 0];
+        if (PIPE) {
+          // the next chunk landed (PF - 1 younger); this chunk's fragments (read one chunk ago) are in v
+          asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(4 * (PF - 1)) : "memory");
+          __builtin_amdgcn_sched_barrier(0);
+          read_frag(cslot, vb[(j + 1) & 1]);   // (past the last tile: a zero-range chunk, never used)
+          __builtin_amdgcn_sched_barrier(0);
+        } else {
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * PF) : "memory");   // this chunk landed
+          read_frag(cslot, v);
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_sched_barrier(0);
         }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
         const float cur[16] = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w,
                                v[2].x, v[2].y, v[2].z, v[2].w, v[3].x, v[3].y, v[3].z, v[3].w};
 #pragma unroll
@@ -512,7 +435,7 @@ __global__ __launch_bounds__(256) void rank_reg(const float* __restrict__ corpus
       if (h == 0) nrm[r] = inv_norm(ss, norm_mode);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_wave_barrier();
-      const int tr0 = (wave + NW * ct) * 32;
+      const int tr0 = (sid + sstep * ct) * 32;
       const uint32_t tq_thr = tau[r];
       const uint32_t own = (uint32_t)(L[KC - 1] >> 32);
       const uint32_t thr = own > tq_thr ? own : tq_thr;
@@ -541,7 +464,8 @@ __global__ __launch_bounds__(256) void rank_reg(const float* __restrict__ corpus
       __builtin_amdgcn_wave_barrier();
     }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // trailing (zero-range) DMAs land before the ring is reused
+  // trailing (zero-range) DMAs and the pipelined read past the last chunk complete before the ring is reused
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();   // ring free -> lists
   uint32_t* Lk = (uint32_t*)smem;
   int32_t* Li = (int32_t*)(smem + NT * KC * 4);
@@ -1090,12 +1014,22 @@ static hipError_t launch_reg(int64_t N, const float* corpus, const float* q, int
   const int64_t rpw = ((N + nwg - 1) / nwg + 127) / 128 * 128;
   nwg = (N + rpw - 1) / rpw;
   C = nwg * k;
+  // interleaved tile order: A/B only (MICLIP_RANK_ILV=1).  scripts/rank_micro.py: 1M x 512 494 us
+  // against 479 with contiguous row ranges, 1M x 768 729 against 717: not the stream's limit
+  const char* ilv = getenv("MICLIP_RANK_ILV");
+  const bool il = ilv && ilv[0] == '1';
   const size_t lds = (size_t)4 * 8 * 4096 + 4 * 32 * 4 + RQ * 4;
   // (a 9-slot ring with 7 chunks in flight, 147 KB of LDS, failed every rank test, N = 1
   // included, for a reason not yet found; the 8-slot ring is bit-identical to rank_stream)
   const char* probe = getenv("MICLIP_RANK_PROBE");
   // (7 chunks in flight measured the same: the stream alone, NOMFMA, reads 5.3 TB/s either way)
-  auto fn = (probe && probe[0] == '1') ? rank_reg<D, 8, 6, true> : rank_reg<D, 8, 6>;
+  // fragment reads one chunk ahead: A/B only (MICLIP_RANK_PIPE=1; 1M x 512 552 us against 558,
+  // within noise: the wait before the MFMAs is not where this kernel loses time)
+  const char* pipe = getenv("MICLIP_RANK_PIPE");
+  const bool pp = pipe && pipe[0] == '1';
+  auto fn = (probe && probe[0] == '1') ? (il ? rank_reg<D, 8, 6, true, true> : rank_reg<D, 8, 6, true>)
+            : il ? (pp ? rank_reg<D, 8, 6, false, true, true> : rank_reg<D, 8, 6, false, true>)
+                 : (pp ? rank_reg<D, 8, 6, false, false, true> : rank_reg<D, 8, 6>);
   hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
   const dim3 grid((unsigned)nwg, (unsigned)((Q + RQ - 1) / RQ));

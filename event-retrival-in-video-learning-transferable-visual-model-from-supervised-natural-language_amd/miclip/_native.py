@@ -31,6 +31,7 @@ EXPORTS = (
     "mi_resample_coeffs", "mi_preprocess_workspace_bytes", "mi_preprocess_frames",
     "mi_jpeg_workspace_bytes", "mi_jpeg_decode",
     "mi_op_quantize_mx", "mi_op_gemm_mx",
+    "mi_mirror_build", "mi_rank_mirror_workspace_bytes", "mi_rank_mirror",
 )
 
 
@@ -83,6 +84,10 @@ def lib():
         "mi_rank_topk": (ctypes.c_int, [P, I64, I64, ctypes.c_int, P, I64, I32, I64, ctypes.c_int, ctypes.c_int,
                                         P, P, P, SZ, P]),
         "mi_rank_merge": (ctypes.c_int, [P, P, I64, I64, I32, ctypes.c_int, P, P, P]),
+        "mi_mirror_build": (ctypes.c_int, [P, I64, I64, ctypes.c_int, P, P]),
+        "mi_rank_mirror_workspace_bytes": (SZ, [I64, I64]),
+        "mi_rank_mirror": (ctypes.c_int, [P, P, I64, I64, ctypes.c_int, P, I64, I32, I64, ctypes.c_int, P, P, P, P,
+                                          SZ, P]),
         "mi_score_matrix": (ctypes.c_int, [P, I64, I64, ctypes.c_int, P, I64, ctypes.c_int, P, P]),
         "mi_rank_of_targets": (ctypes.c_int, [P, I64, I64, P, P, I64, P, P]),
         "mi_op_gemm": (ctypes.c_int, [P, P, P, P, I32, I32, I32, I32, P]),

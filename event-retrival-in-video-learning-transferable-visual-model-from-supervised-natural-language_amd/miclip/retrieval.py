@@ -130,69 +130,78 @@ def rank_of_targets(scores, pair_query, pair_target):
 
 
 class MirroredCorpus:
-    """HBM-resident corpus with a bf16 ranking mirror and the f32 master kept
-    for exact re-scoring.
+    """HBM-resident corpus with an fp16 ranking mirror and the master kept for
+    exact re-scoring (csrc/rank_mirror.hip).
 
-    ``topk`` ranks the bf16 mirror for ``k' = min(REG_K, oversample * k)``
-    candidates per query (half the HBM bytes of the f32 pass), gathers the
-    union of the candidates' f32 rows (ascending corpus order) and re-ranks
-    them with the exact f32 kernel, so scores are bit-identical to
-    ``rank_topk(master, ...)``.  The result is certified per query: with the
-    mirror's score error bounded by ``delta`` (bf16 rounding of the rows,
-    2^-8 relative, on both the dot product and the norm), every row outside the
-    k' candidates scores at most ``s_bf16[k'-1] + delta`` exactly, so once the
-    exact k-th score exceeds that bound no row outside can enter the top-k.
-    Queries that fail the certificate (near-ties across the candidate edge)
-    fall back to the exact f32 pass over the master.
+    The mirror holds every row as an fp16 unit vector (``mi_mirror_build``,
+    the exact path's reciprocal norm), so ``topk`` streams half the f32 bytes
+    on the fp16 MFMA for the top 16 mirror candidates per query, re-scores
+    them against the master with the exact path's arithmetic, and certifies
+    the result per query: with the mirror's score error bounded by delta
+    (rank_mirror.hip), every row outside the candidates scores at most
+    ``s_mirror[15] + delta``, so once the exact k-th score exceeds that bound
+    the answer is bit-identical to ``rank_topk(master, ...)``.  Queries that
+    fail the certificate (near-ties across the candidate edge, NaN rows) and
+    requests the mirror does not cover (k > MAX_K, norm other than "l2",
+    D not in {512, 768}) take the exact pass; ``fallbacks`` counts them.
+    MAX_K = 12 < 16: the certificate needs a score gap between the k-th
+    exact and the 16th mirror candidate, which k = 16 never has.
 
     Reference semantics: ``EmbeddingService.search_top_frames`` ranks
     ``get_embeddings`` rows (embedding_service.py:209-210, 314-320); the stored
-    ``.npy`` rows stay the f32 master (embedding_service.py:505).
+    ``.npy`` rows stay the master (embedding_service.py:505).
     """
 
-    def __init__(self, master, oversample: int = 4):
+    MAX_K = 12
+
+    def __init__(self, master):
         import torch
         if not master.is_cuda:
             raise N.MiClipError("MirroredCorpus lives in HBM: move the master rows to the device first")
-        self.master = _corpus(master).float().contiguous()
-        self.mirror = self.master.to(torch.bfloat16).contiguous()
-        self.oversample = int(oversample)
+        self.master = _corpus(master)
+        n, d = self.master.shape
+        self.mirror = None
         self.fallbacks = 0
+        self.certified = 0
+        if n > 0 and d in (512, 768):
+            self.mirror = torch.empty((n, d), dtype=torch.float16, device=self.master.device)
+            with torch.cuda.device(self.master.device):
+                N.check(N.lib().mi_mirror_build(self.master.data_ptr(), n, d, N.dtype_code(self.master.dtype),
+                                                self.mirror.data_ptr(), N.stream_ptr(self.master.device)),
+                        "mi_mirror_build")
 
     def __len__(self):
         return self.master.shape[0]
 
-    def topk(self, queries, k, norm="l2", nan_policy="first"):
+    def topk(self, queries, k, norm="l2", nan_policy="first", index_base=0):
         import torch
         q = _queries(queries, self.master.device)
-        n = self.master.shape[0]
+        n, d = self.master.shape
+        Q = q.shape[0]
+        if q.shape[1] != d:
+            raise N.MiClipError(f"dimension mismatch: corpus D={d}, queries D={q.shape[1]}")
+        if self.mirror is None or norm != "l2" or not 1 <= k <= self.MAX_K or Q == 0:
+            self.fallbacks += Q
+            return rank_topk(self.master, q, k, index_base=index_base, norm=norm, nan_policy=nan_policy)
+        dev = self.master.device
+        out_s = torch.empty((Q, k), dtype=torch.float32, device=dev)
+        out_i = torch.empty((Q, k), dtype=torch.int64, device=dev)
+        cert = torch.empty(Q, dtype=torch.int32, device=dev)
+        L = N.lib()
+        with torch.cuda.device(dev):
+            ws = _workspace(dev, L.mi_rank_mirror_workspace_bytes(n, Q))
+            N.check(L.mi_rank_mirror(self.mirror.data_ptr(), self.master.data_ptr(), n, d,
+                                     N.dtype_code(self.master.dtype), q.data_ptr(), Q, k, int(index_base),
+                                     _NANS[nan_policy], out_s.data_ptr(), out_i.data_ptr(), cert.data_ptr(),
+                                     ws.data_ptr(), ws.numel(), N.stream_ptr(dev)), "mi_rank_mirror")
+        bad = torch.nonzero(cert == 0).flatten()
+        nb = int(bad.numel())
+        self.fallbacks += nb
+        self.certified += Q - nb
+        if nb:
+            sf, jf = rank_topk(self.master, q.index_select(0, bad), k, index_base=index_base, norm=norm,
+                               nan_policy=nan_policy)
+            out_s[bad, :sf.shape[1]] = sf
+            out_i[bad, :jf.shape[1]] = jf
         kk = min(k, n)
-        kc = min(max(REG_K, kk), max(kk, self.oversample * kk), n)
-        if kk <= 0:
-            return rank_topk(self.master, q, k, norm=norm, nan_policy=nan_policy)
-        s1, i1 = rank_topk(self.mirror, q, kc, norm=norm, nan_policy=nan_policy)
-        if kc >= n:      # every row is a candidate: the exact pass is the answer
-            return rank_topk(self.master, q, k, norm=norm, nan_policy=nan_policy)
-        union = torch.unique(i1.flatten())                    # sorted ascending: index ties keep corpus order
-        s2, j2 = rank_topk(self.master.index_select(0, union), q, kk, norm=norm, nan_policy=nan_policy)
-        i2 = union[j2]
-        # certificate: bf16 rows carry a relative error <= 2^-8 per element, so
-        # |s_bf16 - s_exact| <= delta = 2^-7 |q| (dot and norm) for "l2";
-        # un-normalised scores scale with the row norm, so certify only "l2"
-        if norm != "l2":
-            self.fallbacks += q.shape[0]
-            return rank_topk(self.master, q, k, norm=norm, nan_policy=nan_policy)
-        delta = q.norm(dim=1) * 2.0 ** -7
-        edge = s1[:, kc - 1]
-        ok = (s2[:, kk - 1] > edge + 2 * delta) & torch.isfinite(s2).all(1) & torch.isfinite(s1).all(1)
-        if bool(ok.all()):
-            return s2, i2
-        bad = torch.nonzero(~ok).flatten()
-        self.fallbacks += int(bad.numel())
-        sf, jf = rank_topk(self.master, q.index_select(0, bad), k, norm=norm, nan_policy=nan_policy)
-        s2 = s2.clone()
-        i2 = i2.clone()
-        s2[bad] = sf
-        i2[bad] = jf
-        return s2, i2
-
+        return out_s[:, :kk], out_i[:, :kk]

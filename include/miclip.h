@@ -132,6 +132,30 @@ int mi_rank_topk(const void* corpus, int64_t N, int64_t D, int corpus_dtype,
                  int norm_mode, int nan_policy, float* out_scores, int64_t* out_index,
                  void* workspace, size_t workspace_bytes, void* stream);
 
+/* Ranking mirror of a corpus for mi_rank_mirror (an
+ * HBM-resident half-width mirror beside the f32 master of
+ * EmbeddingService.get_embeddings, embedding_service.py:186-217).
+ * mirror: device fp16 [N,D] = c / ||c|| per row, with the reciprocal norm of
+ * mi_rank_topk's MI_NORM_L2 (a zero row becomes NaN, as E/||E|| does at
+ * embedding_service.py:210).  D = 512 or 768. */
+int mi_mirror_build(const void* corpus, int64_t N, int64_t D, int corpus_dtype, void* mirror_f16, void* stream);
+
+/* Workspace bytes mi_rank_mirror needs for (N, Q). */
+size_t mi_rank_mirror_workspace_bytes(int64_t N, int64_t Q);
+
+/* search_top_frames' ranking (embedding_service.py:314-320, MI_NORM_L2) through
+ * the mirror: one fp16 MFMA pass over the mirror (half the f32 bytes) for the
+ * top 16 mirror candidates per query, then the exact f32 scores of those
+ * candidates from the master with mi_rank_topk's arithmetic and a per-query
+ * certificate.  out_certified[q] = 1: out_scores/out_index [Q,k] are
+ * bit-identical to mi_rank_topk(master, ..., MI_NORM_L2, nan_policy); 0: a
+ * near-tie across the candidate edge or a non-finite score: rank that query
+ * with mi_rank_topk.  1 <= k <= 16. */
+int mi_rank_mirror(const void* mirror_f16, const void* master, int64_t N, int64_t D, int master_dtype,
+                   const float* queries, int64_t Q, int32_t k, int64_t index_base, int nan_policy,
+                   float* out_scores, int64_t* out_index, int32_t* out_certified,
+                   void* workspace, size_t workspace_bytes, void* stream);
+
 /* Merge per-query candidate lists (e.g. the RCCL all-gather of per-shard
  * top-k) into the global top-k with the same order rule.
  * cand_scores f32 [Q,C], cand_index int64 [Q,C] (index -1 = empty slot); 1 <= k <= 64. */

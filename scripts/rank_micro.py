@@ -14,14 +14,16 @@ sys.path.insert(0, os.path.join(ROOT, "event-retrival-in-video-learning-transfer
 import torch  # noqa: E402
 from miclip import retrieval  # noqa: E402
 
-VARIANTS = {"default": {}, "stream12": {"MICLIP_RANK_REG": "0", "MICLIP_RANK_NW": "12"},
+VARIANTS = {"default": {}, "seed0": {"MICLIP_RANK_SEED": "0"}, "pipe0": {"MICLIP_RANK_PIPE": "0"},
+            "ilv1": {"MICLIP_RANK_ILV": "1"}, "stream12": {"MICLIP_RANK_REG": "0", "MICLIP_RANK_NW": "12"},
             "stage1": {"MICLIP_RANK_STAGE1": "1"}, "nomfma": {"MICLIP_RANK_PROBE": "1"}}
 SHAPES = [(125_000, 512, 32, torch.float32), (1_000_000, 512, 32, torch.float32),
           (1_000_000, 512, 32, torch.bfloat16), (1_000_000, 768, 32, torch.float32), (10_000, 512, 32, torch.float32)]
 
 
 def setenv(v):
-    for k in ("MICLIP_RANK_STAGE1", "MICLIP_RANK_NW", "MICLIP_RANK_REG", "MICLIP_RANK_PROBE"):
+    for k in ("MICLIP_RANK_STAGE1", "MICLIP_RANK_NW", "MICLIP_RANK_REG", "MICLIP_RANK_PROBE", "MICLIP_RANK_ILV",
+              "MICLIP_RANK_PIPE", "MICLIP_RANK_SEED"):
         os.environ.pop(k, None)
     os.environ.update(VARIANTS[v])
 

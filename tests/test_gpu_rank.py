@@ -137,26 +137,58 @@ def test_reference_flow_rk_fixture(gpu):
         assert [res[d]["R@1"], res[d]["R@5"], res[d]["R@10"]] == list(arr)
 
 
-@pytest.mark.parametrize("N,D,Q,k", [(20000, 512, 32, 10), (4097, 768, 7, 16), (500, 512, 3, 60)])
-def test_mirrored_corpus_matches_f32(gpu, N, D, Q, k):
-    """bf16 mirror + exact f32 re-scoring == the f32 pass, bit for bit (§8(f) item 2)."""
+@pytest.mark.parametrize("N,D,Q,k,dt", [(20000, 512, 32, 10, "f32"), (4097, 768, 7, 8, "f32"), (4097, 768, 7, 16, "f32"),
+                                        (500, 512, 3, 60, "f32"),
+                                        (3, 512, 2, 10, "f32"), (33, 768, 40, 1, "f32"), (70001, 512, 5, 16, "f16"),
+                                        (9000, 768, 33, 10, "bf16"), (1000, 256, 4, 10, "f32")])
+def test_mirrored_corpus_matches_exact(gpu, N, D, Q, k, dt):
+    """fp16 mirror + exact re-score == the exact pass over the master, bit for
+    bit (§8(f) item 2): certified queries from the mirror, the rest (and
+    k > 12, D outside {512, 768}) from the exact pass."""
+    import torch
     from miclip import retrieval, weights
-    corpus = _t(weights.normal(21, f"m{N}", (N, D)), gpu)
+    tdt = {"f32": torch.float32, "f16": torch.float16, "bf16": torch.bfloat16}[dt]
+    corpus = _t(weights.normal(21, f"m{N}", (N, D)), gpu).to(tdt)
     q = _t(weights.synthetic_corpus(Q, D, seed=22), gpu)
     mc = retrieval.MirroredCorpus(corpus)
     s, i = mc.topk(q, k)
     s0, i0 = retrieval.rank_topk(corpus, q, k)
+    assert s.shape == s0.shape
     assert (i.cpu() == i0.cpu()).all()
     assert (s.cpu() == s0.cpu()).all()
+    if k <= retrieval.MirroredCorpus.MAX_K and D in (512, 768):
+        assert mc.certified >= Q - 1      # random corpora: the certificate holds
+
+
+def test_mirrored_corpus_edge_cases(gpu):
+    """index_base, NaN rows (zero rows: NaN first -> uncertified -> exact pass;
+    NaN last -> certified past them), nan_policy, mirror of the real corpus."""
+    import torch
+    from miclip import retrieval, weights
+    g = golden("rank_video_test_4.npz")
+    rows = np.array(g["corpus"], dtype=np.float32)
+    q = _t(weights.synthetic_corpus(6, rows.shape[1], seed=25), gpu)
+    for zero in (False, True):
+        c = rows.copy()
+        if zero:
+            c[[3, 100]] = 0.0
+        corpus = _t(c, gpu)
+        for pol in ("first", "last"):
+            mc = retrieval.MirroredCorpus(corpus)
+            s, i = mc.topk(q, 10, nan_policy=pol, index_base=1000)
+            s0, i0 = retrieval.rank_topk(corpus, q, 10, index_base=1000, nan_policy=pol)
+            assert (i.cpu() == i0.cpu()).all() and torch.equal(s.cpu().view(torch.int32), s0.cpu().view(torch.int32)), (zero, pol)
+            if zero and pol == "first":
+                assert mc.fallbacks == 6
 
 
 def test_mirrored_corpus_near_ties_fall_back(gpu):
-    """Rows that tie in bf16 across the candidate edge fail the certificate and
+    """Rows that tie in fp16 across the candidate edge fail the certificate and
     take the exact path; the answer is still the f32 one."""
     import torch
     from miclip import retrieval, weights
-    base = weights.normal(23, "tie", (1, 256))
-    rows = np.repeat(base, 400, axis=0) + weights.normal(24, "eps", (400, 256)) * 1e-4   # near-duplicates
+    base = weights.normal(23, "tie", (1, 512))
+    rows = np.repeat(base, 400, axis=0) + weights.normal(24, "eps", (400, 512)) * 1e-4   # near-duplicates
     corpus = _t(rows, gpu)
     q = torch.from_numpy(base / np.linalg.norm(base)).to(gpu)
     mc = retrieval.MirroredCorpus(corpus)
@@ -205,3 +237,23 @@ def test_topk_large_k_matches_fused_path_prefix(gpu):
     s2, i2 = retrieval.rank_topk(corpus, q, 500)
     assert np.array_equal(i1.cpu().numpy(), i2[:, :64].cpu().numpy())
     assert np.array_equal(s1.cpu().numpy(), s2[:, :64].cpu().numpy())
+
+
+def test_mirror_large_corpus_ties_nan(gpu):
+    """300k rows: the mirror path == the exact pass, including exact ties
+    between rows and later duplicates (index ascending) and a NaN row, for
+    both NaN policies."""
+    import torch
+    from miclip import retrieval, weights
+    c = weights.normal(31, "seed", (300_000, 512))
+    c[200_000:200_100] = c[0:100]                   # later duplicates: ties, index ascending
+    c[250_000] = 0.0                                # a NaN row
+    corpus = _t(c, gpu)
+    q = _t(np.concatenate([weights.synthetic_corpus(30, 512, seed=32), c[[5, 77]]]), gpu)
+    mc = retrieval.MirroredCorpus(corpus)
+    for pol in ("first", "last"):
+        s1, i1 = mc.topk(q, 10, nan_policy=pol)
+        s0, i0 = retrieval.rank_topk(corpus, q, 10, nan_policy=pol)
+        assert torch.equal(i1, i0)
+        assert torch.equal(s1.view(torch.int32), s0.view(torch.int32))
+    assert mc.certified >= 30   # NaN-last: certified; NaN-first: the NaN row is a candidate -> exact pass

@@ -234,3 +234,29 @@ def test_search_by_image_matches_reference_flow(service, monkeypatch, reencode):
     png = (frame_dir / names[2]).read_bytes()
     assert search.search_by_image(svc, ds, "data:image/png;base64," + base64.b64encode(png).decode(), 0.0, 5,
                                   "vid") == []
+
+
+def test_large_corpus_ranks_through_mirror(service):
+    """A corpus of >= MIRROR_MIN_ROWS rows gets the fp16 ranking mirror
+    (retrieval.MirroredCorpus); search_top_frames_by_image (top_k <= 12) then
+    ranks through it and returns exactly the exact pass's frames, the order of
+    embedding_service.py:365-372 (argsort(s)[::-1][:k] on normalised rows)."""
+    import torch
+    from miclip import retrieval, service as S, weights
+    svc, frame_dir, names, paths = service
+    n = S.MIRROR_MIN_ROWS + 1000
+    rows = weights.normal(41, "svc", (n, 512))
+    os.makedirs(os.path.dirname(paths.get_embeddings_path("big")), exist_ok=True)
+    np.save(paths.get_embeddings_path("big"), rows)
+    big = [f"f{i:07d}.jpg" for i in range(n)]
+    with open(paths.get_metadata_path("big"), "w") as f:
+        json.dump([{"frame": x} for x in big], f)
+    q = weights.synthetic_corpus(1, 512, seed=42)[0]
+    got = svc.search_top_frames_by_image(q, 10, "big")
+    assert len(svc._mirrors) == 1
+    mc = next(iter(svc._mirrors.values()))
+    assert mc.certified == 1 and mc.fallbacks == 0
+    s, i = retrieval.rank_topk(torch.from_numpy(rows).cuda(), torch.from_numpy(q[None]).cuda(), 10)
+    assert got == [big[j] for j in i[0].cpu().numpy()]
+    got40 = svc.search_top_frames_by_image(q, 40, "big")          # k > 12: the exact pass
+    assert got40[:10] == got and mc.certified == 1
