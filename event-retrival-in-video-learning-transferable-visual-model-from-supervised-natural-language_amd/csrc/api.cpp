@@ -761,10 +761,15 @@ int mi_op_gemm_mx(const void* A, const void* a_scale, const void* W, const void*
                   int32_t M, int32_t N, int32_t K, int32_t epi, void* stream) {
   if (!A || !W || !a_scale || !w_scale || !out || M < 0) return fail(MI_ERR_ARG, "mi_op_gemm_mx: bad arguments");
   if (K % 128 || N % 256 || K <= 0) return fail(MI_ERR_UNSUPPORTED, "mi_op_gemm_mx: needs K %% 128 == 0, N %% 256 == 0");
-  if (epi != 0 && epi != 1 && epi != 3) return fail(MI_ERR_ARG, "mi_op_gemm_mx: epilogue 0 (bf16), 1 (GELU) or 3 (f32)");
+  const int variant = epi >> 8;  // bits 8+: kernel override for A/B (gemm_mx: 1 = 16x16x128, 3 = ping-pong)
+  epi &= 0xff;
+  if (epi != 0 && epi != 1 && epi != 3 && epi != 4)
+    return fail(MI_ERR_ARG, "mi_op_gemm_mx: epilogue 0 (bf16), 1 (GELU), 3 (f32) or 4 (GELU -> MX-fp8)");
   GemmArgs g = gargs((const uint16_t*)A, K, (const uint16_t*)W, K, bias, out, N, M, N, K);
+  g.variant = variant;
   g.a_scale = (const uint8_t*)a_scale;
   g.w_scale = (const uint8_t*)w_scale;
+  if (epi == 4) g.o_scale = (uint8_t*)out + ((int64_t)M * N + 255) / 256 * 256;   // e4m3 [M,N] then its scales
   HIP_TRY(gemm_mx(g, epi, (hipStream_t)stream));
   return MI_OK;
 }

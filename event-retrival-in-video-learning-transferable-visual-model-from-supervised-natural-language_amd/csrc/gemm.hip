@@ -859,6 +859,8 @@ __global__ __launch_bounds__(512) void gemm_ppp_kernel(GemmArgs a) {
   }
 }
 
+}  // namespace
+
 int cu_count() {
   static int n = 0;
   if (!n) {
@@ -869,6 +871,8 @@ int cu_count() {
   }
   return n;
 }
+
+namespace {
 
 // n-blocks per tile group (tile_coords): the largest divisor of tiles_n whose
 // W panel (ng x 256 rows x K bf16) fits ~1.6 MB of the XCD's 4 MB L2; 0 (plain

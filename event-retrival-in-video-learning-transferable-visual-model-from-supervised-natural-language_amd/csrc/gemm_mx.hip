@@ -507,8 +507,12 @@ hipError_t gemm_mx(const GemmArgs& a, int epi, hipStream_t s) {
   if (a.K % MX_BK || a.N % 256 || a.K <= 0 || !a.a_scale || !a.w_scale) return hipErrorInvalidValue;
   if ((a.lda % 16) || (a.ldw % 16) || (a.ldo % 8) || ((uintptr_t)a.out & 15)) return hipErrorInvalidValue;
   const int nt = ((a.M + 255) / 256) * (a.N / 256);
-  // default: the ping-pong 32x32x64 kernel (needs K / 64 >= 3 stages);
-  // MICLIP_GEMM_VARIANT=1: the double-buffered 16x16x128 kernel (A/B)
+  // default: the ping-pong 32x32x64 kernel (needs K / 64 >= 3 stages).  A/B variants:
+  // 1 the double-buffered 16x16x128 kernel; 8 the 8-phase persistent kernel (gemm_mx8q.hip:
+  // bit-identical to 1, but 8-30 % slower than the ping-pong kernel at the L/14@336 shapes,
+  // scripts/gemm_mx_micro.py — at fp8 rate a K = 1024 tile's MFMAs take half the bf16 time
+  // while its epilogue does not shrink)
+  if (a.variant == 8 && gemm_mx8q_ok(a, epi)) return gemm_mx8q(a, epi, s, cu_count());
   if (a.variant != 1 && a.K / 64 >= 3) {
     switch (epi) {
       case EPI_BF16: hipLaunchKernelGGL(gemm_mxpp_kernel<EPI_BF16>, dim3(nt), dim3(512), 0, s, a); break;

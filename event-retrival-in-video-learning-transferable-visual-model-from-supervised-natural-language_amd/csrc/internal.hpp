@@ -83,6 +83,10 @@ hipError_t gemm_8r(const GemmArgs& a, int epi, hipStream_t s, int cus, int mode 
 hipError_t gemm_probe_read(unsigned long long* host, int n);
 // MX-fp8: A, W e4m3 bytes (row strides lda/ldw in BYTES), a_scale/w_scale e8m0; K % 128 == 0, N % 256 == 0
 hipError_t gemm_mx(const GemmArgs& a, int epi, hipStream_t s);
+// MX-fp8 on gemm_8q's 8-phase persistent schedule (gemm_mx8q.hip): bf16 / GELU-bf16 / GELU-MX epilogues
+int gemm_mx8q_ok(const GemmArgs& a, int epi);
+hipError_t gemm_mx8q(const GemmArgs& a, int epi, hipStream_t s, int cus);
+int cu_count();   // compute units of the current device (gemm.hip)
 // bf16 [rows][K] -> e4m3 [rows][K] + e8m0 scales [K/128][rows_pad][2] (one per 64 k; K % 128 == 0)
 hipError_t quantize_mx(const uint16_t* in, int64_t ld_in, uint8_t* q, int64_t ld_q, uint8_t* sc, int rows, int K,
                        hipStream_t s);

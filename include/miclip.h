@@ -253,7 +253,11 @@ int mi_op_residual_ln(void* x, const void* delta, const float* gamma, const floa
  *   [K/128][rows_pad][2] (rows_pad = rows rounded up to even; byte kb & 1 of
  *   row r in stage kb >> 1 scales k-block kb); K % 128 == 0
  * mi_op_gemm_mx: out = (A * 2^sA) . (W * 2^sW)^T (+bias) on the block-scaled MFMA,
- *   A [M][K] / W [N][K] e4m3 with their scales; epilogue 0 bf16, 1 bf16 QuickGELU, 3 f32.
+ *   A [M][K] / W [N][K] e4m3 with their scales; epilogue 0 bf16, 1 bf16 QuickGELU, 3 f32,
+ *   4 QuickGELU -> MX-fp8 (the c_fc -> c_proj hand-off: out holds the e4m3 [M][N] bytes and,
+ *   from byte offset M*N rounded up to 256, their stage-major scales [N/128][M_pad][2]).
+ *   Bits 8+ of epi select a kernel for A/B (0 default: the ping-pong 32x32x64 kernel; 1 the
+ *   double-buffered 16x16x128 kernel; 8 the 8-phase persistent kernel, bit-identical to 1).
  *   K % 128 == 0, N % 256 == 0. */
 int mi_op_quantize_mx(const void* in, void* q, void* scales, int32_t rows, int32_t K, void* stream);
 int mi_op_gemm_mx(const void* A, const void* a_scale, const void* W, const void* w_scale, const float* bias, void* out,

@@ -37,6 +37,10 @@ def main():
                                                  epi, sp), "g"),
             "mxfp8": lambda: N.check(L.mi_op_gemm_mx(qa.data_ptr(), sa.data_ptr(), qw.data_ptr(), sw.data_ptr(),
                                                      bias.data_ptr(), o2.data_ptr(), M, Nn, K, epi, sp), "g"),
+            "mx_pp": lambda: N.check(L.mi_op_gemm_mx(qa.data_ptr(), sa.data_ptr(), qw.data_ptr(), sw.data_ptr(),
+                                                     bias.data_ptr(), o2.data_ptr(), M, Nn, K, epi | (8 << 8), sp), "g"),
+            "mx_v1": lambda: N.check(L.mi_op_gemm_mx(qa.data_ptr(), sa.data_ptr(), qw.data_ptr(), sw.data_ptr(),
+                                                     bias.data_ptr(), o2.data_ptr(), M, Nn, K, epi | (1 << 8), sp), "g"),
             "quant_A": lambda: N.check(L.mi_op_quantize_mx(A.data_ptr(), qa.data_ptr(), sa.data_ptr(), M, K, sp), "q"),
         }
         for f in runs.values():
@@ -55,7 +59,8 @@ def main():
         fl = 2.0 * M * Nn * K
         rel = ((o1.float() - o2.float()).norm() / o1.float().norm()).item()
         print(f"{name:5s} M={M} N={Nn} K={K}: bf16 {best['bf16']:8.1f} us {fl / best['bf16'] / 1e6:7.1f} TF | "
-              f"mxfp8 {best['mxfp8']:8.1f} us {fl / best['mxfp8'] / 1e6:7.1f} TF | quantize A {best['quant_A']:7.1f} us"
+              f"mxfp8 {best['mxfp8']:8.1f} us {fl / best['mxfp8'] / 1e6:7.1f} TF | 8-phase {best['mx_pp']:8.1f} us "
+              f"{fl / best['mx_pp'] / 1e6:7.1f} TF | 16x16x128 {best['mx_v1']:8.1f} us | quantize A {best['quant_A']:7.1f} us"
               f" | rel diff {rel:.3g}", flush=True)
         del A, W, qa, qw, o1, o2
 

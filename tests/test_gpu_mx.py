@@ -110,3 +110,43 @@ def test_gemm_mx_block_scales(gpu, M, N, K):
     # per-row tolerance: rows differ by 2^12 in scale
     err = np.abs(got - ref).max(1) / np.maximum(np.abs(ref).max(1), 1e-30)
     assert err.max() < 1e-4, err.max()
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 512), (1000, 1024, 1024), (4099, 768, 4096), (40000, 1024, 1024)])
+@pytest.mark.parametrize("epi", [0, 1, 4])
+def test_gemm_mx8q_matches_16x16x128_kernel(gpu, M, N, K, epi):
+    """The 8-phase persistent MX kernel (gemm_mx8q.hip, variant 8) runs the same
+    v_mfma_scale_f32_16x16x128_f8f6f4 in the same k order as the
+    double-buffered kernel (variant 1): bit-identical bf16 / GELU / MX-fp8
+    outputs (e4m3 bytes and their scales), with row tails past M, several
+    tiles per workgroup (40000 rows) and K up to 4096."""
+    import torch
+    N_ = _lib()
+    g = torch.Generator(device="cpu").manual_seed(M + K + epi)
+    a = (torch.randn(M, K, generator=g) * 2).bfloat16()
+    w = (torch.randn(N, K, generator=g) * K ** -0.5).bfloat16()
+    bias = torch.randn(N, generator=g).to(gpu)
+    qa, sa = _quant_gpu(a.to(gpu))
+    qw, sw = _quant_gpu(w.to(gpu))
+    outs = []
+    for variant in (8, 1):
+        if epi == 4:
+            mp = M + (M & 1)
+            out = torch.zeros((M * N + 255) // 256 * 256 + (N // 128) * mp * 2, dtype=torch.uint8, device=gpu)
+        else:
+            out = torch.zeros(M, N, dtype=torch.bfloat16, device=gpu)
+        N_.check(N_.lib().mi_op_gemm_mx(qa.data_ptr(), sa.data_ptr(), qw.data_ptr(), sw.data_ptr(), bias.data_ptr(),
+                                        out.data_ptr(), M, N, K, epi | (variant << 8), _stream()), "gemm_mx")
+        outs.append(out)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0].view(torch.uint8), outs[1].view(torch.uint8))
+    if epi == 4:   # and the fp8 output decodes to the oracle's GELU within e4m3 rounding
+        q = outs[0][:M * N].cpu().numpy().reshape(M, N)
+        s = outs[0][(M * N + 255) // 256 * 256:].cpu().numpy()
+        got = mx_ref.E4M3[q] * 2.0 ** (mx_ref.from_stage_major(s, M, N).repeat(64, 1).astype(np.float64) - 127)
+        sa_, sw_ = (mx_ref.from_stage_major(x.cpu().numpy(), r, K) for x, r in ((sa, M), (sw, N)))
+        ref = mx_ref.gemm(qa.cpu().numpy(), sa_, qw.cpu().numpy(), sw_) + bias.double().cpu().numpy()
+        ref = ref / (1 + np.exp(-1.702 * ref))
+        # e4m3 keeps 3 mantissa bits (half an ulp = 2^-4 of the value); block values scaled into
+        # [448, 512) saturate at 448 (up to 1/8); plus the block's subnormal floor
+        assert np.all(np.abs(got - ref) <= 0.125 * np.abs(ref) + 0.01 * np.abs(ref).max())
