@@ -339,8 +339,38 @@ def rank_roofline(dev, reps=20):
         out[name] = {"us": round(us, 1), "gbs": round(nbytes / us / 1e3, 1),
                      "hbm_frac": round(nbytes / us / 1e3 / HBM_PEAK_GBS, 4),
                      "tflops_f32_mfma": round(2.0 * N * Q * D / us / 1e6, 2)}
+        if dt == torch.float32 and N >= 1_000_000:
+            out[name.replace("_f32", "_mirror")] = mirror_timing(corpus, q, reps if Q <= 32 else 3, us)
         del corpus
     return out
+
+
+def mirror_timing(corpus, q, n, exact_us):
+    """The same ranking through the fp16 mirror (retrieval.MirroredCorpus,
+    csrc/rank_mirror.hip): mirror pass + merge + exact re-score of 16
+    candidates per query, certificate read back, exact pass for uncertified
+    queries — the whole MirroredCorpus.topk, results checked identical to the
+    exact pass.  bytes = the fp16 mirror's N*D*2."""
+    import torch
+    from miclip import retrieval
+    mc = retrieval.MirroredCorpus(corpus)
+    s, i = mc.topk(q, 10)
+    s0, i0 = retrieval.rank_topk(corpus, q, 10)
+    identical = bool(torch.equal(i, i0) and torch.equal(s, s0))
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(n):
+        mc.topk(q, 10)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / n
+    nbytes = mc.mirror.numel() * 2
+    return {"us": round(us, 1), "gbs": round(nbytes / us / 1e3, 1),
+            "hbm_frac": round(nbytes / us / 1e3 / HBM_PEAK_GBS, 4),
+            "speedup_vs_exact": round(exact_us / us, 2), "identical_to_exact": identical,
+            "certified": f"{mc.certified}/{mc.certified + mc.fallbacks}"}
 
 
 def launch_workers(args):
