@@ -38,7 +38,41 @@ def _pairs(word):
     return {(a, b) for a, b in zip(word[:-1], word[1:])}
 
 
+# ftfy.fix_text (openai/CLIP basic_clean's first step; ftfy 6 default
+# TextFixerConfig) is not installed here.  Restated: the deterministic fixers
+# that apply to well-formed Unicode input, in ftfy's order — terminal escapes,
+# Latin ligatures, character width, curly quotes, line breaks, control
+# characters, NFC.  Mojibake repair (fix_encoding / decode_inconsistent_utf8)
+# is not restated: it needs ftfy's charset tables, and a query typed or
+# translated into the search box is already well-formed.
+_ANSI = re.compile(r"\x1b\[[\d;]*[@-~]")
+_LIGATURES = {"\u0132": "IJ", "\u0133": "ij", "\u01f1": "DZ", "\u01f2": "Dz", "\u01f3": "dz", "\u01c4": "DŽ",
+              "\u01c5": "Dž", "\u01c6": "dž", "\u01c7": "LJ", "\u01c8": "Lj", "\u01c9": "lj", "\u01ca": "NJ",
+              "\u01cb": "Nj", "\u01cc": "nj", "\ufb00": "ff", "\ufb01": "fi", "\ufb02": "fl", "\ufb03": "ffi",
+              "\ufb04": "ffl", "\ufb05": "ſt", "\ufb06": "st"}
+_QUOTES = {"\u2018": "'", "\u2019": "'", "\u201a": "'", "\u201b": "'", "\u201c": '"', "\u201d": '"',
+           "\u201e": '"', "\u201f": '"', "\u2032": "'", "\u2033": '"'}
+_CONTROL = re.compile(r"[\x00-\x08\x0b\x0e-\x1f\x7f\u206a-\u206f\ufff9-\ufffc\ufeff]")
+
+
+def fix_text_subset(text):
+    import unicodedata
+    text = _ANSI.sub("", text)
+    text = "".join(_LIGATURES.get(c, c) for c in text)
+    # fix_character_width: fullwidth / halfwidth forms and the ideographic space, by NFKC of those characters
+    text = "".join(unicodedata.normalize("NFKC", c) if ("\uff01" <= c <= "\uffee" or c == "\u3000") else c
+                   for c in text)
+    text = "".join(_QUOTES.get(c, c) for c in text)
+    text = text.replace("\r\n", "\n").replace("\r", "\n")
+    for c in ("\u2028", "\u2029", "\u0085"):
+        text = text.replace(c, "\n")
+    text = _CONTROL.sub("", text)
+    return unicodedata.normalize("NFC", text)
+
+
 def _clean(text):
+    """basic_clean + whitespace_clean of openai/CLIP simple_tokenizer."""
+    text = fix_text_subset(text)
     text = html.unescape(html.unescape(text))
     return re.sub(r"\s+", " ", text.strip()).strip()
 

@@ -97,3 +97,21 @@ def test_synthetic_tokens_format():
         L = int(np.argmax(row))
         assert row[0] == 49406 and row[L] == 49407 and 6 <= L <= 31 and (row[L + 1:] == 0).all()
         assert (row[1:L] >= 256).all() and (row[1:L] < 49406).all()
+
+
+def test_tokenizer_clean_restates_ftfy_subset():
+    """basic_clean's ftfy.fix_text step (ftfy is not installed: restated subset,
+    miclip/tokenizer.py), then the double html.unescape and whitespace_clean of
+    openai/CLIP simple_tokenizer.  Expected strings follow ftfy 6's documented
+    fixers (ligatures, character width, curly quotes, line breaks, control
+    characters, terminal escapes, NFC); parity against ftfy itself is unpinned."""
+    import unicodedata
+    from miclip.tokenizer import _clean
+    assert _clean("ﬁsh “quoted”") == 'fish "quoted"'
+    assert _clean("ＡＢＣ　１２３") == "ABC 123"
+    assert _clean("école") == unicodedata.normalize("NFC", "école")
+    assert _clean("line\r\nbreak x") == "line break x"
+    assert _clean("\x1b[31mred\x1b[0m") == "red"
+    assert _clean("tab\x00ctl") == "tabctl"
+    assert _clean("a &amp;amp; b") == "a & b"
+    assert _clean("  plain   query  ") == "plain query"
