@@ -161,7 +161,28 @@ struct mi_clip {
   // MX-fp8 activations (fp8 mode): LN outputs, attention output, QuickGELU(c_fc) + their scales
   uint8_t *hq = nullptr, *hqs = nullptr, *attq = nullptr, *attqs = nullptr, *mlpq = nullptr, *mlpqs = nullptr;
   std::mutex mu;
+  // workspace ordering across streams: the encoders' kernels run on the caller's stream, the
+  // mutex only covers their launch, so a call on another stream first waits for the event
+  // recorded after the previous call's last kernel
+  hipEvent_t ws_evt = nullptr;
+  hipStream_t ws_stream = nullptr;
+  bool ws_used = false;
 };
+
+static hipError_t ws_acquire(mi_clip* c, hipStream_t s) {
+  if (c->ws_used && c->ws_stream != s) return hipStreamWaitEvent(s, c->ws_evt, 0);
+  return hipSuccess;
+}
+
+static hipError_t ws_release(mi_clip* c, hipStream_t s) {
+  if (!c->ws_evt) {
+    hipError_t e = hipEventCreateWithFlags(&c->ws_evt, hipEventDisableTiming);
+    if (e != hipSuccess) return e;
+  }
+  c->ws_stream = s;
+  c->ws_used = true;
+  return hipEventRecord(c->ws_evt, s);
+}
 
 extern "C" {
 
@@ -313,6 +334,7 @@ int mi_clip_destroy(mi_clip* c) {
     if (c->ws) (void)hipFree(c->ws);
     if (c->wdev) (void)hipFree(c->wdev);
     if (c->wq) (void)hipFree(c->wq);
+    if (c->ws_evt) (void)hipEventDestroy(c->ws_evt);
   }
   delete c;
   return MI_OK;
@@ -538,6 +560,7 @@ int mi_clip_encode_image(mi_clip* c, const void* pixels, int64_t B, int in_dtype
   }
   hipStream_t s = (hipStream_t)stream;
   HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(ws_acquire(c, s));
   const mi_clip_arch& a = c->a;
   const int W = a.vision_width, E = a.embed_dim, S = c->S_v, R = a.image_resolution, P = a.vision_patch_size;
   const int G2 = c->G * c->G;
@@ -572,6 +595,7 @@ int mi_clip_encode_image(mi_clip* c, const void* pixels, int64_t B, int in_dtype
     HIP_TRY(gemm_bf16(gargs(c->cls_ln, W, c->vproj_t, W, nullptr, c->y, E, nb, E, W), EPI_F32, s));
     HIP_TRY(finalize_rows(c->y, (char*)out + c0 * E * dtype_size(out_dtype), out_dtype, nb, E, l2_normalize, s));
   }
+  HIP_TRY(ws_release(c, s));
   return MI_OK;
 }
 
@@ -586,6 +610,7 @@ int mi_clip_encode_text(mi_clip* c, const int32_t* tokens, int64_t Q, void* out,
   }
   hipStream_t s = (hipStream_t)stream;
   HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(ws_acquire(c, s));
   const mi_clip_arch& a = c->a;
   const int W = a.text_width, E = a.embed_dim, S = a.context_length;
   for (int64_t c0 = 0; c0 < Q; c0 += c->txt_chunk) {
@@ -598,6 +623,7 @@ int mi_clip_encode_text(mi_clip* c, const int32_t* tokens, int64_t Q, void* out,
     HIP_TRY(gemm_bf16(gargs(c->cls_ln, W, c->tproj_t, W, nullptr, c->y, E, nq, E, W), EPI_F32, s));
     HIP_TRY(finalize_rows(c->y, (char*)out + c0 * E * dtype_size(out_dtype), out_dtype, nq, E, l2_normalize, s));
   }
+  HIP_TRY(ws_release(c, s));
   return MI_OK;
 }
 

@@ -994,6 +994,7 @@ static hipError_t launch_stage1(dim3 grid, size_t lds, hipStream_t s, const void
 hipError_t rank_merge(const float* cs, const int64_t* ci, int64_t Q, int64_t C, int k, int nan_first, float* out_s,
                       int64_t* out_i, hipStream_t s) {
   if (Q <= 0) return hipSuccess;
+  // (64 / 128 threads per query measured slower at C = 2560-4096: scripts/merge_micro.py)
   if (kc_for(k) == 16)
     hipLaunchKernelGGL((rank_merge_kernel<16, 256>), dim3((unsigned)Q), dim3(256), 0, s, cs, ci, C, k, nan_first,
                        out_s, out_i);

@@ -183,3 +183,27 @@ def test_clip_dropin_surface(gpu):
     assert e.shape == (128,) and np.isfinite(e).all()
     li, lt = model(x, torch.from_numpy(np.zeros((1, 77), np.int32)))
     assert li.shape == (1, 1) and lt.shape == (1, 1)
+
+
+def test_context_on_two_streams(gpu):
+    """One context used from two torch streams back to back (the Flask
+    threads' case, SURVEY.md §8(b) threading): the second call waits for the
+    event recorded after the first call's kernels before reusing the shared
+    workspace, so results equal the single-stream ones."""
+    import torch
+    from miclip import weights
+    m = _model("test-small", gpu, image_chunk=4, text_chunk=2)
+    cfg = m.cfg
+    p1 = torch.from_numpy(weights.synthetic_pixels(8, cfg.image_resolution, seed=11)).to(gpu)
+    p2 = torch.from_numpy(weights.synthetic_pixels(8, cfg.image_resolution, seed=12)).to(gpu)
+    r1 = m.encode_image(p1).clone()
+    r2 = m.encode_image(p2).clone()
+    torch.cuda.synchronize()
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    for _ in range(3):
+        with torch.cuda.stream(s1):
+            a = m.encode_image(p1)
+        with torch.cuda.stream(s2):
+            b = m.encode_image(p2)
+        torch.cuda.synchronize()
+        assert torch.equal(a, r1) and torch.equal(b, r2)
