@@ -113,7 +113,7 @@ __global__ __launch_bounds__(64 * NW) void rank_stream(const void* __restrict__ 
   uint32_t* tau = (uint32_t*)(nrm_all + NW * 32);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
-  const int64_t q0 = (int64_t)blockIdx.y * RQ;
+  const int64_t q0 = (int64_t)QB * RQ;
 
   for (int64_t e = tid; e < RQ * D; e += NT) {
     const int qq = (int)(e / D);
@@ -123,7 +123,7 @@ __global__ __launch_bounds__(64 * NW) void rank_stream(const void* __restrict__ 
   if (tid < RQ) tau[tid] = 0u;
   __syncthreads();
 
-  const int64_t r_begin = (int64_t)blockIdx.x * rows_per_wg;
+  const int64_t r_begin = (int64_t)RB * rows_per_wg;
   const int64_t r_end = min(N, r_begin + rows_per_wg);
   float* nrm = nrm_all + wave * 32;
   const int64_t ntw = (r_end - r_begin + 31) / 32;
@@ -235,8 +235,8 @@ __global__ __launch_bounds__(64 * NW) void rank_stream(const void* __restrict__ 
     int pos[2 * NW];
 #pragma unroll
     for (int l = 0; l < 2 * NW; ++l) pos[l] = 0;
-    float* os = ws_s + (q0 + tid) * C + (int64_t)blockIdx.x * k;
-    int64_t* oi = ws_i + (q0 + tid) * C + (int64_t)blockIdx.x * k;
+    float* os = ws_s + (q0 + tid) * C + (int64_t)RB * k;
+    int64_t* oi = ws_i + (q0 + tid) * C + (int64_t)RB * k;
     for (int o = 0; o < k; ++o) {
       uint32_t bk = 0u;
       int32_t bi = INT_MAX;
@@ -308,7 +308,7 @@ __global__ __launch_bounds__(256) void rank_reg(const float* __restrict__ corpus
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, h = lane >> 5;
-  const int64_t q0 = (int64_t)blockIdx.y * RQ;
+  const int64_t q0 = (int64_t)QB * RQ;
   const bool qvalid = q0 + r < Q;
 
   // queries -> registers (zeros past Q)
@@ -330,13 +330,13 @@ __global__ __launch_bounds__(256) void rank_reg(const float* __restrict__ corpus
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  const int G = gridDim.x;
-  const int64_t r_begin = ILV ? 0 : (int64_t)blockIdx.x * rows_per_wg;
+  const int G = NRB;
+  const int64_t r_begin = ILV ? 0 : (int64_t)RB * rows_per_wg;
   const int64_t r_end = ILV ? N : min(N, r_begin + rows_per_wg);
   const int nrows = (int)(r_end - r_begin);
   const int ntw = (nrows + 31) / 32;
   // ILV: tiles (t * NW + wave) * G + blockIdx.x < ntw
-  const int sid = ILV ? wave * G + (int)blockIdx.x : wave;
+  const int sid = ILV ? wave * G + (int)RB : wave;
   const int sstep = ILV ? NW * G : NW;
   const int my_tiles = ntw > sid ? (ntw - 1 - sid) / sstep + 1 : 0;
   float* nrm = nrm_all + wave * 32;
@@ -480,8 +480,8 @@ __global__ __launch_bounds__(256) void rank_reg(const float* __restrict__ corpus
     int pos[2 * NW];
 #pragma unroll
     for (int l = 0; l < 2 * NW; ++l) pos[l] = 0;
-    float* os = ws_s + (q0 + tid) * C + (int64_t)blockIdx.x * k;
-    int64_t* oi = ws_i + (q0 + tid) * C + (int64_t)blockIdx.x * k;
+    float* os = ws_s + (q0 + tid) * C + (int64_t)RB * k;
+    int64_t* oi = ws_i + (q0 + tid) * C + (int64_t)RB * k;
     for (int o = 0; o < k; ++o) {
       uint32_t bk = 0u;
       int32_t bi = INT_MAX;
@@ -521,7 +521,7 @@ __global__ __launch_bounds__(256) void rank_stage1(const void* __restrict__ corp
   float* Ts = (float*)smem;
   float* nrm_all = Ts + RQ * ts_stride;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int64_t q0 = (int64_t)blockIdx.y * RQ;
+  const int64_t q0 = (int64_t)QB * RQ;
 
   for (int64_t e = tid; e < RQ * D; e += 256) {
     const int qq = (int)(e / D);
@@ -530,7 +530,7 @@ __global__ __launch_bounds__(256) void rank_stage1(const void* __restrict__ corp
   }
   __syncthreads();
 
-  const int64_t r_begin = (int64_t)blockIdx.x * rows_per_wg;
+  const int64_t r_begin = (int64_t)RB * rows_per_wg;
   const int64_t r_end = min(N, r_begin + rows_per_wg);
   float* nrm = nrm_all + wave * 32;
 
@@ -571,8 +571,8 @@ __global__ __launch_bounds__(256) void rank_stage1(const void* __restrict__ corp
     int pos[8];
 #pragma unroll
     for (int l = 0; l < 8; ++l) pos[l] = 0;
-    float* os = ws_s + (q0 + tid) * C + (int64_t)blockIdx.x * k;
-    int64_t* oi = ws_i + (q0 + tid) * C + (int64_t)blockIdx.x * k;
+    float* os = ws_s + (q0 + tid) * C + (int64_t)RB * k;
+    int64_t* oi = ws_i + (q0 + tid) * C + (int64_t)RB * k;
     for (int o = 0; o < k; ++o) {
       uint32_t bk = 0u;
       int32_t bi = INT_MAX;
@@ -994,7 +994,7 @@ static hipError_t launch_stage1(dim3 grid, size_t lds, hipStream_t s, const void
 hipError_t rank_merge(const float* cs, const int64_t* ci, int64_t Q, int64_t C, int k, int nan_first, float* out_s,
                       int64_t* out_i, hipStream_t s) {
   if (Q <= 0) return hipSuccess;
-  // (64 / 128 threads per query measured slower at C = 2560-4096: scripts/merge_micro.py)
+  // (64 / 128 threads per query measured slower at C = 2560-4096, Q = 1-1000)
   if (kc_for(k) == 16)
     hipLaunchKernelGGL((rank_merge_kernel<16, 256>), dim3((unsigned)Q), dim3(256), 0, s, cs, ci, C, k, nan_first,
                        out_s, out_i);
@@ -1033,7 +1033,7 @@ static hipError_t launch_reg(int64_t N, const float* corpus, const float* q, int
                  : (pp ? rank_reg<D, 8, 6, false, false, true> : rank_reg<D, 8, 6>);
   hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
-  const dim3 grid((unsigned)nwg, (unsigned)((Q + RQ - 1) / RQ));
+  const dim3 grid((unsigned)((Q + RQ - 1) / RQ), (unsigned)nwg);   // (query blocks, row blocks): RB / QB
   hipLaunchKernelGGL(fn, grid, dim3(256), lds, s, corpus, N, q, Q, k, rpw, nm, nf, base, ws_s, ws_i, C);
   return hipGetLastError();
 }
@@ -1059,7 +1059,7 @@ hipError_t rank_topk(const void* corpus, int64_t N, int64_t D, int dt, const flo
   const int64_t C = nwg * k;
   float* ws_s = (float*)ws;
   int64_t* ws_i = (int64_t*)((char*)ws + (size_t)(Q * nch * k) * sizeof(float));
-  const dim3 grid((unsigned)nwg, (unsigned)((Q + RQ - 1) / RQ));
+  const dim3 grid((unsigned)((Q + RQ - 1) / RQ), (unsigned)nwg);   // (query blocks, row blocks): RB / QB
   const int KC = kc_for(k);
   // streaming kernel for k <= 16 (KC = 16 lists stay in registers); 8 or 12
   // waves per workgroup (MICLIP_RANK_NW A/B), one workgroup per CU either way

@@ -7,6 +7,14 @@
 
 #include "common.hpp"
 
+// Row block / query block of a ranking workgroup.  The grid is (query blocks,
+// row blocks): the workgroups that share a row range are dispatched back to
+// back, so with Q > 32 a range is read from HBM once and by the other query
+// blocks from L2 / the Infinity Cache instead of once per query block.
+#define RB ((int)blockIdx.y)
+#define QB ((int)blockIdx.x)
+#define NRB ((int)gridDim.y)
+
 namespace miclip {
 namespace rankk {
 

@@ -102,7 +102,7 @@ __global__ __launch_bounds__(256) void rank_mirror_kernel(const uint16_t* __rest
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, h = lane >> 5;
-  const int64_t q0 = (int64_t)blockIdx.y * MQ;
+  const int64_t q0 = (int64_t)QB * MQ;
   const bool qvalid = q0 + r < Q;
 
   // queries -> fp16 B fragments: step s holds k = 16 s + 8 h + e (e = 0..7) of query r
@@ -127,12 +127,12 @@ __global__ __launch_bounds__(256) void rank_mirror_kernel(const uint16_t* __rest
   __syncthreads();
 
   // tile t of this wave: 32-row tile sid + t * sstep of rows [r_begin, r_end)
-  const int G = gridDim.x;
-  const int64_t r_begin = ILV ? 0 : (int64_t)blockIdx.x * rows_per_wg;
+  const int G = NRB;
+  const int64_t r_begin = ILV ? 0 : (int64_t)RB * rows_per_wg;
   const int64_t r_end = ILV ? N : min(N, r_begin + rows_per_wg);
   const int64_t nrows = r_end - r_begin;
   const int ntw = (int)((nrows + 31) / 32);
-  const int sid = ILV ? wave * G + (int)blockIdx.x : wave, sstep = ILV ? NW * G : NW;
+  const int sid = ILV ? wave * G + (int)RB : wave, sstep = ILV ? NW * G : NW;
   const int my_tiles = ntw > sid ? (ntw - 1 - sid) / sstep + 1 : 0;
   char* wring = ring + wave * NB * SLOT;
 
@@ -261,8 +261,8 @@ __global__ __launch_bounds__(256) void rank_mirror_kernel(const uint16_t* __rest
     int pos[2 * NW];
 #pragma unroll
     for (int l = 0; l < 2 * NW; ++l) pos[l] = 0;
-    float* os = ws_s + (q0 + tid) * C + (int64_t)blockIdx.x * k;
-    int64_t* oi = ws_i + (q0 + tid) * C + (int64_t)blockIdx.x * k;
+    float* os = ws_s + (q0 + tid) * C + (int64_t)RB * k;
+    int64_t* oi = ws_i + (q0 + tid) * C + (int64_t)RB * k;
     for (int o = 0; o < k; ++o) {
       uint32_t bk = 0u;
       int32_t bi = INT_MAX;
@@ -423,7 +423,7 @@ static hipError_t launch_mirror(const uint16_t* mirror, int64_t N, const float* 
             : v == 3 ? rank_mirror_kernel<D, SPLIT, true> : rank_mirror_kernel<D, SPLIT>;
   hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
-  const dim3 grid((unsigned)nwg, (unsigned)((Q + MQ - 1) / MQ));
+  const dim3 grid((unsigned)((Q + MQ - 1) / MQ), (unsigned)nwg);   // (query blocks, row blocks): RB / QB
   hipLaunchKernelGGL(fn, grid, dim3(256), lds, s, mirror, N, q, Q, kc, rpw, nf, ws_s, ws_i, C);
   return hipGetLastError();
 }
