@@ -138,16 +138,17 @@ def pmc_traffic(shape):
     """HBM bytes per launch of the GEMM at `shape` [M, N, K] from the newest
     committed PMC summary (profiles/*_gemm_traffic.json, made by
     scripts/gpu_traffic.sh + scripts/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE,
-    the gfx950 corrections of MI355X_MICROARCH.md "HBM").  None if absent."""
+    the gfx950 corrections of MI355X_MICROARCH.md "HBM"), with the MFMA-busy
+    fraction of the same summary's GRBM/SQ pass.  None if absent."""
     import glob
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_gemm_traffic.json")), reverse=True):
         try:
             for v in json.load(open(f)).values():
                 if list(v["shape"]) == list(shape):
-                    return v["traffic_bytes"], os.path.relpath(f, ROOT)
+                    return v["traffic_bytes"], os.path.relpath(f, ROOT), v.get("mfma_busy")
         except (OSError, ValueError, KeyError):
             continue
-    return None, None
+    return None, None, None
 
 
 def preprocess_timing(dev, n_px, B=256, H=720, W=1280, reps=10):
@@ -173,7 +174,7 @@ def preprocess_timing(dev, n_px, B=256, H=720, W=1280, reps=10):
             "gbs": round(B * H * W * 3 / us / 1e3, 1), "shape": [B, H, W, 3]}
 
 
-def jpeg_ingest_timing(dev, n_px, B=512, threads=16):
+def jpeg_ingest_timing(dev, n_px, B=2048, threads=16):
     """Frame ingest from JPEG bytes in host memory to preprocessed [B,3,n,n]
     bf16 tensors: the reference's 16 real 1280x720
     frames (tests/golden/ref_frames) repeated to B.  GPU path: header parse +
@@ -525,7 +526,7 @@ def main():
             fl = 2.0 * M * 4 * cfg.vision_width * cfg.vision_width
             ach = fl / (dom["us"] * 1e-6) / 1e12
             shape = [M, 4 * cfg.vision_width, cfg.vision_width]
-            traffic, tsrc = pmc_traffic(shape)
+            traffic, tsrc, busy = pmc_traffic(shape)
             fp8 = args.weights == "fp8"
             peak = FP8_PEAK_TFLOPS if fp8 else BF16_PEAK_TFLOPS
             eb = 1 if fp8 else 2            # operand element bytes (fp8 adds 1/64 B of scales per element)
@@ -535,6 +536,7 @@ def main():
                     "achieved": round(ach, 1), "peak": peak, "unit": "TFLOP/s",
                     "frac": round(ach / peak, 4), "traffic": None if fp8 else traffic,
                     "traffic_source": None if fp8 else tsrc,
+                    "mfma_busy_pmc": None if fp8 else busy,
                     "algorithmic_bytes": int(eb * (1 + fp8 / 64) * (M * cfg.vision_width + 4 * cfg.vision_width ** 2)
                                              + 2 * M * 4 * cfg.vision_width),
                     "flops_per_launch": fl, "launch_shape": [M, 4 * cfg.vision_width, cfg.vision_width],

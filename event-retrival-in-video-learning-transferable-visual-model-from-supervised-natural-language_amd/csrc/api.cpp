@@ -844,9 +844,10 @@ size_t mi_jpeg_workspace_bytes(const int32_t* geom, int32_t B) {
 }
 
 int mi_jpeg_decode(const uint8_t* data, const int64_t* seg_off, const int64_t* seg_end, const void* huff,
-                   const uint16_t* qtab, const int32_t* geom, int32_t B, uint8_t* out_rgb, void* workspace,
-                   size_t workspace_bytes, void* stream) {
+                   const int32_t* huff_idx, int32_t nsets, const uint16_t* qtab, const int32_t* geom, int32_t B,
+                   uint8_t* out_rgb, void* workspace, size_t workspace_bytes, void* stream) {
   if (!geom || B < 0) return fail(MI_ERR_ARG, "mi_jpeg_decode: bad arguments");
+  if (huff_idx && nsets < 1) return fail(MI_ERR_ARG, "mi_jpeg_decode: huff_idx needs nsets >= 1");
   if (B == 0) return MI_OK;
   if (!data || !seg_off || !seg_end || !huff || !qtab || !out_rgb) return fail(MI_ERR_ARG, "mi_jpeg_decode: null pointer");
   const int W = geom[0], H = geom[1], nc = geom[2], ri = geom[3], nseg = geom[4];
@@ -866,7 +867,7 @@ int mi_jpeg_decode(const uint8_t* data, const int64_t* seg_off, const int64_t* s
   const size_t need = jpeg_workspace_bytes(geom, B);
   if (!workspace || workspace_bytes < need)
     return fail(MI_ERR_ARG, "mi_jpeg_decode: workspace too small (%zu < %zu)", workspace_bytes, need);
-  HIP_TRY(jpeg_decode(data, seg_off, seg_end, huff, qtab, geom, B, out_rgb, workspace, workspace_bytes,
+  HIP_TRY(jpeg_decode(data, seg_off, seg_end, huff, huff_idx, nsets, qtab, geom, B, out_rgb, workspace, workspace_bytes,
                       (hipStream_t)stream));
   return MI_OK;
 }

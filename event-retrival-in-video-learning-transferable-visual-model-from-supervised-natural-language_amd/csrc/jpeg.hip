@@ -5,8 +5,9 @@
 // its defaults (JDCT_ISLOW, fancy upsampling, JCS_RGB output), so the three
 // kernels below restate those integer algorithms:
 //   jpeg_entropy_kernel  one lane per frame (or per restart interval):
-//                        sequential Huffman decode of the interleaved scan,
-//                        DC prediction, de-zigzag -> int16 coefficients;
+//                        sequential Huffman decode of the interleaved scan
+//                        (tables in LDS, stream words prefetched), DC
+//                        prediction, de-zigzag -> int16 coefficients;
 //   jpeg_idct_kernel     one thread per 8x8 block: dequantise + the
 //                        LL&M integer IDCT of jidctint.c (CONST_BITS 13,
 //                        PASS1_BITS 2) with its 1024-entry range-limit
@@ -23,6 +24,7 @@
 #include <cstdint>
 
 #include "internal.hpp"
+#include "miclip.h"
 
 namespace miclip {
 namespace {
@@ -39,32 +41,151 @@ __constant__ uint8_t kZigzag[80] = {
 //   maxcode[18]: largest code of each length (-1 none; [17] sentinel)
 //   valoff[18]: values index offset per length (value = vals[code + valoff[l]])
 //   vals[256]
+//   l2base, l2n, look2[1024]: (length << 8) | symbol for the 16-bit windows
+//     [l2base, l2base + l2n) of the 10..16-bit codes (0: corrupt); l2n = 0: walk maxcode
 struct JpegHuff {
   uint16_t look[512];
   int32_t maxcode[18];
   int32_t valoff[18];
   uint8_t vals[256];
+  int32_t l2base, l2n;
+  uint16_t look2[1024];
 };
+static_assert(sizeof(JpegHuff) == MI_JPEG_HUFF_BYTES, "table layout shared with miclip/jpeg.py");
 
+// Entropy-coded bytes of one segment as a left-aligned bit buffer.  A lane
+// decodes its frame serially, and a wave waits on a load for all its lanes
+// (and, vmcnt being in order, for every coefficient store issued before it).
+// So raw bytes come from a per-lane queue of up to 64 bytes in registers that
+// the WHOLE wave tops up at once (refill(): every lane loads as many aligned
+// 16-byte blocks as fit, all issued before the one wait) when any lane runs
+// low: one memory wait per ~40 bytes of the fastest lane instead of one per
+// byte.  Un-stuffing happens in registers; at a marker or the segment end it
+// feeds zeros (libjpeg's "insufficient data" behaviour).
 struct BitReader {
-  const uint8_t* p;
-  const uint8_t* end;
-  uint64_t buf;     // left-aligned bit buffer
+  static constexpr int QW = 16, QB = 4 * QW;   // queue: 16 dwords = 64 bytes
+  static constexpr int LOW = 12;   // a trip reads <= 9 raw bytes (<= 4 data bytes, stuffed, + a marker peek)
+  // (the queue then always holds the 4 bytes the dword path reads when rem >= 4)
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4* fp;         // next aligned 16-byte block to load
+  const u32x4* flast;      // last block holding segment bytes (loads clamp to it)
+  uint32_t q[QW];          // raw byte queue, stream order from q[0]'s top byte
+  int nq;                  // bytes in the queue
+  int64_t rem;             // unread segment bytes
+  uint64_t buf;            // left-aligned bit buffer
   int nbits;
-  bool marker;      // hit a marker: feed zeros (libjpeg "insufficient data")
+  bool marker;             // hit a marker: feed zeros
 
+  __device__ __forceinline__ u32x4 load_block() {
+    typedef __attribute__((address_space(1))) const u32x4 gu4;
+    const u32x4 v = *(gu4*)(fp < flast ? fp : flast);
+    ++fp;
+    return v;
+  }
+  // append 16 bytes (memory order) at byte position nq (nq <= QB - 16)
+  __device__ __forceinline__ void append(u32x4 v) {
+    const uint32_t a[4] = {__builtin_bswap32(v[0]), __builtin_bswap32(v[1]), __builtin_bswap32(v[2]),
+                           __builtin_bswap32(v[3])};
+    const int ws = nq >> 2, bs = (nq & 3) * 8;
+    uint32_t t[5];
+    t[0] = a[0] >> bs;
+#pragma unroll
+    for (int j = 1; j < 4; ++j) t[j] = (a[j] >> bs) | (bs ? a[j - 1] << (32 - bs) : 0u);
+    t[4] = bs ? a[3] << (32 - bs) : 0u;
+#pragma unroll
+    for (int i = 0; i < QW; ++i) {
+      uint32_t x = 0;
+#pragma unroll
+      for (int j = 0; j < 5; ++j)
+        if (i - j >= 0 && i - j <= QW - 4) x |= (ws == i - j) ? t[j] : 0u;
+      q[i] |= x;
+    }
+    nq += 16;
+  }
+  __device__ __forceinline__ void init(const uint8_t* p, const uint8_t* end) {
+    buf = 0;
+    nbits = 0;
+    marker = false;
+    rem = end - p;
+#pragma unroll
+    for (int i = 0; i < QW; ++i) q[i] = 0;
+    nq = 0;
+    if (rem <= 0) {
+      rem = 0;
+      fp = flast = nullptr;
+      return;
+    }
+    const int sh = (int)((uintptr_t)p & 15);
+    fp = (const u32x4*)((uintptr_t)p - sh);
+    flast = (const u32x4*)(((uintptr_t)end - 1) & ~(uintptr_t)15);
+    const u32x4 v0 = load_block(), v1 = load_block();
+    append(v0);
+    append(v1);
+    // drop the sh bytes before p: whole dwords, then the byte remainder
+    const int dw = sh >> 2, bs = (sh & 3) * 8;
+#pragma unroll
+    for (int i = 0; i < QW; ++i) {
+      uint32_t x = q[i];
+#pragma unroll
+      for (int d = 1; d < 4; ++d) x = (dw == d) ? (i + d < QW ? q[i + d] : 0u) : x;
+      q[i] = x;   // in place is safe: q[i + d] is read before it is written (increasing i)
+    }
+    if (bs) {
+#pragma unroll
+      for (int i = 0; i < QW; ++i) q[i] = (q[i] << bs) | (i + 1 < QW ? q[i + 1] >> (32 - bs) : 0u);
+    }
+    nq = 32 - sh;
+  }
+  __device__ __forceinline__ bool low() const { return nq < LOW && rem > nq; }
+  __device__ __forceinline__ void refill() {
+    // the loads first (independent), then the appends: one wait for all
+    // (all three loads unconditional and waited for together: a load left
+    // pending on some path makes the compiler wait inside the main loop)
+    const int n = rem > nq ? min((QB - nq) >> 4, 3) : 0;
+    const u32x4* f0 = fp;
+    const u32x4 v0 = load_block(), v1 = load_block(), v2 = load_block();
+    fp = f0 + n;
+    __builtin_amdgcn_s_waitcnt(0);
+    if (n > 0) append(v0);
+    if (n > 1) append(v1);
+    if (n > 2) append(v2);
+  }
+  __device__ __forceinline__ uint32_t next_byte() {
+    const uint32_t c = q[0] >> 24;
+#pragma unroll
+    for (int i = 0; i + 1 < QW; ++i) q[i] = (q[i] << 8) | (q[i + 1] >> 24);
+    q[QW - 1] <<= 8;
+    --nq;
+    --rem;
+    return c;
+  }
+  // Ensure >= 32 buffered bits (a symbol takes <= 16 + 15).  Usual case: the
+  // next 4 raw bytes hold no 0xFF and go in as one dword; otherwise byte by
+  // byte with un-stuffing.
   __device__ __forceinline__ void fill() {
-    while (nbits <= 56) {
+    if (nbits >= 32) return;
+    const uint32_t d = q[0], nd = ~d;
+    const bool ff = ((nd - 0x01010101u) & ~nd & 0x80808080u) != 0u;
+    if (!ff && !marker && rem >= 4) {
+      buf |= (uint64_t)d << (32 - nbits);
+      nbits += 32;
+#pragma unroll
+      for (int i = 0; i + 1 < QW; ++i) q[i] = q[i + 1];
+      q[QW - 1] = 0;
+      nq -= 4;
+      rem -= 4;
+      return;
+    }
+    while (nbits < 32) {
       uint32_t c = 0;
-      if (!marker && p < end) {
-        c = *p++;
+      if (!marker && rem > 0) {
+        c = next_byte();
         if (c == 0xFF) {
-          const uint32_t n = p < end ? *p : 0xD9;
+          const uint32_t n = rem > 0 ? (q[0] >> 24) : 0xD9;
           if (n == 0x00) {
-            ++p;                 // stuffed zero byte
+            next_byte();         // stuffed zero byte
           } else {
-            marker = true;       // a marker: stop consuming, zeros from here
-            --p;
+            marker = true;       // a marker: zeros from here
             c = 0;
           }
         }
@@ -78,22 +199,22 @@ struct BitReader {
     buf <<= n;
     nbits -= n;
   }
-  __device__ __forceinline__ uint32_t get(int n) {
-    if (n == 0) return 0;
-    const uint32_t v = peek(n);
-    skip(n);
-    return v;
-  }
 };
 
+// Decode one symbol (after fill(): >= 32 bits buffered, a code takes <= 16)
 __device__ __forceinline__ int huff_decode(BitReader& br, const JpegHuff* __restrict__ t) {
-  br.fill();
   const uint32_t lk = t->look[br.peek(9)];
   if (lk) {
     br.skip(lk >> 8);
     return lk & 0xFF;
   }
-  // longer code: libjpeg jpeg_huff_decode (lengths 10..16)
+  // longer code: one second-level lookup, or libjpeg jpeg_huff_decode's walk (lengths 10..16)
+  const int i2 = (int)br.peek(16) - t->l2base;
+  if ((unsigned)i2 < (unsigned)t->l2n) {
+    const uint32_t l2 = t->look2[i2];
+    br.skip(l2 ? (int)(l2 >> 8) : 16);   // 0: corrupt data, libjpeg returns 0 (and warns)
+    return l2 & 0xFF;
+  }
   int l = 10;
   uint32_t code = br.peek(10);
   while (l <= 16 && (int32_t)code > t->maxcode[l]) {
@@ -113,8 +234,9 @@ __device__ __forceinline__ int extend(uint32_t v, int s) {
 }
 
 // Per frame f: entropy-coded bytes at data + off[f] (len[f] bytes), tables at
-// huff[f * 4 + {dc0, ac0, dc1, ac1}], coefficient output coef + f * blocks_per_frame * 64
-// (zeroed by the caller; only nonzero coefficients are written).
+// huff[set * 4 + {dc0, ac0, dc1, ac1}] with set = huff_idx[f] (f without
+// huff_idx), coefficient output coef + f * blocks_per_frame * 64 (zeroed by the
+// caller; only nonzero coefficients are written).
 // Geometry (all frames of a launch share it): ncomp components, component c with
 // sampling (hs[c], vs[c]), block grid width bw[c] (blocks), block base cbase[c]
 // (blocks, within the frame), table selectors dcsel[c] / acsel[c]; MCU grid mcux x mcuy;
@@ -127,56 +249,106 @@ struct JpegGeom {
   int64_t blocks_per_frame;
 };
 
+template <typename T>
+__device__ __forceinline__ T pick3(int c, T a, T b, T d) {
+  return c == 0 ? a : (c == 1 ? b : d);
+}
+
+// One symbol per loop trip (DC or AC of whichever block the lane is in), so
+// lanes of a wave decoding different frames never wait on each other's block
+// structure: a wave runs as many trips as its longest segment has symbols.
+// LDS_T: the launch's table sets (nsets <= JPEG_LDS_SETS) are staged in LDS.
+template <bool LDS_T>
 __global__ __launch_bounds__(64) void jpeg_entropy_kernel(const uint8_t* __restrict__ data,
                                                           const int64_t* __restrict__ seg_off,
                                                           const int64_t* __restrict__ seg_end,
-                                                          const JpegHuff* __restrict__ huff, JpegGeom g, int nframes,
-                                                          int16_t* __restrict__ coef) {
+                                                          const JpegHuff* __restrict__ huff,
+                                                          const int32_t* __restrict__ huff_idx, int nsets,
+                                                          JpegGeom g, int nframes, int16_t* __restrict__ coef) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  JpegHuff* sh = (JpegHuff*)smem;
+  uint8_t* zz = (uint8_t*)smem + (LDS_T ? nsets * 4 * (int)sizeof(JpegHuff) : 0);
+  if (LDS_T) {
+    const uint32_t* src = (const uint32_t*)huff;
+    uint32_t* dst = (uint32_t*)smem;
+    const int nw = nsets * 4 * (int)sizeof(JpegHuff) / 4;
+    for (int i = threadIdx.x; i < nw; i += 64) dst[i] = src[i];
+  }
+  for (int i = threadIdx.x; i < 80; i += 64) zz[i] = kZigzag[i];
+  __syncthreads();
   const int64_t lane = (int64_t)blockIdx.x * 64 + threadIdx.x;
   if (lane >= (int64_t)nframes * g.nseg) return;
   const int f = (int)(lane / g.nseg), s = (int)(lane % g.nseg);
   BitReader br;
-  br.p = data + seg_off[lane];
-  br.end = data + seg_end[lane];
-  br.buf = 0;
-  br.nbits = 0;
-  br.marker = false;
-  const JpegHuff* T = huff + (int64_t)f * 4;
+  br.init(data + seg_off[lane], data + seg_end[lane]);
+  const int set = huff_idx ? huff_idx[f] : f;
+  const JpegHuff* T = (LDS_T ? (const JpegHuff*)sh : huff) + (int64_t)set * 4;
   int16_t* out = coef + (int64_t)f * g.blocks_per_frame * 64;
   const int total = g.mcux * g.mcuy;
-  const int m0 = g.ri ? s * g.ri : 0;
-  const int m1 = g.ri ? min(total, m0 + g.ri) : total;
-  int pred[3] = {0, 0, 0};
-  for (int m = m0; m < m1; ++m) {
-    const int mx = m % g.mcux, my = m / g.mcux;
-    for (int c = 0; c < g.ncomp; ++c) {
-      const JpegHuff* dc = T + g.dcsel[c] * 2;
-      const JpegHuff* ac = T + g.acsel[c] * 2 + 1;
-      for (int v = 0; v < g.vs[c]; ++v)
-        for (int h = 0; h < g.hs[c]; ++h) {
-          int16_t* blk = out + (g.cbase[c] + (int64_t)(my * g.vs[c] + v) * g.bw[c] + (mx * g.hs[c] + h)) * 64;
-          int t = huff_decode(br, dc);
-          int diff = 0;
-          if (t) {
-            br.fill();
-            diff = extend(br.get(t), t);
-          }
-          pred[c] += diff;
-          blk[0] = (int16_t)pred[c];
-          for (int k = 1; k < 64;) {
-            const int rs = huff_decode(br, ac);
-            const int r = rs >> 4, sz = rs & 15;
-            if (sz) {
-              k += r;
-              br.fill();
-              blk[kZigzag[k]] = (int16_t)extend(br.get(sz), sz);
-              ++k;
-            } else {
-              if (r != 15) break;   // EOB
-              k += 16;
+  int m = g.ri ? s * g.ri : 0;
+  const int m1 = g.ri ? min(total, m + g.ri) : total;
+  int mx = m % g.mcux, my = m / g.mcux;
+  int c = 0, bv = 0, bh = 0, k = 0;
+  int p0 = 0, p1 = 0, p2 = 0;
+  const JpegHuff *d0 = T + g.dcsel[0] * 2, *a0 = T + g.acsel[0] * 2 + 1;
+  const JpegHuff *d1 = T + g.dcsel[1] * 2, *a1 = T + g.acsel[1] * 2 + 1;
+  const JpegHuff *d2 = T + g.dcsel[2] * 2, *a2 = T + g.acsel[2] * 2 + 1;
+  int hs_c = g.hs[0], vs_c = g.vs[0];
+  int16_t* blk = out + (g.cbase[0] + (int64_t)(my * vs_c) * g.bw[0] + mx * hs_c) * 64;
+  // Nothing may be in flight when the loop starts: a load still pending at the
+  // loop entry makes the compiler place a vmcnt(0) wait inside the loop body,
+  // which then drains every coefficient store on every trip.
+  __builtin_amdgcn_s_waitcnt(0);
+  while (m < m1) {
+    const JpegHuff* tp = k ? pick3(c, a0, a1, a2) : pick3(c, d0, d1, d2);
+    if (__any(br.low())) br.refill();   // one wave-wide load for every lane with room
+    br.fill();
+    const int sym = huff_decode(br, tp);
+    const int sz = sym & 15;   // DC: the size category (<= 15, host-checked)
+    const int r = k ? (sym >> 4) : 0;
+    const uint32_t bits = sz ? br.peek(sz) : 0u;
+    br.skip(sz);
+    const int val = sz ? extend(bits, sz) : 0;
+    bool endblk;
+    if (k == 0) {
+      const int pv = pick3(c, p0, p1, p2) + val;
+      p0 = c == 0 ? pv : p0;
+      p1 = c == 1 ? pv : p1;
+      p2 = c == 2 ? pv : p2;
+      blk[0] = (int16_t)pv;
+      k = 1;
+      endblk = false;
+    } else if (sz) {
+      k += r;
+      blk[zz[k]] = (int16_t)val;
+      ++k;
+      endblk = k >= 64;
+    } else if (r == 15) {
+      k += 16;
+      endblk = k >= 64;
+    } else {
+      endblk = true;   // EOB
+    }
+    if (endblk) {
+      k = 0;
+      if (++bh == hs_c) {
+        bh = 0;
+        if (++bv == vs_c) {
+          bv = 0;
+          if (++c == g.ncomp) {
+            c = 0;
+            ++m;
+            if (++mx == g.mcux) {
+              mx = 0;
+              ++my;
             }
           }
+          hs_c = pick3(c, g.hs[0], g.hs[1], g.hs[2]);
+          vs_c = pick3(c, g.vs[0], g.vs[1], g.vs[2]);
         }
+      }
+      const int bw_c = pick3(c, g.bw[0], g.bw[1], g.bw[2]), cb_c = pick3(c, g.cbase[0], g.cbase[1], g.cbase[2]);
+      blk = out + (cb_c + (int64_t)(my * vs_c + bv) * bw_c + (mx * hs_c + bh)) * 64;
     }
   }
 }
@@ -360,7 +532,7 @@ __global__ __launch_bounds__(256) void jpeg_color_kernel(const uint8_t* __restri
 
 // Host launch: see include/miclip.h mi_jpeg_decode for the argument contract.
 hipError_t jpeg_decode(const uint8_t* data, const int64_t* seg_off, const int64_t* seg_end, const void* huff,
-                       const uint16_t* qtab, const int32_t* geom, int nframes, uint8_t* out_rgb, void* ws,
+                       const int32_t* huff_idx, int nsets, const uint16_t* qtab, const int32_t* geom, int nframes, uint8_t* out_rgb, void* ws,
                        size_t ws_bytes, hipStream_t s) {
   // geom: [W, H, ncomp, ri, nseg, hs0, vs0, hs1, vs1, hs2, vs2, q0, q1, q2, dc0, dc1, dc2, ac0, ac1, ac2]
   const int W = geom[0], H = geom[1], ncomp = geom[2];
@@ -404,8 +576,13 @@ hipError_t jpeg_decode(const uint8_t* data, const int64_t* seg_off, const int64_
   hipError_t e = hipMemsetAsync(coef, 0, coef_bytes, s);
   if (e != hipSuccess) return e;
   const int64_t lanes = (int64_t)nframes * g.nseg;
-  hipLaunchKernelGGL(jpeg_entropy_kernel, dim3((unsigned)((lanes + 63) / 64)), dim3(64), 0, s, data, seg_off, seg_end,
-                     (const JpegHuff*)huff, g, nframes, coef);
+  const dim3 eg((unsigned)((lanes + 63) / 64));
+  if (huff_idx && nsets >= 1 && nsets <= JPEG_LDS_SETS)
+    hipLaunchKernelGGL(jpeg_entropy_kernel<true>, eg, dim3(64), nsets * 4 * sizeof(JpegHuff) + 80, s, data, seg_off,
+                       seg_end, (const JpegHuff*)huff, huff_idx, nsets, g, nframes, coef);
+  else
+    hipLaunchKernelGGL(jpeg_entropy_kernel<false>, eg, dim3(64), 80, s, data, seg_off, seg_end,
+                       (const JpegHuff*)huff, huff_idx, nsets, g, nframes, coef);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   const int64_t nb = (int64_t)nframes * blocks;

@@ -100,7 +100,7 @@ def lib():
         "mi_preprocess_workspace_bytes": (SZ, [I64, I32, I32, I32, ctypes.c_int]),
         "mi_preprocess_frames": (ctypes.c_int, [P, I64, I32, I32, I32, ctypes.c_int, P, ctypes.c_int, P, SZ, P]),
         "mi_jpeg_workspace_bytes": (SZ, [P, I32]),
-        "mi_jpeg_decode": (ctypes.c_int, [P, P, P, P, P, P, I32, P, P, SZ, P]),
+        "mi_jpeg_decode": (ctypes.c_int, [P, P, P, P, P, I32, P, P, I32, P, P, SZ, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

@@ -6,9 +6,11 @@ of the reference's frame ingest (``Backend/services/embedding_service.py:472-480
 The host reads each file's markers (DQT, SOF0/SOF1, DHT, DRI, SOS), builds the
 Huffman decode tables in libjpeg's derived form (9-bit look-ahead + maxcode /
 value offsets per code length), de-zigzags the quantisation tables, locates
-restart markers, and hands one batch per geometry to the device: the entropy
-decode runs one lane per frame (or per restart interval), the IDCT one thread
-per block, the upsampling + colour conversion one thread per pixel.
+restart markers, and hands one batch per geometry to the device with the
+Huffman tables deduplicated into sets (a video's frames share one): the entropy
+decode runs one lane per frame (or per restart interval) with the sets in LDS,
+the IDCT one thread per block, the upsampling + colour conversion one thread
+per pixel.
 
 Files the device path does not cover (progressive or arithmetic coding,
 12-bit samples, CMYK / Adobe-transform or 4-component images, sampling other
@@ -27,15 +29,33 @@ from . import _native as N
 ZIGZAG = np.array([0, 1, 8, 16, 9, 2, 3, 10, 17, 24, 32, 25, 18, 11, 4, 5, 12, 19, 26, 33, 40, 48, 41, 34, 27, 20,
                    13, 6, 7, 14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51, 58, 59,
                    52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63], dtype=np.int64)
-HUFF_BYTES = 1424
-_HUFF_DT = np.dtype([("look", "<u2", 512), ("maxcode", "<i4", 18), ("valoff", "<i4", 18), ("vals", "u1", 256)])
+HUFF_BYTES = 3480
+L2_MAX = 1024
+_HUFF_DT = np.dtype([("look", "<u2", 512), ("maxcode", "<i4", 18), ("valoff", "<i4", 18), ("vals", "u1", 256),
+                     ("l2base", "<i4"), ("l2n", "<i4"), ("look2", "<u2", L2_MAX)])
 assert _HUFF_DT.itemsize == HUFF_BYTES
+
+
+_HUFF_CACHE = {}
+
+
+def _huff_cached(bits, vals):
+    key = (bytes(bits), bytes(vals))
+    t = _HUFF_CACHE.get(key)
+    if t is None:
+        if len(_HUFF_CACHE) > 4096:
+            _HUFF_CACHE.clear()
+        t = _HUFF_CACHE[key] = build_huff(bits, vals)
+    return key, t
 
 
 def build_huff(bits, vals):
     """libjpeg jpeg_make_d_derived_tbl: canonical codes from the 16 length
     counts; 9-bit look-ahead entries (length << 8) | symbol; maxcode / value
-    offsets for the longer codes."""
+    offsets for the longer codes.  Codes of 10-16 bits are canonical-last, so
+    they and the invalid tail fill the 16-bit window range [l2base, 65536):
+    when that range has <= L2_MAX values, look2 maps each to (length << 8) |
+    symbol (0: corrupt), one LDS lookup instead of libjpeg's per-length walk."""
     t = np.zeros((), dtype=_HUFF_DT)
     t["maxcode"][:] = -1
     t["maxcode"][17] = 0x7FFFFFFF
@@ -54,6 +74,21 @@ def build_huff(bits, vals):
                 p += 1
             t["maxcode"][ln] = code - 1
         code <<= 1
+    code, p, first = 0, 0, None
+    longs = []
+    for ln in range(1, 17):
+        for _ in range(bits[ln - 1]):
+            if ln >= 10:
+                if first is None:
+                    first = code << (16 - ln)
+                longs.append((code << (16 - ln), 1 << (16 - ln), (ln << 8) | vals[p]))
+            code += 1
+            p += 1
+        code <<= 1
+    if first is not None and 65536 - first <= L2_MAX:
+        t["l2base"], t["l2n"] = first, 65536 - first
+        for lo, n, e in longs:
+            t["look2"][lo - first:lo - first + n] = e
     return t
 
 
@@ -162,6 +197,9 @@ def parse(buf: bytes) -> JpegHeader:
                     any((1, t) not in h.huff for t in h.acsel):
                 h.why = "missing table"
                 return h
+            if any(max(h.huff[(0, t)][1], default=0) > 15 for t in h.dcsel):
+                h.why = "DC table symbol > 15"     # libjpeg rejects the table (JERR_BAD_HUFF_TABLE)
+                return h
             if any(q > 3 for q in h.qsel) or h.width < 1 or h.height < 1:
                 h.why = "bad frame header"
                 return h
@@ -244,14 +282,22 @@ def decode_batch(bufs, device="cuda"):
         if not keep:
             continue
         B = len(keep)
-        data = np.frombuffer(bytearray(b"".join(chunks) + b"\xff\xd9" * 4), dtype=np.uint8)
-        huff = np.zeros((B, 4), dtype=_HUFF_DT)
+        data = np.frombuffer(bytearray(b"".join(chunks) + b"\xff\xd9" * 16), dtype=np.uint8)
+        # table sets deduplicated: frames of one encoder share one set, which
+        # the entropy kernel stages in LDS
+        sets, set_of, hidx = [], {}, np.zeros(B, np.int32)
         qt = np.zeros((B, 4, 64), dtype=np.uint16)
         for r, i in enumerate(keep):
             h = heads[i]
+            slots, tabs = [None] * 4, [None] * 4
             for (tc, th), (bits, vals) in h.huff.items():
                 if th <= 1:
-                    huff[r, th * 2 + tc] = build_huff(bits, vals)
+                    slots[th * 2 + tc], tabs[th * 2 + tc] = _huff_cached(bits, vals)
+            key = tuple(slots)
+            if key not in set_of:
+                set_of[key] = len(sets)
+                sets.append(tabs)
+            hidx[r] = set_of[key]
             for tq, q in h.qt.items():
                 if tq <= 3:
                     qt[r, tq] = q
@@ -269,14 +315,20 @@ def decode_batch(bufs, device="cuda"):
         d_data = torch.from_numpy(data).to(dev)
         d_off = torch.tensor(offs, dtype=torch.int64, device=dev)
         d_end = torch.tensor(ends, dtype=torch.int64, device=dev)
+        huff = np.zeros((len(sets), 4), dtype=_HUFF_DT)
+        for u, tabs in enumerate(sets):
+            for j, t in enumerate(tabs):
+                if t is not None:
+                    huff[u, j] = t
         d_huff = torch.from_numpy(huff.view(np.uint8).reshape(-1)).to(dev)
+        d_hidx = torch.from_numpy(hidx).to(dev)
         d_qt = torch.from_numpy(qt).to(dev)
         rgb = torch.empty(B, H, W, 3, dtype=torch.uint8, device=dev)
         gp = geom.ctypes.data
         nb = L.mi_jpeg_workspace_bytes(gp, B)
         ws = torch.empty(max(nb, 1), dtype=torch.uint8, device=dev)
         N.check(L.mi_jpeg_decode(d_data.data_ptr(), d_off.data_ptr(), d_end.data_ptr(), d_huff.data_ptr(),
-                                 d_qt.data_ptr(), gp, B, rgb.data_ptr(), ws.data_ptr(), nb,
+                                 d_hidx.data_ptr(), len(sets), d_qt.data_ptr(), gp, B, rgb.data_ptr(), ws.data_ptr(), nb,
                                  N.stream_ptr(dev)), "mi_jpeg_decode")
         for r, i in enumerate(keep):
             out[i] = rgb[r]

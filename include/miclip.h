@@ -206,10 +206,14 @@ int mi_preprocess_frames(const uint8_t* frames, int64_t B, int32_t H, int32_t W,
  * output bit-identical to Pillow (libjpeg ISLOW IDCT, fancy upsampling, JCS_RGB).
  * The caller (miclip/jpeg.py) parses headers and builds the tables; all pointers
  * are device memory:
- *   data      concatenated entropy-coded segments of all frames (bytes after SOS)
+ *   data      concatenated entropy-coded segments of all frames (bytes after SOS),
+ *             readable for 16 bytes past the last segment end (aligned 16-byte reads)
  *   seg_off / seg_end  [B * nseg] byte offsets of each restart segment (nseg = 1
  *             without restart markers); a segment ends at its RSTn / EOI marker
- *   huff      [B][4] decode tables {dc0, ac0, dc1, ac1}, MI_JPEG_HUFF_BYTES each
+ *   huff      [nsets][4] decode tables {dc0, ac0, dc1, ac1}, MI_JPEG_HUFF_BYTES each
+ *   huff_idx  [B] int32 table set of each frame, in [0, nsets) (frames of one
+ *             encoder share a set; up to 11 sets are staged in LDS), or NULL:
+ *             frame f uses set f (nsets ignored)
  *   qtab      [B][4][64] uint16 quantisation tables in natural order
  *   geom      host int32[20]: W, H, ncomp (1 or 3), restart interval (MCUs),
  *             nseg, (h, v) sampling per component, quant / dc / ac table
@@ -217,11 +221,11 @@ int mi_preprocess_frames(const uint8_t* frames, int64_t B, int32_t H, int32_t W,
  *   out_rgb   [B, H, W, 3] uint8
  * Supported: 8-bit, 1 component, or 3 components with chroma 1x1 and luma
  * 1x1 / 2x1 / 2x2. */
-#define MI_JPEG_HUFF_BYTES 1424
+#define MI_JPEG_HUFF_BYTES 3480
 size_t mi_jpeg_workspace_bytes(const int32_t* geom, int32_t B);
 int mi_jpeg_decode(const uint8_t* data, const int64_t* seg_off, const int64_t* seg_end, const void* huff,
-                   const uint16_t* qtab, const int32_t* geom, int32_t B, uint8_t* out_rgb, void* workspace,
-                   size_t workspace_bytes, void* stream);
+                   const int32_t* huff_idx, int32_t nsets, const uint16_t* qtab, const int32_t* geom, int32_t B,
+                   uint8_t* out_rgb, void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---- operator-level entry points (per-kernel parity tests) ----
  * mi_op_gemm: out = A[M,K] . W[N,K]^T (+bias) with epilogue

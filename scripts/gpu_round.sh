@@ -1,6 +1,7 @@
-# Round check on one GPU: every GPU test, smoke, PMC traffic of the four bench GEMMs
-# (FETCH_SIZE / WRITE_SIZE passes, written to profiles/ on the box so the bench line
-# picks them up), the bench line, and a rocprofv3 kernel trace of the bench.
+# Round check on one GPU: every GPU test, smoke, PMC traffic (FETCH_SIZE / WRITE_SIZE
+# passes) and MFMA busy (GRBM + SQ pass) of the four bench GEMMs, written to profiles/
+# on the box so the bench line picks them up, the bench line, and a rocprofv3 kernel
+# trace of the bench.
 # usage: TAG=r02_v2 bash scripts/gpu_round.sh
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 TAG=${TAG:-rXX}
@@ -14,6 +15,9 @@ for c in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 120 rocprofv3 --pmc $c --output-format csv -d gpurun_out/prof/$c -o run -- \
     python3 scripts/gemm_micro.py 1 fc500,qkv500,out500,proj500 > gpurun_out/prof/$c.log 2>&1 || exit $?
 done
+timeout -s KILL 120 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES \
+  --output-format csv -d gpurun_out/prof/MFMA -o run -- \
+  python3 scripts/gemm_micro.py 1 fc500,qkv500,out500,proj500 > gpurun_out/prof/MFMA.log 2>&1 || exit $?
 python3 scripts/pmc_traffic.py gpurun_out/prof fc500,qkv500,out500,proj500 gpurun_out/${TAG}_gemm_traffic.json || exit $?
 cp gpurun_out/${TAG}_gemm_traffic.json profiles/
 timeout -k 10 600 python bench.py ${BENCH_ARGS:---steps 20 --warmup 3} > gpurun_out/bench.log 2>&1 || exit $?

@@ -7,6 +7,12 @@ libmiclip kernels belongs to shapes[i // 4].  Units and gfx950 corrections
 of the bytes of a 16-B/lane streaming read (the LDS-DMA operand loads are that
 form), so it is doubled; WRITE_SIZE is exact for 16-B/lane streaming stores.
 
+With a third pass in <prof dir>/MFMA (`--kernel-trace --pmc GRBM_GUI_ACTIVE
+SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES`), each shape also gets its MFMA
+utilisation: SQ_VALU_MFMA_BUSY_CYCLES (cycles, summed over all SIMDs) over
+(GRBM_GUI_ACTIVE / 8 XCDs) x 1024 SIMDs, and the shader clock that pass ran at
+(GRBM_GUI_ACTIVE / 8 over the dispatch's duration in the kernel trace).
+
 usage: python scripts/pmc_traffic.py <prof dir> <shapes,comma> <out.json>
 """
 import csv
@@ -29,10 +35,37 @@ def per_dispatch(path):
     return [rows[d] for d in sorted(rows)]
 
 
+def mfma_pass(root):
+    d = os.path.join(root, "MFMA")
+    cnt = os.path.join(d, "run_counter_collection.csv")
+    if not os.path.exists(cnt):
+        return None
+    per = {}
+    for r in csv.DictReader(open(cnt)):
+        if "miclip" not in r["Kernel_Name"]:
+            continue
+        c = per.setdefault(int(r["Dispatch_Id"]), {})
+        c[r["Counter_Name"]] = c.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    dur = {}
+    kt = os.path.join(d, "run_kernel_trace.csv")
+    if os.path.exists(kt):
+        for r in csv.DictReader(open(kt)):
+            dur[int(r["Dispatch_Id"])] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
+    out = []
+    for k in sorted(per):
+        c = per[k]
+        cyc = c.get("GRBM_GUI_ACTIVE", 0.0) / 8
+        busy = c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / (cyc * 1024) if cyc else None
+        out.append({"mfma_busy": busy, "clock_ghz": cyc / dur[k] / 1e9 if k in dur and dur[k] > 0 else None,
+                    "us": dur[k] * 1e6 if k in dur else None})
+    return out
+
+
 def main():
     root, shapes, out = sys.argv[1], sys.argv[2].split(","), sys.argv[3]
     fetch = per_dispatch(os.path.join(root, "FETCH_SIZE", "run_counter_collection.csv"))
     write = per_dispatch(os.path.join(root, "WRITE_SIZE", "run_counter_collection.csv"))
+    mf = mfma_pass(root)
     res = {}
     for i, name in enumerate(shapes):
         M, N, K, epi = SHAPES[name]
@@ -45,10 +78,16 @@ def main():
                      "fetch_bytes": round(fb), "write_bytes": round(wb), "traffic_bytes": round(fb + wb),
                      "algorithmic_bytes": alg, "traffic_over_algorithmic": round((fb + wb) / alg, 3),
                      "fetch_size_kib_raw": f, "write_size_kib_raw": w}
+        if mf and len(mf) >= 4 * i + 4:
+            m = [x for x in mf[4 * i:4 * i + 4] if x["mfma_busy"] is not None]
+            if m:
+                res[name]["mfma_busy"] = round(sum(x["mfma_busy"] for x in m) / len(m), 4)
+                ck = [x["clock_ghz"] for x in m if x["clock_ghz"]]
+                res[name]["clock_ghz_mfma_pass"] = round(sum(ck) / len(ck), 3) if ck else None
     json.dump(res, open(out, "w"), indent=1)
     for k, v in res.items():
         print(k, v["traffic_bytes"] / 1e6, "MB vs", v["algorithmic_bytes"] / 1e6, "MB alg",
-              v["traffic_over_algorithmic"])
+              v["traffic_over_algorithmic"], "mfma busy", v.get("mfma_busy"))
 
 
 if __name__ == "__main__":

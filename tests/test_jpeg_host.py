@@ -39,7 +39,7 @@ def test_huff_tables_decode_every_code():
     Image.fromarray((np.random.default_rng(1).random((40, 40, 3)) * 255).astype(np.uint8)).save(
         b, "JPEG", quality=60, optimize=True)
     bufs.append(b.getvalue())
-    n = 0
+    n, n2 = 0, [0]
     for buf in bufs:
         for (bits, vals) in jpeg.parse(buf).huff.values():
             t = jpeg.build_huff(bits, vals)
@@ -56,8 +56,14 @@ def test_huff_tables_decode_every_code():
                         l += 1
                         c = code >> (ln - l) if l <= ln else code << (l - ln)
                     assert l == ln and t["vals"][(c + t["valoff"][l]) & 0xFF] == vals[k]
+                    if t["l2n"]:   # second-level table: every 16-bit window under this code
+                        lo = (code << (16 - ln)) - int(t["l2base"])
+                        for tail in (0, (1 << (16 - ln)) - 1):
+                            assert 0 <= lo + tail < t["l2n"]
+                            assert int(t["look2"][lo + tail]) == (ln << 8) | vals[k]
+                        n2[0] += 1
                 n += 1
-    assert n > 300
+    assert n > 300 and n2[0] > 100
 
 
 def test_unsupported_kinds_are_flagged():
