@@ -919,6 +919,11 @@ hipError_t launch(const GemmArgs& a, hipStream_t s) {
     hipLaunchKernelGGL((gemm_pp_kernel<EPI, 1, false, true>), dim3(nt), dim3(512), 0, s, a);
     return hipGetLastError();
   }
+  if (v >= 131 && v <= 139 && bf16_out && gemm_8q_ok(a)) {   // 8-phase, n-tiles in groups of (v - 130); 131: raster
+    GemmArgs ga = a;
+    ga.ngroup = v == 131 ? -1 : v - 130;
+    return gemm_8q(ga, EPI, s, cu_count(), 0);
+  }
   if (v >= 120 && v <= 124 && bf16_out) {   // 256 x 128 tiles, deferred epilogue (v98 where it does not apply)
     if (gemm_8r_ok(a)) return gemm_8r(a, EPI, s, cu_count(), v - 120);
     v = 98;

@@ -447,8 +447,23 @@ int gemm_8q_ok(const GemmArgs& a) {
 
 // mode: 0 = default (descriptors), 2 = no-MFMA probe,
 // 3 = flat global_load_lds addressing, 4 = no-epilogue probe
+// Tile order: n-tiles walked in groups of ng over all m-tiles, so each XCD's
+// L2 (4 MB) keeps its group's weight panel (ng x 256 x K bf16) while the
+// activation rows stream through: chosen when the tiles split into >= 6-wide
+// groups of <= 2.4 MB.  Measured at the B/32 c_fc shape (M = 500k, N = 3072,
+// K = 768, ng = 6): FETCH 7.8 -> 3.6 GB per launch, shader clock ~1.6 ->
+// ~1.85 GHz, 2282 -> 2207 us (scripts/gpu_gemm_group.sh).  Narrower groups,
+// and qkv's 9 n-tiles in groups of 3, were slower; ngroup < 0 forces the raster.
+int default_ngroup_8q(int tiles_n, int K) {
+  if (tiles_n < 12) return 0;
+  for (int ng = tiles_n / 2; ng >= 6; --ng)
+    if (tiles_n % ng == 0 && (int64_t)ng * 256 * K * 2 <= 2400000) return ng;
+  return 0;
+}
+
 hipError_t gemm_8q(const GemmArgs& a0, int epi, hipStream_t s, int cus, int mode) {
   GemmArgs a = a0;
+  if (a.ngroup == 0) a.ngroup = default_ngroup_8q(a.N / BN, a.K);
   if (mode == 5 || mode == 6 || mode == 7 || mode == 8) {   // start-stagger probes: 2 / 4 / 2 phases of ~1/2, 1/4, 1/4 tile
     const int tile_ticks = (int)(2200LL * a.K / 768);   // ~22 us per 256 x 256 tile at K = 768
     a.stagger_phases = mode == 6 ? 4 : 2;
