@@ -243,11 +243,12 @@ def _segments(buf, h):
     return segs
 
 
-def decode_batch(bufs, device="cuda"):
+def decode_batch(bufs, device="cuda", dedupe=True):
     """Decode JPEG byte strings on the GPU where the geometry allows, Pillow
     otherwise.  Returns a list of uint8 [H, W, 3] device tensors (None for a
     file neither path can read) in input order; frames of one geometry are
-    decoded in one launch."""
+    decoded in one launch.  ``dedupe=False`` passes one table set per frame
+    (no index array: the kernel's global-memory table path)."""
     import torch
     L = N.lib()
     heads = [parse(b) for b in bufs]
@@ -293,7 +294,7 @@ def decode_batch(bufs, device="cuda"):
             for (tc, th), (bits, vals) in h.huff.items():
                 if th <= 1:
                     slots[th * 2 + tc], tabs[th * 2 + tc] = _huff_cached(bits, vals)
-            key = tuple(slots)
+            key = tuple(slots) if dedupe else r
             if key not in set_of:
                 set_of[key] = len(sets)
                 sets.append(tabs)
@@ -328,7 +329,7 @@ def decode_batch(bufs, device="cuda"):
         nb = L.mi_jpeg_workspace_bytes(gp, B)
         ws = torch.empty(max(nb, 1), dtype=torch.uint8, device=dev)
         N.check(L.mi_jpeg_decode(d_data.data_ptr(), d_off.data_ptr(), d_end.data_ptr(), d_huff.data_ptr(),
-                                 d_hidx.data_ptr(), len(sets), d_qt.data_ptr(), gp, B, rgb.data_ptr(), ws.data_ptr(), nb,
+                                 d_hidx.data_ptr() if dedupe else None, len(sets), d_qt.data_ptr(), gp, B, rgb.data_ptr(), ws.data_ptr(), nb,
                                  N.stream_ptr(dev)), "mi_jpeg_decode")
         for r, i in enumerate(keep):
             out[i] = rgb[r]

@@ -41,9 +41,9 @@ def _save(im, **kw):
     return b.getvalue()
 
 
-def _check(bufs, expect_device=None):
+def _check(bufs, expect_device=None, **kw):
     from miclip import jpeg
-    got = jpeg.decode_batch(bufs, "cuda")
+    got = jpeg.decode_batch(bufs, "cuda", **kw)
     for i, (b, g) in enumerate(zip(bufs, got)):
         ref = _pil(b)
         assert g is not None, i
@@ -76,6 +76,26 @@ def test_restart_markers_bit_exact(gpu, kw):
     for b in bufs:
         assert b.count(b"\xff\xdd") == 1
     _check(bufs, expect_device=[True] * len(bufs))
+
+
+@pytest.mark.parametrize("n", [3, 7])
+def test_per_image_huffman_tables(gpu, n):
+    """optimize=True gives every image its own Huffman tables: 3 distinct sets
+    are staged in LDS, 7 exceed the LDS budget (4) and are read from global
+    memory through the per-frame set index."""
+    from miclip import jpeg
+    bufs = [_save(_img(96, 128, 20 + s), quality=50 + 7 * s, optimize=True) for s in range(n)]
+    sets = {tuple(sorted((k, bytes(b), v) for k, (b, v) in jpeg.parse(x).huff.items())) for x in bufs}
+    assert len(sets) == n
+    _check(bufs, expect_device=[True] * n)
+
+
+def test_per_frame_tables_without_index(gpu):
+    """huff_idx = NULL (one table set per frame, global-memory tables) gives
+    the same pixels as the deduplicated LDS path."""
+    files = sorted(glob.glob(os.path.join(ROOT, "golden", "ref_frames", "*.jpg")))[:3]
+    bufs = [open(f, "rb").read() for f in files] + [_save(_img(720, 1280, 9), quality=80)]
+    _check(bufs, dedupe=False)
 
 
 def test_grayscale_and_mixed_batch(gpu):
