@@ -174,14 +174,16 @@ def preprocess_timing(dev, n_px, B=256, H=720, W=1280, reps=10):
             "gbs": round(B * H * W * 3 / us / 1e3, 1), "shape": [B, H, W, 3]}
 
 
-def jpeg_ingest_timing(dev, n_px, B=2048, threads=16):
+def jpeg_ingest_timing(dev, n_px, B=8192, threads=16, pil_frames=1024):
     """Frame ingest from JPEG bytes in host memory to preprocessed [B,3,n,n]
     bf16 tensors: the reference's 16 real 1280x720
     frames (tests/golden/ref_frames) repeated to B.  GPU path: header parse +
     table build on the host, mi_jpeg_decode + mi_preprocess_frames on the
     device (bit-identical to Pillow, tests/test_gpu_jpeg.py); host path: Pillow
     decode on `threads` host threads, as the reference decodes, + the same GPU
-    preprocessing.  Wall-clock, synchronised; not part of the timed step."""
+    preprocessing, timed on the first `pil_frames` frames.  The GPU decode
+    runs one lane per frame, so its rate grows with the batch (8192 frames =
+    128 waves).  Wall-clock, synchronised; not part of the timed step."""
     import glob
     import io
     import time
@@ -208,20 +210,24 @@ def jpeg_ingest_timing(dev, n_px, B=2048, threads=16):
 
     def host():
         with ThreadPoolExecutor(threads) as ex:
-            arrs = list(ex.map(pil_one, bufs))
+            arrs = list(ex.map(pil_one, bufs[:pil_frames]))
         return preprocess_frames(torch.from_numpy(np.stack(arrs)).to(dev), n_px, out_dtype=torch.bfloat16)
 
-    res = {"frames": B, "source": "tests/golden/ref_frames (16 reference frames, 1280x720 4:2:0)",
-           "host_threads": threads}
-    for name, fn in (("gpu_decode", gpu), ("pil_decode", host)):
-        fn()
+    res = {"frames": B, "pil_frames": pil_frames,
+           "source": "tests/golden/ref_frames (16 reference frames, 1280x720 4:2:0)", "host_threads": threads}
+    for name, fn, n in (("gpu_decode", gpu, B), ("pil_decode", host, pil_frames)):
+        out = fn()
         torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
+        best = 1e9
         for _ in range(2):
+            out = None
+            t0 = time.perf_counter()
             out = fn()
-        torch.cuda.synchronize(dev)
-        res[name + "_frames_per_s"] = round(2 * B / (time.perf_counter() - t0), 1)
+            torch.cuda.synchronize(dev)
+            best = min(best, time.perf_counter() - t0)
+        res[name + "_frames_per_s"] = round(n / best, 1)
         del out
+    torch.cuda.empty_cache()
     return res
 
 

@@ -21,6 +21,7 @@ on the host, so every frame gets the reference's pixels.
 from __future__ import annotations
 
 import struct
+import threading
 
 import numpy as np
 
@@ -97,9 +98,59 @@ class JpegHeader:
                  "supported", "why")
 
 
+_HEAD_CACHE = {}
+
+
+def _scan_start(buf):
+    """Byte offset just past the first SOS segment (a bare marker walk), or None."""
+    n = len(buf)
+    if n < 4 or buf[0] != 0xFF or buf[1] != 0xD8:
+        return None
+    i = 2
+    while i + 4 <= n:
+        if buf[i] != 0xFF:
+            return None
+        m = buf[i + 1]
+        if m == 0xFF:
+            i += 1
+            continue
+        if m in (0xD8, 0x01) or 0xD0 <= m <= 0xD7:
+            i += 2
+            continue
+        if m == 0xD9:
+            return None
+        ln = (buf[i + 2] << 8) | buf[i + 3]
+        if m == 0xDA:
+            return i + 2 + ln
+        i += 2 + ln
+    return None
+
+
 def parse(buf: bytes) -> JpegHeader:
     """Marker walk up to the first SOS; sets ``supported`` False (with ``why``)
-    for anything the device decoder does not restate."""
+    for anything the device decoder does not restate.  Frames of one encoder
+    share their header bytes, so the parsed header is cached by those bytes
+    (everything before the entropy-coded data); only the end-of-image check is
+    per file."""
+    ss = _scan_start(buf)
+    if ss is None:
+        return _parse(buf)
+    key = bytes(buf[:ss])
+    h = _HEAD_CACHE.get(key)
+    if h is None:
+        if len(_HEAD_CACHE) > 1024:
+            _HEAD_CACHE.clear()
+        h = _HEAD_CACHE[key] = _parse(buf, check_eoi=False)
+    if h.supported and buf.rfind(b"\xff\xd9") <= h.scan_start:   # truncated: Pillow raises; let it
+        t = JpegHeader()
+        for f in JpegHeader.__slots__:
+            setattr(t, f, getattr(h, f))
+        t.supported, t.why = False, "no EOI after the scan"
+        return t
+    return h
+
+
+def _parse(buf, check_eoi=True) -> JpegHeader:
     h = JpegHeader()
     h.supported, h.why = False, ""
     h.qt, h.huff, h.ri = {}, {}, 0
@@ -203,7 +254,7 @@ def parse(buf: bytes) -> JpegHeader:
             if any(q > 3 for q in h.qsel) or h.width < 1 or h.height < 1:
                 h.why = "bad frame header"
                 return h
-            if buf.rfind(b"\xff\xd9") <= h.scan_start:   # truncated: Pillow raises; let it
+            if check_eoi and buf.rfind(b"\xff\xd9") <= h.scan_start:   # truncated: Pillow raises; let it
                 h.why = "no EOI after the scan"
                 return h
             h.supported = True
@@ -243,6 +294,38 @@ def _segments(buf, h):
     return segs
 
 
+_STAGE = [None]
+_STAGE_LOCK = threading.Lock()
+_PAD = np.frombuffer(b"\xff\xd9" * 16, np.uint8)
+
+
+def _upload(bufs, keep, segl, starts, total, dev):
+    """Entropy-coded bytes of the kept frames, concatenated straight into a
+    reused pinned staging buffer (16 host threads for big batches), then one
+    DMA to the device; 32 bytes of EOI markers as padding."""
+    import torch
+    from concurrent.futures import ThreadPoolExecutor
+    with _STAGE_LOCK:
+        st = _STAGE[0]
+        if st is None or st.numel() < total + 32:
+            st = torch.empty(max(total + 32, 1 << 26), dtype=torch.uint8, pin_memory=True)
+            _STAGE[0] = st
+        v = st.numpy()
+
+        def cp(r):
+            a, n = segl[r][0][0], int(starts[r + 1] - starts[r])
+            v[starts[r]:starts[r + 1]] = np.frombuffer(bufs[keep[r]], np.uint8, n, a)
+
+        if len(keep) >= 64:
+            with ThreadPoolExecutor(16) as ex:
+                list(ex.map(cp, range(len(keep))))
+        else:
+            for r in range(len(keep)):
+                cp(r)
+        v[total:total + 32] = _PAD
+        return st[:total + 32].to(dev)   # synchronous: the staging buffer is free again on return
+
+
 def decode_batch(bufs, device="cuda", dedupe=True):
     """Decode JPEG byte strings on the GPU where the geometry allows, Pillow
     otherwise.  Returns a list of uint8 [H, W, 3] device tensors (None for a
@@ -266,42 +349,55 @@ def decode_batch(bufs, device="cuda", dedupe=True):
         mcux = -(-W // (8 * (max(s[0] for s in samp) if nc == 3 else 1)))
         mcuy = -(-H // (8 * (max(s[1] for s in samp) if nc == 3 else 1)))
         nseg = -(-(mcux * mcuy) // ri) if ri else 1
-        offs, ends, chunks, pos = [], [], [], 0
-        keep = []
+        keep, segl = [], []
         for i in idx:
-            segs = _segments(bufs[i], heads[i])
-            if len(segs) != nseg:     # restart markers not where DRI says: leave it to the host decoder
-                out[i] = _host_decode(bufs[i], device)
-                continue
+            h = heads[i]
+            if ri:
+                segs = _segments(bufs[i], h)
+                if len(segs) != nseg:     # restart markers not where DRI says: leave it to the host decoder
+                    out[i] = _host_decode(bufs[i], device)
+                    continue
+            else:
+                segs = ((h.scan_start, len(bufs[i])),)
             keep.append(i)
-            for a, b in segs:
-                offs.append(pos + a - segs[0][0])
-                ends.append(pos + b - segs[0][0])
-            seg_bytes = bufs[i][segs[0][0]:segs[-1][1]]
-            chunks.append(seg_bytes)
-            pos += len(seg_bytes)
+            segl.append(segs)
         if not keep:
             continue
         B = len(keep)
-        data = np.frombuffer(bytearray(b"".join(chunks) + b"\xff\xd9" * 16), dtype=np.uint8)
-        # table sets deduplicated: frames of one encoder share one set, which
-        # the entropy kernel stages in LDS
+        lens = np.array([sg[-1][1] - sg[0][0] for sg in segl], np.int64)
+        starts = np.zeros(B + 1, np.int64)
+        np.cumsum(lens, out=starts[1:])
+        total = int(starts[-1])
+        if ri:
+            offs = [int(starts[r]) + a - sg[0][0] for r, sg in enumerate(segl) for a, _ in sg]
+            ends = [int(starts[r]) + b - sg[0][0] for r, sg in enumerate(segl) for _, b in sg]
+        else:
+            offs, ends = starts[:-1], starts[1:]
+        # table sets deduplicated: frames of one encoder share one set (and one
+        # cached header object), which the entropy kernel stages in LDS
         sets, set_of, hidx = [], {}, np.zeros(B, np.int32)
-        qt = np.zeros((B, 4, 64), dtype=np.uint16)
+        qts, qidx, per_head = [], np.zeros(B, np.int64), {}
         for r, i in enumerate(keep):
             h = heads[i]
-            slots, tabs = [None] * 4, [None] * 4
-            for (tc, th), (bits, vals) in h.huff.items():
-                if th <= 1:
-                    slots[th * 2 + tc], tabs[th * 2 + tc] = _huff_cached(bits, vals)
-            key = tuple(slots) if dedupe else r
+            e = per_head.get(id(h))
+            if e is None:
+                slots, tabs = [None] * 4, [None] * 4
+                for (tc, th), (bits, vals) in h.huff.items():
+                    if th <= 1:
+                        slots[th * 2 + tc], tabs[th * 2 + tc] = _huff_cached(bits, vals)
+                q4 = np.zeros((4, 64), np.uint16)
+                for tq, q in h.qt.items():
+                    if tq <= 3:
+                        q4[tq] = q
+                qts.append(q4)
+                e = per_head[id(h)] = (tuple(slots), tabs, len(qts) - 1)
+            key = e[0] if dedupe else r
             if key not in set_of:
                 set_of[key] = len(sets)
-                sets.append(tabs)
+                sets.append(e[1])
             hidx[r] = set_of[key]
-            for tq, q in h.qt.items():
-                if tq <= 3:
-                    qt[r, tq] = q
+            qidx[r] = e[2]
+        qt = np.ascontiguousarray(np.stack(qts)[qidx])
         geom = np.zeros(20, np.int32)
         geom[:5] = (W, H, nc, ri, nseg)
         for c in range(nc):
@@ -313,9 +409,9 @@ def decode_batch(bufs, device="cuda", dedupe=True):
             for i, ok in zip(keep, sel_ok):
                 out[i] = _host_decode(bufs[i], device)
             continue
-        d_data = torch.from_numpy(data).to(dev)
-        d_off = torch.tensor(offs, dtype=torch.int64, device=dev)
-        d_end = torch.tensor(ends, dtype=torch.int64, device=dev)
+        d_data = _upload(bufs, keep, segl, starts, total, dev)
+        d_off = torch.as_tensor(np.asarray(offs, np.int64)).to(dev)
+        d_end = torch.as_tensor(np.asarray(ends, np.int64)).to(dev)
         huff = np.zeros((len(sets), 4), dtype=_HUFF_DT)
         for u, tabs in enumerate(sets):
             for j, t in enumerate(tabs):

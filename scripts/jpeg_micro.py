@@ -28,16 +28,19 @@ def main():
     res = {}
     for B in sizes:
         bufs = [raw[i % len(raw)] for i in range(B)]
-        jpeg.decode_batch(bufs[:64], dev)
+        del jpeg.decode_batch(bufs, dev)[:]   # warm: pinned staging, allocator pools at this size
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         heads = [jpeg.parse(b) for b in bufs]
         t_parse = time.perf_counter() - t0
         del heads
-        t0 = time.perf_counter()
-        out = jpeg.decode_batch(bufs, dev)
-        torch.cuda.synchronize(dev)
-        t_gpu = time.perf_counter() - t0
+        t_gpu = 1e9
+        for _ in range(2):
+            out = None
+            t0 = time.perf_counter()
+            out = jpeg.decode_batch(bufs, dev)
+            torch.cuda.synchronize(dev)
+            t_gpu = min(t_gpu, time.perf_counter() - t0)
         ok = all(o is not None for o in out)
         # bit-exactness on the first 16
         for i in range(min(16, B)):
