@@ -21,6 +21,7 @@
 // 12-bit / CMYK / other sampling layouts stay on the host decoder.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 
 #include "internal.hpp"
@@ -585,11 +586,17 @@ hipError_t jpeg_decode(const uint8_t* data, const int64_t* seg_off, const int64_
                        (const JpegHuff*)huff, huff_idx, nsets, g, nframes, coef);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
-  const int64_t nb = (int64_t)nframes * blocks;
-  hipLaunchKernelGGL(jpeg_idct_kernel, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, s, coef, qtab, g, pl, nframes,
-                     planes);
-  e = hipGetLastError();
-  if (e != hipSuccess) return e;
+  // A dispatch counts its work-items in 32 bits (grid x block < 2^32): the
+  // per-block and per-pixel kernels run over frame chunks of < 2^31 items.
+  const int64_t fc_idct = blocks > 0 ? std::max<int64_t>(1, ((int64_t)1 << 31) / blocks) : nframes;
+  for (int64_t f0 = 0; f0 < nframes; f0 += fc_idct) {
+    const int nfc = (int)std::min<int64_t>(fc_idct, nframes - f0);
+    const int64_t nb = (int64_t)nfc * blocks;
+    hipLaunchKernelGGL(jpeg_idct_kernel, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, s,
+                       coef + f0 * blocks * 64, qtab + f0 * 4 * 64, g, pl, nfc, planes + f0 * bytes);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
   // chroma layout relative to luma (components 1, 2 share it)
   int cmode = 0, cdw = W, cdh = H;
   if (ncomp == 3) {
@@ -598,10 +605,17 @@ hipError_t jpeg_decode(const uint8_t* data, const int64_t* seg_off, const int64_
     cdw = (W * g.hs[1] + hmax - 1) / hmax;   // libjpeg downsampled_width
     cdh = (H * g.vs[1] + vmax - 1) / vmax;
   }
-  const int64_t np = (int64_t)nframes * W * H;
-  hipLaunchKernelGGL(jpeg_color_kernel, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, s, planes, pl, W, H, ncomp,
-                     cmode, cdw, cdh, nframes, out_rgb);
-  return hipGetLastError();
+  const int64_t px = (int64_t)W * H;
+  const int64_t fc_px = std::max<int64_t>(1, ((int64_t)1 << 31) / px);
+  for (int64_t f0 = 0; f0 < nframes; f0 += fc_px) {
+    const int nfc = (int)std::min<int64_t>(fc_px, nframes - f0);
+    const int64_t np = (int64_t)nfc * px;
+    hipLaunchKernelGGL(jpeg_color_kernel, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, s, planes + f0 * bytes, pl,
+                       W, H, ncomp, cmode, cdw, cdh, nfc, out_rgb + f0 * px * 3);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 size_t jpeg_workspace_bytes(const int32_t* geom, int nframes) {

@@ -277,21 +277,32 @@ hipError_t preprocess_frames(const uint8_t* frames, int64_t B, int H, int W, int
   Tables t;
   hipError_t e = get_tables(H, W, n, mode, t);
   if (e != hipSuccess) return e;
-  uint8_t* tmp = (uint8_t*)ws;
-  const int64_t th = B * t.rows * n;
-  hipLaunchKernelGGL(resample_h_kernel, dim3((unsigned)((th + 255) / 256)), dim3(256), 0, s, frames, tmp, t.kh,
-                     t.bh, t.ksh, H, W, n, t.r0, t.rows, th);
   // the constants as torchvision builds them: Python floats (double) -> float32
   const Norm nm = {{(float)0.48145466, (float)0.4578275, (float)0.40821073},
                    {(float)0.26862954, (float)0.26130258, (float)0.27577711}};
-  const int64_t tv = B * n * n;
-  if (out_bf16)
-    hipLaunchKernelGGL(resample_v_kernel<true>, dim3((unsigned)((tv + 255) / 256)), dim3(256), 0, s, tmp, out, t.kv,
-                       t.bv, t.ksv, t.rows, n, t.r0, nm, tv);
-  else
-    hipLaunchKernelGGL(resample_v_kernel<false>, dim3((unsigned)((tv + 255) / 256)), dim3(256), 0, s, tmp, out, t.kv,
-                       t.bv, t.ksv, t.rows, n, t.r0, nm, tv);
-  return hipGetLastError();
+  // A dispatch counts its work-items in 32 bits (grid x block < 2^32): big
+  // batches run as several launches of at most 2^31 work-items each.
+  const int64_t per = (int64_t)t.rows * n > (int64_t)n * n ? (int64_t)t.rows * n : (int64_t)n * n;
+  const int64_t bc = per > 0 ? (((int64_t)1 << 31) / per > 0 ? ((int64_t)1 << 31) / per : 1) : B;
+  for (int64_t f0 = 0; f0 < B; f0 += bc) {
+    const int64_t nb = B - f0 < bc ? B - f0 : bc;
+    const uint8_t* src = frames + f0 * H * W * 3;
+    uint8_t* tmp = (uint8_t*)ws + f0 * t.rows * n * 3;
+    char* dst = (char*)out + f0 * 3 * n * n * (out_bf16 ? 2 : 4);
+    const int64_t th = nb * t.rows * n;
+    hipLaunchKernelGGL(resample_h_kernel, dim3((unsigned)((th + 255) / 256)), dim3(256), 0, s, src, tmp, t.kh,
+                       t.bh, t.ksh, H, W, n, t.r0, t.rows, th);
+    const int64_t tv = nb * n * n;
+    if (out_bf16)
+      hipLaunchKernelGGL(resample_v_kernel<true>, dim3((unsigned)((tv + 255) / 256)), dim3(256), 0, s, tmp, dst,
+                         t.kv, t.bv, t.ksv, t.rows, n, t.r0, nm, tv);
+    else
+      hipLaunchKernelGGL(resample_v_kernel<false>, dim3((unsigned)((tv + 255) / 256)), dim3(256), 0, s, tmp, dst,
+                         t.kv, t.bv, t.ksv, t.rows, n, t.r0, nm, tv);
+    const hipError_t le = hipGetLastError();
+    if (le != hipSuccess) return le;
+  }
+  return hipSuccess;
 }
 
 }  // namespace miclip

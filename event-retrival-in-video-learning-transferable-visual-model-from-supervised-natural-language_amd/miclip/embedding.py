@@ -23,7 +23,7 @@ from pathlib import Path
 import numpy as np
 
 from . import api
-from .preprocess import Transform, load_frames
+from .preprocess import Transform, decode_chunk, load_frames
 
 
 def walk_frames(folder_path):
@@ -50,14 +50,18 @@ def extract_and_save_embeddings_from_folder(folder_path, model_name, video_name=
     output_file = os.path.join(output_dir, f"{video_name}_embeddings.npy")
     paths = walk_frames(folder_path)
     rows = []
-    for i in range(0, len(paths), batch_size):
-        chunk = paths[i:i + batch_size]
-        if isinstance(preprocess, Transform):  # this package's transform: GPU resize/crop/normalise
-            batch, _ = load_frames(chunk, preprocess.n_px, device=model.device, squash=preprocess.squash,
-                                   strict=True)
-        else:
-            batch = torch.stack([preprocess(Image.open(p).convert("RGB")) for p in chunk])
-        rows.append(model.encode_image(batch, out_dtype=torch.float32).cpu().numpy())
+    gpu_prep = isinstance(preprocess, Transform)   # this package's transform: GPU decode/resize/crop/normalise
+    step = decode_chunk(batch_size) if gpu_prep else batch_size
+    for j in range(0, len(paths), step):
+        if gpu_prep:
+            frames, _ = load_frames(paths[j:j + step], preprocess.n_px, device=model.device,
+                                    squash=preprocess.squash, strict=True)
+        for i in range(0, min(step, len(paths) - j), batch_size):
+            if gpu_prep:
+                batch = frames[i:i + batch_size]
+            else:
+                batch = torch.stack([preprocess(Image.open(p).convert("RGB")) for p in paths[j + i:j + i + batch_size]])
+            rows.append(model.encode_image(batch, out_dtype=torch.float32).cpu().numpy())
     all_embeddings = np.vstack(rows) if rows else np.zeros((0, model.visual.output_dim), np.float32)
     np.save(output_file, all_embeddings)
     return output_file

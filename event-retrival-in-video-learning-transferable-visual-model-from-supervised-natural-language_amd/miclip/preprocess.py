@@ -95,6 +95,20 @@ def preprocess_frames(frames, n_px: int = 224, squash: bool = False, out_dtype=N
     return out
 
 
+DECODE_CHUNK = 8192
+
+
+def decode_chunk(batch_size: int) -> int:
+    """Frames per load_frames call in the folder-ingest loops: the GPU JPEG
+    decode runs one lane per frame, so its rate grows with the batch (2048
+    frames ~5k frames/s, 8192 ~13k) while the encode keeps the
+    caller's batch size; a multiple of it (``$MICLIP_DECODE_CHUNK`` overrides).
+    8192 720p frames hold ~70 GB of device memory while they decode."""
+    n = int(os.environ.get("MICLIP_DECODE_CHUNK", DECODE_CHUNK))
+    b = max(1, batch_size)
+    return max(b, n // b * b)
+
+
 def load_frames(paths, n_px: int = 224, device="cuda", squash: bool = False, out_dtype=None, threads: int = 8,
                 strict: bool = False, gpu_decode=None):
     """Decode frame files and preprocess them on the GPU.  Returns

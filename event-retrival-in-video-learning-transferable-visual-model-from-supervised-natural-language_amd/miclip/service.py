@@ -26,7 +26,7 @@ import os
 import numpy as np
 
 from . import api
-from .preprocess import load_frames
+from .preprocess import decode_chunk, load_frames
 from .retrieval import MirroredCorpus, rank_topk
 
 # corpora from this many rows on also get an fp16 ranking mirror (scripts/mirror_micro.py:
@@ -268,11 +268,15 @@ class EmbeddingService:
         model = self._clip()
         R = model.cfg.image_resolution
         out = []
-        for i in range(0, len(frame_files), batch_size):
-            # host decode + GPU resize/crop/normalise (Pillow-exact, miclip.preprocess.load_frames)
-            batch, _ = load_frames([os.path.join(folder_path, f) for f in frame_files[i:i + batch_size]], R,
-                                   device=model.device)
-            out.append(model.encode_image(batch, normalize=True, out_dtype=torch.float32).cpu().numpy())
+        step = decode_chunk(batch_size)
+        for j in range(0, len(frame_files), step):
+            # GPU JPEG decode + resize/crop/normalise (Pillow-exact, miclip.preprocess.load_frames) over a
+            # large chunk (the decode runs one lane per frame), then the reference's encode batches
+            frames, _ = load_frames([os.path.join(folder_path, f) for f in frame_files[j:j + step]], R,
+                                    device=model.device)
+            for i in range(0, frames.shape[0], batch_size):
+                out.append(model.encode_image(frames[i:i + batch_size], normalize=True,
+                                              out_dtype=torch.float32).cpu().numpy())
         embeddings = np.vstack(out)
         np.save(embeddings_path, embeddings)
         metadata_path = self.path_service.get_metadata_path(video_name)

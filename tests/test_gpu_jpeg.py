@@ -98,6 +98,24 @@ def test_per_frame_tables_without_index(gpu):
     _check(bufs, dedupe=False)
 
 
+def test_large_batch_beyond_32bit_dispatch(gpu):
+    """4800 reference frames (4.4e9 output pixels): a single per-pixel dispatch
+    would overflow the 32-bit work-item count (frames past ~4660 came out
+    stale); the IDCT / colour launches are chunked.  Every frame must equal
+    Pillow's decode."""
+    import torch
+    from miclip import jpeg
+    files = sorted(glob.glob(os.path.join(ROOT, "golden", "ref_frames", "*.jpg")))
+    raw = [open(f, "rb").read() for f in files]
+    refs = [torch.from_numpy(_pil(b)).cuda() for b in raw]
+    B = 4800
+    got = jpeg.decode_batch([raw[i % len(raw)] for i in range(B)], "cuda")
+    bad = [i for i in range(B) if got[i] is None or not torch.equal(got[i], refs[i % len(raw)])]
+    assert not bad, f"{len(bad)} frames differ, first {bad[:5]}"
+    del got
+    torch.cuda.empty_cache()
+
+
 def test_grayscale_and_mixed_batch(gpu):
     bufs = [_save(_img(45, 61, 1, "L"), quality=90), _save(_img(45, 61, 2), quality=90),
             _save(_img(45, 61, 3, "L"), quality=40), _save(_img(30, 30, 4), quality=90, subsampling=1)]
