@@ -261,6 +261,21 @@ def _cpu_model():
     return platform.processor() or "unknown"
 
 
+def _usable_cores():
+    """Host cores this process may run on: BASELINE.md's plan is
+    torch.set_num_threads(os.cpu_count()), but on the GPU box os.cpu_count()
+    reports the whole host (256) while the process's share is a cgroup CPU quota
+    (16); threads beyond the share only contend.  min(affinity, quota)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, -(-int(q) // int(p))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
 def cpu_baseline(cfg, n_frames_metric, Q, k, b1_frames, b64_frames):
     """The reference CPU path timed on this box's host cores (BASELINE.md
     CPU-baseline plan): the torch-CPU fp32 restatement of openai/CLIP
@@ -275,7 +290,7 @@ def cpu_baseline(cfg, n_frames_metric, Q, k, b1_frames, b64_frames):
     import torch
     from miclip import weights
     from oracle import clip_ref, clip_torch, rank_ref
-    threads = int(os.environ.get("OMP_NUM_THREADS") or 0) or os.cpu_count()
+    threads = _usable_cores()
     torch.set_num_threads(threads)
     sd = weights.make_state_dict(cfg)
     m = clip_torch.TorchCLIP(sd, cfg)
@@ -306,7 +321,7 @@ def cpu_baseline(cfg, n_frames_metric, Q, k, b1_frames, b64_frames):
         return n_frames_metric / (n_frames_metric * t_img + Q * t_txt + Q * t_rank)
 
     return {"value": round(rate(t_b1), 2), "unit": "frames/s", "cores": int(threads), "kind": "port",
-            "nproc": os.cpu_count(), "cpu_model": _cpu_model(),
+            "nproc": os.cpu_count(), "cores_available": _usable_cores(), "cpu_model": _cpu_model(),
             "batch64_value": round(rate(t_b64), 2), "numpy_batch64_value": round(rate(t_np), 2),
             "sample": f"torch-CPU fp32 restatement of openai/CLIP (oracle/clip_torch.py), {threads} threads: "
                       f"{b1_frames} frames one per call as Backend/embedding.py:39-52 ({t_b1 * 1e3:.1f} ms/frame; "
@@ -524,7 +539,9 @@ def main():
         rank_roof = None if args.no_rank_roofline else rank_roofline(dev)
         F_frame, F_text = cfg.image_flops(), cfg.text_flops()
         step_flops = Nf * world * F_frame + Q * world * F_text + 2.0 * Nf * world * Q * cfg.embed_dim
-        mfma_frac = step_flops / (ms / 1e3) / (BF16_PEAK_TFLOPS * 1e12) / world
+        # against the peak of the arithmetic the step's GEMMs run on (fp8 runs: the MX-fp8 peak)
+        step_peak = FP8_PEAK_TFLOPS if args.weights == "fp8" else BF16_PEAK_TFLOPS
+        mfma_frac = step_flops / (ms / 1e3) / (step_peak * 1e12) / world
         dom = kern.get("gemm_fc")
         M = chunk * cfg.vision_tokens
         roof = None

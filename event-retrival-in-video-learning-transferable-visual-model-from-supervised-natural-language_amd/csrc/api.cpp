@@ -54,6 +54,8 @@ uint16_t f2bf_host(float f) {
 struct Layer {
   const float *ln1_g, *ln1_b, *b_qkv, *b_out, *ln2_g, *ln2_b, *b_fc, *b_proj;
   const uint16_t *w_qkv, *w_out, *w_fc, *w_proj;
+  // f32 GEMM weights (weight_dtype MI_F32): the same [N][K] matrices kept in f32
+  const float *f_qkv = nullptr, *f_out = nullptr, *f_fc = nullptr, *f_proj = nullptr;
   // MX-fp8 copies (weight_dtype MI_FP8, vision tower): e4m3 codes + stage-major e8m0 scales
   const uint8_t *q_qkv = nullptr, *s_qkv = nullptr, *q_out = nullptr, *s_out = nullptr;
   const uint8_t *q_fc = nullptr, *s_fc = nullptr, *q_proj = nullptr, *s_proj = nullptr;
@@ -86,6 +88,31 @@ struct Builder {
     if (p) memcpy(img.data() + o, p, n * 4);
     return o;
   }
+  // rows x cols fp32 matrix -> f32 [rows][ldp] (zero padded columns)
+  size_t f32_pad(int64_t rows, int64_t cols, int64_t ldp) {
+    const float* p = take(rows * cols);
+    size_t o = align();
+    img.resize(o + rows * ldp * 4);
+    float* d = (float*)(img.data() + o);
+    for (int64_t r = 0; r < rows; ++r)
+      for (int64_t c = 0; c < ldp; ++c) d[r * ldp + c] = (p && c < cols) ? p[r * cols + c] : 0.f;
+    return o;
+  }
+  // [rows][cols] fp32 used as x @ P  ->  f32 P^T [cols][rows]
+  size_t f32_t(int64_t rows, int64_t cols) {
+    const float* p = take(rows * cols);
+    size_t o = align();
+    img.resize(o + rows * cols * 4);
+    float* d = (float*)(img.data() + o);
+    for (int64_t c = 0; c < cols; ++c)
+      for (int64_t r = 0; r < rows; ++r) d[c * rows + r] = p ? p[r * cols + c] : 0.f;
+    return o;
+  }
+  // GEMM weight in the context's precision
+  size_t mat(bool full, int64_t rows, int64_t cols, int64_t ldp) {
+    return full ? f32_pad(rows, cols, ldp) : bf16(rows, cols, ldp);
+  }
+  size_t mat_t(bool full, int64_t rows, int64_t cols) { return full ? f32_t(rows, cols) : bf16_t(rows, cols); }
   // rows x cols fp32 matrix -> bf16 [rows][ldp] (zero padded columns)
   size_t bf16(int64_t rows, int64_t cols, int64_t ldp) {
     const float* p = take(rows * cols);
@@ -112,21 +139,21 @@ struct LayerOff {
   size_t ln1_g, ln1_b, w_qkv, b_qkv, w_out, b_out, ln2_g, ln2_b, w_fc, b_fc, w_proj, b_proj;
 };
 
-void build_tower(Builder& b, int W, int L, std::vector<LayerOff>& out) {
+void build_tower(Builder& b, int W, int L, std::vector<LayerOff>& out, bool full) {
   out.resize(L);
   for (int i = 0; i < L; ++i) {
     LayerOff& l = out[i];
     l.ln1_g = b.f32(W);
     l.ln1_b = b.f32(W);
-    l.w_qkv = b.bf16(3 * W, W, W);
+    l.w_qkv = b.mat(full, 3 * W, W, W);
     l.b_qkv = b.f32(3 * W);
-    l.w_out = b.bf16(W, W, W);
+    l.w_out = b.mat(full, W, W, W);
     l.b_out = b.f32(W);
     l.ln2_g = b.f32(W);
     l.ln2_b = b.f32(W);
-    l.w_fc = b.bf16(4 * W, W, W);
+    l.w_fc = b.mat(full, 4 * W, W, W);
     l.b_fc = b.f32(4 * W);
-    l.w_proj = b.bf16(W, 4 * W, 4 * W);
+    l.w_proj = b.mat(full, W, 4 * W, 4 * W);
     l.b_proj = b.f32(W);
   }
 }
@@ -141,6 +168,9 @@ struct mi_clip {
   int S_v = 0, G = 0, Kp = 0;
   char* wdev = nullptr;
   bool fp8 = false;       // vision tower GEMMs on the MX-fp8 MFMA
+  bool f32 = false;       // weight_dtype MI_F32: every GEMM, activation and the residual stream in f32 (precise.hip)
+  int Kp32 = 0;           // f32 mode: conv1 K padded to the f32 GEMM's 32-k stage
+  const float *conv_f = nullptr, *vproj_f = nullptr, *tproj_f = nullptr;
   char* wq = nullptr;     // MX-fp8 weight copies
   // vision
   const uint16_t* conv_w = nullptr;
@@ -204,8 +234,9 @@ int mi_clip_create(const mi_clip_arch* arch, const float* weights, int64_t numel
                    mi_clip** out) {
   if (!arch || !weights || !out) return fail(MI_ERR_ARG, "mi_clip_create: null argument");
   *out = nullptr;
-  if (weight_dtype != MI_BF16 && weight_dtype != MI_FP8)
-    return fail(MI_ERR_UNSUPPORTED, "mi_clip_create: weight_dtype must be MI_BF16 or MI_FP8");
+  if (weight_dtype != MI_BF16 && weight_dtype != MI_FP8 && weight_dtype != MI_F32)
+    return fail(MI_ERR_UNSUPPORTED, "mi_clip_create: weight_dtype must be MI_BF16, MI_FP8 or MI_F32");
+  const bool full = weight_dtype == MI_F32;
   const mi_clip_arch& a = *arch;
   if (a.vision_width % 128 || a.text_width % 128 || a.vision_width > 1024 || a.text_width > 1024)
     return fail(MI_ERR_UNSUPPORTED, "widths must be multiples of 128 and <= 1024 (got %d/%d)", a.vision_width,
@@ -231,24 +262,26 @@ int mi_clip_create(const mi_clip_arch* arch, const float* weights, int64_t numel
   const int W = a.vision_width, TW = a.text_width, E = a.embed_dim;
   const int K = 3 * a.vision_patch_size * a.vision_patch_size;
   c->Kp = (K + 63) / 64 * 64;
+  c->Kp32 = (K + 31) / 32 * 32;
+  c->f32 = full;
 
   Builder b;
   b.src = weights;
   b.numel = numel;
-  b.img.reserve((size_t)numel * 2 + (size_t)a.vocab_size * TW * 2 + (1 << 20));
-  const size_t o_conv = b.bf16(W, K, c->Kp);
+  b.img.reserve((size_t)numel * (full ? 4 : 2) + (size_t)a.vocab_size * TW * 2 + (1 << 20));
+  const size_t o_conv = b.mat(full, W, K, full ? c->Kp32 : c->Kp);
   const size_t o_cls = b.f32(W);
   const size_t o_vpos = b.f32((int64_t)c->S_v * W);
   const size_t o_lnpre_g = b.f32(W), o_lnpre_b = b.f32(W);
   std::vector<LayerOff> vlo, tlo;
-  build_tower(b, W, a.vision_layers, vlo);
+  build_tower(b, W, a.vision_layers, vlo, full);
   const size_t o_lnpost_g = b.f32(W), o_lnpost_b = b.f32(W);
-  const size_t o_vproj = b.bf16_t(W, E);
+  const size_t o_vproj = b.mat_t(full, W, E);
   const size_t o_tok = b.f32((int64_t)a.vocab_size * TW);
   const size_t o_tpos = b.f32((int64_t)a.context_length * TW);
-  build_tower(b, TW, a.text_layers, tlo);
+  build_tower(b, TW, a.text_layers, tlo, full);
   const size_t o_lnf_g = b.f32(TW), o_lnf_b = b.f32(TW);
-  const size_t o_tproj = b.bf16_t(TW, E);
+  const size_t o_tproj = b.mat_t(full, TW, E);
   const float* ls = b.take(1);
   if (!b.ok || b.pos != numel || !ls) {
     delete c;
@@ -265,25 +298,37 @@ int mi_clip_create(const mi_clip_arch* arch, const float* weights, int64_t numel
   char* d = c->wdev;
   auto F = [&](size_t o) { return (const float*)(d + o); };
   auto H = [&](size_t o) { return (const uint16_t*)(d + o); };
-  c->conv_w = H(o_conv);
+  c->conv_w = full ? nullptr : H(o_conv);
+  c->conv_f = full ? F(o_conv) : nullptr;
   c->cls = F(o_cls);
   c->vpos = F(o_vpos);
   c->ln_pre_g = F(o_lnpre_g);
   c->ln_pre_b = F(o_lnpre_b);
   c->ln_post_g = F(o_lnpost_g);
   c->ln_post_b = F(o_lnpost_b);
-  c->vproj_t = H(o_vproj);
+  c->vproj_t = full ? nullptr : H(o_vproj);
+  c->vproj_f = full ? F(o_vproj) : nullptr;
   c->tok_emb = F(o_tok);
   c->tpos = F(o_tpos);
   c->lnf_g = F(o_lnf_g);
   c->lnf_b = F(o_lnf_b);
-  c->tproj_t = H(o_tproj);
+  c->tproj_t = full ? nullptr : H(o_tproj);
+  c->tproj_f = full ? F(o_tproj) : nullptr;
   auto conv_layers = [&](const std::vector<LayerOff>& lo, std::vector<Layer>& L) {
     L.resize(lo.size());
     for (size_t i = 0; i < lo.size(); ++i) {
       const LayerOff& o = lo[i];
-      L[i] = Layer{F(o.ln1_g), F(o.ln1_b), F(o.b_qkv), F(o.b_out), F(o.ln2_g), F(o.ln2_b), F(o.b_fc), F(o.b_proj),
-                   H(o.w_qkv), H(o.w_out), H(o.w_fc), H(o.w_proj)};
+      if (full) {
+        L[i] = Layer{F(o.ln1_g), F(o.ln1_b), F(o.b_qkv), F(o.b_out), F(o.ln2_g), F(o.ln2_b), F(o.b_fc), F(o.b_proj),
+                     nullptr, nullptr, nullptr, nullptr};
+        L[i].f_qkv = F(o.w_qkv);
+        L[i].f_out = F(o.w_out);
+        L[i].f_fc = F(o.w_fc);
+        L[i].f_proj = F(o.w_proj);
+      } else {
+        L[i] = Layer{F(o.ln1_g), F(o.ln1_b), F(o.b_qkv), F(o.b_out), F(o.ln2_g), F(o.ln2_b), F(o.b_fc), F(o.b_proj),
+                     H(o.w_qkv), H(o.w_out), H(o.w_fc), H(o.w_proj)};
+      }
     }
   };
   conv_layers(vlo, c->vl);
@@ -352,14 +397,15 @@ static int reserve_locked(mi_clip* c, int64_t ic, int64_t tc) {
   const int64_t rows_max = mx(ic, tc);
   size_t off = 0;
   auto carve = [&](size_t bytes) { size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
+  const size_t es = c->f32 ? 4 : 2;   // activation element size (f32 mode: every buffer f32)
   const size_t o_x = carve(xw * 4);
-  const size_t o_h = carve(xw * 2);
-  const size_t o_qkv = carve(3 * xw * 2);
-  const size_t o_att = carve(xw * 2);
-  const size_t o_delta = carve(xw * 2);
-  const size_t o_mlp = carve(4 * xw * 2);
-  const size_t o_pat = carve((size_t)ic * c->G * c->G * c->Kp * 2);
-  const size_t o_cls = carve((size_t)rows_max * mx(Wv, Wt) * 2);
+  const size_t o_h = carve(xw * es);
+  const size_t o_qkv = carve(3 * xw * es);
+  const size_t o_att = carve(xw * es);
+  const size_t o_delta = c->f32 ? carve(0) : carve(xw * 2);
+  const size_t o_mlp = carve(4 * xw * es);
+  const size_t o_pat = carve((size_t)ic * c->G * c->G * (c->f32 ? c->Kp32 * 4 : c->Kp * 2));
+  const size_t o_cls = carve((size_t)rows_max * mx(Wv, Wt) * es);
   const size_t o_y = carve((size_t)rows_max * a.embed_dim * 4);
   size_t o_hq = 0, o_hqs = 0, o_attq = 0, o_attqs = 0, o_mlpq = 0, o_mlpqs = 0;
   if (c->fp8) {
@@ -548,11 +594,69 @@ static int run_tower_mx(mi_clip* c, const std::vector<Layer>& layers, int B, int
 
 static size_t dtype_size(int dt) { return dt == MI_F32 ? 4 : 2; }
 
+// The fp32 tower (weight_dtype MI_F32; kernels in precise.hip).  openai/CLIP
+// ResidualAttentionBlock with every tensor f32, the residual adds in the
+// out_proj / c_proj GEMM epilogues:
+//   h = ln_1(x) ; qkv = h W_qkv^T + b ; att = MHA(qkv) ; x += att W_o^T + b_o
+//   h = ln_2(x) ; m = QuickGELU(h W_fc^T + b_fc) ; x += m W_pr^T + b_pr
+static int run_tower_f32(mi_clip* c, const std::vector<Layer>& layers, int B, int S, int W, int causal,
+                         hipStream_t s) {
+  const int M = B * S;
+  float* h = (float*)c->h;
+  float* qkv = (float*)c->qkv;
+  float* att = (float*)c->att;
+  float* mlp = (float*)c->mlp;
+  for (const Layer& L : layers) {
+    HIP_TRY(layernorm_f32(c->x, W, L.ln1_g, L.ln1_b, h, W, M, W, s));
+    HIP_TRY(gemm_f32(h, W, L.f_qkv, W, L.b_qkv, qkv, 3 * W, M, 3 * W, W, EPI_F32, s));
+    HIP_TRY(attention_f32(qkv, att, B, S, W, causal, s));
+    HIP_TRY(gemm_f32(att, W, L.f_out, W, L.b_out, c->x, W, M, W, W, EPI_RESID_F32, s));
+    HIP_TRY(layernorm_f32(c->x, W, L.ln2_g, L.ln2_b, h, W, M, W, s));
+    HIP_TRY(gemm_f32(h, W, L.f_fc, W, L.b_fc, mlp, 4 * W, M, 4 * W, W, EPI_GELU_BF16, s));
+    HIP_TRY(gemm_f32(mlp, 4 * W, L.f_proj, 4 * W, L.b_proj, c->x, W, M, W, 4 * W, EPI_RESID_F32, s));
+  }
+  return MI_OK;
+}
+
+static int encode_image_f32(mi_clip* c, const char* px, int nb, int in_dtype, char* out, int out_dtype,
+                            int l2_normalize, hipStream_t s) {
+  const mi_clip_arch& a = c->a;
+  const int W = a.vision_width, E = a.embed_dim, S = c->S_v, R = a.image_resolution, P = a.vision_patch_size;
+  const int G2 = c->G * c->G;
+  float* patches = (float*)c->patches;
+  HIP_TRY(im2col_f32(px, in_dtype == MI_BF16, patches, nb, R, P, c->Kp32, s));
+  HIP_TRY(gemm_f32(patches, c->Kp32, c->conv_f, c->Kp32, nullptr, c->x, W, nb * G2, W, c->Kp32, EPI_F32, s, G2, S,
+                   1));
+  HIP_TRY(vision_embed_ln(c->x, c->cls, c->vpos, c->ln_pre_g, c->ln_pre_b, nb, S, W, s));
+  int r = run_tower_f32(c, c->vl, nb, S, W, 0, s);
+  if (r) return r;
+  float* cls = (float*)c->cls_ln;
+  HIP_TRY(layernorm_f32(c->x, (int64_t)S * W, c->ln_post_g, c->ln_post_b, cls, W, nb, W, s));
+  HIP_TRY(gemm_f32(cls, W, c->vproj_f, W, nullptr, c->y, E, nb, E, W, EPI_F32, s));
+  HIP_TRY(finalize_rows(c->y, out, out_dtype, nb, E, l2_normalize, s));
+  return MI_OK;
+}
+
+static int encode_text_f32(mi_clip* c, const int32_t* tk, int nq, char* out, int out_dtype, int l2_normalize,
+                           hipStream_t s) {
+  const mi_clip_arch& a = c->a;
+  const int W = a.text_width, E = a.embed_dim, S = a.context_length;
+  HIP_TRY(text_embed(tk, c->tok_emb, c->tpos, c->x, nq, S, W, a.vocab_size, s));
+  int r = run_tower_f32(c, c->tl, nq, S, W, 1, s);
+  if (r) return r;
+  float* cls = (float*)c->cls_ln;
+  HIP_TRY(layernorm_f32(c->x, W, c->lnf_g, c->lnf_b, cls, W, nq, W, s, tk, S));
+  HIP_TRY(gemm_f32(cls, W, c->tproj_f, W, nullptr, c->y, E, nq, E, W, EPI_F32, s));
+  HIP_TRY(finalize_rows(c->y, out, out_dtype, nq, E, l2_normalize, s));
+  return MI_OK;
+}
+
 int mi_clip_encode_image(mi_clip* c, const void* pixels, int64_t B, int in_dtype, void* out, int out_dtype,
                          int l2_normalize, void* stream) {
   if (!c || (!pixels && B > 0) || (!out && B > 0) || B < 0) return fail(MI_ERR_ARG, "encode_image: bad arguments");
   if (in_dtype != MI_F32 && in_dtype != MI_BF16) return fail(MI_ERR_ARG, "encode_image: in_dtype must be f32/bf16");
   if (out_dtype < MI_F32 || out_dtype > MI_F16) return fail(MI_ERR_ARG, "encode_image: bad out_dtype");
+  if (l2_normalize < 0 || l2_normalize > 2) return fail(MI_ERR_ARG, "encode_image: l2_normalize must be 0, 1 or 2");
   std::lock_guard<std::mutex> g(c->mu);
   if (!c->ws) {
     int r = reserve_locked(c, 256, 64);
@@ -568,6 +672,12 @@ int mi_clip_encode_image(mi_clip* c, const void* pixels, int64_t B, int in_dtype
   for (int64_t c0 = 0; c0 < B; c0 += c->img_chunk) {
     const int nb = (int)((B - c0) < c->img_chunk ? (B - c0) : c->img_chunk);
     const char* px = (const char*)pixels + c0 * in_img;
+    if (c->f32) {
+      int r = encode_image_f32(c, px, nb, in_dtype, (char*)out + c0 * E * dtype_size(out_dtype), out_dtype,
+                               l2_normalize, s);
+      if (r) return r;
+      continue;
+    }
     const bool fused = patch_fused() && in_dtype == MI_BF16 && P == 32 && c->Kp == 3 * P * P && R % 8 == 0 &&
                        ((uintptr_t)px & 15) == 0 && (int64_t)nb * G2 >= 1024;
     GemmArgs pg;
@@ -603,6 +713,7 @@ int mi_clip_encode_text(mi_clip* c, const int32_t* tokens, int64_t Q, void* out,
                         void* stream) {
   if (!c || (!tokens && Q > 0) || (!out && Q > 0) || Q < 0) return fail(MI_ERR_ARG, "encode_text: bad arguments");
   if (out_dtype < MI_F32 || out_dtype > MI_F16) return fail(MI_ERR_ARG, "encode_text: bad out_dtype");
+  if (l2_normalize < 0 || l2_normalize > 2) return fail(MI_ERR_ARG, "encode_text: l2_normalize must be 0, 1 or 2");
   std::lock_guard<std::mutex> g(c->mu);
   if (!c->ws) {
     int r = reserve_locked(c, 256, 64);
@@ -616,6 +727,11 @@ int mi_clip_encode_text(mi_clip* c, const int32_t* tokens, int64_t Q, void* out,
   for (int64_t c0 = 0; c0 < Q; c0 += c->txt_chunk) {
     const int nq = (int)((Q - c0) < c->txt_chunk ? (Q - c0) : c->txt_chunk);
     const int32_t* tk = tokens + c0 * S;
+    if (c->f32) {
+      int r = encode_text_f32(c, tk, nq, (char*)out + c0 * E * dtype_size(out_dtype), out_dtype, l2_normalize, s);
+      if (r) return r;
+      continue;
+    }
     HIP_TRY(text_embed(tk, c->tok_emb, c->tpos, c->x, nq, S, W, a.vocab_size, s));
     int r = run_tower(c, c->tl, nq, S, W, 1, s);
     if (r) return r;
@@ -741,6 +857,16 @@ int mi_op_gemm(const void* A, const void* W, const float* bias, void* out, int32
   GemmArgs g = gargs((const uint16_t*)A, K, (const uint16_t*)W, K, bias, out, N, M, N, K);
   if (variant) g.variant = variant;
   HIP_TRY(gemm_bf16(g, epi, (hipStream_t)stream));
+  return MI_OK;
+}
+
+int mi_op_gemm_f32(const float* A, const float* W, const float* bias, float* out, int32_t M, int32_t N, int32_t K,
+                   int32_t epi, void* stream) {
+  if (!A || !W || !out || M < 0 || N < 1) return fail(MI_ERR_ARG, "mi_op_gemm_f32: bad arguments");
+  if (K % 32 || K <= 0) return fail(MI_ERR_UNSUPPORTED, "mi_op_gemm_f32: needs K %% 32 == 0");
+  static const int epis[4] = {EPI_F32, EPI_GELU_BF16, EPI_RESID_F32, EPI_RELU_F32};
+  if (epi < 0 || epi > 3) return fail(MI_ERR_ARG, "mi_op_gemm_f32: epilogue 0 (store), 1 (QuickGELU), 2 (+=), 3 (ReLU)");
+  HIP_TRY(gemm_f32(A, K, W, K, bias, out, N, M, N, K, epis[epi], (hipStream_t)stream));
   return MI_OK;
 }
 

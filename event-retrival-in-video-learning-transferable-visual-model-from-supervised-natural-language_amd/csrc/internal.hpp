@@ -10,7 +10,8 @@ enum GemmEpi {
   EPI_GELU_BF16 = 1,   // out bf16 = quick_gelu(acc + bias)
   EPI_RESID_F32 = 2,   // out f32 += acc + bias   (residual stream, in place)
   EPI_F32 = 3,         // out f32 = acc (+ bias)
-  EPI_GELU_MX = 4      // MX-fp8 GEMM only: out e4m3 = MX(quick_gelu(acc + bias)), scales -> o_scale
+  EPI_GELU_MX = 4,     // MX-fp8 GEMM only: out e4m3 = MX(quick_gelu(acc + bias)), scales -> o_scale
+  EPI_RELU_F32 = 5     // f32 GEMM only: out f32 = max(acc + bias, 0)
 };
 
 // MX block quantisation shared by the fp8 producers (gemm_mx.hip, encoder.hip):
@@ -123,6 +124,22 @@ hipError_t attention(const uint16_t* qkv, uint16_t* out, int B, int S, int W, in
 // y [rows, D] f32 -> out (f32/bf16/f16), optional L2 normalisation
 hipError_t finalize_rows(const float* y, void* out, int out_dtype, int rows, int D, int l2,
                          hipStream_t s);
+
+// ---- fp32 tower (precise.hip; weight_dtype MI_F32) ----
+// out = A[M,K] . W[N,K]^T (+bias), all f32, K % 32 == 0; epi EPI_F32 (store),
+// EPI_GELU_BF16 (QuickGELU, stored f32), EPI_RESID_F32 (out += ...); group /
+// gstride / goffset remap output rows as GemmArgs does
+hipError_t gemm_f32(const float* A, int64_t lda, const float* W, int64_t ldw, const float* bias, float* out,
+                    int64_t ldo, int M, int N, int K, int epi, hipStream_t s, int group = 0, int gstride = 0,
+                    int goffset = 0);
+// out[r] = LN(x[r * in_stride]) f32; tokens != nullptr: source row r*S + argmax(tokens[r]) (EOT pooling)
+hipError_t layernorm_f32(const float* x, int64_t in_stride, const float* g, const float* b, float* out,
+                         int64_t out_stride, int rows, int W, hipStream_t s, const int32_t* tokens = nullptr,
+                         int S = 0);
+// MHA core over qkv f32 [B*S, 3W] -> out f32 [B*S, W], head dim 64
+hipError_t attention_f32(const float* qkv, float* out, int B, int S, int W, int causal, hipStream_t s);
+// pixels [B,3,R,R] (f32 / bf16) -> patches f32 [B*G*G, Kp]
+hipError_t im2col_f32(const void* pixels, int in_bf16, float* out, int B, int R, int P, int Kp, hipStream_t s);
 
 }  // namespace miclip
 

@@ -1,0 +1,318 @@
+// fp32 tower kernels (gfx950): the weight_dtype MI_F32 mode of mi_clip_create.
+//
+// openai/CLIP computes in fp32 when its weights are fp32: on the CPU
+// (clip.load(device="cpu") calls model.float(); Backend/embedding.py:21-22 is
+// BASELINE configs[0]) and after `clip_model.float()` (CLIPWithClassifier,
+// Backend/services/embedding_service.py:22).  compare_models.py's R@K flow
+// (:908-1100) run on a CPU is this arithmetic too.  This mode keeps every
+// activation and weight in f32 so that encoder outputs sit within f32 rounding
+// of the reference's and R@1/5/10 come out identical (miclip/evaluate.py,
+// tests/test_gpu_rk_flow.py), at the f32 MFMA rate (157 TF, 1/16 of bf16).
+//
+//   gemm_f32   out = A[M,K] . W[N,K]^T (+bias) on v_mfma_f32_32x32x2_f32 (exact f32
+//              products, f32 accumulation); epilogues: store, QuickGELU, residual add
+//   ln_f32     LayerNorm rows in f32 -> f32 (optionally the EOT row of each token row)
+//   attn_f32   softmax(q k^T / 8 [+ causal]) v per (sequence, head), f32
+//   im2col_f32 conv1 patches in f32
+#include "common.hpp"
+#include "internal.hpp"
+
+namespace miclip {
+namespace {
+
+constexpr float LN_EPS = 1e-5f;
+
+// ------------------------------------------------------------------ GEMM
+// 128 x 128 tile, K staged 32 wide through LDS (register prefetch of the next
+// stage), 4 waves as 2 x 2, each wave 64 x 64 = 2 x 2 blocks of the 32x32x2
+// MFMA.  Lane (r = lane & 31, h = lane >> 5) feeds A[row r][k = 16h + i] and
+// W[col r][k = 16h + i] to MFMA i, so 16 MFMAs cover the stage's 32 k.
+constexpr int GT = 128, GK = 32, GLD = GK + 4;
+
+template <int EPI>
+__global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__ A, int64_t lda,
+                                                       const float* __restrict__ W, int64_t ldw,
+                                                       const float* __restrict__ bias, float* __restrict__ out,
+                                                       int64_t ldo, int M, int N, int K, int group, int gstride,
+                                                       int goffset) {
+  __shared__ __attribute__((aligned(16))) float As[GT * GLD];
+  __shared__ __attribute__((aligned(16))) float Ws[GT * GLD];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int m0 = blockIdx.y * GT, n0 = blockIdx.x * GT;
+  // staging: thread t loads rows t/8 + 32 j (j = 0..3), 4 k at 4 (t % 8)
+  const int lr = tid >> 3, lk = (tid & 7) * 4;
+  const float* ap[4];
+  const float* wp[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int r = lr + 32 * j;
+    ap[j] = A + (int64_t)min(m0 + r, M - 1) * lda + lk;
+    wp[j] = W + (int64_t)min(n0 + r, N - 1) * ldw + lk;
+  }
+  float4 ra[4], rw[4];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      ra[j] = *(const float4*)(ap[j] + k0);
+      rw[j] = *(const float4*)(wp[j] + k0);
+    }
+  };
+  auto sstore = [&]() {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      *(float4*)&As[(lr + 32 * j) * GLD + lk] = ra[j];
+      *(float4*)&Ws[(lr + 32 * j) * GLD + lk] = rw[j];
+    }
+  };
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = f32x16{};
+  const int r = lane & 31, h = lane >> 5;
+  const int nk = K / GK;
+  gload(0);
+  sstore();
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) gload((kt + 1) * GK);
+    float fa[2][16], fw[2][16];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float4 va = *(const float4*)&As[(64 * wm + 32 * a + r) * GLD + 16 * h + 4 * i];
+        const float4 vw = *(const float4*)&Ws[(64 * wn + 32 * a + r) * GLD + 16 * h + 4 * i];
+        fa[a][4 * i] = va.x; fa[a][4 * i + 1] = va.y; fa[a][4 * i + 2] = va.z; fa[a][4 * i + 3] = va.w;
+        fw[a][4 * i] = vw.x; fw[a][4 * i + 1] = vw.y; fw[a][4 * i + 2] = vw.z; fw[a][4 * i + 3] = vw.w;
+      }
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[a][i], fw[b][i], acc[a][b], 0, 0, 0);
+    __syncthreads();
+    if (kt + 1 < nk) {
+      sstore();
+      __syncthreads();
+    }
+  }
+  // epilogue: C layout col = lane & 31, row = (q & 3) + 8 (q >> 2) + 4 h
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    const int n = n0 + 64 * wn + 32 * b + r;
+    if (n >= N) continue;
+    const float bv = bias ? bias[n] : 0.f;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int m = m0 + 64 * wm + 32 * a + (q & 3) + 8 * (q >> 2) + 4 * h;
+        if (m >= M) continue;
+        const int64_t orow = group ? (int64_t)(m / group) * gstride + goffset + m % group : m;
+        float v = acc[a][b][q] + bv;
+        float* o = out + orow * ldo + n;
+        if (EPI == EPI_GELU_BF16) v = v * (1.0f / (1.0f + expf(-1.702f * v)));   // QuickGELU x * sigmoid(1.702 x)
+        if (EPI == EPI_RELU_F32) v = fmaxf(v, 0.f);
+        if (EPI == EPI_RESID_F32) *o = *o + v;
+        else *o = v;
+      }
+  }
+}
+
+// ------------------------------------------------------------- LayerNorm
+// One wave per row, W <= 1024, two-pass mean / variance in f32 (torch's
+// LayerNorm on fp32).  tokens != nullptr: row q of the output is the row
+// q * S + argmax(tokens[q]) of x (text pooling at EOT, first index on ties).
+__global__ __launch_bounds__(256) void ln_f32_kernel(const float* __restrict__ x, int64_t in_stride,
+                                                     const float* __restrict__ g, const float* __restrict__ b,
+                                                     float* __restrict__ out, int64_t out_stride, int rows, int W,
+                                                     const int32_t* __restrict__ tokens, int S) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  int64_t src = (int64_t)row * in_stride;
+  if (tokens) {
+    int best = -2147483647 - 1, bi = 0x7fffffff;
+    for (int t = lane; t < S; t += 64) {
+      const int v = tokens[(int64_t)row * S + t];
+      if (v > best || (v == best && t < bi)) { best = v; bi = t; }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      const int ov = __shfl_xor(best, o, 64), oi = __shfl_xor(bi, o, 64);
+      if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
+    }
+    src = ((int64_t)row * S + bi) * in_stride;
+  }
+  const float* xr = x + src;
+  float v[16];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int c = lane + 64 * i;
+    v[i] = c < W ? xr[c] : 0.f;
+    s += v[i];
+  }
+  const float mean = wave_sum(s) / (float)W;
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int c = lane + 64 * i;
+    if (c < W) ss += (v[i] - mean) * (v[i] - mean);
+  }
+  const float rstd = 1.0f / sqrtf(wave_sum(ss) / (float)W + LN_EPS);
+  float* o = out + (int64_t)row * out_stride;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int c = lane + 64 * i;
+    if (c < W) o[c] = (v[i] - mean) * rstd * g[c] + b[c];
+  }
+}
+
+// ------------------------------------------------------------- attention
+// One workgroup per (sequence, head); a thread owns one query row (q scaled
+// by 1/8 = head_dim^-1/2, exact), keys and values stream through LDS in
+// chunks of 64 with an online softmax (per-chunk max, one rescale per chunk).
+template <int NT>
+__global__ __launch_bounds__(NT) void attn_f32_kernel(const float* __restrict__ qkv, float* __restrict__ out, int S,
+                                                      int W, int causal) {
+  __shared__ float Ks[64 * 64];
+  __shared__ float Vs[64 * 64];
+  const int H = W / 64;
+  const int bseq = blockIdx.x / H, head = blockIdx.x % H;
+  const int64_t ld = 3 * (int64_t)W;
+  const float* base = qkv + (int64_t)bseq * S * ld;
+  const int tid = threadIdx.x;
+  for (int q0 = 0; q0 < S; q0 += NT) {
+    const int qi = q0 + tid;
+    const bool valid = qi < S;
+    float qv[64], acc[64];
+    float m = -INFINITY, l = 0.f;
+#pragma unroll
+    for (int d = 0; d < 64; ++d) {
+      qv[d] = valid ? base[(int64_t)qi * ld + head * 64 + d] * 0.125f : 0.f;
+      acc[d] = 0.f;
+    }
+    const int kend = causal ? min(S, q0 + NT) : S;
+    for (int k0 = 0; k0 < kend; k0 += 64) {
+      __syncthreads();
+      for (int e = tid; e < 64 * 64; e += NT) {
+        const int j = e >> 6, d = e & 63;
+        const bool in = k0 + j < S;
+        Ks[e] = in ? base[(int64_t)(k0 + j) * ld + W + head * 64 + d] : 0.f;
+        Vs[e] = in ? base[(int64_t)(k0 + j) * ld + 2 * W + head * 64 + d] : 0.f;
+      }
+      __syncthreads();
+      float s[64];
+      float cmax = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < 64; ++j) {
+        float t = 0.f;
+#pragma unroll
+        for (int d = 0; d < 64; ++d) t = fmaf(qv[d], Ks[j * 64 + d], t);
+        const bool ok = k0 + j < S && (!causal || k0 + j <= qi);
+        s[j] = ok ? t : -INFINITY;
+        cmax = fmaxf(cmax, s[j]);
+      }
+      if (!valid || cmax == -INFINITY) continue;
+      const float mn = fmaxf(m, cmax);
+      const float corr = expf(m - mn);
+      l *= corr;
+#pragma unroll
+      for (int d = 0; d < 64; ++d) acc[d] *= corr;
+#pragma unroll
+      for (int j = 0; j < 64; ++j) {
+        const float p = expf(s[j] - mn);
+        l += p;
+#pragma unroll
+        for (int d = 0; d < 64; ++d) acc[d] = fmaf(p, Vs[j * 64 + d], acc[d]);
+      }
+      m = mn;
+    }
+    if (valid) {
+      const float inv = 1.0f / l;
+      float* o = out + ((int64_t)bseq * S + qi) * W + head * 64;
+#pragma unroll
+      for (int d = 0; d < 64; ++d) o[d] = acc[d] * inv;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ im2col
+// patches [B*G*G, Kp] f32, k = c*P*P + kh*P + kw (conv1 weight order), zero pad.
+__global__ __launch_bounds__(256) void im2col_f32_kernel(const void* __restrict__ pixels, int in_bf16,
+                                                         float* __restrict__ out, int64_t total, int R, int P, int G,
+                                                         int Kp) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int64_t prow = i / Kp;
+  const int k = (int)(i % Kp);
+  const int PP = P * P;
+  float v = 0.f;
+  if (k < 3 * PP) {
+    const int64_t bimg = prow / (G * G);
+    const int p = (int)(prow % (G * G));
+    const int gy = p / G, gx = p % G;
+    const int c = k / PP, rem = k % PP, kh = rem / P, kw = rem % P;
+    const int64_t off = ((bimg * 3 + c) * R + (gy * P + kh)) * (int64_t)R + gx * P + kw;
+    v = in_bf16 ? bf2f(((const uint16_t*)pixels)[off]) : ((const float*)pixels)[off];
+  }
+  out[i] = v;
+}
+
+}  // namespace
+
+hipError_t gemm_f32(const float* A, int64_t lda, const float* W, int64_t ldw, const float* bias, float* out,
+                    int64_t ldo, int M, int N, int K, int epi, hipStream_t s, int group, int gstride, int goffset) {
+  if (M <= 0 || N <= 0) return hipSuccess;
+  if (K <= 0 || K % GK || lda % 4 || ldw % 4) return hipErrorInvalidValue;
+  const dim3 grid((N + GT - 1) / GT, (M + GT - 1) / GT), block(256);
+  if (epi == EPI_F32)
+    hipLaunchKernelGGL(gemm_f32_kernel<EPI_F32>, grid, block, 0, s, A, lda, W, ldw, bias, out, ldo, M, N, K, group,
+                       gstride, goffset);
+  else if (epi == EPI_GELU_BF16)
+    hipLaunchKernelGGL(gemm_f32_kernel<EPI_GELU_BF16>, grid, block, 0, s, A, lda, W, ldw, bias, out, ldo, M, N, K,
+                       group, gstride, goffset);
+  else if (epi == EPI_RELU_F32)
+    hipLaunchKernelGGL(gemm_f32_kernel<EPI_RELU_F32>, grid, block, 0, s, A, lda, W, ldw, bias, out, ldo, M, N, K,
+                       group, gstride, goffset);
+  else if (epi == EPI_RESID_F32)
+    hipLaunchKernelGGL(gemm_f32_kernel<EPI_RESID_F32>, grid, block, 0, s, A, lda, W, ldw, bias, out, ldo, M, N, K,
+                       group, gstride, goffset);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+hipError_t layernorm_f32(const float* x, int64_t in_stride, const float* g, const float* b, float* out,
+                         int64_t out_stride, int rows, int W, hipStream_t s, const int32_t* tokens, int S) {
+  if (rows <= 0) return hipSuccess;
+  if (W > 1024 || W < 1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(ln_f32_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, x, in_stride, g, b, out, out_stride, rows,
+                     W, tokens, S);
+  return hipGetLastError();
+}
+
+hipError_t attention_f32(const float* qkv, float* out, int B, int S, int W, int causal, hipStream_t s) {
+  if (B <= 0) return hipSuccess;
+  if (W % 64 || S < 1) return hipErrorInvalidValue;
+  const dim3 grid((unsigned)B * (W / 64));
+  if (S <= 64)
+    hipLaunchKernelGGL(attn_f32_kernel<64>, grid, dim3(64), 0, s, qkv, out, S, W, causal);
+  else
+    hipLaunchKernelGGL(attn_f32_kernel<256>, grid, dim3(256), 0, s, qkv, out, S, W, causal);
+  return hipGetLastError();
+}
+
+hipError_t im2col_f32(const void* pixels, int in_bf16, float* out, int B, int R, int P, int Kp, hipStream_t s) {
+  const int G = R / P;
+  const int64_t total = (int64_t)B * G * G * Kp;
+  if (total <= 0) return hipSuccess;
+  hipLaunchKernelGGL(im2col_f32_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, pixels, in_bf16, out,
+                     total, R, P, G, Kp);
+  return hipGetLastError();
+}
+
+}  // namespace miclip

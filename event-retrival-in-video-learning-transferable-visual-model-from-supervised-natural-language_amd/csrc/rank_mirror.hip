@@ -26,8 +26,9 @@
 //   outside row can reach (or tie) the top-k: the result is then bit-identical
 //   to mi_rank_topk over the master.  Uncertified queries (near-ties across the
 //   candidate edge, non-finite scores) are flagged for the exact pass.
-// delta (per query, |q| its f32 norm): the mirror rounding 2^-12 (fp16 RNE of
-//   a unit row, relative), the query split (2^-22 SPLIT / 2^-11 hi only), the
+// delta (per query, |q| its f32 norm): the mirror rounding 2^-11 (fp16 RNE of
+//   a unit row: the unit roundoff of an 11-bit significand, per element
+//   |m_i - u_i| <= 2^-11 |u_i|, so |q.m - q.u| <= 2^-11 |q| by Cauchy-Schwarz), the query split (2^-22 SPLIT / 2^-11 hi only), the
 //   f32 accumulation of both paths (bounded by 8 D 2^-24, covering the fp16
 //   MFMA's internal sums), the subnormal floor 2^-25 sqrt(D) on both sides; the
 //   sum is scaled by 1.25.
@@ -403,11 +404,23 @@ hipError_t mirror_build(const void* master, int64_t N, int64_t D, int dt, uint16
 // delta = d_rel |q| + d_abs (file comment)
 static void mirror_delta(int64_t D, bool split, float& d_rel, float& d_abs) {
   const double sq = std::sqrt((double)D) * std::ldexp(1.0, -25);
-  const double rel = std::ldexp(1.0, -12) + (split ? std::ldexp(1.0, -22) : std::ldexp(1.0, -11)) +
+  const double rel = std::ldexp(1.0, -11) + (split ? std::ldexp(1.0, -22) : std::ldexp(1.0, -11)) +
                      8.0 * (double)D * std::ldexp(1.0, -24) + sq;
   d_rel = (float)(1.25 * rel);
   d_abs = (float)(1.25 * sq);
 }
+
+}  // namespace miclip
+
+// Diagnostics (not part of include/miclip.h): the certificate's delta terms, so
+// a host test can hold them against the analytic worst case (tests/test_abi.py).
+extern "C" int mi_debug_mirror_delta(int64_t D, int split, float* d_rel, float* d_abs) {
+  if (!d_rel || !d_abs || D < 1) return -1;   // MI_ERR_ARG
+  miclip::mirror_delta(D, split != 0, *d_rel, *d_abs);
+  return 0;
+}
+
+namespace miclip {
 
 template <int D, bool SPLIT>
 static hipError_t launch_mirror(const uint16_t* mirror, int64_t N, const float* q, int64_t Q, int kc, int nf,

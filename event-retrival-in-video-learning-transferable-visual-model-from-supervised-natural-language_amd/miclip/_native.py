@@ -27,7 +27,7 @@ EXPORTS = (
     "mi_abi_version", "mi_last_error", "mi_clip_weights_numel", "mi_clip_create", "mi_clip_destroy",
     "mi_clip_reserve", "mi_clip_encode_image", "mi_clip_encode_text", "mi_rank_workspace_bytes",
     "mi_rank_topk", "mi_rank_merge", "mi_score_matrix", "mi_rank_of_targets",
-    "mi_op_gemm", "mi_op_layernorm", "mi_op_attention", "mi_op_residual_ln",
+    "mi_op_gemm", "mi_op_gemm_f32", "mi_op_layernorm", "mi_op_attention", "mi_op_residual_ln",
     "mi_resample_coeffs", "mi_preprocess_workspace_bytes", "mi_preprocess_frames",
     "mi_jpeg_workspace_bytes", "mi_jpeg_decode",
     "mi_op_quantize_mx", "mi_op_gemm_mx",
@@ -91,6 +91,7 @@ def lib():
         "mi_score_matrix": (ctypes.c_int, [P, I64, I64, ctypes.c_int, P, I64, ctypes.c_int, P, P]),
         "mi_rank_of_targets": (ctypes.c_int, [P, I64, I64, P, P, I64, P, P]),
         "mi_op_gemm": (ctypes.c_int, [P, P, P, P, I32, I32, I32, I32, P]),
+        "mi_op_gemm_f32": (ctypes.c_int, [P, P, P, P, I32, I32, I32, I32, P]),
         "mi_op_layernorm": (ctypes.c_int, [P, P, P, P, I32, I32, P]),
         "mi_op_attention": (ctypes.c_int, [P, P, I32, I32, I32, I32, P]),
         "mi_op_residual_ln": (ctypes.c_int, [P, P, P, P, P, I32, I32, I32, P]),

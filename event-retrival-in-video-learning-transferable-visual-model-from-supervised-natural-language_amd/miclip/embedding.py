@@ -37,13 +37,15 @@ def walk_frames(folder_path):
 
 
 def extract_and_save_embeddings_from_folder(folder_path, model_name, video_name=None, output_dir="embedding",
-                                            batch_size=256, model=None, preprocess=None):
+                                            batch_size=256, model=None, preprocess=None, weights="bf16"):
+    """``weights="fp32"`` runs the reference's CPU arithmetic (configs[0]: the
+    fp32 model ``clip.load`` builds on a CPU) on the fp32 tower."""
     import torch
     from PIL import Image
 
     if model is None:
         device = "cuda" if torch.cuda.is_available() else "cpu"
-        model, preprocess = api.load(model_name, device=device)
+        model, preprocess = api.load(model_name, device=device, weights=weights)
     os.makedirs(output_dir, exist_ok=True)
     if not video_name:
         video_name = Path(folder_path).name

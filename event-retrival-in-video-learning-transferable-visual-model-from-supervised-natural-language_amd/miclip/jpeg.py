@@ -161,6 +161,7 @@ def _parse(buf, check_eoi=True) -> JpegHeader:
         return h
     i = 2
     adobe_transform = None
+    jfif = False
     while i + 4 <= len(buf):
         if buf[i] != 0xFF:
             h.why = "bad marker"
@@ -209,6 +210,8 @@ def _parse(buf, check_eoi=True) -> JpegHeader:
                 j += 17 + n
         elif m == 0xDD:                                   # DRI
             h.ri = struct.unpack(">H", seg[:2])[0]
+        elif m == 0xE0 and seg[:5] == b"JFIF\x00":
+            jfif = True
         elif m == 0xEE and seg[:5] == b"Adobe" and len(seg) >= 12:
             adobe_transform = seg[11]
         elif m == 0xDA:                                   # SOS
@@ -234,6 +237,11 @@ def _parse(buf, check_eoi=True) -> JpegHeader:
             if h.ncomp == 3:
                 if adobe_transform == 0:
                     h.why = "Adobe RGB (no YCbCr transform)"
+                    return h
+                # libjpeg default_decompress_parms guesses the colour space from the component ids
+                # when there is neither a JFIF nor an Adobe marker ('R','G','B' -> no transform)
+                if not jfif and adobe_transform is None and tuple(c[0] for c in comps) != (1, 2, 3):
+                    h.why = "no JFIF / Adobe marker and component ids other than 1, 2, 3"
                     return h
                 if h.samp[1] != (1, 1) or h.samp[2] != (1, 1) or h.samp[0] not in ((1, 1), (2, 1), (2, 2)):
                     h.why = f"sampling {h.samp}"
@@ -264,6 +272,21 @@ def _parse(buf, check_eoi=True) -> JpegHeader:
         i += 2 + ln
     h.why = h.why or "no scan"
     return h
+
+
+def decoded_bytes(h) -> int:
+    """Device bytes one frame holds while ``mi_jpeg_decode`` runs: the RGB
+    output plus the coefficient workspace (int16 + 1 byte per sample of every
+    component block, ``jpeg_workspace_bytes``); host-decoded frames hold their
+    RGB only."""
+    W, H = max(h.width, 1), max(h.height, 1)
+    if not h.supported:
+        return 3 * W * H
+    hs = [s[0] for s in h.samp] if h.ncomp == 3 else [1]
+    vs = [s[1] for s in h.samp] if h.ncomp == 3 else [1]
+    mcux, mcuy = -(-W // (8 * max(hs))), -(-H // (8 * max(vs)))
+    blocks = sum(mcux * a * mcuy * b for a, b in zip(hs, vs))
+    return 3 * W * H + 192 * blocks
 
 
 def _geom_key(h):
@@ -332,16 +355,29 @@ def decode_batch(bufs, device="cuda", dedupe=True):
     file neither path can read) in input order; frames of one geometry are
     decoded in one launch.  ``dedupe=False`` passes one table set per frame
     (no index array: the kernel's global-memory table path)."""
+    out = [None] * len(bufs)
+    for idx, rgb in decode_groups(bufs, device, dedupe=dedupe):
+        if rgb is not None:
+            for r, i in enumerate(idx):
+                out[i] = rgb[r]
+    return out
+
+
+def decode_groups(bufs, device="cuda", dedupe=True, heads=None):
+    """``decode_batch`` by launch: yields (indices, uint8 [len(indices), H, W, 3]
+    device tensor) per geometry group in one buffer (frames the host decodes
+    come one per group; (indices, None) for a file neither path can read), so a
+    consumer can take each group's frames without restacking them."""
     import torch
     L = N.lib()
-    heads = [parse(b) for b in bufs]
-    out = [None] * len(bufs)
+    if heads is None:
+        heads = [parse(b) for b in bufs]
     groups = {}
     for i, h in enumerate(heads):
         if h.supported:
             groups.setdefault(_geom_key(h), []).append(i)
         else:
-            out[i] = _host_decode(bufs[i], device)
+            yield _host_group(bufs, i, device)
     dev = torch.device(device)
     for key, idx in groups.items():
         W, H, nc, samp, ri = key
@@ -355,7 +391,7 @@ def decode_batch(bufs, device="cuda", dedupe=True):
             if ri:
                 segs = _segments(bufs[i], h)
                 if len(segs) != nseg:     # restart markers not where DRI says: leave it to the host decoder
-                    out[i] = _host_decode(bufs[i], device)
+                    yield _host_group(bufs, i, device)
                     continue
             else:
                 segs = ((h.scan_start, len(bufs[i])),)
@@ -406,8 +442,8 @@ def decode_batch(bufs, device="cuda", dedupe=True):
         # per-frame table selectors must agree within the group (they come from the SOS / SOF)
         sel_ok = [heads[i].qsel == h0.qsel and heads[i].dcsel == h0.dcsel and heads[i].acsel == h0.acsel for i in keep]
         if not all(sel_ok):
-            for i, ok in zip(keep, sel_ok):
-                out[i] = _host_decode(bufs[i], device)
+            for i in keep:
+                yield _host_group(bufs, i, device)
             continue
         d_data = _upload(bufs, keep, segl, starts, total, dev)
         d_off = torch.as_tensor(np.asarray(offs, np.int64)).to(dev)
@@ -427,9 +463,13 @@ def decode_batch(bufs, device="cuda", dedupe=True):
         N.check(L.mi_jpeg_decode(d_data.data_ptr(), d_off.data_ptr(), d_end.data_ptr(), d_huff.data_ptr(),
                                  d_hidx.data_ptr() if dedupe else None, len(sets), d_qt.data_ptr(), gp, B, rgb.data_ptr(), ws.data_ptr(), nb,
                                  N.stream_ptr(dev)), "mi_jpeg_decode")
-        for r, i in enumerate(keep):
-            out[i] = rgb[r]
-    return out
+        del ws, d_data
+        yield keep, rgb
+
+
+def _host_group(bufs, i, device):
+    t = _host_decode(bufs[i], device)
+    return [i], (t.unsqueeze(0) if t is not None else None)
 
 
 def _host_decode(buf, device):

@@ -5,7 +5,8 @@
   model.encode_text(tokens)        embedding_service.py:174,177, compare_models.py:1204
   model.visual.output_dim          embedding_service.py:25
   model.logit_scale                embedding_service.py:34
-  model.float() / .eval() / .to()  embedding_service.py:22, :118-119
+  model.float() / .eval() / .to()  embedding_service.py:22, :118-119 (float(): the fp32 tower, as
+                                   openai/CLIP's float() makes every weight and activation fp32)
   model.state_dict() / load_state_dict()  (OpenAI keys; CLIPWithClassifier wraps them as clip_model.*)
   model(image, text)               -> (logits_per_image, logits_per_text)
 
@@ -23,6 +24,14 @@ from . import _native as N
 from .config import CLIPConfig, from_state_dict
 
 
+def _norm_code(normalize):
+    """False: raw features; True: f / ||f|| (embedding_service.py:502);
+    "guarded": f / ||f|| if ||f|| > 1e-8 else f (compare_models.py:1166-1171)."""
+    if normalize == "guarded":
+        return 2
+    return int(bool(normalize))
+
+
 class _Visual:
     def __init__(self, cfg: CLIPConfig):
         self.output_dim = cfg.embed_dim
@@ -37,13 +46,21 @@ class CLIP:
 
     def __init__(self, cfg: CLIPConfig, state_dict: dict, device="cuda", image_chunk=None, text_chunk=64,
                  weights: str = "bf16"):
-        """``weights``: "bf16" (the parity mode) or "fp8" — the vision tower's
-        GEMMs on the block-scaled fp8 MFMA with MX-fp8 weights and activations
-        (BASELINE.json configs[4], "fp8 MFMA weights")."""
+        """``weights``:
+
+        * "bf16" — bf16 MFMA GEMMs, fp16 vision residual stream (the throughput
+          mode; the reference's own GPU path runs fp16, openai/CLIP convert_weights);
+        * "fp32" — every GEMM on the exact-f32 MFMA, every activation and the
+          residual stream f32 (the reference's CPU arithmetic, BASELINE.json
+          configs[0]; ``model.float()`` selects it, as openai/CLIP's float() does
+          for ``CLIPWithClassifier``, embedding_service.py:22) — the parity mode
+          in which the R@K flow reproduces the reference's ranks (miclip.evaluate);
+        * "fp8" — the vision tower's GEMMs on the block-scaled fp8 MFMA with
+          MX-fp8 weights and activations (BASELINE.json configs[4])."""
         import torch
 
-        if weights not in ("bf16", "fp8"):
-            raise N.MiClipError(f"weights must be 'bf16' or 'fp8', got {weights!r}")
+        if weights not in ("bf16", "fp8", "fp32"):
+            raise N.MiClipError(f"weights must be 'bf16', 'fp32' or 'fp8', got {weights!r}")
         self.weights = weights
 
         self.cfg = cfg
@@ -76,7 +93,7 @@ class CLIP:
         blob = N.pack_weights(self._sd, self.cfg)
         arch = N.Arch.from_config(self.cfg)
         ctx = ctypes.c_void_p()
-        wdt = N.MI_FP8 if self.weights == "fp8" else N.MI_BF16
+        wdt = {"fp8": N.MI_FP8, "fp32": N.MI_F32}.get(self.weights, N.MI_BF16)
         N.check(L.mi_clip_create(ctypes.byref(arch), blob.ctypes.data, blob.size, self.device.index, wdt,
                                  ctypes.byref(ctx)), "mi_clip_create")
         self._ctx = ctx
@@ -107,8 +124,14 @@ class CLIP:
         return self
 
     def float(self):
+        """openai/CLIP ``model.float()``: weights (and so every activation) fp32.
+        Here: rebuild the context on the fp32 tower (a no-op when it already is)."""
         import torch
         self._out_dtype = torch.float32
+        if self.weights != "fp32":
+            self.close()
+            self.weights = "fp32"
+            self._build()
         return self
 
     def half(self):
@@ -179,7 +202,7 @@ class CLIP:
         out = self._out(x.shape[0], out_dtype)
         with torch.cuda.device(self.device), self._lock:
             N.check(N.lib().mi_clip_encode_image(self._ctx, x.data_ptr(), x.shape[0], N.dtype_code(x.dtype),
-                                                 out.data_ptr(), N.dtype_code(out.dtype), int(bool(normalize)),
+                                                 out.data_ptr(), N.dtype_code(out.dtype), _norm_code(normalize),
                                                  N.stream_ptr(self.device)), "mi_clip_encode_image")
         return out
 
@@ -193,7 +216,7 @@ class CLIP:
         out = self._out(t.shape[0], out_dtype)
         with torch.cuda.device(self.device), self._lock:
             N.check(N.lib().mi_clip_encode_text(self._ctx, t.data_ptr(), t.shape[0], out.data_ptr(),
-                                                N.dtype_code(out.dtype), int(bool(normalize)),
+                                                N.dtype_code(out.dtype), _norm_code(normalize),
                                                 N.stream_ptr(self.device)), "mi_clip_encode_text")
         return out
 

@@ -96,6 +96,7 @@ def preprocess_frames(frames, n_px: int = 224, squash: bool = False, out_dtype=N
 
 
 DECODE_CHUNK = 8192
+DECODE_BUDGET_GB = 32
 
 
 def decode_chunk(batch_size: int) -> int:
@@ -103,10 +104,30 @@ def decode_chunk(batch_size: int) -> int:
     decode runs one lane per frame, so its rate grows with the batch (2048
     frames ~5k frames/s, 8192 ~13k) while the encode keeps the
     caller's batch size; a multiple of it (``$MICLIP_DECODE_CHUNK`` overrides).
-    8192 720p frames hold ~70 GB of device memory while they decode."""
+    What one decode launch holds on the device is bounded separately, by bytes
+    (``decode_budget``), so large frames (1080p, 4K) decode in smaller launches."""
     n = int(os.environ.get("MICLIP_DECODE_CHUNK", DECODE_CHUNK))
     b = max(1, batch_size)
     return max(b, n // b * b)
+
+
+def decode_budget() -> int:
+    """Device bytes a GPU decode launch may hold (RGB output + coefficient
+    workspace, ``jpeg.decoded_bytes``): ``$MICLIP_DECODE_BUDGET_GB``, default 32 GB
+    (~4.6k 720p frames, ~500 4K frames per launch; HBM is 288 GB)."""
+    return int(float(os.environ.get("MICLIP_DECODE_BUDGET_GB", DECODE_BUDGET_GB)) * (1 << 30))
+
+
+def _budget_slices(sizes, budget):
+    """Consecutive [a, b) ranges whose summed sizes stay within budget (at least one item each)."""
+    a, n = 0, len(sizes)
+    while a < n:
+        b, used = a, 0
+        while b < n and (b == a or used + sizes[b] <= budget):
+            used += sizes[b]
+            b += 1
+        yield a, b
+        a = b
 
 
 def load_frames(paths, n_px: int = 224, device="cuda", squash: bool = False, out_dtype=None, threads: int = 8,
@@ -143,24 +164,29 @@ def load_frames(paths, n_px: int = 224, device="cuda", squash: bool = False, out
 
         with ThreadPoolExecutor(max(1, threads)) as ex:
             bufs = list(ex.map(read, paths))
-        frames = jpeg.decode_batch(bufs, device)
+        heads = [jpeg.parse(b) for b in bufs]
         out = torch.zeros(len(paths), 3, n_px, n_px, dtype=out_dtype or torch.float32, device=device)
-        groups, failed = {}, []
-        for i, fr in enumerate(frames):
-            if fr is None:
-                if strict:      # Pillow's own error
-                    with Image.open(paths[i]) as im:
-                        im.convert("RGB")
-                if bufs[i]:
-                    print(f"Error preprocessing image {paths[i]}: cannot identify or decode image file")
-                failed.append(i)
-            else:
-                groups.setdefault(tuple(fr.shape), []).append(i)
-        for idx in groups.values():
-            batch = torch.stack([frames[i] for i in idx])
-            out[torch.tensor(idx, device=out.device)] = preprocess_frames(batch, n_px, squash=squash,
-                                                                           out_dtype=out.dtype)
-        return out, failed
+        failed = []
+        for a, b in _budget_slices([jpeg.decoded_bytes(h) for h in heads], decode_budget()):
+            # each geometry group's decoded frames go to the resampler as the decoder's own [B,H,W,3] buffer
+            for idx, rgb in jpeg.decode_groups(bufs[a:b], device, heads=heads[a:b]):
+                idx = [a + i for i in idx]
+                if rgb is None:
+                    i = idx[0]
+                    if strict:      # Pillow's own error
+                        with Image.open(paths[i]) as im:
+                            im.convert("RGB")
+                    if bufs[i]:
+                        print(f"Error preprocessing image {paths[i]}: cannot identify or decode image file")
+                    failed.append(i)
+                    continue
+                res = preprocess_frames(rgb, n_px, squash=squash, out_dtype=out.dtype)
+                del rgb
+                if idx == list(range(idx[0], idx[0] + len(idx))):
+                    out[idx[0]:idx[0] + len(idx)] = res
+                else:
+                    out[torch.tensor(idx, device=out.device)] = res
+        return out, sorted(failed)
 
     def load(p):
         try:

@@ -32,22 +32,70 @@ from .retrieval import MirroredCorpus, rank_topk
 # corpora from this many rows on also get an fp16 ranking mirror (scripts/mirror_micro.py:
 # 1M rows 1.6-1.9x faster than the exact pass, 125k rows slower: fixed merge/re-score cost)
 MIRROR_MIN_ROWS = 262_144
-from .weights import load_state_dict
+from .weights import load_classifier, load_state_dict
+
+
+def gemm_f32(a, w, bias=None, relu=False):
+    """f32 [M,K] . [N,K]^T (+bias) (+ReLU) through ``mi_op_gemm_f32`` (the fp32
+    tower's exact-f32 MFMA GEMM); K is zero-padded to a multiple of 32."""
+    import torch
+    from . import _native as N
+    a = a.float().contiguous()
+    w = w.float().contiguous()
+    M, K = a.shape
+    Nn = w.shape[0]
+    if K % 32:
+        pad = 32 - K % 32
+        a = torch.nn.functional.pad(a, (0, pad))
+        w = torch.nn.functional.pad(w, (0, pad))
+        K += pad
+    out = torch.empty(M, Nn, dtype=torch.float32, device=a.device)
+    if M == 0:
+        return out
+    b = bias.float().contiguous() if bias is not None else None
+    with torch.cuda.device(a.device):
+        N.check(N.lib().mi_op_gemm_f32(a.data_ptr(), w.data_ptr(), b.data_ptr() if b is not None else None,
+                                       out.data_ptr(), M, Nn, K, 3 if relu else 0, N.stream_ptr(a.device)),
+                "mi_op_gemm_f32")
+    return out
 
 
 class FinetunedCLIP:
-    """Inference side of ``CLIPWithClassifier`` (embedding_service.py:16-67):
-    ``model(images)`` = L2-normalised image features; the 3-class head is only
-    used for training and is not evaluated here."""
+    """``CLIPWithClassifier`` (embedding_service.py:16-67) on the device:
+    ``clip_model.float()`` (:22, the fp32 tower), ``model(images)`` = L2-normalised
+    image features (:36-49); with texts, the CLIP logits (logit_scale.exp() *
+    I . T^T) and the 3-class head Linear(D, 512) -> ReLU -> Dropout (identity at
+    inference) -> Linear(512, 3) on the checkpoint's ``classifier.*`` weights
+    (:51-67)."""
 
-    def __init__(self, clip_model):
+    def __init__(self, clip_model, classifier=None):
+        import torch
         self.clip_model = clip_model.float()
         self.logit_scale = clip_model.logit_scale
+        self.classifier = None
+        if classifier is not None:
+            dev = self.clip_model.device
+            self.classifier = {k: torch.from_numpy(v).to(dev) for k, v in classifier.items()}
 
     def __call__(self, images, texts=None, get_embeddings=False):
-        if texts is not None:
-            raise NotImplementedError("classification head forward is training-only (out of scope)")
-        return self.clip_model.encode_image(images, normalize=True)
+        import torch
+        image_features = self.clip_model.encode_image(images, normalize=True, out_dtype=torch.float32)
+        if texts is None:
+            return image_features
+        text_features = self.clip_model.encode_text(texts, normalize=True, out_dtype=torch.float32)
+        from .retrieval import score_matrix
+        scale = float(np.exp(np.float32(self.logit_scale.item())))
+        # (logit_scale * image_features) @ text_features.t()  (:57-58)
+        logits_per_image = score_matrix(text_features, image_features * scale, norm="none")
+        logits_per_text = logits_per_image.t()
+        if self.classifier is None:
+            raise ValueError("this checkpoint has no classifier.* weights: class logits are unavailable")
+        c = self.classifier
+        hidden = gemm_f32(image_features, c["0.weight"], c["0.bias"], relu=True)
+        class_logits = gemm_f32(hidden, c["3.weight"], c["3.bias"])
+        if get_embeddings:
+            return image_features, text_features, logits_per_image, logits_per_text, class_logits
+        return logits_per_image, logits_per_text, class_logits
 
     def eval(self):
         return self
@@ -83,7 +131,7 @@ class EmbeddingService:
         sd = load_state_dict(checkpoint_path)       # unwraps model_state_dict / clip_model.*
         model, _ = api.load(self.model_name, device=self.device)
         model.load_state_dict(sd)
-        self.finetuned_model = FinetunedCLIP(model)
+        self.finetuned_model = FinetunedCLIP(model, load_classifier(checkpoint_path))
 
     def set_active_model(self, model_name):
         if model_name == "original":

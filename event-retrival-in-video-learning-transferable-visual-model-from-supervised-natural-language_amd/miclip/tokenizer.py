@@ -50,9 +50,14 @@ _LIGATURES = {"\u0132": "IJ", "\u0133": "ij", "\u01f1": "DZ", "\u01f2": "Dz", "\
               "\u01c5": "Dž", "\u01c6": "dž", "\u01c7": "LJ", "\u01c8": "Lj", "\u01c9": "lj", "\u01ca": "NJ",
               "\u01cb": "Nj", "\u01cc": "nj", "\ufb00": "ff", "\ufb01": "fi", "\ufb02": "fl", "\ufb03": "ffi",
               "\ufb04": "ffl", "\ufb05": "ſt", "\ufb06": "st"}
-_QUOTES = {"\u2018": "'", "\u2019": "'", "\u201a": "'", "\u201b": "'", "\u201c": '"', "\u201d": '"',
-           "\u201e": '"', "\u201f": '"', "\u2032": "'", "\u2033": '"'}
-_CONTROL = re.compile(r"[\x00-\x08\x0b\x0e-\x1f\x7f\u206a-\u206f\ufff9-\ufffc\ufeff]")
+# ftfy uncurl_quotes: SINGLE_QUOTE_RE [\u02bc\u2018-\u201b] -> ', DOUBLE_QUOTE_RE [\u201c-\u201f] -> "
+# (primes U+2032 / U+2033 are left alone)
+_QUOTES = {"\u02bc": "'", "\u2018": "'", "\u2019": "'", "\u201a": "'", "\u201b": "'", "\u201c": '"',
+           "\u201d": '"', "\u201e": '"', "\u201f": '"'}
+# ftfy chardata CONTROL_CHARS: U+0000-0008, 000B, 000E-001F, 007F, 206A-206F, FEFF, FFF9-FFFC,
+# 1D173-1D17A (musical formatting), E0000-E007F (tags)
+_CONTROL = re.compile(r"[\x00-\x08\x0b\x0e-\x1f\x7f\u206a-\u206f\ufff9-\ufffc\ufeff"
+                      r"\U0001d173-\U0001d17a\U000e0000-\U000e007f]")
 
 
 def fix_text_subset(text):

@@ -208,9 +208,22 @@ def read_torchscript_tensors(path: str) -> dict:
             self.name = name
 
     def rebuild_tensor(storage, offset, size, stride, *rest):
+        # as_strided does no bounds checking: a crafted offset / size / stride must not read
+        # outside the storage buffer, so the extent is checked first
         base = storage
+        size, stride = tuple(size), tuple(stride)
+        if not isinstance(offset, int) or offset < 0 or len(size) != len(stride) or \
+                any(not isinstance(v, int) or v < 0 for v in size + stride):
+            raise pickle.UnpicklingError(f"bad tensor geometry: offset {offset}, size {size}, stride {stride}")
+        numel = int(np.prod(size, dtype=np.int64)) if size else 1
+        if numel > 0:
+            last = offset + sum((n - 1) * st for n, st in zip(size, stride))
+            if last >= len(base):
+                raise pickle.UnpicklingError(f"tensor extends past its storage ({last} >= {len(base)})")
+        elif offset > len(base):
+            raise pickle.UnpicklingError(f"tensor offset {offset} past its storage ({len(base)})")
         return np.lib.stride_tricks.as_strided(
-            base[offset:], shape=tuple(size), strides=tuple(s * base.itemsize for s in stride)).copy()
+            base[offset:], shape=size, strides=tuple(st * base.itemsize for st in stride)).copy()
 
     def rebuild_parameter(data, *rest):
         return data
@@ -289,6 +302,26 @@ def load_state_dict(path: str) -> dict:
     ``Backend/services/embedding_service.py:112-113``) is unwrapped to its
     ``clip_model.*`` part.  Any other file is refused with the loader's own
     error (no second, less restricted deserializer is tried)."""
+    sd = _read_tensors(path)
+    if any(k.startswith("clip_model.") for k in sd):
+        sd = {k[len("clip_model."):]: v for k, v in sd.items() if k.startswith("clip_model.")}
+    for k in ("input_resolution", "context_length", "vocab_size"):
+        sd.pop(k, None)
+    return {k: np.ascontiguousarray(v, dtype=np.float32) for k, v in sd.items()}
+
+
+def load_classifier(path: str):
+    """The ``classifier.*`` head of a fine-tuned ``CLIPWithClassifier`` checkpoint
+    (nn.Sequential(Linear(D, 512), ReLU, Dropout, Linear(512, 3)):
+    ``{'0.weight', '0.bias', '3.weight', '3.bias'}``, embedding_service.py:26-31),
+    or None when the file has none.  Same loaders as ``load_state_dict``."""
+    sd = _read_tensors(path)
+    head = {k[len("classifier."):]: np.ascontiguousarray(v, dtype=np.float32) for k, v in sd.items()
+            if k.startswith("classifier.")}
+    return head or None
+
+
+def _read_tensors(path: str) -> dict:
     import torch
 
     if path.endswith(".safetensors"):
@@ -303,11 +336,7 @@ def load_state_dict(path: str) -> dict:
         if not isinstance(obj, dict):
             raise RuntimeError(f"{path}: expected a state dict, got {type(obj).__name__}")
         sd = {k: (v.float().numpy() if hasattr(v, "numpy") else np.asarray(v)) for k, v in obj.items()}
-    if any(k.startswith("clip_model.") for k in sd):
-        sd = {k[len("clip_model."):]: v for k, v in sd.items() if k.startswith("clip_model.")}
-    for k in ("input_resolution", "context_length", "vocab_size"):
-        sd.pop(k, None)
-    return {k: np.ascontiguousarray(v, dtype=np.float32) for k, v in sd.items()}
+    return sd
 
 
 SYNTHETIC_ENV = "MICLIP_SYNTHETIC_WEIGHTS"

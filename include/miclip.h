@@ -82,11 +82,17 @@ int64_t mi_clip_weights_numel(const mi_clip_arch* arch);
  * (call sites Backend/embedding.py:22, Backend/services/embedding_service.py:86,106,
  * compare_models.py:316).  `weights` is a HOST float32 blob of
  * mi_clip_weights_numel(arch) elements; weights are converted to `weight_dtype`
- * and uploaded to `device`: MI_BF16 (the parity mode), or MI_FP8 — the vision
- * tower's four GEMMs per block run on the block-scaled fp8 MFMA with MX-fp8
- * weights (e4m3 + e8m0 per 64 k) and MX-fp8 activations produced by the
- * LayerNorm / attention / QuickGELU kernels (BASELINE.json configs[4]).
- * MI_F32 is rejected. */
+ * and uploaded to `device`:
+ *   MI_BF16  bf16 MFMA GEMMs, fp16 vision residual stream (throughput mode; the
+ *            reference's GPU path is fp16, openai/CLIP convert_weights);
+ *   MI_F32   every GEMM on the exact-f32 MFMA, every activation and the residual
+ *            stream f32 — the reference's CPU / `model.float()` arithmetic
+ *            (Backend/embedding.py:21-22 on a CPU, CLIPWithClassifier
+ *            embedding_service.py:22): the parity mode of the R@K flow;
+ *   MI_FP8   the vision tower's four GEMMs per block on the block-scaled fp8 MFMA
+ *            with MX-fp8 weights (e4m3 + e8m0 per 64 k) and MX-fp8 activations
+ *            produced by the LayerNorm / attention / QuickGELU kernels
+ *            (BASELINE.json configs[4]). */
 int mi_clip_create(const mi_clip_arch* arch, const float* weights, int64_t numel,
                    int device, int weight_dtype, mi_clip** out);
 int mi_clip_destroy(mi_clip* ctx);
@@ -99,7 +105,8 @@ int mi_clip_reserve(mi_clip* ctx, int64_t image_chunk, int64_t text_chunk);
 /* Replaces `model.encode_image(x)` (VisionTransformer.forward; call sites
  * Backend/embedding.py:49, embedding_service.py:490, compare_models.py:1118)
  * and, with l2_normalize=1, the normalisation that follows it
- * (embedding_service.py:502, CLIPWithClassifier.forward :45).
+ * (embedding_service.py:502, CLIPWithClassifier.forward :45); l2_normalize=2 is
+ * compare_models.py's guarded form (f/||f|| if ||f|| > 1e-8 else f, :1166-1171).
  * pixels: device [B,3,R,R] in `in_dtype` (MI_F32 / MI_BF16);
  * out: device [B,embed_dim] in `out_dtype` (MI_F32 / MI_BF16 / MI_F16). */
 int mi_clip_encode_image(mi_clip* ctx, const void* pixels, int64_t B, int in_dtype,
@@ -238,6 +245,12 @@ int mi_jpeg_decode(const uint8_t* data, const int64_t* seg_off, const int64_t* s
  *   A/B and parity tests (one-wave S <= 96 / chunk-streaming flash S > 64) */
 int mi_op_gemm(const void* A, const void* W, const float* bias, void* out, int32_t M, int32_t N, int32_t K,
                int32_t epilogue, void* stream);
+/* mi_op_gemm_f32: f32 out[M,N] = A[M,K] . W[N,K]^T (+bias) on the exact-f32 MFMA (the
+ *   MI_F32 tower's GEMM, precise.hip); epilogue 0 store, 1 QuickGELU, 2 out += (residual),
+ *   3 ReLU (CLIPWithClassifier's classifier head, embedding_service.py:26-31).  K % 32 == 0,
+ *   any M, N; rows of A / W contiguous (lda = ldw = K, ldo = N). */
+int mi_op_gemm_f32(const float* A, const float* W, const float* bias, float* out, int32_t M, int32_t N, int32_t K,
+                   int32_t epilogue, void* stream);
 int mi_op_layernorm(const float* x, const float* gamma, const float* beta, void* out, int32_t rows, int32_t W,
                     void* stream);
 int mi_op_attention(const void* qkv, void* out, int32_t B, int32_t S, int32_t W, int32_t causal, void* stream);

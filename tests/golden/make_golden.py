@@ -119,7 +119,75 @@ def rk_golden():
     print("wrote", out, "seed", seed, ref["t2i"], ref["i2t"])
 
 
+RK_E2E_GAP = 1e-5          # decisive score gaps of the end-to-end R@K fixture (>> the f32 tower's ~1e-7)
+
+
+def rk_e2e_golden(n_img=100, n_cap=500, n_pool=600, gap=RK_E2E_GAP):
+    """The compare_models.py:908-1100 flow end to end on ViT-B/32 (seed-2
+    weights): n_img synthetic frames and n_pool synthetic caption token rows
+    encoded by the float64 oracle; features cast to f32 as the reference's fp32
+    model returns them, guarded L2 (:1166-1171, :1254-1259), S = I . T^T (:999),
+    ranks (:1004-1062) by the literal restatement.
+
+    Captions are assigned to images so that every comparison that decides a
+    rank (a ground-truth score against every other score of its t2i column and
+    its i2t row) differs by more than ``gap``: each image takes 5 captions from
+    the pool whose scores are isolated by > gap in its row and column (greedy,
+    pool order).  The parity claim is then independent of f32 summation order;
+    the fixture records the smallest such gap."""
+    cfg = config.get_config("ViT-B/32")
+    sd = weights.make_state_dict(cfg)
+    px = weights.synthetic_pixels(n_img, cfg.image_resolution, seed=101)
+    tk = weights.synthetic_tokens(n_pool, cfg.context_length, cfg.vocab_size, seed=102)
+    from oracle import clip_ref
+    img64 = clip_ref.encode_image(px, sd, cfg, np.float64)
+    txt64 = np.concatenate([clip_ref.encode_text(tk[i:i + 50], sd, cfg, np.float64) for i in range(0, n_pool, 50)])
+    img = rank_ref.normalize_rows_guarded(img64.astype(np.float32))
+    txt = rank_ref.normalize_rows_guarded(txt64.astype(np.float32))
+    S = img.astype(np.float64) @ txt.T.astype(np.float64)          # [n_img, n_pool]
+    used = np.zeros(n_pool, bool)
+    picks = []
+    for j in range(n_img):
+        row = S[j]
+        got = []
+        for c in range(n_pool):
+            if used[c]:
+                continue
+            if np.min(np.abs(np.delete(row, c) - row[c])) <= gap:
+                continue
+            col = S[:, c]
+            if np.min(np.abs(np.delete(col, j) - col[j])) <= gap:
+                continue
+            got.append(c)
+            used[c] = True
+            if len(got) == n_cap // n_img:
+                break
+        if len(got) < n_cap // n_img:
+            raise SystemExit(f"image {j}: only {len(got)} isolated captions at gap {gap}")
+        picks += [(c, j) for c in got]
+    picks.sort()                                                    # captions in pool order
+    cap_idx = np.array([c for c, _ in picks], np.int64)
+    cap_ids = np.array([j for _, j in picks], np.int64)
+    Ssel = S[:, cap_idx]
+    mg = np.inf
+    for t, j in enumerate(cap_ids):
+        mg = min(mg, np.min(np.abs(np.delete(Ssel[:, t], j) - Ssel[j, t])), np.min(np.abs(np.delete(Ssel[j], t) - Ssel[j, t])))
+    ref = rank_ref.retrieval_metrics_ref(img.astype(np.float32), txt[cap_idx].astype(np.float32), list(cap_ids),
+                                         list(range(n_img)))
+    out = os.path.join(HERE, "rk_e2e_b32.npz")
+    np.savez_compressed(out, pixel_seed=101, token_seed=102, n_img=n_img, n_pool=n_pool, caption_index=cap_idx,
+                        caption_image_ids=cap_ids, image_features=img.astype(np.float32),
+                        text_features=txt[cap_idx].astype(np.float32), t2i_ranks=ref["t2i_ranks"],
+                        i2t_ranks=ref["i2t_ranks"], gap=gap, min_gap=mg,
+                        t2i=np.array([ref["t2i"][m] for m in ("R@1", "R@5", "R@10", "MRR", "Median_Rank", "Mean_Rank")]),
+                        i2t=np.array([ref["i2t"][m] for m in ("R@1", "R@5", "R@10", "MRR", "Median_Rank", "Mean_Rank")]))
+    print("wrote", out, "min decisive gap", mg, ref["t2i"], ref["i2t"])
+
+
 if __name__ == "__main__":
+    if "--rk-e2e" in sys.argv:
+        rk_e2e_golden()
+        sys.exit(0)
     if "--only" in sys.argv:  # one encoder golden, e.g. --only ViT-L/14@336px
         encoder_golden(sys.argv[sys.argv.index("--only") + 1], 2, 2)
         sys.exit(0)

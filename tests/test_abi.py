@@ -64,7 +64,9 @@ def test_argument_errors_without_gpu():
     blob = np.zeros(10, np.float32)
     rc = L.mi_clip_create(ctypes.byref(arch), blob.ctypes.data, 10, 0, 1, ctypes.byref(ctx))
     assert rc == -1 and b"expected" in L.mi_last_error()
-    rc = L.mi_clip_create(ctypes.byref(arch), blob.ctypes.data, 10, 0, 0, ctypes.byref(ctx))
+    rc = L.mi_clip_create(ctypes.byref(arch), blob.ctypes.data, 10, 0, 0, ctypes.byref(ctx))    # MI_F32: accepted
+    assert rc == -1 and b"expected" in L.mi_last_error()
+    rc = L.mi_clip_create(ctypes.byref(arch), blob.ctypes.data, 10, 0, 2, ctypes.byref(ctx))    # MI_F16: no
     assert rc == -3
     assert L.mi_rank_workspace_bytes(1_000_000, 32, 10) > 0
 
@@ -85,3 +87,24 @@ def test_no_cpu_execution_path():
     from miclip import config
     with pytest.raises(_native.MiClipError):
         M.CLIP(config.get_config("test-tiny"), state_dict("test-tiny"), device="cpu")
+
+
+def test_mirror_certificate_delta_covers_worst_case():
+    """The mirror certificate's |s_mirror - s_exact| bound (rank_mirror.hip
+    mirror_delta) against the analytic worst case per unit |q|: fp16 RNE of a
+    unit row (unit roundoff 2^-11), the query split (2^-22 with the
+    hi/lo split, 2^-11 hi only), f32 accumulation of both dot products
+    (2 gamma_D, gamma_D = D u / (1 - D u), u = 2^-24) and the subnormal floor."""
+    from miclip import _native
+    L = _native.lib()
+    fn = L.mi_debug_mirror_delta
+    fn.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]
+    u = 2.0 ** -24
+    for D in (512, 768):
+        for split in (1, 0):
+            dr, da = ctypes.c_float(), ctypes.c_float()
+            assert fn(D, split, ctypes.byref(dr), ctypes.byref(da)) == 0
+            gamma = D * u / (1 - D * u)
+            worst = 2.0 ** -11 + (2.0 ** -22 if split else 2.0 ** -11) + 2 * gamma + 2 * np.sqrt(D) * 2.0 ** -25
+            assert dr.value >= worst, (D, split, dr.value, worst)
+            assert da.value >= np.sqrt(D) * 2.0 ** -25

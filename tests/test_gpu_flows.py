@@ -67,6 +67,28 @@ def test_embedding_py_flow_configs0(gpu, tmp_path):
     assert np.abs(np.linalg.norm(rows, axis=1) - 1).max() > 0.1
 
 
+def test_embedding_py_flow_configs0_fp32(gpu, tmp_path):
+    """configs[0] at the reference's precision: the fp32 model Backend/embedding.py
+    builds on a CPU (clip.load(device="cpu") -> float()), here the fp32 tower.
+    Every row within f32 rounding of the float64 oracle."""
+    from PIL import Image
+    from miclip import config, embedding, preprocess
+    from oracle import clip_ref
+    frames = tmp_path / "video_a"
+    _png_tree(frames, 64)
+    out = embedding.extract_and_save_embeddings_from_folder(str(frames), "ViT-B/32", output_dir=str(tmp_path / "emb"),
+                                                            batch_size=24, weights="fp32")
+    rows = np.load(out)
+    order = [os.path.join(r, f) for r, _, fs in os.walk(frames) for f in fs if f.endswith(".png")]
+    cfg = config.get_config("ViT-B/32")
+    tf = preprocess.Transform(cfg.image_resolution)
+    px = np.stack([tf(Image.open(p).convert("RGB")).numpy() for p in order])
+    ref = clip_ref.encode_image(px, state_dict("ViT-B/32"), cfg, np.float64)
+    rel = np.abs(rows - ref).max() / np.abs(ref).max()
+    assert rel < 2e-5, rel
+    assert clip_ref.cosine(rows, ref).min() > 1 - 1e-9
+
+
 def test_embedding_py_unreadable_frame_raises(gpu, tmp_path):
     """Backend/embedding.py:45 has no handler: an unreadable image propagates."""
     from miclip import embedding
@@ -131,6 +153,36 @@ def test_finetuned_checkpoint_inference(ft_service):
     orig = svc.original_model.encode_image(torch.from_numpy(px), normalize=True).cpu().numpy()
     assert clip_ref.cosine(got, orig).max() < 0.999          # it really is the other model
     assert svc.set_active_model("original") and not svc.set_active_model("nonsense")
+
+
+def test_finetuned_full_forward_with_texts(ft_service, tmp_path):
+    """CLIPWithClassifier.forward(images, texts) (embedding_service.py:51-67):
+    logits_per_image = logit_scale.exp() * I . T^T, logits_per_text its
+    transpose, class_logits = Linear(512,3)(ReLU(Linear(D,512)(I))) on the
+    checkpoint's classifier.* weights; against the float64 oracle encoders and
+    a numpy head (fp32 tower: rel. error ~1e-6)."""
+    import torch
+    from miclip import weights
+    from oracle import clip_ref
+    svc, frame_dir, names, paths, ft_sd, cfg = ft_service
+    ft = svc.finetuned_model
+    px = weights.synthetic_pixels(4, cfg.image_resolution)
+    tk = weights.synthetic_tokens(3, cfg.context_length, cfg.vocab_size)
+    lpi, lpt, cls = ft(torch.from_numpy(px), torch.from_numpy(tk))
+    img, txt, lpi2, lpt2, cls2 = ft(torch.from_numpy(px), torch.from_numpy(tk), get_embeddings=True)
+    assert lpi.shape == (4, 3) and lpt.shape == (3, 4) and cls.shape == (4, 3)
+    assert torch.equal(lpi, lpi2) and torch.equal(cls, cls2) and torch.equal(lpt, lpi.t())
+    n = lambda a: a / np.linalg.norm(a, axis=-1, keepdims=True)               # noqa: E731
+    ri = n(clip_ref.encode_image(px, ft_sd, cfg, np.float64))
+    rt = n(clip_ref.encode_text(tk, ft_sd, cfg, np.float64))
+    scale = np.exp(np.float64(ft_sd["logit_scale"]))
+    np.testing.assert_allclose(lpi.cpu().numpy(), scale * ri @ rt.T, rtol=0, atol=1e-4 * scale)
+    ckpt = torch.load(str(tmp_path / "final_checkpoint.pt"), weights_only=True)["model_state_dict"]
+    w0, b0 = ckpt["classifier.0.weight"].double().numpy(), ckpt["classifier.0.bias"].double().numpy()
+    w3, b3 = ckpt["classifier.3.weight"].double().numpy(), ckpt["classifier.3.bias"].double().numpy()
+    ref_cls = np.maximum(ri @ w0.T + b0, 0) @ w3.T + b3
+    np.testing.assert_allclose(cls.cpu().numpy(), ref_cls, rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(img.cpu().numpy(), ri, atol=1e-5)
 
 
 def test_finetuned_ingest_and_search(ft_service):

@@ -115,3 +115,8 @@ def test_tokenizer_clean_restates_ftfy_subset():
     assert _clean("tab\x00ctl") == "tabctl"
     assert _clean("a &amp;amp; b") == "a & b"
     assert _clean("  plain   query  ") == "plain query"
+    # ftfy uncurl_quotes tables: U+02BC and U+2018-201B -> ', U+201C-201F -> ", primes untouched
+    assert _clean("it\u02bcs \u201bx\u201f") == "it's 'x\""
+    assert _clean("5\u2032 10\u2033") == "5\u2032 10\u2033"
+    # ftfy CONTROL_CHARS includes musical formatting U+1D173-1D17A and tags U+E0000-E007F
+    assert _clean("a\U0001d173b\U000e0041c\U000e007fd") == "abcd"

@@ -77,3 +77,62 @@ def test_unsupported_kinds_are_flagged():
     im.convert("CMYK").save(b, "JPEG")
     assert not jpeg.parse(b.getvalue()).supported
     assert not jpeg.parse(b"\x89PNG....").supported
+
+
+def _segments_of(buf):
+    """(marker, start, end) of the marker segments before the scan data."""
+    out, i = [], 2
+    while i + 4 <= len(buf):
+        m = buf[i + 1]
+        ln = (buf[i + 2] << 8) | buf[i + 3]
+        out.append((m, i, i + 2 + ln))
+        if m == 0xDA:
+            break
+        i += 2 + ln
+    return out
+
+
+def test_colour_space_guess_without_jfif():
+    """libjpeg (Pillow) guesses the colour space of a 3-component file with no
+    JFIF / Adobe marker from its component ids ('R','G','B' = no YCbCr
+    transform): such files go to the host decoder; JFIF files and ids 1, 2, 3
+    stay on the GPU path."""
+    from PIL import Image
+    from miclip import jpeg
+    b = io.BytesIO()
+    Image.fromarray((np.random.default_rng(3).random((16, 24, 3)) * 255).astype(np.uint8)).save(b, "JPEG")
+    buf = bytearray(b.getvalue())
+    assert jpeg._parse(bytes(buf)).supported
+    app0 = [(s, e) for m, s, e in _segments_of(buf) if m == 0xE0]
+    assert app0
+    s0, e0 = app0[0]
+    nojfif = buf[:s0] + buf[e0:]
+    assert jpeg._parse(bytes(nojfif)).supported                   # ids 1, 2, 3: YCbCr either way
+
+    def with_ids(b0, ids):
+        b0 = bytearray(b0)
+        for m, s, e in _segments_of(b0):
+            if m == 0xC0:
+                for c in range(3):
+                    b0[s + 4 + 6 + 3 * c] = ids[c]
+            if m == 0xDA:
+                for c in range(3):
+                    b0[s + 4 + 1 + 2 * c] = ids[c]
+        return bytes(b0)
+
+    rgb_ids = [ord("R"), ord("G"), ord("B")]
+    h = jpeg._parse(with_ids(nojfif, rgb_ids))
+    assert not h.supported and "JFIF" in h.why
+    assert jpeg._parse(with_ids(buf, rgb_ids)).supported           # JFIF marker: YCbCr regardless of ids
+
+
+def test_decode_budget_slices():
+    """Decode launches bounded by device bytes (4K frames would not fit 8192 at a time)."""
+    from miclip import jpeg
+    from miclip.preprocess import _budget_slices
+    assert list(_budget_slices([5, 5, 5, 5], 10)) == [(0, 2), (2, 4)]
+    assert list(_budget_slices([30, 5, 5], 10)) == [(0, 1), (1, 3)]          # an oversized item goes alone
+    assert list(_budget_slices([], 10)) == []
+    h = jpeg.parse(open(sorted(glob.glob(os.path.join(ROOT, "golden", "ref_frames", "*.jpg")))[0], "rb").read())
+    # 1280x720 4:2:0: RGB 2.76 MB + (14400 + 2 * 3600) blocks * 192 B
+    assert jpeg.decoded_bytes(h) == 3 * 1280 * 720 + 192 * 21600

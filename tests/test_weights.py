@@ -151,3 +151,50 @@ def test_cpu_device_policy():
         # Backend/embedding.py:21-22 picks "cpu" on a GPU-less host: the mirror says why it cannot run
         with pytest.raises(_native.MiClipError, match="oracle"):
             embedding.extract_and_save_embeddings_from_folder(".", "test-tiny")
+
+
+def _ts_archive(path, size, stride, offset=0):
+    """A minimal TorchScript-layout zip whose data.pkl rebuilds one tensor of
+    the given geometry over a 16-float storage."""
+    import collections
+    import io
+    import pickle
+    import zipfile
+    import torch
+
+    class _Store:
+        pass
+
+    class _P(pickle.Pickler):
+        def persistent_id(self, obj):
+            return ("storage", torch.FloatStorage, "0", "cpu", 16) if obj is _Store else None
+
+    class _T:
+        def __reduce__(self):
+            return (torch._utils._rebuild_tensor_v2, (_Store, offset, size, stride, False, collections.OrderedDict()))
+
+    buf = io.BytesIO()
+    _P(buf, protocol=2).dump({"w": _T()})
+    with zipfile.ZipFile(path, "w") as zf:
+        zf.writestr("m/data.pkl", buf.getvalue())
+        zf.writestr("m/code/__torch__.py", "")
+        zf.writestr("m/data/0", np.arange(16, dtype=np.float32).tobytes())
+
+
+def test_torchscript_reader_bounds_checks_geometry(tmp_path):
+    """A crafted archive must not make the reader stride outside the storage
+    (as_strided has no bounds check)."""
+    import pickle
+    from miclip import weights
+    ok = tmp_path / "ok.pt"
+    _ts_archive(ok, (4, 4), (4, 1))
+    np.testing.assert_array_equal(weights.read_torchscript_tensors(str(ok))["w"],
+                                  np.arange(16, dtype=np.float32).reshape(4, 4))
+    _ts_archive(ok, (2, 2), (1, 4), offset=10)                     # transposed view ending at element 15
+    np.testing.assert_array_equal(weights.read_torchscript_tensors(str(ok))["w"], [[10, 14], [11, 15]])
+    for i, (size, stride, off) in enumerate([((4, 4), (4, 1000), 0), ((4, 4), (4, 1), 1), ((2,), (1,), -1),
+                                             ((3,), (-1,), 2), ((1 << 40,), (1,), 0)]):
+        bad = tmp_path / f"bad{i}.pt"
+        _ts_archive(bad, size, stride, off)
+        with pytest.raises(pickle.UnpicklingError):
+            weights.read_torchscript_tensors(str(bad))
