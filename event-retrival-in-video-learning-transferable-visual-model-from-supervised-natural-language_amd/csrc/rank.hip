@@ -292,6 +292,13 @@ __global__ __launch_bounds__(64 * NW) void rank_stream(const void* __restrict__ 
 // register buffers), so the LDS latency hides under the previous chunk's MFMAs
 // instead of sitting between the wait and the MFMAs; the DMA lookahead is then
 // PF - 1 chunks beyond the one being read.
+// Dynamic LDS of rank_reg<.., NB, ..>: the ring [NW = 4][NB][4 KB], the per-wave
+// row norms [4][32] f32 and tau [RQ] u32.  The launcher sizes the allocation
+// with this same function: a kernel whose ring is larger than the allocation
+// puts its norms (and the last wave's slots) past the end of the workgroup's
+// LDS, where reads return zero — every score comes out 0.
+constexpr size_t rank_reg_lds_bytes(int NB) { return (size_t)4 * NB * (32 * 128) + 4 * 32 * 4 + RQ * 4; }
+
 template <int D, int NB = 8, int PF = 6, bool NOMFMA = false, bool ILV = false, bool PIPE = false>
 __global__ __launch_bounds__(256) void rank_reg(const float* __restrict__ corpus, int64_t N,
                                                 const float* __restrict__ queries, int64_t Q, int k,
@@ -301,6 +308,17 @@ __global__ __launch_bounds__(256) void rank_reg(const float* __restrict__ corpus
   // NB ring slots per wave, PF chunks in flight (NB >= PF + 1: a refilled slot was read, and its
   // reads waited for, in an earlier chunk iteration)
   constexpr int SLOT = 32 * 128;           // 4 KB
+  // the invariants the ring's correctness rests on:
+  //  * a slot is refilled (chunk c + PF into slot (c + PF) % NB, issued at the top of chunk c's
+  //    iteration) only after the chunk it held, c + PF - NB, was read and its reads waited for
+  //    (lgkmcnt(0) in that chunk's iteration): c + PF - NB <= c - 1;
+  //  * the counted wait vmcnt(4 PF) (4 DMA instructions per chunk) fits the 6-bit vmcnt field;
+  //  * the ring, norms and tau fit the CU's 160 KB of LDS (and the launcher allocates exactly
+  //    rank_reg_lds_bytes(NB), which the list merge's 32 KB also fits in).
+  static_assert(NB >= PF + 1, "rank_reg: a refilled ring slot must have been read in an earlier chunk");
+  static_assert(4 * PF <= 63, "rank_reg: vmcnt(4 PF) exceeds the counter");
+  static_assert(rank_reg_lds_bytes(NB) <= 160 * 1024, "rank_reg: ring exceeds the LDS");
+  static_assert(rank_reg_lds_bytes(NB) >= (size_t)NT * KC * 8, "rank_reg: list merge area exceeds the allocation");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* ring = smem;                       // [NW][NB][SLOT]
   float* nrm_all = (float*)(smem + NW * NB * SLOT);
@@ -1019,16 +1037,20 @@ static hipError_t launch_reg(int64_t N, const float* corpus, const float* q, int
   // against 479 with contiguous row ranges, 1M x 768 729 against 717: not the stream's limit
   const char* ilv = getenv("MICLIP_RANK_ILV");
   const bool il = ilv && ilv[0] == '1';
-  const size_t lds = (size_t)4 * 8 * 4096 + 4 * 32 * 4 + RQ * 4;
-  // (a 9-slot ring with 7 chunks in flight, 147 KB of LDS, failed every rank test, N = 1
-  // included, for a reason not yet found; the 8-slot ring is bit-identical to rank_stream)
+  // ring slots: MICLIP_RANK_NB=9 selects a 9-slot ring with 7 chunks in flight (A/B; round 2's
+  // 9-slot attempt kept this allocation at 8 slots' size, so its norms sat past the end of the
+  // LDS and read as zeros: every test failed, N = 1 included).  The size now follows NB.
+  const char* nbs = getenv("MICLIP_RANK_NB");
+  const bool nb9 = nbs && atoi(nbs) == 9;
+  const size_t lds = rank_reg_lds_bytes(nb9 ? 9 : 8);
   const char* probe = getenv("MICLIP_RANK_PROBE");
   // (7 chunks in flight measured the same: the stream alone, NOMFMA, reads 5.3 TB/s either way)
   // fragment reads one chunk ahead: A/B only (MICLIP_RANK_PIPE=1; 1M x 512 552 us against 558,
   // within noise: the wait before the MFMAs is not where this kernel loses time)
   const char* pipe = getenv("MICLIP_RANK_PIPE");
   const bool pp = pipe && pipe[0] == '1';
-  auto fn = (probe && probe[0] == '1') ? (il ? rank_reg<D, 8, 6, true, true> : rank_reg<D, 8, 6, true>)
+  auto fn = nb9 ? rank_reg<D, 9, 7>
+            : (probe && probe[0] == '1') ? (il ? rank_reg<D, 8, 6, true, true> : rank_reg<D, 8, 6, true>)
             : il ? (pp ? rank_reg<D, 8, 6, false, true, true> : rank_reg<D, 8, 6, false, true>)
                  : (pp ? rank_reg<D, 8, 6, false, false, true> : rank_reg<D, 8, 6>);
   hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

@@ -49,10 +49,13 @@ def sharded_topk(local_corpus, queries, k, index_base, group=None, nan_policy="f
     world = dist.get_world_size(group)
     if world == 1:
         return merge(s, i, k, nan_policy=nan_policy)
-    gs = [torch.empty_like(s) for _ in range(world)]
-    gi = [torch.empty_like(i) for _ in range(world)]
-    dist.all_gather(gs, s, group=group)
-    dist.all_gather(gi, i, group=group)
-    cand_s = torch.cat(gs, dim=1).contiguous()     # [Q, world*k]
-    cand_i = torch.cat(gi, dim=1).contiguous()
+    # ONE collective: each rank's [Q, k] f32 scores and int64 indices packed as
+    # [Q, 3k] 32-bit words (12 B per candidate), all-gathered, then unpacked
+    Q = s.shape[0]
+    packed = torch.cat([s.contiguous().view(torch.int32), i.contiguous().view(torch.int32)], dim=1).contiguous()
+    gp = [torch.empty_like(packed) for _ in range(world)]
+    dist.all_gather(gp, packed, group=group)
+    cand_s = torch.cat([g[:, :k].contiguous().view(torch.float32) for g in gp], dim=1).contiguous()   # [Q, world*k]
+    cand_i = torch.cat([g[:, k:].contiguous().view(torch.int64) for g in gp], dim=1).contiguous()
+    assert cand_s.shape == (Q, world * k) and cand_i.shape == (Q, world * k)
     return merge(cand_s, cand_i, k, nan_policy=nan_policy)

@@ -257,3 +257,22 @@ def test_mirror_large_corpus_ties_nan(gpu):
         assert torch.equal(i1, i0)
         assert torch.equal(s1.view(torch.int32), s0.view(torch.int32))
     assert mc.certified >= 30   # NaN-last: certified; NaN-first: the NaN row is a candidate -> exact pass
+
+
+@pytest.mark.parametrize("N,Q", [(1, 1), (9, 3), (1000, 32), (10000, 33), (100003, 32)])
+def test_rank_reg_nine_slot_ring_bit_identical(gpu, monkeypatch, N, Q):
+    """rank_reg's 9-slot / 7-in-flight ring (MICLIP_RANK_NB=9), with its LDS
+    allocation sized from the same rank_reg_lds_bytes(NB) as the kernel's ring
+    (round 2's attempt allocated 8 slots' worth: the norms sat past the end of
+    the LDS, read as zeros, and every test failed): bit-identical to the
+    default 8-slot ring, including N = 1."""
+    import torch
+    from miclip import retrieval, weights
+    corpus = _t(weights.normal(21, f"nb{N}", (N, 512)), gpu)
+    q = _t(weights.synthetic_corpus(Q, 512, seed=22), gpu)
+    monkeypatch.delenv("MICLIP_RANK_NB", raising=False)
+    s8, i8 = retrieval.rank_topk(corpus, q, 10)
+    monkeypatch.setenv("MICLIP_RANK_NB", "9")
+    s9, i9 = retrieval.rank_topk(corpus, q, 10)
+    torch.cuda.synchronize()
+    assert torch.equal(i8, i9) and torch.equal(s8, s9)
