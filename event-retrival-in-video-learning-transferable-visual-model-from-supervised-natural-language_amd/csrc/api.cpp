@@ -453,11 +453,23 @@ int mi_clip_reserve(mi_clip* c, int64_t image_chunk, int64_t text_chunk) {
   return reserve_locked(c, image_chunk, text_chunk);
 }
 
+// A/B switches (MICLIP_* environment overrides of the measured defaults) are
+// read only by the A/B build (scripts/ab, MICLIP_AB=1); the product library
+// always runs the defaults.
+static const char* ab_getenv(const char* name) {
+#if MICLIP_AB
+  return getenv(name);
+#else
+  (void)name;
+  return nullptr;
+#endif
+}
+
 // GEMM main-loop schedule (gemm.hip): MICLIP_GEMM_VARIANT overrides the default.
 static int gemm_variant() {
   static int v = -1;
   if (v < 0) {
-    const char* e = getenv("MICLIP_GEMM_VARIANT");
+    const char* e = ab_getenv("MICLIP_GEMM_VARIANT");
     v = e ? atoi(e) : 0;
   }
   return v;
@@ -471,7 +483,7 @@ static int gemm_variant_for(int which) {
   static const char* names[4] = {"MICLIP_GEMM_VARIANT_QKV", "MICLIP_GEMM_VARIANT_OUT", "MICLIP_GEMM_VARIANT_FC",
                                  "MICLIP_GEMM_VARIANT_PROJ"};
   if (v[which] < 0) {
-    const char* e = getenv(names[which]);
+    const char* e = ab_getenv(names[which]);
     v[which] = e ? atoi(e) : 0;
   }
   return v[which];
@@ -499,7 +511,7 @@ static GemmArgs gargs(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t
 static int resid16() {
   static int v = -1;
   if (v < 0) {
-    const char* e = getenv("MICLIP_RESID16");
+    const char* e = ab_getenv("MICLIP_RESID16");
     v = e ? atoi(e) != 0 : 1;
   }
   return v;
@@ -510,7 +522,7 @@ static int resid16() {
 static int patch_fused() {
   static int v = -1;
   if (v < 0) {
-    const char* e = getenv("MICLIP_PATCH_FUSED");
+    const char* e = ab_getenv("MICLIP_PATCH_FUSED");
     v = e ? atoi(e) != 0 : 1;
   }
   return v;
@@ -520,7 +532,7 @@ static int patch_fused() {
 static int embed_ln1() {
   static int v = -1;
   if (v < 0) {
-    const char* e = getenv("MICLIP_EMBED_LN1");
+    const char* e = ab_getenv("MICLIP_EMBED_LN1");
     v = e ? atoi(e) != 0 : 1;
   }
   return v;
@@ -852,6 +864,7 @@ int mi_op_gemm(const void* A, const void* W, const float* bias, void* out, int32
   if (!A || !W || !out || M < 0) return fail(MI_ERR_ARG, "mi_op_gemm: bad arguments");
   if (K % 64 || N % 128 || K <= 0) return fail(MI_ERR_UNSUPPORTED, "mi_op_gemm: needs K %% 64 == 0, N %% 128 == 0");
   const int variant = epi >> 8;  // bits 8+: schedule override for A/B measurements
+  if (variant && !MICLIP_AB) return fail(MI_ERR_UNSUPPORTED, "mi_op_gemm: schedule overrides need the A/B build (make ab)");
   epi &= 0xff;
   if (epi < 0 || epi > 3) return fail(MI_ERR_ARG, "mi_op_gemm: bad epilogue");
   GemmArgs g = gargs((const uint16_t*)A, K, (const uint16_t*)W, K, bias, out, N, M, N, K);
@@ -905,6 +918,7 @@ int mi_op_residual_ln(void* x, const void* delta, const float* g, const float* b
 int mi_op_attention(const void* qkv, void* out, int32_t B, int32_t S, int32_t W, int32_t causal, void* stream) {
   if (!qkv || !out || B < 0 || S < 1) return fail(MI_ERR_ARG, "mi_op_attention: bad arguments");
   if (W % 64 || S > 640 || (causal & ~0x301)) return fail(MI_ERR_UNSUPPORTED, "mi_op_attention: W %% 64 == 0 and S <= 640");
+  if ((causal & 0x100) && !MICLIP_AB) return fail(MI_ERR_UNSUPPORTED, "mi_op_attention: the one-wave kernel (bit 8) is in the A/B build");
   HIP_TRY(attention((const uint16_t*)qkv, (uint16_t*)out, B, S, W, causal, (hipStream_t)stream));
   return MI_OK;
 }
@@ -914,6 +928,7 @@ int mi_op_gemm_mx(const void* A, const void* a_scale, const void* W, const void*
   if (!A || !W || !a_scale || !w_scale || !out || M < 0) return fail(MI_ERR_ARG, "mi_op_gemm_mx: bad arguments");
   if (K % 128 || N % 256 || K <= 0) return fail(MI_ERR_UNSUPPORTED, "mi_op_gemm_mx: needs K %% 128 == 0, N %% 256 == 0");
   const int variant = epi >> 8;  // bits 8+: kernel override for A/B (gemm_mx: 1 = 16x16x128, 3 = ping-pong)
+  if (variant && !MICLIP_AB) return fail(MI_ERR_UNSUPPORTED, "mi_op_gemm_mx: kernel overrides need the A/B build (make ab)");
   epi &= 0xff;
   if (epi != 0 && epi != 1 && epi != 3 && epi != 4)
     return fail(MI_ERR_ARG, "mi_op_gemm_mx: epilogue 0 (bf16), 1 (GELU), 3 (f32) or 4 (GELU -> MX-fp8)");

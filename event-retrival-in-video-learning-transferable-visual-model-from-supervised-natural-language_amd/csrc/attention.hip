@@ -573,7 +573,12 @@ hipError_t attention(const uint16_t* qkv, uint16_t* out, int B, int S, int W, in
   // 30.0, L/14 408 vs 572 and L/14@336 547 vs 1004 for the per-query-tile-K
   // kernel it replaced).  Causal bit 8 selects the one-wave kernel for S <= 96
   // (A/B and parity tests of both paths; it has no fp8 output).
+#if MICLIP_AB
   const bool one_wave = ((causal >> 8) & 1) && S <= 96 && !q8;
+#else
+  if ((causal >> 8) & 1) return hipErrorNotSupported;   // the one-wave kernel is in the A/B build only
+  constexpr bool one_wave = false;
+#endif
   const bool old_flash = (causal >> 9) & 1;   // A/B: the chunk-streaming flash kernel for S > 64
   causal &= 1;
   const dim3 grid(items);
@@ -592,12 +597,14 @@ hipError_t attention(const uint16_t* qkv, uint16_t* out, int B, int S, int W, in
     hipLaunchKernelGGL(attention_res_kernel<8>, grid, dim3(512), lds, s, qkv, out, S, W, H, q8, qs, rp);
     return hipGetLastError();
   }
+#if MICLIP_AB
   if (one_wave) {
     if (S <= 32) hipLaunchKernelGGL(attention_kernel<32>, grid, dim3(64), 0, s, qkv, out, S, W, H, causal, items);
     else if (S <= 64) hipLaunchKernelGGL(attention_kernel<64>, grid, dim3(64), 0, s, qkv, out, S, W, H, causal, items);
     else hipLaunchKernelGGL(attention_kernel<96>, grid, dim3(64), 0, s, qkv, out, S, W, H, causal, items);
     return hipGetLastError();
   }
+#endif
   // NT = ceil(tiles / 8) query tiles per wave on 8 waves; S <= 64: one tile on
   // each of 4 waves, single slot.  Fewer waves with fewer idle tile slots
   // measured slower (L/14 257 tokens on 6 waves x 3 tiles: 470 vs 421 us; text

@@ -3,6 +3,14 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// MICLIP_AB = 1 builds the A/B library (scripts/ab/libmiclip_ab.so, `make ab`):
+// every measured alternative schedule, ablation and timing probe of the
+// kernels plus their MICLIP_* environment switches.  The product library
+// (libmiclip.so, MICLIP_AB = 0) holds the measured defaults only.
+#ifndef MICLIP_AB
+#define MICLIP_AB 0
+#endif
+
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));

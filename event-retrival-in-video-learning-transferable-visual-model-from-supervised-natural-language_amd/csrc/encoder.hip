@@ -413,11 +413,15 @@ hipError_t residual_ln(float* x, const uint16_t* delta, int64_t stride, int writ
   // per LN and next touched milliseconds later; keeping it out of the Infinity
   // Cache leaves that to the GEMM/attention operands): +1.8 % end to end on
   // B/32.  MICLIP_LN_NT=0 selects plain accesses (A/B).
+#if MICLIP_AB
   static int nts = -1;
   if (nts < 0) {
     const char* e = getenv("MICLIP_LN_NT");
     nts = e ? atoi(e) : 1;
   }
+#else
+  constexpr int nts = 1;
+#endif
   const dim3 grid((rows + 3) / 4), block(256);
 #define RLN(NT, XM) hipLaunchKernelGGL((residual_ln_kernel<NT, XM>), grid, block, 0, s, x, delta, stride, write_x, g, b, out, rows, W, q, qs)
   if (nts) {
@@ -425,9 +429,11 @@ hipError_t residual_ln(float* x, const uint16_t* delta, int64_t stride, int writ
     else if (xmode == RES_F32_TO_F16) RLN(true, RES_F32_TO_F16);
     else RLN(true, RES_F16);
   } else {
+#if MICLIP_AB
     if (xmode == RES_F32) RLN(false, RES_F32);
     else if (xmode == RES_F32_TO_F16) RLN(false, RES_F32_TO_F16);
     else RLN(false, RES_F16);
+#endif
   }
 #undef RLN
   return hipGetLastError();

@@ -885,8 +885,13 @@ int n_group(int tiles_n, int K) {
   return 0;
 }
 
+#if MICLIP_AB
+// A/B build (scripts/ab, MICLIP_AB=1): every schedule, ablation and probe
+// variant of rounds 1-2 stays selectable by GemmArgs::variant for
+// scripts/gemm_micro.py and the bit-identity tests; the product library
+// (MICLIP_AB=0) compiles only the default path below.
 template <int EPI>
-hipError_t launch(const GemmArgs& a, hipStream_t s) {
+hipError_t launch_ab(const GemmArgs& a, hipStream_t s) {
   const bool big = a.N % 256 == 0 && a.M >= 1024;
   // variant 0 (default): ping-pong, one 32-MFMA cluster per stage, direct
   // permlane-swapped row stores for bf16 outputs (16, or its persistent form
@@ -1026,11 +1031,61 @@ hipError_t launch(const GemmArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+#endif  // MICLIP_AB
+
+// Product dispatch: the 8-phase kernel (gemm_8q.hip) for bf16 outputs whenever
+// it applies (every tower GEMM of B/32, L/14, L/14@336 and the text towers
+// with >= 256 rows); otherwise the ping-pong kernels — persistent (18) on wide
+// N or K <= 1024, one tile per workgroup (16) on N = 768 with long K, LDS-staged
+// rows (3) for f32 outputs (patch embedding, projections) — and the generic
+// tiled kernel for shapes too small for them.
+template <int EPI>
+hipError_t launch(const GemmArgs& a, hipStream_t s) {
+  const bool big = a.N % 256 == 0 && a.M >= 1024;
+  const bool bf16_out = EPI == EPI_BF16 || EPI == EPI_GELU_BF16;
+  if (a.patch_R) {  // fused patch gather: f32 output rows, ping-pong only
+    if (!big || a.K != 3 * 32 * 32 || (a.patch_R & 31)) return hipErrorInvalidValue;
+    const int nt = ((a.M + 255) / 256) * (a.N / 256);
+    hipLaunchKernelGGL((gemm_pp_kernel<EPI, 1, false, false, false, true>), dim3(nt), dim3(512), 0, s, a);
+    return hipGetLastError();
+  }
+#if MICLIP_AB
+  if (a.variant != 0) return launch_ab<EPI>(a, s);
+#else
+  if (a.variant != 0) return hipErrorNotSupported;   // schedule overrides exist in the A/B build only
+#endif
+  if (bf16_out && gemm_8q_ok(a)) return gemm_8q(a, EPI, s, cu_count(), 0);
+  const int nt = ((a.M + 255) / 256) * (a.N / 256);
+  const bool staged = big && a.K / BK >= LEAD;
+  if (staged && bf16_out && !a.group && (a.N >= 2048 || a.K <= 1024)) {   // persistent ping-pong (18)
+    const int grid = nt < cu_count() ? nt : cu_count();
+    hipLaunchKernelGGL((gemm_ppp_kernel<EPI>), dim3(grid), dim3(512), 0, s, a);
+  } else if (staged && bf16_out) {                                         // ping-pong, direct row stores (16)
+    hipLaunchKernelGGL((gemm_pp_kernel<EPI, 1, false, true>), dim3(nt), dim3(512), 0, s, a);
+  } else if (staged) {                                                     // ping-pong, LDS-staged f32 rows (3)
+    hipLaunchKernelGGL((gemm_pp_kernel<EPI, 1, false>), dim3(nt), dim3(512), 0, s, a);
+  } else if (big) {
+    const int g = nt < cu_count() ? nt : cu_count();
+    hipLaunchKernelGGL((gemm_kernel<EPI, 256, 256, 2, 4>), dim3(g), dim3(512), 0, s, a);
+  } else {
+    const int nt2 = ((a.M + 127) / 128) * (a.N / 128);
+    const int g = nt2 < 2 * cu_count() ? nt2 : 2 * cu_count();
+    hipLaunchKernelGGL((gemm_kernel<EPI, 128, 128, 2, 2>), dim3(g), dim3(256), 0, s, a);
+  }
+  return hipGetLastError();
+}
+
 }  // namespace
 
 hipError_t gemm_probe_read(unsigned long long* host, int n) {
+#if MICLIP_AB
   if (n > 4096 * 4) n = 4096 * 4;
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_gemm_probe), n * sizeof(unsigned long long), 0, hipMemcpyDeviceToHost);
+#else
+  (void)host;
+  (void)n;
+  return hipErrorNotSupported;   // the timing probe (variant 19) is in the A/B build only
+#endif
 }
 
 hipError_t gemm_bf16(const GemmArgs& a, int epi, hipStream_t s) {

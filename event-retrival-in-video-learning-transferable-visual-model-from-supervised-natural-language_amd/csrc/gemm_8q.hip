@@ -473,6 +473,7 @@ hipError_t gemm_8q(const GemmArgs& a0, int epi, hipStream_t s, int cus, int mode
   const int nt = ((a.M + BM - 1) / BM) * (a.N / BN);
   const int grid = nt < cus ? nt : cus;
 #define L8Q(E, ABL_, F_) hipLaunchKernelGGL((gemm_8q_kernel<E, ABL_, F_>), dim3(grid), dim3(512), 0, s, a)
+#if MICLIP_AB   // ablation / stamp probes: A/B build only
 #define L8Q_ALL(E)                   \
   if (mode == 0) L8Q(E, 0, 0);       \
   else if (mode == 2) L8Q(E, 2, 0);  \
@@ -481,6 +482,11 @@ hipError_t gemm_8q(const GemmArgs& a0, int epi, hipStream_t s, int cus, int mode
   else if (mode == 9) L8Q(E, 9, 0);  \
   else if (mode == 1) L8Q(E, 10, 0);  \
   else return hipErrorInvalidValue;
+#else
+#define L8Q_ALL(E)                   \
+  if (mode == 0) L8Q(E, 0, 0);       \
+  else return hipErrorNotSupported;
+#endif
   if (epi == EPI_GELU_BF16) {
     L8Q_ALL(EPI_GELU_BF16)
   } else if (epi == EPI_BF16) {
@@ -497,7 +503,13 @@ hipError_t gemm_8q(const GemmArgs& a0, int epi, hipStream_t s, int cus, int mode
 
 namespace miclip {
 hipError_t gemm8q_probe_read(unsigned long long* host, int n) {
+#if MICLIP_AB
   if (n > 1024 * 2 * 9) n = 1024 * 2 * 9;
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_probe8q), n * sizeof(unsigned long long), 0, hipMemcpyDeviceToHost);
+#else
+  (void)host;
+  (void)n;
+  return hipErrorNotSupported;   // stamp probe: A/B build only
+#endif
 }
 }  // namespace miclip

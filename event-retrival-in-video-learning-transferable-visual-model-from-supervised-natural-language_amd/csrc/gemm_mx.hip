@@ -512,8 +512,14 @@ hipError_t gemm_mx(const GemmArgs& a, int epi, hipStream_t s) {
   // bit-identical to 1, but 8-30 % slower than the ping-pong kernel at the L/14@336 shapes,
   // scripts/gemm_mx_micro.py — at fp8 rate a K = 1024 tile's MFMAs take half the bf16 time
   // while its epilogue does not shrink)
+#if MICLIP_AB
   if (a.variant == 8 && gemm_mx8q_ok(a, epi)) return gemm_mx8q(a, epi, s, cu_count());
-  if (a.variant != 1 && a.K / 64 >= 3) {
+  const bool force_dbuf = a.variant == 1;
+#else
+  if (a.variant != 0) return hipErrorNotSupported;   // kernel overrides exist in the A/B build only
+  const bool force_dbuf = false;
+#endif
+  if (!force_dbuf && a.K / 64 >= 3) {
     switch (epi) {
       case EPI_BF16: hipLaunchKernelGGL(gemm_mxpp_kernel<EPI_BF16>, dim3(nt), dim3(512), 0, s, a); break;
       case EPI_GELU_BF16: hipLaunchKernelGGL(gemm_mxpp_kernel<EPI_GELU_BF16>, dim3(nt), dim3(512), 0, s, a); break;

@@ -3,6 +3,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#ifndef MICLIP_AB   // 1: the A/B build (common.hpp)
+#define MICLIP_AB 0
+#endif
+
 namespace miclip {
 
 enum GemmEpi {

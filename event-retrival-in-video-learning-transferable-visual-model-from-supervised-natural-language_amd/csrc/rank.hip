@@ -1035,6 +1035,7 @@ static hipError_t launch_reg(int64_t N, const float* corpus, const float* q, int
   C = nwg * k;
   // interleaved tile order: A/B only (MICLIP_RANK_ILV=1).  scripts/rank_micro.py: 1M x 512 494 us
   // against 479 with contiguous row ranges, 1M x 768 729 against 717: not the stream's limit
+#if MICLIP_AB
   const char* ilv = getenv("MICLIP_RANK_ILV");
   const bool il = ilv && ilv[0] == '1';
   // ring slots: MICLIP_RANK_NB=9 selects a 9-slot ring with 7 chunks in flight (A/B; round 2's
@@ -1053,6 +1054,11 @@ static hipError_t launch_reg(int64_t N, const float* corpus, const float* q, int
             : (probe && probe[0] == '1') ? (il ? rank_reg<D, 8, 6, true, true> : rank_reg<D, 8, 6, true>)
             : il ? (pp ? rank_reg<D, 8, 6, false, true, true> : rank_reg<D, 8, 6, false, true>)
                  : (pp ? rank_reg<D, 8, 6, false, false, true> : rank_reg<D, 8, 6>);
+#else   // product: the measured default (8 slots, 6 chunks in flight, contiguous row ranges)
+  const bool il = false;
+  const size_t lds = rank_reg_lds_bytes(8);
+  auto fn = rank_reg<D, 8, 6>;
+#endif
   hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
   const dim3 grid((unsigned)((Q + RQ - 1) / RQ), (unsigned)nwg);   // (query blocks, row blocks): RB / QB
@@ -1087,14 +1093,20 @@ hipError_t rank_topk(const void* corpus, int64_t N, int64_t D, int dt, const flo
   // waves per workgroup (MICLIP_RANK_NW A/B), one workgroup per CU either way
   // (~150 VGPRs, LDS = the list area).  KC = 64 keeps rank_stage1 (its 64-deep
   // lists would go to scratch in the streaming kernel).
+#if MICLIP_AB
   const char* nwenv = getenv("MICLIP_RANK_NW");
   const int NW = nwenv && atoi(nwenv) == 8 ? 8 : 12;
+  const char* legacy = getenv("MICLIP_RANK_STAGE1");   // A/B: the previous one-tile-at-a-time kernel
+  const char* noreg = getenv("MICLIP_RANK_REG");        // A/B: 0 = rank_stream for f32 D = 512 too
+#else
+  constexpr int NW = 12;
+  const char* legacy = nullptr;
+  const char* noreg = nullptr;
+#endif
   const size_t qa = (size_t)RQ * (D + 4) * 4 + (size_t)NW * 32 * 4 + RQ * 4;
   const size_t la = (size_t)64 * NW * KC * 8;
   const size_t lds = qa > la ? qa : la;
   hipError_t e;
-  const char* legacy = getenv("MICLIP_RANK_STAGE1");   // A/B: the previous one-tile-at-a-time kernel
-  const char* noreg = getenv("MICLIP_RANK_REG");        // A/B: 0 = rank_stream for f32 D = 512 too
   if (KC == 16 && dt == 0 && D == 512 && !(legacy && legacy[0] == '1') && !(noreg && noreg[0] == '0')) {
     int64_t Creg = 0;
     // (D = 768 would hold 384 query VGPRs: hipcc spills ~230, so it keeps rank_stream)
@@ -1112,8 +1124,11 @@ hipError_t rank_topk(const void* corpus, int64_t N, int64_t D, int dt, const flo
   } else {
 #define MI_RS(DTV, NWV) \
   launch_stream<DTV, NWV>(grid, lds, s, corpus, N, D, q, Q, k, rpw, norm_mode, nan_first, base, ws_s, ws_i, C)
+#if MICLIP_AB
     if (NW == 8) e = dt == 0 ? MI_RS(0, 8) : dt == 1 ? MI_RS(1, 8) : MI_RS(2, 8);
-    else e = dt == 0 ? MI_RS(0, 12) : dt == 1 ? MI_RS(1, 12) : MI_RS(2, 12);
+    else
+#endif
+      e = dt == 0 ? MI_RS(0, 12) : dt == 1 ? MI_RS(1, 12) : MI_RS(2, 12);
 #undef MI_RS
   }
   if (e != hipSuccess) return e;

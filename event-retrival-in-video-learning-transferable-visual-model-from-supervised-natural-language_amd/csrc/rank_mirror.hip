@@ -429,11 +429,15 @@ static hipError_t launch_mirror(const uint16_t* mirror, int64_t N, const float* 
   const int64_t rpw = ((N + nwg - 1) / nwg + 127) / 128 * 128;   // whole tiles per wave round
   // MICLIP_MIRROR_VAR (A/B): 1 fragments read after the wait (no PIPE), 2 seven chunks in
   // flight, 3 interleaved tiles
+#if MICLIP_AB
   const char* var = getenv("MICLIP_MIRROR_VAR");
   const int v = var ? atoi(var) : 0;
   auto fn = v == 1 ? rank_mirror_kernel<D, SPLIT, false, false>
             : v == 2 ? rank_mirror_kernel<D, SPLIT, false, true, 8, 7>
             : v == 3 ? rank_mirror_kernel<D, SPLIT, true> : rank_mirror_kernel<D, SPLIT>;
+#else
+  auto fn = rank_mirror_kernel<D, SPLIT>;
+#endif
   hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
   const dim3 grid((unsigned)((Q + MQ - 1) / MQ), (unsigned)nwg);   // (query blocks, row blocks): RB / QB

@@ -15,6 +15,11 @@ from .config import CLIPConfig
 
 LIB_NAME = "libmiclip.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+# the A/B build (csrc `make ab`): the same C-ABI plus every alternative kernel
+# schedule, ablation and probe; used by scripts/*_micro.py (MICLIP_LIB=ab) and
+# the bit-identity tests of the alternatives, never by the product path
+AB_LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
+                           "scripts", "ab", "libmiclip_ab.so")
 
 MI_F32, MI_BF16, MI_F16, MI_FP8 = 0, 1, 2, 3
 MI_NAN_FIRST, MI_NAN_LAST = 0, 1
@@ -52,23 +57,44 @@ class Arch(ctypes.Structure):
 
 
 _lib = None
+_lib_ab = None
 
 
 def lib():
-    """Load libmiclip.so once; raise if it is absent (no silent fallback)."""
+    """Load libmiclip.so once; raise if it is absent (no silent fallback).
+    ``$MICLIP_LIB=ab`` loads the A/B build instead (measurement scripts)."""
     global _lib
     if _lib is not None:
+        return _lib
+    if os.environ.get("MICLIP_LIB") == "ab":
+        _lib = lib_ab()
         return _lib
     if not os.path.isfile(LIB_PATH):
         raise MiClipError(f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
                           " or `make -C <pkg>/csrc`")
+    _lib = _bind(LIB_PATH)
+    return _lib
+
+
+def lib_ab():
+    """The A/B library (scripts/ab/libmiclip_ab.so); raises if it is not built."""
+    global _lib_ab
+    if _lib_ab is not None:
+        return _lib_ab
+    if not os.path.isfile(AB_LIB_PATH):
+        raise MiClipError(f"{AB_LIB_PATH} not found: `make -C <pkg>/csrc ab`")
+    _lib_ab = _bind(AB_LIB_PATH)
+    return _lib_ab
+
+
+def _bind(path):
     # torch ships its own libamdhip64 with the same SONAME (libamdhip64.so.7)
     # as /opt/rocm's.  Loading torch first makes the dynamic linker bind
     # libmiclip to torch's HIP runtime, so tensors, streams and our kernels
     # live in ONE runtime; the other order makes torch bind to /opt/rocm's
     # runtime and fail ("No HIP GPUs are available").
     import torch  # noqa: F401
-    L = ctypes.CDLL(LIB_PATH)
+    L = ctypes.CDLL(path)
     P, I32, I64, SZ = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_size_t
     sig = {
         "mi_abi_version": (ctypes.c_int, []),
@@ -109,7 +135,6 @@ def lib():
         fn.argtypes = args
     if L.mi_abi_version() != 1:
         raise MiClipError("libmiclip ABI version mismatch")
-    _lib = L
     return L
 
 

@@ -11,6 +11,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+os.environ.setdefault("MICLIP_LIB", "ab")   # A/B build: schedule variants, probes and MICLIP_* switches
 sys.path.insert(0, os.path.join(os.path.dirname(ROOT), "event-retrival-in-video-learning-transferable-visual-model-from-supervised-natural-language_amd"))
 
 import torch  # noqa: E402

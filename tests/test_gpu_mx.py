@@ -135,8 +135,11 @@ def test_gemm_mx8q_matches_16x16x128_kernel(gpu, M, N, K, epi):
             out = torch.zeros((M * N + 255) // 256 * 256 + (N // 128) * mp * 2, dtype=torch.uint8, device=gpu)
         else:
             out = torch.zeros(M, N, dtype=torch.bfloat16, device=gpu)
-        N_.check(N_.lib().mi_op_gemm_mx(qa.data_ptr(), sa.data_ptr(), qw.data_ptr(), sw.data_ptr(), bias.data_ptr(),
-                                        out.data_ptr(), M, N, K, epi | (variant << 8), _stream()), "gemm_mx")
+        AB = N_.lib_ab()          # kernel overrides: the A/B build (scripts/ab)
+        rc = AB.mi_op_gemm_mx(qa.data_ptr(), sa.data_ptr(), qw.data_ptr(), sw.data_ptr(), bias.data_ptr(),
+                              out.data_ptr(), M, N, K, epi | (variant << 8), _stream())
+        if rc:
+            raise N_.MiClipError(f"gemm_mx v{variant}: {AB.mi_last_error()}")
         outs.append(out)
     torch.cuda.synchronize()
     assert torch.equal(outs[0].view(torch.uint8), outs[1].view(torch.uint8))

@@ -51,18 +51,24 @@ def test_gemm_8phase_schedules_bit_identical(gpu, M, N, K, epi):
     """The 8-phase kernels (gemm_8p v98, gemm_8q v110 block epilogue / v113 flat DMAs; gemm_8r v120 256 x 128 deferred epilogue
     DMAs) run the same MFMA order and epilogue arithmetic, so their outputs
     must match bit for bit, over multi-tile persistent walks, partial last
-    M-tiles and one-pair K; v98 is also checked against torch fp32."""
+    M-tiles and one-pair K; v98 is also checked against torch fp32.  The
+    variants live in the A/B build (scripts/ab); the product library's default
+    path must equal them too."""
     import torch
     N_ = _lib()
+    AB = N_.lib_ab()
     g = torch.Generator(device="cpu").manual_seed(M + N + K)
     A = (torch.rand(M, K, generator=g) * 2 - 1).bfloat16().to(gpu)
     W = ((torch.rand(N, K, generator=g) * 2 - 1) * K ** -0.5).bfloat16().to(gpu)
     bias = torch.randn(N, generator=g).float().to(gpu)
     outs = {}
-    for v in (98, 110, 113, 120):
+    for v in (98, 110, 113, 120, 0):
         out = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=gpu)
-        N_.check(N_.lib().mi_op_gemm(A.data_ptr(), W.data_ptr(), bias.data_ptr(), out.data_ptr(), M, N, K,
-                                     epi | (v << 8), _stream()), f"gemm v{v}")
+        L = N_.lib() if v == 0 else AB            # v = 0: the product library's default dispatch
+        rc = L.mi_op_gemm(A.data_ptr(), W.data_ptr(), bias.data_ptr(), out.data_ptr(), M, N, K, epi | (v << 8),
+                          _stream())
+        if rc:
+            raise N_.MiClipError(f"gemm v{v}: {L.mi_last_error()}")
         outs[v] = out
     torch.cuda.synchronize()
     ref = A.float() @ W.float().t() + bias
@@ -70,8 +76,12 @@ def test_gemm_8phase_schedules_bit_identical(gpu, M, N, K, epi):
         ref = ref * torch.sigmoid(1.702 * ref)
     err = (outs[98].float() - ref).abs().max().item()
     assert err < 2e-2 * max(1.0, ref.abs().max().item()), err
-    for v in (110, 113, 120):
+    for v in (110, 113, 120, 0):
         assert torch.equal(outs[v], outs[98]), f"v{v} differs from v98"
+    # the product library has no schedule overrides: they fail loudly instead of falling back
+    rc = N_.lib().mi_op_gemm(A.data_ptr(), W.data_ptr(), bias.data_ptr(), outs[0].data_ptr(), M, N, K,
+                             epi | (98 << 8), _stream())
+    assert rc == -3 and b"A/B build" in N_.lib().mi_last_error()      # MI_ERR_UNSUPPORTED
 
 
 def test_gemm_asymmetric_identity(gpu):
@@ -154,7 +164,10 @@ def test_attention(gpu, B, S, W, causal, flash):
     g = torch.Generator(device="cpu").manual_seed(B * S + W + causal)
     qkv = (torch.randn(B * S, 3 * W, generator=g) * 1.5).bfloat16().to(gpu)
     out = torch.empty(B * S, W, dtype=torch.bfloat16, device=gpu)
-    N_.check(N_.lib().mi_op_attention(qkv.data_ptr(), out.data_ptr(), B, S, W, causal | flash, _stream()), "attention")
+    L = N_.lib_ab() if flash == 0x100 else N_.lib()   # the one-wave kernel is in the A/B build
+    rc = L.mi_op_attention(qkv.data_ptr(), out.data_ptr(), B, S, W, causal | flash, _stream())
+    if rc:
+        raise N_.MiClipError(f"attention: {L.mi_last_error()}")
     torch.cuda.synchronize()
     H = W // 64
     x = qkv.double().reshape(B, S, 3, H, 64)

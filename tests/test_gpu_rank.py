@@ -261,18 +261,18 @@ def test_mirror_large_corpus_ties_nan(gpu):
 
 @pytest.mark.parametrize("N,Q", [(1, 1), (9, 3), (1000, 32), (10000, 33), (100003, 32)])
 def test_rank_reg_nine_slot_ring_bit_identical(gpu, monkeypatch, N, Q):
-    """rank_reg's 9-slot / 7-in-flight ring (MICLIP_RANK_NB=9), with its LDS
+    """rank_reg's 9-slot / 7-in-flight ring (A/B build, MICLIP_RANK_NB=9), with its LDS
     allocation sized from the same rank_reg_lds_bytes(NB) as the kernel's ring
     (round 2's attempt allocated 8 slots' worth: the norms sat past the end of
     the LDS, read as zeros, and every test failed): bit-identical to the
     default 8-slot ring, including N = 1."""
     import torch
-    from miclip import retrieval, weights
+    from miclip import _native, retrieval, weights
     corpus = _t(weights.normal(21, f"nb{N}", (N, 512)), gpu)
     q = _t(weights.synthetic_corpus(Q, 512, seed=22), gpu)
-    monkeypatch.delenv("MICLIP_RANK_NB", raising=False)
-    s8, i8 = retrieval.rank_topk(corpus, q, 10)
-    monkeypatch.setenv("MICLIP_RANK_NB", "9")
+    s8, i8 = retrieval.rank_topk(corpus, q, 10)                    # product library: the 8-slot ring
+    monkeypatch.setattr(_native, "lib", _native.lib_ab)             # the A/B build, whose MICLIP_RANK_NB=9 ...
+    monkeypatch.setenv("MICLIP_RANK_NB", "9")                       # ... selects rank_reg<512, 9, 7>
     s9, i9 = retrieval.rank_topk(corpus, q, 10)
     torch.cuda.synchronize()
     assert torch.equal(i8, i9) and torch.equal(s8, s9)
