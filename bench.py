@@ -181,9 +181,9 @@ def jpeg_ingest_timing(dev, n_px, B=8192, threads=16, pil_frames=1024):
     table build on the host, mi_jpeg_decode + mi_preprocess_frames on the
     device (bit-identical to Pillow, tests/test_gpu_jpeg.py); host path: Pillow
     decode on `threads` host threads, as the reference decodes, + the same GPU
-    preprocessing, timed on the first `pil_frames` frames.  The GPU decode
-    runs one lane per frame, so its rate grows with the batch (8192 frames =
-    128 waves).  Wall-clock, synchronised; not part of the timed step."""
+    preprocessing, timed on the first `pil_frames` frames.  The GPU entropy
+    decode runs one lane per 1-KB chunk of a frame's scan (jpeg.hip, chunked
+    speculative decode).  Wall-clock, synchronised; not part of the timed step."""
     import glob
     import io
     import time
@@ -200,9 +200,8 @@ def jpeg_ingest_timing(dev, n_px, B=8192, threads=16, pil_frames=1024):
     raw = [open(f, "rb").read() for f in files]
     bufs = [raw[i % len(raw)] for i in range(B)]
 
-    def gpu():
-        fr = jpeg.decode_batch(bufs, dev)
-        return preprocess_frames(torch.stack(fr), n_px, out_dtype=torch.bfloat16)
+    def gpu():   # each geometry group's decoded [B,H,W,3] buffer goes straight to the resampler
+        return [preprocess_frames(rgb, n_px, out_dtype=torch.bfloat16) for _, rgb in jpeg.decode_groups(bufs, dev)]
 
     def pil_one(b):
         with Image.open(io.BytesIO(b)) as im:

@@ -979,15 +979,15 @@ int mi_preprocess_frames(const uint8_t* frames, int64_t B, int32_t H, int32_t W,
   return MI_OK;
 }
 
-size_t mi_jpeg_workspace_bytes(const int32_t* geom, int32_t B) {
+size_t mi_jpeg_workspace_bytes(const int32_t* geom, int32_t B, int64_t data_bytes) {
   if (!geom || B < 0) return 0;
-  return jpeg_workspace_bytes(geom, B);
+  return jpeg_workspace_bytes(geom, B, data_bytes);
 }
 
-int mi_jpeg_decode(const uint8_t* data, const int64_t* seg_off, const int64_t* seg_end, const void* huff,
+int mi_jpeg_decode(const uint8_t* data, int64_t data_bytes, const int64_t* seg_off, const int64_t* seg_end, const void* huff,
                    const int32_t* huff_idx, int32_t nsets, const uint16_t* qtab, const int32_t* geom, int32_t B,
                    uint8_t* out_rgb, void* workspace, size_t workspace_bytes, void* stream) {
-  if (!geom || B < 0) return fail(MI_ERR_ARG, "mi_jpeg_decode: bad arguments");
+  if (!geom || B < 0 || data_bytes < 0) return fail(MI_ERR_ARG, "mi_jpeg_decode: bad arguments");
   if (huff_idx && nsets < 1) return fail(MI_ERR_ARG, "mi_jpeg_decode: huff_idx needs nsets >= 1");
   if (B == 0) return MI_OK;
   if (!data || !seg_off || !seg_end || !huff || !qtab || !out_rgb) return fail(MI_ERR_ARG, "mi_jpeg_decode: null pointer");
@@ -1005,10 +1005,10 @@ int mi_jpeg_decode(const uint8_t* data, const int64_t* seg_off, const int64_t* s
     if (geom[11 + c] < 0 || geom[11 + c] > 3 || geom[14 + c] < 0 || geom[14 + c] > 1 || geom[17 + c] < 0 ||
         geom[17 + c] > 1)
       return fail(MI_ERR_ARG, "mi_jpeg_decode: bad table selector");
-  const size_t need = jpeg_workspace_bytes(geom, B);
+  const size_t need = jpeg_workspace_bytes(geom, B, data_bytes);
   if (!workspace || workspace_bytes < need)
     return fail(MI_ERR_ARG, "mi_jpeg_decode: workspace too small (%zu < %zu)", workspace_bytes, need);
-  HIP_TRY(jpeg_decode(data, seg_off, seg_end, huff, huff_idx, nsets, qtab, geom, B, out_rgb, workspace, workspace_bytes,
+  HIP_TRY(jpeg_decode(data, data_bytes, seg_off, seg_end, huff, huff_idx, nsets, qtab, geom, B, out_rgb, workspace, workspace_bytes,
                       (hipStream_t)stream));
   return MI_OK;
 }

@@ -78,10 +78,10 @@ hipError_t gemm_8q(const GemmArgs& a, int epi, hipStream_t s, int cus, int mode 
 hipError_t gemm8q_probe_read(unsigned long long* host, int n);   // ABL 9 stamps (gemm_8q.hip)
 // baseline JPEG decode (jpeg.hip); geom as mi_jpeg_decode
 constexpr int JPEG_LDS_SETS = 4;   // table sets staged in LDS (4 x 3480 B each, <= 64 KB)
-hipError_t jpeg_decode(const uint8_t* data, const int64_t* seg_off, const int64_t* seg_end, const void* huff,
-                       const int32_t* huff_idx, int nsets, const uint16_t* qtab, const int32_t* geom, int nframes, uint8_t* out_rgb, void* ws,
-                       size_t ws_bytes, hipStream_t s);
-size_t jpeg_workspace_bytes(const int32_t* geom, int nframes);
+hipError_t jpeg_decode(const uint8_t* data, int64_t data_bytes, const int64_t* seg_off, const int64_t* seg_end,
+                       const void* huff, const int32_t* huff_idx, int nsets, const uint16_t* qtab, const int32_t* geom,
+                       int nframes, uint8_t* out_rgb, void* ws, size_t ws_bytes, hipStream_t s);
+size_t jpeg_workspace_bytes(const int32_t* geom, int nframes, int64_t data_bytes);
 // 256 x 128 tiles, deferred (drained) epilogue, three-slot ring (gemm_8r.hip)
 int gemm_8r_ok(const GemmArgs& a);
 hipError_t gemm_8r(const GemmArgs& a, int epi, hipStream_t s, int cus, int mode = 0);

@@ -23,6 +23,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 
 #include "internal.hpp"
 #include "miclip.h"
@@ -354,6 +355,447 @@ __global__ __launch_bounds__(64) void jpeg_entropy_kernel(const uint8_t* __restr
   }
 }
 
+// ---- speculative parallel entropy decode (scans without restart markers) --
+// A lane per frame leaves the chip mostly idle (8192 frames = 128 waves) and a
+// frame takes ~0.3 s of one lane.  For a scan without restart markers the
+// frame's entropy-coded data is instead split into chunks of JP_CHUNK bytes,
+// decoded by one lane each (Weissenberger & Schmidt's self-synchronising
+// parallel Huffman decoding, extended with JPEG's block state):
+//   1. unstuff: the scan's bytes with the 0x00 after each 0xFF removed and
+//      everything from the first marker on dropped (libjpeg then feeds zeros,
+//      as BitReader does) -> a plain bit stream per frame (jp_unstuff_*);
+//   2. phase 1: the lane of chunk t starts at the chunk's first bit GUESSING
+//      the state "block 0 of an MCU, coefficient 0" and decodes up to the
+//      first symbol boundary at or past the chunk's end: its exit state
+//      (bit position, block within the MCU, coefficient index), the blocks it
+//      completed and its DC-difference sums per component (jp_sync, round 0);
+//   3. rounds: the lane of chunk t re-decodes from the exit state of chunk
+//      t - 1 whenever that changed in the previous round; a chunk whose exit
+//      state does not change is consistent with its predecessor.  Chunk 0
+//      starts at the true state, so after a round with no change every chunk
+//      is, and its exit states are the true ones.  Huffman codes resynchronise
+//      within a few symbols: on the reference frames, 224 of 225 1-KB chunks
+//      had the true exit state after phase 1 (scripts/jpeg_sync_proto.py);
+//   4. prefix sums of the block counts and DC sums per frame give each chunk
+//      its first block index and DC predictors (jp_prefix);
+//   5. the final pass decodes every chunk from its true entry state and writes
+//      the coefficients (jp_final).  A frame still changing after the last
+//      round (never seen) is decoded serially by its chunk-0 lane instead, so
+//      the output is always the serial decode's.
+// Same table look-ups, symbol semantics, zero feed and block walk as
+// jpeg_entropy_kernel, so the coefficients are bit-identical to it.
+constexpr int JP_CHUNK = 1024;    // unstuffed bytes per chunk (scripts/jpeg_sync_proto.py)
+constexpr int JP_ROUNDS = 4;      // consistency rounds after phase 1
+
+// bit reader over an unstuffed, 4-byte-aligned stream of L bytes (zeros past the end)
+struct UReader {
+  const uint32_t* w;
+  uint32_t L;
+  uint32_t wi;      // next word to load
+  uint64_t buf;     // left-aligned
+  int nbits;
+  uint32_t pos;     // bit position of the next unconsumed bit
+  __device__ __forceinline__ uint32_t word(uint32_t i) const {
+    if (i >= (L + 3) >> 2) return 0u;
+    uint32_t v = __builtin_bswap32(w[i]);
+    const uint32_t have = L - i * 4;
+    if (have < 4) v &= ~(0xFFFFFFFFu >> (8 * have));
+    return v;
+  }
+  __device__ __forceinline__ void init(const uint32_t* base, uint32_t Lbytes, uint32_t p) {
+    w = base;
+    L = Lbytes;
+    pos = p;
+    const uint32_t i = p >> 5, sh = p & 31;
+    const uint64_t v = ((uint64_t)word(i) << 32) | word(i + 1);
+    buf = v << sh;
+    nbits = 64 - (int)sh;
+    wi = i + 2;
+  }
+  __device__ __forceinline__ void fill() {
+    if (nbits <= 32) {
+      buf |= (uint64_t)word(wi++) << (32 - nbits);
+      nbits += 32;
+    }
+  }
+  __device__ __forceinline__ uint32_t peek(int n) const { return (uint32_t)(buf >> (64 - n)); }
+  __device__ __forceinline__ void skip(int n) {
+    buf <<= n;
+    nbits -= n;
+    pos += n;
+  }
+};
+
+// huff_decode on the unstuffed reader (same look-up / second-level / maxcode walk)
+__device__ __forceinline__ int huff_decode_u(UReader& br, const JpegHuff* __restrict__ t) {
+  const uint32_t lk = t->look[br.peek(9)];
+  if (lk) {
+    br.skip(lk >> 8);
+    return lk & 0xFF;
+  }
+  const int i2 = (int)br.peek(16) - t->l2base;
+  if ((unsigned)i2 < (unsigned)t->l2n) {
+    const uint32_t l2 = t->look2[i2];
+    br.skip(l2 ? (int)(l2 >> 8) : 16);
+    return l2 & 0xFF;
+  }
+  int l = 10;
+  uint32_t code = br.peek(10);
+  while (l <= 16 && (int32_t)code > t->maxcode[l]) {
+    ++l;
+    code = br.peek(l);
+  }
+  if (l > 16) {
+    br.skip(16);
+    return 0;
+  }
+  br.skip(l);
+  return t->vals[(code + t->valoff[l]) & 0xFF];
+}
+
+// The MCU's block walk: block b of an MCU belongs to component comp[b] at
+// (dh[b], dv[b]) within that component's hs x vs blocks.
+struct JpegMcu {
+  int bpm;
+  int8_t comp[16], dh[16], dv[16];
+};
+
+__device__ __forceinline__ int64_t block_addr(const JpegGeom& g, const JpegMcu& mc, int64_t blk) {
+  const int64_t m = blk / mc.bpm;
+  const int bb = (int)(blk - m * mc.bpm);
+  const int c = mc.comp[bb];
+  const int64_t my = m / g.mcux, mx = m - my * g.mcux;
+  const int hs_c = pick3(c, g.hs[0], g.hs[1], g.hs[2]), vs_c = pick3(c, g.vs[0], g.vs[1], g.vs[2]);
+  const int bw_c = pick3(c, g.bw[0], g.bw[1], g.bw[2]), cb_c = pick3(c, g.cbase[0], g.cbase[1], g.cbase[2]);
+  return cb_c + (my * vs_c + mc.dv[bb]) * bw_c + mx * hs_c + mc.dh[bb];
+}
+
+// Decode from the reader's position in state (b, k) until the position reaches
+// `stop` (at a symbol boundary) or, when writing, the frame's last block is
+// done.  nblk counts completed blocks; dc[] accumulates DC differences (WRITE:
+// the running predictors, stored as each block's coefficient 0).
+template <bool WRITE>
+__device__ __forceinline__ void jp_run(UReader& br, const JpegHuff* __restrict__ T, const JpegGeom& g,
+                                       const JpegMcu& mc, const uint8_t* __restrict__ zz, int& b, int& k,
+                                       uint32_t stop, int64_t blk, int64_t total, int& nblk, int (&dc)[3],
+                                       int16_t* __restrict__ out) {
+  int16_t* bp = WRITE ? out + block_addr(g, mc, blk) * 64 : nullptr;
+  while (br.pos < stop && (!WRITE || blk < total)) {
+    const int c = mc.comp[b];
+    const JpegHuff* tp = k ? T + pick3(c, g.acsel[0], g.acsel[1], g.acsel[2]) * 2 + 1
+                           : T + pick3(c, g.dcsel[0], g.dcsel[1], g.dcsel[2]) * 2;
+    br.fill();
+    const int sym = huff_decode_u(br, tp);
+    const int sz = sym & 15;
+    const int r = k ? (sym >> 4) : 0;
+    const uint32_t bits = sz ? br.peek(sz) : 0u;
+    br.skip(sz);
+    const int val = sz ? extend(bits, sz) : 0;
+    bool endblk;
+    if (k == 0) {
+      const int pv = pick3(c, dc[0], dc[1], dc[2]) + val;
+      dc[0] = c == 0 ? pv : dc[0];
+      dc[1] = c == 1 ? pv : dc[1];
+      dc[2] = c == 2 ? pv : dc[2];
+      if (WRITE) bp[0] = (int16_t)pv;
+      k = 1;
+      endblk = false;
+    } else if (sz) {
+      k += r;
+      if (WRITE) bp[zz[k]] = (int16_t)val;
+      ++k;
+      endblk = k >= 64;
+    } else if (r == 15) {
+      k += 16;
+      endblk = k >= 64;
+    } else {
+      endblk = true;
+    }
+    if (endblk) {
+      k = 0;
+      b = b + 1 == mc.bpm ? 0 : b + 1;
+      ++nblk;
+      ++blk;
+      if (WRITE && blk < total) bp = out + block_addr(g, mc, blk) * 64;
+    }
+  }
+}
+
+// frame bookkeeping shared by the chunk kernels
+struct JpChunks {
+  const int64_t* cbase;    // [B + 1] first chunk of each frame
+  const int32_t* cframe;   // [nchunks] frame of each chunk
+  const int64_t* ubase;    // [B] unstuffed stream of frame f at ustuff + ubase[f] (4-byte aligned)
+  const uint32_t* ulen;    // [B] unstuffed bytes of frame f
+};
+
+// chunk layout: T_f = max(1, ceil(raw bytes / JP_CHUNK)) chunks per frame; one workgroup
+__global__ __launch_bounds__(1024) void jp_layout_kernel(const int64_t* __restrict__ seg_off,
+                                                         const int64_t* __restrict__ seg_end, int nframes,
+                                                         int64_t* __restrict__ cbase, int64_t* __restrict__ ubase) {
+  __shared__ int64_t part[1024];
+  const int tid = threadIdx.x;
+  const int per = (nframes + 1023) / 1024;
+  const int f0 = tid * per, f1 = min(nframes, f0 + per);
+  int64_t sum = 0;
+  for (int f = f0; f < f1; ++f) {
+    const int64_t len = seg_end[f] - seg_off[f];
+    sum += len > JP_CHUNK ? (len + JP_CHUNK - 1) / JP_CHUNK : 1;
+  }
+  part[tid] = sum;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {   // inclusive Hillis-Steele scan
+    const int64_t v = tid >= o ? part[tid - o] : 0;
+    __syncthreads();
+    part[tid] += v;
+    __syncthreads();
+  }
+  int64_t run = part[tid] - sum;
+  for (int f = f0; f < f1; ++f) {
+    cbase[f] = run;
+    const int64_t len = seg_end[f] - seg_off[f];
+    run += len > JP_CHUNK ? (len + JP_CHUNK - 1) / JP_CHUNK : 1;
+    // unstuffed stream: 4-byte aligned, never past the next frame's start (unstuffed <= raw bytes)
+    ubase[f] = (seg_off[f] + 4 * (int64_t)f + 3) & ~(int64_t)3;
+  }
+  if (tid == 1023) cbase[nframes] = part[1023];
+}
+
+__global__ __launch_bounds__(256) void jp_chunk_frame_kernel(const int64_t* __restrict__ cbase, int nframes,
+                                                             int32_t* __restrict__ cframe) {
+  const int f = blockIdx.x * 256 + threadIdx.x;
+  if (f >= nframes) return;
+  for (int64_t c = cbase[f]; c < cbase[f + 1]; ++c) cframe[c] = f;
+}
+
+// raw byte i of a frame's scan [s, e): kept unless it is the 0x00 after a 0xFF;
+// the first 0xFF not followed by 0x00 (a marker, or the segment's last byte)
+// ends the data
+__global__ __launch_bounds__(256) void jp_unstuff_count_kernel(const uint8_t* __restrict__ data,
+                                                               const int64_t* __restrict__ seg_off,
+                                                               const int64_t* __restrict__ seg_end, JpChunks ch,
+                                                               int64_t nchunks_max, int32_t* __restrict__ cnt,
+                                                               uint8_t* __restrict__ mk) {
+  const int64_t ci = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (ci >= nchunks_max) return;
+  const int f = ch.cframe[ci];
+  if (f < 0) return;
+  const int64_t t = ci - ch.cbase[f];
+  const int64_t fs = seg_off[f], fe = seg_end[f];
+  const int64_t s = fs + t * JP_CHUNK, e = min(fe, s + JP_CHUNK);
+  int n = 0;
+  uint8_t marker = 0;
+  for (int64_t i = s; i < e; ++i) {
+    const uint8_t c = data[i];
+    if (c == 0x00 && i > fs && data[i - 1] == 0xFF) continue;
+    if (c == 0xFF && !(i + 1 < fe && data[i + 1] == 0x00)) {
+      marker = 1;
+      break;
+    }
+    ++n;
+  }
+  cnt[ci] = n;
+  mk[ci] = marker;
+}
+
+// per frame: exclusive offsets of the chunks' kept bytes (chunks after a marker keep nothing)
+__global__ __launch_bounds__(256) void jp_unstuff_scan_kernel(JpChunks ch, int nframes, int32_t* __restrict__ cnt,
+                                                              const uint8_t* __restrict__ mk,
+                                                              uint32_t* __restrict__ coff, uint32_t* __restrict__ ulen) {
+  const int f = blockIdx.x * 256 + threadIdx.x;
+  if (f >= nframes) return;
+  uint32_t run = 0;
+  bool dead = false;
+  for (int64_t c = ch.cbase[f]; c < ch.cbase[f + 1]; ++c) {
+    coff[c] = run;
+    if (dead) {
+      cnt[c] = 0;
+      continue;
+    }
+    run += (uint32_t)cnt[c];
+    dead = mk[c] != 0;
+  }
+  ulen[f] = run;
+}
+
+__global__ __launch_bounds__(256) void jp_unstuff_scatter_kernel(const uint8_t* __restrict__ data,
+                                                                 const int64_t* __restrict__ seg_off,
+                                                                 const int64_t* __restrict__ seg_end, JpChunks ch,
+                                                                 int64_t nchunks_max, const int32_t* __restrict__ cnt,
+                                                                 const uint32_t* __restrict__ coff,
+                                                                 uint8_t* __restrict__ ustuff) {
+  const int64_t ci = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (ci >= nchunks_max) return;
+  const int f = ch.cframe[ci];
+  if (f < 0) return;
+  int n = cnt[ci];
+  if (n <= 0) return;
+  const int64_t t = ci - ch.cbase[f];
+  const int64_t fs = seg_off[f], fe = seg_end[f];
+  int64_t i = fs + t * JP_CHUNK;
+  uint8_t* o = ustuff + ch.ubase[f] + coff[ci];
+  while (n > 0) {
+    const uint8_t c = data[i];
+    const bool stuffed = c == 0x00 && i > fs && data[i - 1] == 0xFF;
+    ++i;
+    if (stuffed) continue;
+    *o++ = c;
+    --n;
+  }
+  (void)fe;
+}
+
+struct JpState {        // per chunk, per buffer: exit state, blocks completed, DC sums
+  uint64_t* x;          // pos << 16 | b << 8 | k  (pos: bit index in the frame's unstuffed stream)
+  int32_t* nb;
+  int32_t* dc;          // [3] per chunk
+  uint8_t* changed;
+};
+
+__device__ __forceinline__ uint64_t pack_state(uint32_t pos, int b, int k) {
+  return ((uint64_t)pos << 16) | ((uint64_t)b << 8) | (uint64_t)k;
+}
+
+// round 0: every chunk from its first bit in the guessed state (block 0, coefficient 0);
+// round r >= 1: chunks whose predecessor's exit changed in round r - 1 re-decode from it
+template <bool LDS_T>
+__global__ __launch_bounds__(256) void jp_sync_kernel(const uint8_t* __restrict__ ustuff, JpChunks ch,
+                                                      int64_t nchunks_max, const JpegHuff* __restrict__ huff,
+                                                      const int32_t* __restrict__ huff_idx, int nsets, JpegGeom g,
+                                                      JpegMcu mc, int round, JpState src, JpState dst,
+                                                      int32_t* __restrict__ frame_changed /* this round's [B] */) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  if (LDS_T) {
+    const uint32_t* s = (const uint32_t*)huff;
+    uint32_t* d = (uint32_t*)smem;
+    const int nw = nsets * 4 * (int)sizeof(JpegHuff) / 4;
+    for (int i = threadIdx.x; i < nw; i += 256) d[i] = s[i];
+    __syncthreads();
+  }
+  const int64_t ci = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (ci >= nchunks_max) return;
+  const int f = ch.cframe[ci];
+  if (f < 0) return;
+  const int64_t t = ci - ch.cbase[f];
+  const uint32_t L = ch.ulen[f];
+  const uint32_t first = (uint32_t)t * (JP_CHUNK * 8u);
+  if ((uint64_t)t * JP_CHUNK >= L) {   // an empty chunk (the stream is shorter than the raw bytes)
+    dst.x[ci] = pack_state(first, 0, 0);
+    dst.nb[ci] = 0;
+    dst.dc[3 * ci] = dst.dc[3 * ci + 1] = dst.dc[3 * ci + 2] = 0;
+    dst.changed[ci] = 0;
+    return;
+  }
+  uint32_t start = first;
+  int b = 0, k = 0;
+  bool redo = round == 0;
+  if (round > 0 && t > 0 && src.changed[ci - 1]) {
+    const uint64_t xs = src.x[ci - 1];
+    start = (uint32_t)(xs >> 16);
+    b = (int)((xs >> 8) & 0xFF);
+    k = (int)(xs & 0xFF);
+    redo = true;
+  }
+  if (!redo) {   // nothing upstream changed: keep the state
+    dst.x[ci] = src.x[ci];
+    dst.nb[ci] = src.nb[ci];
+    dst.dc[3 * ci] = src.dc[3 * ci];
+    dst.dc[3 * ci + 1] = src.dc[3 * ci + 1];
+    dst.dc[3 * ci + 2] = src.dc[3 * ci + 2];
+    dst.changed[ci] = 0;
+    return;
+  }
+  const int set = huff_idx ? huff_idx[f] : f;
+  const JpegHuff* T = (LDS_T ? (const JpegHuff*)smem : huff) + (int64_t)set * 4;
+  const uint32_t stop = (uint64_t)(t + 1) * JP_CHUNK >= L ? L * 8u : first + JP_CHUNK * 8u;
+  UReader br;
+  br.init((const uint32_t*)(ustuff + ch.ubase[f]), L, start);
+  int nblk = 0;
+  int dc[3] = {0, 0, 0};
+  jp_run<false>(br, T, g, mc, nullptr, b, k, stop, 0, 0, nblk, dc, nullptr);
+  const uint64_t x = pack_state(br.pos, b, k);
+  dst.x[ci] = x;
+  dst.nb[ci] = nblk;
+  dst.dc[3 * ci] = dc[0];
+  dst.dc[3 * ci + 1] = dc[1];
+  dst.dc[3 * ci + 2] = dc[2];
+  const bool ch_ = round == 0 ? true : x != src.x[ci];
+  dst.changed[ci] = ch_ ? 1 : 0;
+  if (ch_ && round > 0) frame_changed[f] = 1;
+}
+
+// per frame: each chunk's first block and DC predictors (exclusive prefix sums)
+__global__ __launch_bounds__(256) void jp_prefix_kernel(JpChunks ch, int nframes, JpState st,
+                                                        int64_t* __restrict__ bfirst, int32_t* __restrict__ pred) {
+  const int f = blockIdx.x * 256 + threadIdx.x;
+  if (f >= nframes) return;
+  int64_t blk = 0;
+  int p0 = 0, p1 = 0, p2 = 0;
+  for (int64_t c = ch.cbase[f]; c < ch.cbase[f + 1]; ++c) {
+    bfirst[c] = blk;
+    pred[3 * c] = p0;
+    pred[3 * c + 1] = p1;
+    pred[3 * c + 2] = p2;
+    blk += st.nb[c];
+    p0 += st.dc[3 * c];
+    p1 += st.dc[3 * c + 1];
+    p2 += st.dc[3 * c + 2];
+  }
+}
+
+template <bool LDS_T>
+__global__ __launch_bounds__(256) void jp_final_kernel(const uint8_t* __restrict__ ustuff, JpChunks ch,
+                                                       int64_t nchunks_max, const JpegHuff* __restrict__ huff,
+                                                       const int32_t* __restrict__ huff_idx, int nsets, JpegGeom g,
+                                                       JpegMcu mc, JpState st, const int64_t* __restrict__ bfirst,
+                                                       const int32_t* __restrict__ pred,
+                                                       const int32_t* __restrict__ frame_changed,
+                                                       int16_t* __restrict__ coef) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  JpegHuff* sh = (JpegHuff*)smem;
+  uint8_t* zz = (uint8_t*)smem + (LDS_T ? nsets * 4 * (int)sizeof(JpegHuff) : 0);
+  if (LDS_T) {
+    const uint32_t* s = (const uint32_t*)huff;
+    uint32_t* d = (uint32_t*)smem;
+    const int nw = nsets * 4 * (int)sizeof(JpegHuff) / 4;
+    for (int i = threadIdx.x; i < nw; i += 256) d[i] = s[i];
+  }
+  for (int i = threadIdx.x; i < 80; i += 256) zz[i] = kZigzag[i];
+  __syncthreads();
+  const int64_t ci = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (ci >= nchunks_max) return;
+  const int f = ch.cframe[ci];
+  if (f < 0) return;
+  const int64_t t = ci - ch.cbase[f];
+  const uint32_t L = ch.ulen[f];
+  const bool serial = frame_changed[f] != 0;   // still changing after the last round: decode the frame serially
+  if (serial && t > 0) return;
+  if (!serial && t > 0 && (uint64_t)t * JP_CHUNK >= L) return;   // empty chunk
+  const int64_t total = (int64_t)g.mcux * g.mcuy * mc.bpm;
+  uint32_t start = 0;
+  int b = 0, k = 0;
+  int64_t blk = 0;
+  int dc[3] = {0, 0, 0};
+  if (!serial && t > 0) {
+    const uint64_t xs = st.x[ci - 1];
+    start = (uint32_t)(xs >> 16);
+    b = (int)((xs >> 8) & 0xFF);
+    k = (int)(xs & 0xFF);
+    blk = bfirst[ci];
+    dc[0] = pred[3 * ci];
+    dc[1] = pred[3 * ci + 1];
+    dc[2] = pred[3 * ci + 2];
+  }
+  const bool last = serial || (uint64_t)(t + 1) * JP_CHUNK >= L;
+  const uint32_t stop = last ? 0xFFFFFFFFu : (uint32_t)(t + 1) * (JP_CHUNK * 8u);
+  const int set = huff_idx ? huff_idx[f] : f;
+  const JpegHuff* T = (LDS_T ? (const JpegHuff*)sh : huff) + (int64_t)set * 4;
+  UReader br;
+  br.init((const uint32_t*)(ustuff + ch.ubase[f]), L, start);
+  int nblk = 0;
+  jp_run<true>(br, T, g, mc, zz, b, k, stop, blk, total, nblk, dc, coef + (int64_t)f * g.blocks_per_frame * 64);
+}
+
 // ---- IDCT (jidctint.c jpeg_idct_islow) -----------------------------------
 constexpr int CONST_BITS = 13, PASS1_BITS = 2;
 constexpr int32_t F0298 = 2446, F0390 = 3196, F0541 = 4433, F0765 = 6270, F0899 = 7373, F1175 = 9633,
@@ -531,10 +973,54 @@ __global__ __launch_bounds__(256) void jpeg_color_kernel(const uint8_t* __restri
 
 }  // namespace
 
+// Workspace of the chunked entropy decode (after the coefficients and planes).
+struct JpWs {
+  size_t bytes;
+  size_t o_ustuff, o_cbase, o_ubase, o_ulen, o_cframe, o_cnt, o_coff, o_mk, o_x[2], o_nb[2], o_dc[2], o_ch[2],
+      o_bfirst, o_pred, o_fch;
+  int64_t nmax;
+};
+
+static JpWs jp_layout(int nframes, int64_t data_bytes) {
+  JpWs w{};
+  size_t off = 0;
+  auto carve = [&](size_t n) { const size_t o = off; off += (n + 255) & ~(size_t)255; return o; };
+  const int64_t B = nframes;
+  w.nmax = data_bytes / JP_CHUNK + B + 1;   // >= sum over frames of max(1, ceil(raw bytes / JP_CHUNK))
+  w.o_ustuff = carve((size_t)data_bytes + 4 * (size_t)B + 64);
+  w.o_cbase = carve((size_t)(B + 1) * 8);
+  w.o_ubase = carve((size_t)B * 8);
+  w.o_ulen = carve((size_t)B * 4);
+  w.o_cframe = carve((size_t)w.nmax * 4);
+  w.o_cnt = carve((size_t)w.nmax * 4);
+  w.o_coff = carve((size_t)w.nmax * 4);
+  w.o_mk = carve((size_t)w.nmax);
+  for (int i = 0; i < 2; ++i) {
+    w.o_x[i] = carve((size_t)w.nmax * 8);
+    w.o_nb[i] = carve((size_t)w.nmax * 4);
+    w.o_dc[i] = carve((size_t)w.nmax * 12);
+    w.o_ch[i] = carve((size_t)w.nmax);
+  }
+  w.o_bfirst = carve((size_t)w.nmax * 8);
+  w.o_pred = carve((size_t)w.nmax * 12);
+  w.o_fch = carve((size_t)(JP_ROUNDS + 1) * B * 4);
+  w.bytes = off;
+  return w;
+}
+
+static bool jp_serial_forced() {
+#if MICLIP_AB
+  const char* e = getenv("MICLIP_JPEG_SERIAL");   // A/B: the lane-per-frame entropy kernel for every scan
+  return e && e[0] == '1';
+#else
+  return false;
+#endif
+}
+
 // Host launch: see include/miclip.h mi_jpeg_decode for the argument contract.
-hipError_t jpeg_decode(const uint8_t* data, const int64_t* seg_off, const int64_t* seg_end, const void* huff,
-                       const int32_t* huff_idx, int nsets, const uint16_t* qtab, const int32_t* geom, int nframes, uint8_t* out_rgb, void* ws,
-                       size_t ws_bytes, hipStream_t s) {
+hipError_t jpeg_decode(const uint8_t* data, int64_t data_bytes, const int64_t* seg_off, const int64_t* seg_end,
+                       const void* huff, const int32_t* huff_idx, int nsets, const uint16_t* qtab, const int32_t* geom,
+                       int nframes, uint8_t* out_rgb, void* ws, size_t ws_bytes, hipStream_t s) {
   // geom: [W, H, ncomp, ri, nseg, hs0, vs0, hs1, vs1, hs2, vs2, q0, q1, q2, dc0, dc1, dc2, ac0, ac1, ac2]
   const int W = geom[0], H = geom[1], ncomp = geom[2];
   JpegGeom g{};
@@ -571,21 +1057,88 @@ hipError_t jpeg_decode(const uint8_t* data, const int64_t* seg_off, const int64_
   g.blocks_per_frame = blocks;
   pl.plane_frame_bytes = bytes;
   const size_t coef_bytes = (size_t)nframes * blocks * 64 * sizeof(int16_t);
-  if (ws_bytes < coef_bytes + (size_t)nframes * bytes) return hipErrorInvalidValue;
+  const size_t base_bytes = (coef_bytes + (size_t)nframes * bytes + 255) & ~(size_t)255;
+  const bool chunked = g.nseg == 1 && !jp_serial_forced();
+  const JpWs jw = jp_layout(nframes, data_bytes);
+  if (ws_bytes < base_bytes + (chunked ? jw.bytes : 0)) return hipErrorInvalidValue;
   int16_t* coef = (int16_t*)ws;
   uint8_t* planes = (uint8_t*)ws + coef_bytes;
   hipError_t e = hipMemsetAsync(coef, 0, coef_bytes, s);
   if (e != hipSuccess) return e;
-  const int64_t lanes = (int64_t)nframes * g.nseg;
-  const dim3 eg((unsigned)((lanes + 63) / 64));
-  if (huff_idx && nsets >= 1 && nsets <= JPEG_LDS_SETS)
-    hipLaunchKernelGGL(jpeg_entropy_kernel<true>, eg, dim3(64), nsets * 4 * sizeof(JpegHuff) + 80, s, data, seg_off,
-                       seg_end, (const JpegHuff*)huff, huff_idx, nsets, g, nframes, coef);
-  else
-    hipLaunchKernelGGL(jpeg_entropy_kernel<false>, eg, dim3(64), 80, s, data, seg_off, seg_end,
-                       (const JpegHuff*)huff, huff_idx, nsets, g, nframes, coef);
-  e = hipGetLastError();
-  if (e != hipSuccess) return e;
+  const bool lds_t = huff_idx && nsets >= 1 && nsets <= JPEG_LDS_SETS;
+  if (chunked) {
+    char* w = (char*)ws + base_bytes;
+    uint8_t* ustuff = (uint8_t*)(w + jw.o_ustuff);
+    int64_t* cbase = (int64_t*)(w + jw.o_cbase);
+    int64_t* ubase = (int64_t*)(w + jw.o_ubase);
+    uint32_t* ulen = (uint32_t*)(w + jw.o_ulen);
+    int32_t* cframe = (int32_t*)(w + jw.o_cframe);
+    int32_t* cnt = (int32_t*)(w + jw.o_cnt);
+    uint32_t* coff = (uint32_t*)(w + jw.o_coff);
+    uint8_t* mk = (uint8_t*)(w + jw.o_mk);
+    JpState st[2];
+    for (int i = 0; i < 2; ++i)
+      st[i] = JpState{(uint64_t*)(w + jw.o_x[i]), (int32_t*)(w + jw.o_nb[i]), (int32_t*)(w + jw.o_dc[i]),
+                      (uint8_t*)(w + jw.o_ch[i])};
+    int64_t* bfirst = (int64_t*)(w + jw.o_bfirst);
+    int32_t* pred = (int32_t*)(w + jw.o_pred);
+    int32_t* fch = (int32_t*)(w + jw.o_fch);
+    const int64_t nmax = jw.nmax;
+    if ((e = hipMemsetAsync(cframe, 0xFF, (size_t)nmax * 4, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(fch, 0, (size_t)(JP_ROUNDS + 1) * nframes * 4, s)) != hipSuccess) return e;
+    // block walk of one MCU (component order, then rows, then columns within the component)
+    JpegMcu mc{};
+    for (int c = 0; c < ncomp; ++c)
+      for (int bv = 0; bv < g.vs[c]; ++bv)
+        for (int bh = 0; bh < g.hs[c]; ++bh) {
+          mc.comp[mc.bpm] = (int8_t)c;
+          mc.dh[mc.bpm] = (int8_t)bh;
+          mc.dv[mc.bpm] = (int8_t)bv;
+          ++mc.bpm;
+        }
+    const dim3 fg((unsigned)((nframes + 255) / 256)), cg((unsigned)((nmax + 255) / 256));
+    hipLaunchKernelGGL(jp_layout_kernel, dim3(1), dim3(1024), 0, s, seg_off, seg_end, nframes, cbase, ubase);
+    hipLaunchKernelGGL(jp_chunk_frame_kernel, fg, dim3(256), 0, s, cbase, nframes, cframe);
+    const JpChunks ch{cbase, cframe, ubase, ulen};
+    hipLaunchKernelGGL(jp_unstuff_count_kernel, cg, dim3(256), 0, s, data, seg_off, seg_end, ch, nmax, cnt, mk);
+    hipLaunchKernelGGL(jp_unstuff_scan_kernel, fg, dim3(256), 0, s, ch, nframes, cnt, mk, coff, ulen);
+    hipLaunchKernelGGL(jp_unstuff_scatter_kernel, cg, dim3(256), 0, s, data, seg_off, seg_end, ch, nmax, cnt, coff,
+                       ustuff);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    const size_t tl = lds_t ? nsets * 4 * sizeof(JpegHuff) : 0;
+    for (int r = 0; r <= JP_ROUNDS; ++r) {
+      const JpState& src = st[(r + 1) & 1];   // round r reads round r - 1's buffer
+      const JpState& dst = st[r & 1];
+      if (lds_t)
+        hipLaunchKernelGGL(jp_sync_kernel<true>, cg, dim3(256), tl, s, ustuff, ch, nmax, (const JpegHuff*)huff,
+                           huff_idx, nsets, g, mc, r, src, dst, fch + (int64_t)r * nframes);
+      else
+        hipLaunchKernelGGL(jp_sync_kernel<false>, cg, dim3(256), 0, s, ustuff, ch, nmax, (const JpegHuff*)huff,
+                           huff_idx, nsets, g, mc, r, src, dst, fch + (int64_t)r * nframes);
+      if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    const JpState& fin = st[JP_ROUNDS & 1];
+    hipLaunchKernelGGL(jp_prefix_kernel, fg, dim3(256), 0, s, ch, nframes, fin, bfirst, pred);
+    const int32_t* last_changed = fch + (int64_t)JP_ROUNDS * nframes;
+    if (lds_t)
+      hipLaunchKernelGGL(jp_final_kernel<true>, cg, dim3(256), tl + 80, s, ustuff, ch, nmax, (const JpegHuff*)huff,
+                         huff_idx, nsets, g, mc, fin, bfirst, pred, last_changed, coef);
+    else
+      hipLaunchKernelGGL(jp_final_kernel<false>, cg, dim3(256), 80, s, ustuff, ch, nmax, (const JpegHuff*)huff,
+                         huff_idx, nsets, g, mc, fin, bfirst, pred, last_changed, coef);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  } else {
+    const int64_t lanes = (int64_t)nframes * g.nseg;
+    const dim3 eg((unsigned)((lanes + 63) / 64));
+    if (lds_t)
+      hipLaunchKernelGGL(jpeg_entropy_kernel<true>, eg, dim3(64), nsets * 4 * sizeof(JpegHuff) + 80, s, data, seg_off,
+                         seg_end, (const JpegHuff*)huff, huff_idx, nsets, g, nframes, coef);
+    else
+      hipLaunchKernelGGL(jpeg_entropy_kernel<false>, eg, dim3(64), 80, s, data, seg_off, seg_end,
+                         (const JpegHuff*)huff, huff_idx, nsets, g, nframes, coef);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
   // A dispatch counts its work-items in 32 bits (grid x block < 2^32): the
   // per-block and per-pixel kernels run over frame chunks of < 2^31 items.
   const int64_t fc_idct = blocks > 0 ? std::max<int64_t>(1, ((int64_t)1 << 31) / blocks) : nframes;
@@ -618,7 +1171,7 @@ hipError_t jpeg_decode(const uint8_t* data, const int64_t* seg_off, const int64_
   return hipSuccess;
 }
 
-size_t jpeg_workspace_bytes(const int32_t* geom, int nframes) {
+size_t jpeg_workspace_bytes(const int32_t* geom, int nframes, int64_t data_bytes) {
   const int W = geom[0], H = geom[1], ncomp = geom[2];
   int hmax = 1, vmax = 1, hs[3] = {1, 1, 1}, vs[3] = {1, 1, 1};
   for (int c = 0; c < ncomp && ncomp == 3; ++c) {
@@ -630,7 +1183,8 @@ size_t jpeg_workspace_bytes(const int32_t* geom, int nframes) {
   const int64_t mcux = (W + 8 * hmax - 1) / (8 * hmax), mcuy = (H + 8 * vmax - 1) / (8 * vmax);
   int64_t blocks = 0;
   for (int c = 0; c < ncomp; ++c) blocks += mcux * hs[c] * mcuy * vs[c];
-  return (size_t)nframes * blocks * 64 * (sizeof(int16_t) + 1);
+  const size_t base = ((size_t)nframes * blocks * 64 * (sizeof(int16_t) + 1) + 255) & ~(size_t)255;
+  return base + (geom[4] == 1 ? jp_layout(nframes, data_bytes < 0 ? 0 : data_bytes).bytes : 0);
 }
 
 }  // namespace miclip

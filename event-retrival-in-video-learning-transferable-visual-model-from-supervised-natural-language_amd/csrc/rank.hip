@@ -1055,7 +1055,6 @@ static hipError_t launch_reg(int64_t N, const float* corpus, const float* q, int
             : il ? (pp ? rank_reg<D, 8, 6, false, true, true> : rank_reg<D, 8, 6, false, true>)
                  : (pp ? rank_reg<D, 8, 6, false, false, true> : rank_reg<D, 8, 6>);
 #else   // product: the measured default (8 slots, 6 chunks in flight, contiguous row ranges)
-  const bool il = false;
   const size_t lds = rank_reg_lds_bytes(8);
   auto fn = rank_reg<D, 8, 6>;
 #endif

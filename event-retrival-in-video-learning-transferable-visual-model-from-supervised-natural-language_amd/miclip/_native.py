@@ -126,14 +126,14 @@ def _bind(path):
         "mi_resample_coeffs": (ctypes.c_int, [I32, ctypes.c_double, ctypes.c_double, I32, ctypes.c_int, P, I64, P]),
         "mi_preprocess_workspace_bytes": (SZ, [I64, I32, I32, I32, ctypes.c_int]),
         "mi_preprocess_frames": (ctypes.c_int, [P, I64, I32, I32, I32, ctypes.c_int, P, ctypes.c_int, P, SZ, P]),
-        "mi_jpeg_workspace_bytes": (SZ, [P, I32]),
-        "mi_jpeg_decode": (ctypes.c_int, [P, P, P, P, P, I32, P, P, I32, P, P, SZ, P]),
+        "mi_jpeg_workspace_bytes": (SZ, [P, I32, I64]),
+        "mi_jpeg_decode": (ctypes.c_int, [P, I64, P, P, P, P, I32, P, P, I32, P, P, SZ, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
-    if L.mi_abi_version() != 1:
+    if L.mi_abi_version() != 2:
         raise MiClipError("libmiclip ABI version mismatch")
     return L
 

@@ -458,9 +458,9 @@ def decode_groups(bufs, device="cuda", dedupe=True, heads=None):
         d_qt = torch.from_numpy(qt).to(dev)
         rgb = torch.empty(B, H, W, 3, dtype=torch.uint8, device=dev)
         gp = geom.ctypes.data
-        nb = L.mi_jpeg_workspace_bytes(gp, B)
+        nb = L.mi_jpeg_workspace_bytes(gp, B, total)
         ws = torch.empty(max(nb, 1), dtype=torch.uint8, device=dev)
-        N.check(L.mi_jpeg_decode(d_data.data_ptr(), d_off.data_ptr(), d_end.data_ptr(), d_huff.data_ptr(),
+        N.check(L.mi_jpeg_decode(d_data.data_ptr(), total, d_off.data_ptr(), d_end.data_ptr(), d_huff.data_ptr(),
                                  d_hidx.data_ptr() if dedupe else None, len(sets), d_qt.data_ptr(), gp, B, rgb.data_ptr(), ws.data_ptr(), nb,
                                  N.stream_ptr(dev)), "mi_jpeg_decode")
         del ws, d_data

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define MICLIP_ABI_VERSION 1
+#define MICLIP_ABI_VERSION 2   /* 2: mi_jpeg_workspace_bytes / mi_jpeg_decode take the data size */
 
 enum mi_dtype { MI_F32 = 0, MI_BF16 = 1, MI_F16 = 2, MI_FP8 = 3 /* weights only: MX-fp8 vision GEMMs */ };
 enum mi_status { MI_OK = 0, MI_ERR_ARG = -1, MI_ERR_HIP = -2, MI_ERR_UNSUPPORTED = -3, MI_ERR_STATE = -4 };
@@ -214,7 +214,8 @@ int mi_preprocess_frames(const uint8_t* frames, int64_t B, int32_t H, int32_t W,
  * The caller (miclip/jpeg.py) parses headers and builds the tables; all pointers
  * are device memory:
  *   data      concatenated entropy-coded segments of all frames (bytes after SOS),
- *             readable for 16 bytes past the last segment end (aligned 16-byte reads)
+ *             readable for 16 bytes past the last segment end (aligned 16-byte reads);
+ *             data_bytes = its size (the segments lie in [0, data_bytes))
  *   seg_off / seg_end  [B * nseg] byte offsets of each restart segment (nseg = 1
  *             without restart markers); a segment ends at its RSTn / EOI marker
  *   huff      [nsets][4] decode tables {dc0, ac0, dc1, ac1}, MI_JPEG_HUFF_BYTES each
@@ -227,10 +228,14 @@ int mi_preprocess_frames(const uint8_t* frames, int64_t B, int32_t H, int32_t W,
  *             selector per component
  *   out_rgb   [B, H, W, 3] uint8
  * Supported: 8-bit, 1 component, or 3 components with chroma 1x1 and luma
- * 1x1 / 2x1 / 2x2. */
+ * 1x1 / 2x1 / 2x2.  Scans without restart markers (nseg = 1) are entropy-decoded
+ * by 1-KB chunks in parallel (speculative decode + consistency rounds, jpeg.hip),
+ * scans with restart intervals one lane per interval; the workspace holds the
+ * coefficients, the component planes and, for nseg = 1, the chunk state and an
+ * unstuffed copy of the data. */
 #define MI_JPEG_HUFF_BYTES 3480
-size_t mi_jpeg_workspace_bytes(const int32_t* geom, int32_t B);
-int mi_jpeg_decode(const uint8_t* data, const int64_t* seg_off, const int64_t* seg_end, const void* huff,
+size_t mi_jpeg_workspace_bytes(const int32_t* geom, int32_t B, int64_t data_bytes);
+int mi_jpeg_decode(const uint8_t* data, int64_t data_bytes, const int64_t* seg_off, const int64_t* seg_end, const void* huff,
                    const int32_t* huff_idx, int32_t nsets, const uint16_t* qtab, const int32_t* geom, int32_t B,
                    uint8_t* out_rgb, void* workspace, size_t workspace_bytes, void* stream);
 

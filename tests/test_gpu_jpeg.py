@@ -163,3 +163,80 @@ def test_load_frames_gpu_decode_matches_host_path(gpu, tmp_path):
         assert fg == fh == [len(paths) - 1]
         assert torch.equal(g, h)
         assert not g[-1].any()
+
+
+def _serial_reference(bufs, monkeypatch):
+    """The same batch through the A/B build's lane-per-frame entropy kernel
+    (MICLIP_JPEG_SERIAL=1): the decode the chunked kernels must reproduce."""
+    from miclip import _native, jpeg
+    monkeypatch.setattr(_native, "lib", _native.lib_ab)
+    monkeypatch.setenv("MICLIP_JPEG_SERIAL", "1")
+    out = [None if g is None else g.cpu().numpy() for g in jpeg.decode_batch(bufs, "cuda")]
+    monkeypatch.undo()
+    return out
+
+
+def _corrupt(buf, seed):
+    """Flip bytes of the entropy-coded data (markers and stuffing included by
+    chance), keeping the headers and the final EOI: still a device-path file."""
+    from miclip import jpeg
+    h = jpeg.parse(buf)
+    b = bytearray(buf)
+    rng = np.random.default_rng(seed)
+    lo, hi = h.scan_start, len(b) - 2
+    for i in rng.integers(lo, hi, size=1 + seed % 5):
+        b[i] = int(rng.integers(0, 256))
+    if seed % 3 == 0:                                 # a marker in the middle of the scan
+        i = int(rng.integers(lo, hi - 2))
+        b[i:i + 2] = b"\xff\xd3"
+    return bytes(b)
+
+
+def test_chunked_entropy_matches_serial_on_corrupt_and_truncated(gpu, monkeypatch):
+    """The chunked (speculative, self-synchronising) entropy decode must give
+    the serial decode's coefficients on ANY byte stream — corrupt codes, a
+    marker mid-scan (zero feed from there), truncation — since its consistency
+    rounds only accept exit states reached from the true entry state."""
+    from miclip import jpeg
+    base = [_save(_img(h, w, s), quality=q) for h, w, s, q in
+            ((720, 1280, 1, 90), (480, 640, 2, 50), (1080, 1920, 3, 95), (64, 72, 4, 75), (8, 8, 5, 30))]
+    ref_frames = sorted(glob.glob(os.path.join(ROOT, "golden", "ref_frames", "*.jpg")))[:3]
+    base += [open(f, "rb").read() for f in ref_frames]
+    bufs = []
+    for i, b in enumerate(base):
+        bufs.append(_corrupt(b, i))
+        h = jpeg.parse(b)
+        cut = h.scan_start + (len(b) - h.scan_start) * (i + 1) // (len(base) + 2)
+        bufs.append(b[:cut] + b"\xff\xd9")              # truncated mid-scan
+    assert all(jpeg.parse(b).supported for b in bufs)
+    ser = _serial_reference(bufs, monkeypatch)
+    got = jpeg.decode_batch(bufs, "cuda")
+    for i, (g, r) in enumerate(zip(got, ser)):
+        assert g is not None and r is not None, i
+        assert np.array_equal(g.cpu().numpy(), r), f"buffer {i}: chunked decode differs from the serial kernel"
+
+
+@pytest.mark.parametrize("quality", [20, 75, 100])
+def test_chunked_entropy_large_frames_bit_exact(gpu, quality):
+    """1080p / 4K frames (hundreds of 1-KB chunks per frame, DC prediction
+    carried across every chunk edge) against Pillow."""
+    bufs = [_save(_img(1080, 1920, 7), quality=quality), _save(_img(2160, 3840, 8), quality=quality),
+            _save(_img(1080, 1920, 9), quality=quality, subsampling=0)]
+    _check(bufs, expect_device=[True, True, True])
+
+
+def test_load_frames_decode_budget(gpu, monkeypatch):
+    """Decode launches bounded by device bytes (MICLIP_DECODE_BUDGET_GB): a
+    budget of ~2 frames splits 16 reference frames into 8 launches with the
+    same output as one launch."""
+    from miclip.preprocess import load_frames
+    files = sorted(glob.glob(os.path.join(ROOT, "golden", "ref_frames", "*.jpg")))
+    one, bad1 = load_frames(files, 224)
+    monkeypatch.setenv("MICLIP_DECODE_BUDGET_GB", str(2 * 7e6 / (1 << 30)))
+    many, bad2 = load_frames(files, 224)
+    assert bad1 == bad2 == [] and torch_equal(one, many)
+
+
+def torch_equal(a, b):
+    import torch
+    return torch.equal(a, b)
