@@ -13,8 +13,10 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <algorithm>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/miclip.h"
@@ -1010,6 +1012,37 @@ int mi_jpeg_decode(const uint8_t* data, int64_t data_bytes, const int64_t* seg_o
     return fail(MI_ERR_ARG, "mi_jpeg_decode: workspace too small (%zu < %zu)", workspace_bytes, need);
   HIP_TRY(jpeg_decode(data, data_bytes, seg_off, seg_end, huff, huff_idx, nsets, qtab, geom, B, out_rgb, workspace, workspace_bytes,
                       (hipStream_t)stream));
+  return MI_OK;
+}
+
+int mi_host_gather(void* dst, const void* const* src, const int64_t* len, int64_t n, int32_t threads) {
+  if (!dst || n < 0 || (n > 0 && (!src || !len))) return fail(MI_ERR_ARG, "mi_host_gather: bad arguments");
+  std::vector<int64_t> off((size_t)n + 1, 0);
+  for (int64_t i = 0; i < n; ++i) {
+    if (len[i] < 0 || (len[i] > 0 && !src[i])) return fail(MI_ERR_ARG, "mi_host_gather: bad piece %lld", (long long)i);
+    off[i + 1] = off[i] + len[i];
+  }
+  const int64_t total = off[n];
+  int T = threads < 1 ? 1 : (threads > 64 ? 64 : threads);
+  if (total < (1 << 22)) T = 1;
+  // thread t copies the byte range [t * total / T, (t + 1) * total / T) of the output,
+  // piece by piece (pieces split across two threads are copied in two parts)
+  auto work = [&](int64_t b0, int64_t b1) {
+    int64_t i = std::upper_bound(off.begin(), off.end(), b0) - off.begin() - 1;
+    for (int64_t b = b0; b < b1 && i < n; ++i) {
+      const int64_t e = std::min(b1, off[i + 1]);
+      if (e > b) memcpy((char*)dst + b, (const char*)src[i] + (b - off[i]), (size_t)(e - b));
+      b = e;
+    }
+  };
+  if (T == 1) {
+    work(0, total);
+    return MI_OK;
+  }
+  std::vector<std::thread> th;
+  th.reserve(T);
+  for (int t = 0; t < T; ++t) th.emplace_back(work, total * t / T, total * (t + 1) / T);
+  for (auto& x : th) x.join();
   return MI_OK;
 }
 

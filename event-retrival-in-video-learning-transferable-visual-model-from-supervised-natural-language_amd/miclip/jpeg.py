@@ -317,36 +317,46 @@ def _segments(buf, h):
     return segs
 
 
-_STAGE = [None]
+_STAGE = [None, None]            # two pinned staging buffers (double-buffered uploads)
+_STAGE_EVT = [None, None]        # the last H2D copy out of each
 _STAGE_LOCK = threading.Lock()
 _PAD = np.frombuffer(b"\xff\xd9" * 16, np.uint8)
+SUB_FRAMES = 2048                # frames per decode launch: the host gathers launch j + 1 while the GPU decodes j
 
 
-def _upload(bufs, keep, segl, starts, total, dev):
-    """Entropy-coded bytes of the kept frames, concatenated straight into a
-    reused pinned staging buffer (16 host threads for big batches), then one
-    DMA to the device; 32 bytes of EOI markers as padding."""
+def _upload(bufs, keep, segl, starts, total, dev, slot=0):
+    """Entropy-coded bytes of the kept frames gathered straight into pinned
+    staging buffer `slot` by 16 native threads (mi_host_gather, no GIL), then
+    an asynchronous DMA to the device on the current stream; 32 bytes of EOI
+    markers as padding.  The buffer is reused only after its previous copy
+    has completed (event), so a caller alternating slots overlaps the next
+    gather with this copy and the kernels that follow it."""
+    import ctypes
     import torch
-    from concurrent.futures import ThreadPoolExecutor
     with _STAGE_LOCK:
-        st = _STAGE[0]
+        if _STAGE_EVT[slot] is not None:
+            _STAGE_EVT[slot].synchronize()
+        st = _STAGE[slot]
         if st is None or st.numel() < total + 32:
             st = torch.empty(max(total + 32, 1 << 26), dtype=torch.uint8, pin_memory=True)
-            _STAGE[0] = st
-        v = st.numpy()
-
-        def cp(r):
-            a, n = segl[r][0][0], int(starts[r + 1] - starts[r])
-            v[starts[r]:starts[r + 1]] = np.frombuffer(bufs[keep[r]], np.uint8, n, a)
-
-        if len(keep) >= 64:
-            with ThreadPoolExecutor(16) as ex:
-                list(ex.map(cp, range(len(keep))))
-        else:
-            for r in range(len(keep)):
-                cp(r)
-        v[total:total + 32] = _PAD
-        return st[:total + 32].to(dev)   # synchronous: the staging buffer is free again on return
+            _STAGE[slot] = st
+        n = len(keep)
+        ptrs = np.empty(n, np.uint64)
+        lens = np.empty(n, np.int64)
+        for r in range(n):
+            b = bufs[keep[r]]
+            ptrs[r] = ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p).value + segl[r][0][0]
+            lens[r] = starts[r + 1] - starts[r]
+        keepalive = [bufs[i] for i in keep]
+        N.check(N.lib().mi_host_gather(st.data_ptr(), ptrs.ctypes.data, lens.ctypes.data, n, 16), "mi_host_gather")
+        del keepalive
+        st.numpy()[total:total + 32] = _PAD
+        d = torch.empty(total + 32, dtype=torch.uint8, device=dev)
+        d.copy_(st[:total + 32], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(dev))
+        _STAGE_EVT[slot] = ev
+        return d
 
 
 def decode_batch(bufs, device="cuda", dedupe=True):
@@ -445,25 +455,36 @@ def decode_groups(bufs, device="cuda", dedupe=True, heads=None):
             for i in keep:
                 yield _host_group(bufs, i, device)
             continue
-        d_data = _upload(bufs, keep, segl, starts, total, dev)
-        d_off = torch.as_tensor(np.asarray(offs, np.int64)).to(dev)
-        d_end = torch.as_tensor(np.asarray(ends, np.int64)).to(dev)
         huff = np.zeros((len(sets), 4), dtype=_HUFF_DT)
         for u, tabs in enumerate(sets):
             for j, t in enumerate(tabs):
                 if t is not None:
                     huff[u, j] = t
         d_huff = torch.from_numpy(huff.view(np.uint8).reshape(-1)).to(dev)
-        d_hidx = torch.from_numpy(hidx).to(dev)
-        d_qt = torch.from_numpy(qt).to(dev)
+        offs = np.asarray(offs, np.int64)
+        ends = np.asarray(ends, np.int64)
         rgb = torch.empty(B, H, W, 3, dtype=torch.uint8, device=dev)
         gp = geom.ctypes.data
-        nb = L.mi_jpeg_workspace_bytes(gp, B, total)
+        # launches of SUB_FRAMES frames: the host gathers launch j + 1 into the other
+        # pinned buffer while the GPU copies and decodes launch j
+        step = max(1, min(B, SUB_FRAMES))
+        subs = [(j0, min(B, j0 + step)) for j0 in range(0, B, step)]
+        nb = max(L.mi_jpeg_workspace_bytes(gp, j1 - j0, int(starts[j1] - starts[j0])) for j0, j1 in subs)
         ws = torch.empty(max(nb, 1), dtype=torch.uint8, device=dev)
-        N.check(L.mi_jpeg_decode(d_data.data_ptr(), total, d_off.data_ptr(), d_end.data_ptr(), d_huff.data_ptr(),
-                                 d_hidx.data_ptr() if dedupe else None, len(sets), d_qt.data_ptr(), gp, B, rgb.data_ptr(), ws.data_ptr(), nb,
-                                 N.stream_ptr(dev)), "mi_jpeg_decode")
-        del ws, d_data
+        for u, (j0, j1) in enumerate(subs):
+            base, sub_total = int(starts[j0]), int(starts[j1] - starts[j0])
+            d_data = _upload(bufs, keep[j0:j1], segl[j0:j1], starts[j0:j1 + 1] - base, sub_total, dev, slot=u & 1)
+            d_off = torch.from_numpy(offs[j0 * nseg:j1 * nseg] - base).to(dev, non_blocking=False)
+            d_end = torch.from_numpy(ends[j0 * nseg:j1 * nseg] - base).to(dev, non_blocking=False)
+            d_hidx = torch.from_numpy(np.ascontiguousarray(hidx[j0:j1])).to(dev)
+            d_qt = torch.from_numpy(np.ascontiguousarray(qt[j0:j1])).to(dev)
+            # without dedupe frame f uses set f: this launch's frames start at set j0
+            hp = d_huff.data_ptr() + (0 if dedupe else j0 * 4 * HUFF_BYTES)
+            N.check(L.mi_jpeg_decode(d_data.data_ptr(), sub_total, d_off.data_ptr(), d_end.data_ptr(), hp,
+                                     d_hidx.data_ptr() if dedupe else None, len(sets), d_qt.data_ptr(), gp, j1 - j0,
+                                     rgb[j0:j1].data_ptr(), ws.data_ptr(), nb, N.stream_ptr(dev)), "mi_jpeg_decode")
+            del d_data
+        del ws
         yield keep, rgb
 
 

@@ -239,6 +239,13 @@ int mi_jpeg_decode(const uint8_t* data, int64_t data_bytes, const int64_t* seg_o
                    const int32_t* huff_idx, int32_t nsets, const uint16_t* qtab, const int32_t* geom, int32_t B,
                    uint8_t* out_rgb, void* workspace, size_t workspace_bytes, void* stream);
 
+/* Host-side gather of the frames' entropy-coded bytes into one (pinned) staging
+ * buffer before the upload: n pieces src[i] of len[i] bytes concatenated into
+ * dst on `threads` host threads (plain memcpy; the Python caller's bytes
+ * objects stay where they are).  Replaces the reference's per-file host decode
+ * inputs (embedding_service.py:472-480) on the way to mi_jpeg_decode. */
+int mi_host_gather(void* dst, const void* const* src, const int64_t* len, int64_t n, int32_t threads);
+
 /* ---- operator-level entry points (per-kernel parity tests) ----
  * mi_op_gemm: out = A[M,K] . W[N,K]^T (+bias) with epilogue
  *   0: bf16 out; 1: bf16 QuickGELU out; 2: f32 out += (residual); 3: f32 out.

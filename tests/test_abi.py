@@ -108,3 +108,23 @@ def test_mirror_certificate_delta_covers_worst_case():
             worst = 2.0 ** -11 + (2.0 ** -22 if split else 2.0 ** -11) + 2 * gamma + 2 * np.sqrt(D) * 2.0 ** -25
             assert dr.value >= worst, (D, split, dr.value, worst)
             assert da.value >= np.sqrt(D) * 2.0 ** -25
+
+
+def test_host_gather_concatenates_pieces():
+    """mi_host_gather (host only): pieces of bytes objects, at offsets, in order,
+    on 1 and 16 threads, byte ranges split across threads."""
+    import ctypes
+    from miclip import _native
+    L = _native.lib()
+    rng = np.random.default_rng(0)
+    pieces = [rng.integers(0, 256, int(n), dtype=np.uint8).tobytes() for n in rng.integers(0, 300_000, 40)]
+    skip = [int(x) for x in rng.integers(0, 100, 40)]
+    want = b"".join(p[min(s, len(p)):] for p, s in zip(pieces, skip))
+    ptrs = np.array([ctypes.cast(ctypes.c_char_p(p), ctypes.c_void_p).value + min(s, len(p)) for p, s in zip(pieces, skip)],
+                    np.uint64)
+    lens = np.array([len(p) - min(s, len(p)) for p, s in zip(pieces, skip)], np.int64)
+    for threads in (1, 16):
+        out = np.zeros(len(want), np.uint8)
+        assert L.mi_host_gather(out.ctypes.data, ptrs.ctypes.data, lens.ctypes.data, len(pieces), threads) == 0
+        assert out.tobytes() == want
+    assert L.mi_host_gather(None, None, None, 1, 1) == -1
