@@ -3,6 +3,7 @@
 // tower), restated in oracle/clip_ref.py::_mha.  Built with -fno-honor-nans
 // (Makefile): the softmax max/sum chains then compile to v_max3 without NaN
 // canonicalisation; -inf masking is unaffected.
+#include <cstdlib>
 #include <type_traits>
 
 #include "common.hpp"
@@ -378,7 +379,7 @@ __global__ __launch_bounds__(512) void attention_flash_kernel(const uint16_t* __
 //   per 64-key chunk: S^T = K Q^T (8 MFMA), online softmax in the log2
 //   domain with lazy rescale (flash kernel above), P to bf16, 8 PV MFMAs;
 //   the partial last chunk runs only its valid 16-key tiles (NKT template).
-template <int NW>
+template <int NW, bool TT2 = true>
 __global__ __launch_bounds__(NW * 64) void attention_res_kernel(const uint16_t* __restrict__ qkv,
                                                                 uint16_t* __restrict__ out, int S, int W, int H,
                                                                 uint8_t* __restrict__ q8, uint8_t* __restrict__ qs,
@@ -427,72 +428,94 @@ __global__ __launch_bounds__(NW * 64) void attention_res_kernel(const uint16_t* 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  for (int t = wave; t < nqt; t += NW) {
-    bf16x8 qf[2];
-    {
-      const int qrow = min(t * 16 + fr, S - 1);
+  // A wave's query tiles are w, w + NW, w + 2 NW, ...; it runs them two at a
+  // time (TT = 2): each K / V^T fragment read from LDS feeds both tiles' MFMAs,
+  // and one tile's softmax VALU has the other tile's MFMAs beside it (one tile
+  // at a time, the QK MFMA -> max -> exp -> PV MFMA chain left the matrix pipe
+  // idle behind its own dependencies).  An odd last tile runs alone (TT = 1).
+  auto tiles = [&](auto tt_c, int t0, int t1) {
+    constexpr int TT = decltype(tt_c)::value;
+    const int tq[2] = {t0, t1};
+    bf16x8 qf[TT][2];
 #pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) qf[s2] = *(const bf16x8*)(qb + (int64_t)qrow * ld + 32 * s2 + 8 * g);
+    for (int u = 0; u < TT; ++u) {
+      const int qrow = min(tq[u] * 16 + fr, S - 1);
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) qf[u][s2] = *(const bf16x8*)(qb + (int64_t)qrow * ld + 32 * s2 + 8 * g);
     }
-    float m = -INFINITY, l = 0.f;
-    f32x4 o[4];
+    float m[TT], l[TT];
+    f32x4 o[TT][4];
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int u = 0; u < TT; ++u) {
+      m[u] = -INFINITY;
+      l[u] = 0.f;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) o[u][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
 
     // one 64-key chunk; NKT valid 16-key tiles, MASK: keys >= S inside them
     auto chunk = [&](auto nkt_c, auto mask_c, int c) {
       constexpr int NKT = decltype(nkt_c)::value;
       constexpr bool MASK = decltype(mask_c)::value;
       const char* kc = Kimg + c * 64 * 128;
-      f32x4 sc[NKT];
+      f32x4 sc[TT][NKT];
 #pragma unroll
       for (int kt = 0; kt < NKT; ++kt) {
         const bf16x8 k0 = *(const bf16x8*)(kc + kt * 16 * 128 + rk0);
         const bf16x8 k1 = *(const bf16x8*)(kc + kt * 16 * 128 + rk1);
-        f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k0, qf[0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-        sc[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k1, qf[1], acc, 0, 0, 0);
+#pragma unroll
+        for (int u = 0; u < TT; ++u) {
+          const f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k0, qf[u][0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+          sc[u][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k1, qf[u][1], acc, 0, 0, 0);
+        }
       }
-      // sc[kt][j]: query t*16 + fr, key c*64 + kt*16 + 4g + j
-      if (MASK) {
+      // sc[u][kt][j]: query tq[u]*16 + fr, key c*64 + kt*16 + 4g + j
 #pragma unroll
-        for (int kt = 0; kt < NKT; ++kt)
+      for (int u = 0; u < TT; ++u) {
+        if (MASK) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j)
-            if (c * 64 + kt * 16 + 4 * g + j >= S) sc[kt][j] = -INFINITY;
+          for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (c * 64 + kt * 16 + 4 * g + j >= S) sc[u][kt][j] = -INFINITY;
+        }
+        float cm = fmaxf(fmaxf(sc[u][0][0], sc[u][0][1]), fmaxf(sc[u][0][2], sc[u][0][3]));
+#pragma unroll
+        for (int kt = 1; kt < NKT; ++kt)
+          cm = fmaxf(cm, fmaxf(fmaxf(sc[u][kt][0], sc[u][kt][1]), fmaxf(sc[u][kt][2], sc[u][kt][3])));
+        {
+          const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(cm), __float_as_uint(cm), false, false);
+          cm = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+          const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(cm), __float_as_uint(cm), false, false);
+          cm = fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+        }
+        const float cmu = cm * sl2;   // finite: chunk 0 holds key 0 for every row
+        if (cmu > m[u] + RESCALE) {
+          const float alpha = __builtin_amdgcn_exp2f(m[u] - cmu);
+          l[u] *= alpha;
+#pragma unroll
+          for (int dt = 0; dt < 4; ++dt) o[u][dt] *= alpha;
+          m[u] = cmu;
+        }
+        float ps = 0.f;
+#pragma unroll
+        for (int kt = 0; kt < NKT; ++kt) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) sc[u][kt][j] = __builtin_amdgcn_exp2f(fmaf(sc[u][kt][j], sl2, -m[u]));
+          ps += (sc[u][kt][0] + sc[u][kt][1]) + (sc[u][kt][2] + sc[u][kt][3]);
+        }
+        l[u] += ps;
       }
-      float cm = fmaxf(fmaxf(sc[0][0], sc[0][1]), fmaxf(sc[0][2], sc[0][3]));
-#pragma unroll
-      for (int kt = 1; kt < NKT; ++kt) cm = fmaxf(cm, fmaxf(fmaxf(sc[kt][0], sc[kt][1]), fmaxf(sc[kt][2], sc[kt][3])));
-      {
-        const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(cm), __float_as_uint(cm), false, false);
-        cm = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
-        const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(cm), __float_as_uint(cm), false, false);
-        cm = fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
-      }
-      const float cmu = cm * sl2;   // finite: chunk 0 holds key 0 for every row
-      if (cmu > m + RESCALE) {
-        const float alpha = __builtin_amdgcn_exp2f(m - cmu);
-        l *= alpha;
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
-        m = cmu;
-      }
-      float ps = 0.f;
-#pragma unroll
-      for (int kt = 0; kt < NKT; ++kt) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) sc[kt][j] = __builtin_amdgcn_exp2f(fmaf(sc[kt][j], sl2, -m));
-        ps += (sc[kt][0] + sc[kt][1]) + (sc[kt][2] + sc[kt][3]);
-      }
-      l += ps;
 #pragma unroll
       for (int s2 = 0; s2 < (NKT + 1) / 2; ++s2) {
-        bf16x8 pb;
+        bf16x8 pb[TT];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          pb[j] = (__bf16)sc[2 * s2][j];
-          pb[4 + j] = 2 * s2 + 1 < NKT ? (__bf16)sc[(2 * s2 + 1) < NKT ? 2 * s2 + 1 : 0][j] : (__bf16)0.f;
-        }
+        for (int u = 0; u < TT; ++u)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            pb[u][j] = (__bf16)sc[u][2 * s2][j];
+            pb[u][4 + j] = 2 * s2 + 1 < NKT ? (__bf16)sc[u][(2 * s2 + 1) < NKT ? 2 * s2 + 1 : 0][j] : (__bf16)0.f;
+          }
         const char* vc = Vimg + (c * 64 + 32 * s2) * 128 + rvb;
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) {
@@ -501,7 +524,8 @@ __global__ __launch_bounds__(NW * 64) void attention_res_kernel(const uint16_t* 
           typedef short s16x8 __attribute__((ext_vector_type(8)));
           const s16x8 v8 = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
           const bf16x8 vf = __builtin_bit_cast(bf16x8, v8);
-          o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pb, o[dt], 0, 0, 0);
+#pragma unroll
+          for (int u = 0; u < TT; ++u) o[u][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pb[u], o[u][dt], 0, 0, 0);
         }
       }
     };
@@ -520,42 +544,53 @@ __global__ __launch_bounds__(NW * 64) void attention_res_kernel(const uint16_t* 
       else chunk(I1{}, BT{}, c);
     }
 
-    float lt = l;
-    {
-      const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(lt), __float_as_uint(lt), false, false);
-      lt = __uint_as_float(a[0]) + __uint_as_float(a[1]);
-      const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(lt), __float_as_uint(lt), false, false);
-      lt = __uint_as_float(b[0]) + __uint_as_float(b[1]);
-    }
-    const float inv = 1.0f / lt;
-    const int qrow = t * 16 + fr;
-    // o[dt][j]: query qrow, head dim dt*16 + 4g + j
-    if (q8) {  // MX-fp8 output: this head's 64 dims are one 64-k block of out_proj
-      float amax = 0.f;
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) amax = fmaxf(amax, fabsf(o[dt][j] * inv));
-      amax = fmaxf(amax, __shfl_xor(amax, 16, 64));
-      amax = fmaxf(amax, __shfl_xor(amax, 32, 64));
-      const int X = mx_block_exp(amax);
-      const float scl = ldexpf(1.0f, -X);
-      if (qrow < S) {
-        const int64_t row = (int64_t)bseq * S + qrow;
-        uint8_t* dst = q8 + row * W + h * 64 + 4 * g;
+    for (int u = 0; u < TT; ++u) {
+      float lt = l[u];
+      {
+        const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(lt), __float_as_uint(lt), false, false);
+        lt = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+        const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(lt), __float_as_uint(lt), false, false);
+        lt = __uint_as_float(b[0]) + __uint_as_float(b[1]);
+      }
+      const float inv = 1.0f / lt;
+      const int qrow = tq[u] * 16 + fr;
+      // o[u][dt][j]: query qrow, head dim dt*16 + 4g + j
+      if (q8) {  // MX-fp8 output: this head's 64 dims are one 64-k block of out_proj
+        float amax = 0.f;
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt)
-          *(uint32_t*)(dst + dt * 16) = mx_pack4(o[dt][0] * inv, o[dt][1] * inv, o[dt][2] * inv, o[dt][3] * inv, scl);
-        if (g == 0) qs[mx_scale_index(row, h, rows_pad)] = (uint8_t)(X + 127);
-      }
-      continue;
-    }
-    if (qrow < S) {
-      uint16_t* dst = out + ((int64_t)bseq * S + qrow) * W + h * 64 + 4 * g;
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt)
-        *(uint2*)(dst + dt * 16) = make_uint2(pack_bf16x2(o[dt][0] * inv, o[dt][1] * inv),
-                                              pack_bf16x2(o[dt][2] * inv, o[dt][3] * inv));
+          for (int j = 0; j < 4; ++j) amax = fmaxf(amax, fabsf(o[u][dt][j] * inv));
+        amax = fmaxf(amax, __shfl_xor(amax, 16, 64));
+        amax = fmaxf(amax, __shfl_xor(amax, 32, 64));
+        const int X = mx_block_exp(amax);
+        const float scl = ldexpf(1.0f, -X);
+        if (qrow < S) {
+          const int64_t row = (int64_t)bseq * S + qrow;
+          uint8_t* dst = q8 + row * W + h * 64 + 4 * g;
+#pragma unroll
+          for (int dt = 0; dt < 4; ++dt)
+            *(uint32_t*)(dst + dt * 16) =
+                mx_pack4(o[u][dt][0] * inv, o[u][dt][1] * inv, o[u][dt][2] * inv, o[u][dt][3] * inv, scl);
+          if (g == 0) qs[mx_scale_index(row, h, rows_pad)] = (uint8_t)(X + 127);
+        }
+        continue;
+      }
+      if (qrow < S) {
+        uint16_t* dst = out + ((int64_t)bseq * S + qrow) * W + h * 64 + 4 * g;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+          *(uint2*)(dst + dt * 16) = make_uint2(pack_bf16x2(o[u][dt][0] * inv, o[u][dt][1] * inv),
+                                                pack_bf16x2(o[u][dt][2] * inv, o[u][dt][3] * inv));
+      }
+    }
+  };
+  for (int t = wave; t < nqt; t += 2 * NW) {
+    if (TT2 && t + NW < nqt) tiles(std::integral_constant<int, 2>{}, t, t + NW);
+    else {
+      tiles(std::integral_constant<int, 1>{}, t, t);
+      if (!TT2 && t + NW < nqt) tiles(std::integral_constant<int, 1>{}, t + NW, t + NW);
     }
   }
 }
@@ -586,15 +621,27 @@ hipError_t attention(const uint16_t* qkv, uint16_t* out, int B, int S, int W, in
     // vision towers (257 / 577 tokens): K/V resident in LDS, no per-chunk barriers
     const int spad = (S + 31) & ~31;
     const size_t lds = 2 * (size_t)spad * 128;
-    static bool attr_set = false;
-    if (!attr_set) {
-      hipError_t e = hipFuncSetAttribute((const void*)attention_res_kernel<8>,
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    // variants: 1 = 8 waves, one query tile at a time (round 2); 2 = 8 waves, two tiles at a
+    // time; 3 = 16 waves (4 per SIMD sharing the K/V image), one tile at a time
+#if MICLIP_AB
+    const char* ve = std::getenv("MICLIP_ATTN_VAR");   // A/B
+    int var = ve ? std::atoi(ve) : 0;
+#else
+    int var = 0;
+#endif
+    if (var < 1 || var > 3) var = S > 320 ? 2 : 1;
+    const void* fns[4] = {nullptr, (const void*)attention_res_kernel<8, false>, (const void*)attention_res_kernel<8, true>,
+                          (const void*)attention_res_kernel<16, false>};
+    static bool attr_set[4] = {false, false, false, false};
+    if (!attr_set[var]) {
+      hipError_t e = hipFuncSetAttribute(fns[var], hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       if (e != hipSuccess) return e;
-      attr_set = true;
+      attr_set[var] = true;
     }
     const int64_t rp = ((int64_t)B * S + 1) & ~1;
-    hipLaunchKernelGGL(attention_res_kernel<8>, grid, dim3(512), lds, s, qkv, out, S, W, H, q8, qs, rp);
+    if (var == 1) hipLaunchKernelGGL((attention_res_kernel<8, false>), grid, dim3(512), lds, s, qkv, out, S, W, H, q8, qs, rp);
+    else if (var == 2) hipLaunchKernelGGL((attention_res_kernel<8, true>), grid, dim3(512), lds, s, qkv, out, S, W, H, q8, qs, rp);
+    else hipLaunchKernelGGL((attention_res_kernel<16, false>), grid, dim3(1024), lds, s, qkv, out, S, W, H, q8, qs, rp);
     return hipGetLastError();
   }
 #if MICLIP_AB

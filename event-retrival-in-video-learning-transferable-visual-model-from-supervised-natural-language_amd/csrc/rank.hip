@@ -103,8 +103,8 @@ template <int DT, int NW>
 __global__ __launch_bounds__(64 * NW) void rank_stream(const void* __restrict__ corpus, int64_t N, int64_t D,
                                                        const float* __restrict__ queries, int64_t Q, int k,
                                                        int64_t rows_per_wg, int norm_mode, int nan_first,
-                                                       int64_t index_base, float* __restrict__ ws_s,
-                                                       int64_t* __restrict__ ws_i, int64_t C) {
+                                                       int64_t index_base, FoldWs f, float* __restrict__ out_s,
+                                                       int64_t* __restrict__ out_i) {
   constexpr int NT = 64 * NW, KC = 16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int ts_stride = (int)D + 4;
@@ -230,37 +230,8 @@ __global__ __launch_bounds__(64 * NW) void rank_stream(const void* __restrict__ 
     Li[tid * KC + p] = real ? (int32_t)~(uint32_t)L[p] : INT_MAX;
   }
   __syncthreads();
-  if (tid < RQ && q0 + tid < Q) {
-    // 2*NW sorted lists for query tid: lanes {w*64 + tid, w*64 + 32 + tid}
-    int pos[2 * NW];
-#pragma unroll
-    for (int l = 0; l < 2 * NW; ++l) pos[l] = 0;
-    float* os = ws_s + (q0 + tid) * C + (int64_t)RB * k;
-    int64_t* oi = ws_i + (q0 + tid) * C + (int64_t)RB * k;
-    for (int o = 0; o < k; ++o) {
-      uint32_t bk = 0u;
-      int32_t bi = INT_MAX;
-      int bl = 0;
-#pragma unroll
-      for (int l = 0; l < 2 * NW; ++l) {
-        const int src = (l >> 1) * 64 + (l & 1) * 32 + tid;
-        if (pos[l] < KC) {
-          const uint32_t kk = Lk[src * KC + pos[l]];
-          const int32_t ii = Li[src * KC + pos[l]];
-          if (better(kk, ii, bk, bi)) { bk = kk; bi = ii; bl = l; }
-        }
-      }
-#pragma unroll
-      for (int l = 0; l < 2 * NW; ++l) pos[l] += (l == bl) ? 1 : 0;
-      if (bi == INT_MAX) {
-        os[o] = -INFINITY;
-        oi[o] = -1;
-      } else {
-        os[o] = decode_key(bk, nan_first);
-        oi[o] = index_base + r_begin + bi;
-      }
-    }
-  }
+  fold_publish<2 * NW>(Lk, Li, KC, q0, Q, k, r_begin, f);
+  fold_reduce<NT>(smem, f, q0, Q, k, nan_first, index_base, out_s, out_i);
 }
 
 // Register-query streaming stage 1 (f32 corpus, D = 512, k <= 16:
@@ -299,12 +270,16 @@ __global__ __launch_bounds__(64 * NW) void rank_stream(const void* __restrict__ 
 // LDS, where reads return zero — every score comes out 0.
 constexpr size_t rank_reg_lds_bytes(int NB) { return (size_t)4 * NB * (32 * 128) + 4 * 32 * 4 + RQ * 4; }
 
-template <int D, int NB = 8, int PF = 6, bool NOMFMA = false, bool ILV = false, bool PIPE = false>
-__global__ __launch_bounds__(256) void rank_reg(const float* __restrict__ corpus, int64_t N,
+template <int D, int NB = 8, int PF = 6, bool NOMFMA = false, bool ILV = false, bool PIPE = false, int DT = 0>
+__global__ __launch_bounds__(256) void rank_reg(const void* __restrict__ corpus, int64_t N,
                                                 const float* __restrict__ queries, int64_t Q, int k,
                                                 int64_t rows_per_wg, int norm_mode, int nan_first, int64_t index_base,
-                                                float* __restrict__ ws_s, int64_t* __restrict__ ws_i, int64_t C) {
-  constexpr int NW = 4, NT = 64 * NW, KC = 16, NCH = D / 32;
+                                                FoldWs f, float* __restrict__ out_s, int64_t* __restrict__ out_i) {
+  // DT 0: f32 rows, a ring chunk = 32 k; DT 1 / 2 (bf16 / fp16 rows): a ring chunk = 64 k, two
+  // 32-k MFMA groups, converted to f32 (exactly) after the fragment read — the arithmetic of
+  // rank_stream<DT> (load_chunk's conversion, the same k order), so its candidates bit for bit.
+  constexpr int ES = DT ? 2 : 4, NG = DT ? 2 : 1, NCH = D / (32 * NG), NQ = D / 32;
+  constexpr int NW = 4, NT = 64 * NW, KC = 16;
   // NB ring slots per wave, PF chunks in flight (NB >= PF + 1: a refilled slot was read, and its
   // reads waited for, in an earlier chunk iteration)
   constexpr int SLOT = 32 * 128;           // 4 KB
@@ -319,6 +294,7 @@ __global__ __launch_bounds__(256) void rank_reg(const float* __restrict__ corpus
   static_assert(4 * PF <= 63, "rank_reg: vmcnt(4 PF) exceeds the counter");
   static_assert(rank_reg_lds_bytes(NB) <= 160 * 1024, "rank_reg: ring exceeds the LDS");
   static_assert(rank_reg_lds_bytes(NB) >= (size_t)NT * KC * 8, "rank_reg: list merge area exceeds the allocation");
+  static_assert(rank_reg_lds_bytes(NB) >= fold_lds(NT), "rank_reg: in-launch merge area exceeds the allocation");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* ring = smem;                       // [NW][NB][SLOT]
   float* nrm_all = (float*)(smem + NW * NB * SLOT);
@@ -330,11 +306,11 @@ __global__ __launch_bounds__(256) void rank_reg(const float* __restrict__ corpus
   const bool qvalid = q0 + r < Q;
 
   // queries -> registers (zeros past Q)
-  float qv[NCH][16];
+  float qv[NQ][16];
   {
     const float* qp = queries + (qvalid ? (q0 + r) : 0) * D + 16 * h;
 #pragma unroll
-    for (int j = 0; j < NCH; ++j)
+    for (int j = 0; j < NQ; ++j)
 #pragma unroll
       for (int i4 = 0; i4 < 4; ++i4) {
         const float4 t = *(const float4*)(qp + 32 * j + 4 * i4);
@@ -367,7 +343,7 @@ __global__ __launch_bounds__(256) void rank_reg(const float* __restrict__ corpus
   for (int m = 0; m < 4; ++m) {
     const int row = 8 * m + (lane >> 3);
     const int c = (lane & 7) ^ ((row >> 1) & 7);
-    voff[m] = (uint32_t)(row * D * 4 + c * 16);
+    voff[m] = (uint32_t)(row * D * ES + c * 16);
   }
   int lt = 0, lj = 0, lslot = 0;           // load cursor: tile ordinal, chunk, ring slot
   __amdgpu_buffer_rsrc_t rs;
@@ -375,10 +351,10 @@ __global__ __launch_bounds__(256) void rank_reg(const float* __restrict__ corpus
     const int trow = (sid + sstep * lt) * 32;   // relative to r_begin
     const int rows = max(0, min(32, nrows - trow));
     // wave-uniform by construction; readfirstlane makes it provable (no waterfall loop per load, guide T20)
-    const uint64_t base = (uint64_t)(uintptr_t)(corpus + (r_begin + (rows ? trow : 0)) * (int64_t)D);
+    const uint64_t base = (uint64_t)(uintptr_t)((const char*)corpus + (r_begin + (rows ? trow : 0)) * (int64_t)D * ES);
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)base);
     const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
-    const int nrec = __builtin_amdgcn_readfirstlane(rows * D * 4);
+    const int nrec = __builtin_amdgcn_readfirstlane(rows * D * ES);
     rs = __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)(((uint64_t)hi << 32) | lo), (short)0, nrec, 0x00020000);
   };
   make_rs();
@@ -394,7 +370,8 @@ __global__ __launch_bounds__(256) void rank_reg(const float* __restrict__ corpus
       make_rs();
     }
   };
-  // fragment read: row r, k 16h .. 16h + 15 = slots 4h .. 4h + 3 (permuted)
+  // fragment read: row r, f32: k 16h .. 16h + 15 = slots 4h .. 4h + 3; 16-bit: k 32g + 16h .. + 15 =
+  // slots 4g + 2h, 4g + 2h + 1 for g = 0, 1 (permuted)
   const int rbase = r * 128;
   const int sw = (r >> 1) & 7;
   uint64_t L[KC];
@@ -405,7 +382,8 @@ __global__ __launch_bounds__(256) void rank_reg(const float* __restrict__ corpus
     const char* src = wring + slot * SLOT + rbase;
 #pragma unroll
     for (int i4 = 0; i4 < 4; ++i4) {
-      const uint32_t a = (uint32_t)(uintptr_t)(const LDS_AS char*)(src + (((4 * h + i4) ^ sw) << 4));
+      const int sl = DT ? (i4 >> 1) * 4 + 2 * h + (i4 & 1) : 4 * h + i4;
+      const uint32_t a = (uint32_t)(uintptr_t)(const LDS_AS char*)(src + ((sl ^ sw) << 4));
       asm volatile("ds_read_b128 %0, %1" : "=v"(v[i4]) : "v"(a) : "memory");
     }
   };
@@ -438,13 +416,37 @@ __global__ __launch_bounds__(256) void rank_reg(const float* __restrict__ corpus
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           __builtin_amdgcn_sched_barrier(0);
         }
-        const float cur[16] = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w,
-                               v[2].x, v[2].y, v[2].z, v[2].w, v[3].x, v[3].y, v[3].z, v[3].w};
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          if (NOMFMA) asm volatile("" ::"v"(cur[i]), "v"(qv[j][i]));
-          else acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[i], qv[j][i], acc, 0, 0, 0);
-          ss = fmaf(cur[i], cur[i], ss);
+        for (int g = 0; g < NG; ++g) {
+          float cur[16];
+          if (DT == 0) {
+            const float c0[16] = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w,
+                                  v[2].x, v[2].y, v[2].z, v[2].w, v[3].x, v[3].y, v[3].z, v[3].w};
+#pragma unroll
+            for (int i = 0; i < 16; ++i) cur[i] = c0[i];
+          } else {
+            const float4 a = v[2 * g], b = v[2 * g + 1];
+            const uint32_t w[8] = {__float_as_uint(a.x), __float_as_uint(a.y), __float_as_uint(a.z), __float_as_uint(a.w),
+                                   __float_as_uint(b.x), __float_as_uint(b.y), __float_as_uint(b.z), __float_as_uint(b.w)};
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              if (DT == 1) {
+                cur[2 * e] = __uint_as_float(w[e] << 16);
+                cur[2 * e + 1] = __uint_as_float(w[e] & 0xffff0000u);
+              } else {
+                union { uint32_t u; _Float16 hh[2]; } cv;
+                cv.u = w[e];
+                cur[2 * e] = (float)cv.hh[0];
+                cur[2 * e + 1] = (float)cv.hh[1];
+              }
+            }
+          }
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            if (NOMFMA) asm volatile("" ::"v"(cur[i]), "v"(qv[j * NG + g][i]));
+            else acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[i], qv[j * NG + g][i], acc, 0, 0, 0);
+            ss = fmaf(cur[i], cur[i], ss);
+          }
         }
         cslot = cslot == NB - 1 ? 0 : cslot + 1;
       }
@@ -494,36 +496,8 @@ __global__ __launch_bounds__(256) void rank_reg(const float* __restrict__ corpus
     Li[tid * KC + p] = real ? (int32_t)~(uint32_t)L[p] : INT_MAX;
   }
   __syncthreads();
-  if (tid < RQ && q0 + tid < Q) {
-    int pos[2 * NW];
-#pragma unroll
-    for (int l = 0; l < 2 * NW; ++l) pos[l] = 0;
-    float* os = ws_s + (q0 + tid) * C + (int64_t)RB * k;
-    int64_t* oi = ws_i + (q0 + tid) * C + (int64_t)RB * k;
-    for (int o = 0; o < k; ++o) {
-      uint32_t bk = 0u;
-      int32_t bi = INT_MAX;
-      int bl = 0;
-#pragma unroll
-      for (int l = 0; l < 2 * NW; ++l) {
-        const int src = (l >> 1) * 64 + (l & 1) * 32 + tid;
-        if (pos[l] < KC) {
-          const uint32_t kk = Lk[src * KC + pos[l]];
-          const int32_t ii = Li[src * KC + pos[l]];
-          if (better(kk, ii, bk, bi)) { bk = kk; bi = ii; bl = l; }
-        }
-      }
-#pragma unroll
-      for (int l = 0; l < 2 * NW; ++l) pos[l] += (l == bl) ? 1 : 0;
-      if (bi == INT_MAX) {
-        os[o] = -INFINITY;
-        oi[o] = -1;
-      } else {
-        os[o] = decode_key(bk, nan_first);
-        oi[o] = index_base + r_begin + bi;
-      }
-    }
-  }
+  fold_publish<2 * NW>(Lk, Li, KC, q0, Q, k, r_begin, f);
+  fold_reduce<NT>(smem, f, q0, Q, k, nan_first, index_base, out_s, out_i);
 }
 
 // stage-1 LDS: queries [32][D+4] f32, per-wave norms [4][32]; the lists
@@ -989,7 +963,9 @@ int64_t rank_chunks(int64_t N) {
 size_t rank_workspace_bytes(int64_t N, int64_t Q, int k) {
   if (k > RANK_REG_K) return large_ws_bytes(N, Q, k);
   const int64_t nch = N > 0 ? rank_chunks(N) : 1;
-  return (size_t)(Q * nch * k) * (sizeof(float) + sizeof(int64_t));
+  const size_t lists = (size_t)(Q * nch * k) * (sizeof(float) + sizeof(int64_t));   // rank_stage1 + rank_merge
+  const size_t fold = kc_for(k) == 16 ? fold_ws_bytes(nch, Q) : 0;                   // in-launch merge (k <= 16)
+  return lists > fold ? lists : fold;
 }
 
 static size_t stage1_lds(int64_t D, int KC) {
@@ -1022,9 +998,9 @@ hipError_t rank_merge(const float* cs, const int64_t* ci, int64_t Q, int64_t C, 
   return hipGetLastError();
 }
 
-template <int D>
-static hipError_t launch_reg(int64_t N, const float* corpus, const float* q, int64_t Q, int k, int nm, int nf,
-                             int64_t base, float* ws_s, int64_t* ws_i, int64_t& C, hipStream_t s) {
+template <int D, int DT>
+static hipError_t launch_reg(int64_t N, const void* corpus, const float* q, int64_t Q, int k, int nm, int nf,
+                             int64_t base, void* ws, float* out_s, int64_t* out_i, hipStream_t s) {
   // one workgroup per CU (LDS ring 128 KB), rows per workgroup a multiple of 128
   // (one 32-row tile per wave); never more workgroups than rank_chunks (workspace)
   int64_t nwg = rank_chunks(N);
@@ -1032,7 +1008,7 @@ static hipError_t launch_reg(int64_t N, const float* corpus, const float* q, int
   if (nwg > (N + 127) / 128) nwg = (N + 127) / 128;
   const int64_t rpw = ((N + nwg - 1) / nwg + 127) / 128 * 128;
   nwg = (N + rpw - 1) / rpw;
-  C = nwg * k;
+  const FoldWs f = fold_ws(ws, nwg, Q);
   // interleaved tile order: A/B only (MICLIP_RANK_ILV=1).  scripts/rank_micro.py: 1M x 512 494 us
   // against 479 with contiguous row ranges, 1M x 768 729 against 717: not the stream's limit
 #if MICLIP_AB
@@ -1050,29 +1026,33 @@ static hipError_t launch_reg(int64_t N, const float* corpus, const float* q, int
   // within noise: the wait before the MFMAs is not where this kernel loses time)
   const char* pipe = getenv("MICLIP_RANK_PIPE");
   const bool pp = pipe && pipe[0] == '1';
-  auto fn = nb9 ? rank_reg<D, 9, 7>
-            : (probe && probe[0] == '1') ? (il ? rank_reg<D, 8, 6, true, true> : rank_reg<D, 8, 6, true>)
-            : il ? (pp ? rank_reg<D, 8, 6, false, true, true> : rank_reg<D, 8, 6, false, true>)
-                 : (pp ? rank_reg<D, 8, 6, false, false, true> : rank_reg<D, 8, 6>);
+  auto fn = nb9 ? rank_reg<D, 9, 7, false, false, false, DT>
+            : (probe && probe[0] == '1') ? (il ? rank_reg<D, 8, 6, true, true, false, DT> : rank_reg<D, 8, 6, true, false, false, DT>)
+            : il ? (pp ? rank_reg<D, 8, 6, false, true, true, DT> : rank_reg<D, 8, 6, false, true, false, DT>)
+                 : (pp ? rank_reg<D, 8, 6, false, false, true, DT> : rank_reg<D, 8, 6, false, false, false, DT>);
 #else   // product: the measured default (8 slots, 6 chunks in flight, contiguous row ranges)
   const size_t lds = rank_reg_lds_bytes(8);
-  auto fn = rank_reg<D, 8, 6>;
+  auto fn = rank_reg<D, 8, 6, false, false, false, DT>;
 #endif
   hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
+  if ((e = fold_zero(f, s)) != hipSuccess) return e;
   const dim3 grid((unsigned)((Q + RQ - 1) / RQ), (unsigned)nwg);   // (query blocks, row blocks): RB / QB
-  hipLaunchKernelGGL(fn, grid, dim3(256), lds, s, corpus, N, q, Q, k, rpw, nm, nf, base, ws_s, ws_i, C);
+  hipLaunchKernelGGL(fn, grid, dim3(256), lds, s, corpus, N, q, Q, k, rpw, nm, nf, base, f, out_s, out_i);
   return hipGetLastError();
 }
 
 template <int DT, int NW>
 static hipError_t launch_stream(dim3 grid, size_t lds, hipStream_t s, const void* corpus, int64_t N, int64_t D,
                                 const float* q, int64_t Q, int k, int64_t rpw, int nm, int nf, int64_t base,
-                                float* ws_s, int64_t* ws_i, int64_t C) {
+                                void* ws, float* out_s, int64_t* out_i) {
   auto fn = rank_stream<DT, NW>;
-  hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  const size_t l = lds > fold_lds(64 * NW) ? lds : fold_lds(64 * NW);
+  hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)l);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(fn, grid, dim3(64 * NW), lds, s, corpus, N, D, q, Q, k, rpw, nm, nf, base, ws_s, ws_i, C);
+  const FoldWs f = fold_ws(ws, grid.y, Q);
+  if ((e = fold_zero(f, s)) != hipSuccess) return e;
+  hipLaunchKernelGGL(fn, grid, dim3(64 * NW), l, s, corpus, N, D, q, Q, k, rpw, nm, nf, base, f, out_s, out_i);
   return hipGetLastError();
 }
 
@@ -1106,12 +1086,11 @@ hipError_t rank_topk(const void* corpus, int64_t N, int64_t D, int dt, const flo
   const size_t la = (size_t)64 * NW * KC * 8;
   const size_t lds = qa > la ? qa : la;
   hipError_t e;
-  if (KC == 16 && dt == 0 && D == 512 && !(legacy && legacy[0] == '1') && !(noreg && noreg[0] == '0')) {
-    int64_t Creg = 0;
+  if (KC == 16 && D == 512 && !(legacy && legacy[0] == '1') && !(noreg && noreg[0] == '0')) {
     // (D = 768 would hold 384 query VGPRs: hipcc spills ~230, so it keeps rank_stream)
-    e = launch_reg<512>(N, (const float*)corpus, q, Q, k, norm_mode, nan_first, base, ws_s, ws_i, Creg, s);
-    if (e != hipSuccess) return e;
-    return rank_merge(ws_s, ws_i, Q, Creg, k, nan_first, out_s, out_i, s);
+    return dt == 0   ? launch_reg<512, 0>(N, corpus, q, Q, k, norm_mode, nan_first, base, ws, out_s, out_i, s)
+           : dt == 1 ? launch_reg<512, 1>(N, corpus, q, Q, k, norm_mode, nan_first, base, ws, out_s, out_i, s)
+                     : launch_reg<512, 2>(N, corpus, q, Q, k, norm_mode, nan_first, base, ws, out_s, out_i, s);
   }
   if (KC == 64 || (legacy && legacy[0] == '1')) {
 #define MI_S1(KCV, DTV) \
@@ -1120,18 +1099,17 @@ hipError_t rank_topk(const void* corpus, int64_t N, int64_t D, int dt, const flo
     if (KC == 16) e = dt == 0 ? MI_S1(16, 0) : dt == 1 ? MI_S1(16, 1) : MI_S1(16, 2);
     else e = dt == 0 ? MI_S1(64, 0) : dt == 1 ? MI_S1(64, 1) : MI_S1(64, 2);
 #undef MI_S1
-  } else {
-#define MI_RS(DTV, NWV) \
-  launch_stream<DTV, NWV>(grid, lds, s, corpus, N, D, q, Q, k, rpw, norm_mode, nan_first, base, ws_s, ws_i, C)
-#if MICLIP_AB
-    if (NW == 8) e = dt == 0 ? MI_RS(0, 8) : dt == 1 ? MI_RS(1, 8) : MI_RS(2, 8);
-    else
-#endif
-      e = dt == 0 ? MI_RS(0, 12) : dt == 1 ? MI_RS(1, 12) : MI_RS(2, 12);
-#undef MI_RS
+    if (e != hipSuccess) return e;
+    return rank_merge(ws_s, ws_i, Q, C, k, nan_first, out_s, out_i, s);
   }
-  if (e != hipSuccess) return e;
-  return rank_merge(ws_s, ws_i, Q, C, k, nan_first, out_s, out_i, s);
+  // k <= 16: rank_stream with the in-launch merge
+#define MI_RS(DTV, NWV) \
+  launch_stream<DTV, NWV>(grid, lds, s, corpus, N, D, q, Q, k, rpw, norm_mode, nan_first, base, ws, out_s, out_i)
+#if MICLIP_AB
+  if (NW == 8) return dt == 0 ? MI_RS(0, 8) : dt == 1 ? MI_RS(1, 8) : MI_RS(2, 8);
+#endif
+  return dt == 0 ? MI_RS(0, 12) : dt == 1 ? MI_RS(1, 12) : MI_RS(2, 12);
+#undef MI_RS
 }
 
 hipError_t score_matrix(const void* corpus, int64_t N, int64_t D, int dt, const float* q, int64_t Q, int norm_mode,

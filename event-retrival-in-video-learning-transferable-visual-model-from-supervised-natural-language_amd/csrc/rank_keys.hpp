@@ -5,6 +5,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <climits>
+#include <cmath>
+
 #include "common.hpp"
 
 // Row block / query block of a ranking workgroup.  The grid is (query blocks,
@@ -129,6 +132,201 @@ __device__ __forceinline__ void load_chunk(const void* corpus, int64_t row, int6
       }
     }
   }
+}
+
+constexpr int FQ = 32;   // queries per ranking workgroup (MFMA N)
+
+// ---- in-launch merge (rank_stream / rank_reg / rank_mirror_kernel, k <= 16):
+// replaces the rank_merge_kernel launch after them.  Each workgroup publishes, per query of
+// its block, its sorted top-k as 16 packed entries (key << 32 | ~row, row
+// relative to index_base; 0 = no entry) in a 128-B slab line of its own, and
+// raises the query's global threshold gtau[q] to its k-th key (a lower bound of
+// the query's final k-th key: that workgroup alone holds k rows at or above
+// it).  The last workgroup of the query block to arrive (agent-scope release,
+// ticket fetch_add, acquire: cdna_hip_programming.md §6 G16's counter form)
+// reduces: per query a group of threads reads the slabs' heads, keeps the
+// entries at or above gtau in a register top-16 each, appends those to LDS,
+// and ranks every appended entry by counting the entries that beat it
+// (packed keys are unique: index asc breaks ties).  The counters and gtau
+// are zeroed by a hipMemsetAsync ahead of the launch.
+constexpr size_t fold_lds(int NT) { return 256 + (size_t)NT * 16 * 8; }
+
+struct FoldWs {
+  uint64_t* slab;    // [nwg][Qpad][16]
+  uint32_t* cnt;     // [query blocks]
+  uint32_t* gtau;    // [Qpad]
+  int64_t Qpad;
+};
+
+template <int NL>
+__device__ __forceinline__ void fold_publish(const uint32_t* Lk, const int32_t* Li, int KC, int64_t q0, int64_t Q,
+                                             int k, int64_t r_begin, const FoldWs& f) {
+  const int tid = threadIdx.x;
+  if (tid < FQ && q0 + tid < Q) {
+    int pos[NL];
+#pragma unroll
+    for (int l = 0; l < NL; ++l) pos[l] = 0;
+    uint64_t* dst = f.slab + ((int64_t)RB * f.Qpad + q0 + tid) * 16;
+    uint32_t kth = 0u;
+    bool full = false;
+    for (int o = 0; o < 16; ++o) {
+      uint64_t e = 0ull;
+      if (o < k) {
+        uint32_t bk = 0u;
+        int32_t bi = INT_MAX;
+        int bl = 0;
+#pragma unroll
+        for (int l = 0; l < NL; ++l) {
+          const int src = (l >> 1) * 64 + (l & 1) * 32 + tid;
+          if (pos[l] < KC) {
+            const uint32_t kk = Lk[src * KC + pos[l]];
+            const int32_t ii = Li[src * KC + pos[l]];
+            if (better(kk, ii, bk, bi)) { bk = kk; bi = ii; bl = l; }
+          }
+        }
+#pragma unroll
+        for (int l = 0; l < NL; ++l) pos[l] += (l == bl) ? 1 : 0;
+        if (bi != INT_MAX) {
+          e = ((uint64_t)bk << 32) | (uint32_t)~(uint32_t)(r_begin + bi);
+          if (o == k - 1) { kth = bk; full = true; }
+        }
+      }
+      dst[o] = e;
+    }
+    if (full) __hip_atomic_fetch_max(&f.gtau[q0 + tid], kth, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// smem: at least FOLD_LDS(NT) bytes (the caller's list area, free here)
+template <int NT>
+__device__ __forceinline__ void fold_reduce(char* smem, const FoldWs& f, int64_t q0, int64_t Q, int k, int nan_first,
+                                            int64_t index_base, float* __restrict__ out_s,
+                                            int64_t* __restrict__ out_i) {
+  const int tid = threadIdx.x;
+  uint32_t* hdr = (uint32_t*)smem;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's slab stores and gtau atomics
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    hdr[FQ] = __hip_atomic_fetch_add(&f.cnt[QB], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (hdr[FQ] != (uint32_t)NRB - 1) return;            // not the last arrival of this query block
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  if (tid < FQ) hdr[tid] = 0u;
+  __syncthreads();
+  uint64_t* buf = (uint64_t*)(smem + 256);
+  const int nq = (int)(Q - q0 < FQ ? Q - q0 : FQ);
+  int g = 1;
+  while (g < nq) g <<= 1;
+  const int tpq = NT / g;                              // threads per query (>= NT / 32)
+  const int qi = tid / tpq, sub = tid - qi * tpq;
+  const bool act = qi < nq;
+  const int64_t q = q0 + qi;
+  uint64_t L[16];
+#pragma unroll
+  for (int p = 0; p < 16; ++p) L[p] = 0ull;
+  auto take = [&](uint64_t e, uint64_t tauP) {        // into the sorted (desc) top-16
+    if (e < tauP || e <= L[15]) return;
+#pragma unroll
+    for (int p = 15; p > 0; --p) L[p] = e > L[p - 1] ? L[p - 1] : (e > L[p] ? e : L[p]);
+    L[0] = e > L[0] ? e : L[0];
+  };
+  if (act) {
+    const uint64_t tauP = (uint64_t)__hip_atomic_fetch_max(&f.gtau[q], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                          << 32;
+    const int nwg = NRB;
+    constexpr int BATCH = 8;
+    for (int w0 = sub; w0 < nwg; w0 += BATCH * tpq) {
+      uint4 h0[BATCH], h1[BATCH];                      // entries 0..3 of BATCH slabs, loads in flight together
+#pragma unroll
+      for (int b = 0; b < BATCH; ++b) {
+        const int w = w0 + b * tpq;
+        const uint4* p = (const uint4*)(f.slab + ((int64_t)(w < nwg ? w : 0) * f.Qpad + q) * 16);
+        h0[b] = p[0];
+        h1[b] = p[1];
+      }
+#pragma unroll
+      for (int b = 0; b < BATCH; ++b) {
+        const int w = w0 + b * tpq;
+        if (w >= nwg) continue;
+        take(((uint64_t)h0[b].y << 32) | h0[b].x, tauP);
+        take(((uint64_t)h0[b].w << 32) | h0[b].z, tauP);
+        take(((uint64_t)h1[b].y << 32) | h1[b].x, tauP);
+        const uint64_t e3 = ((uint64_t)h1[b].w << 32) | h1[b].z;
+        take(e3, tauP);
+        if (k > 4 && e3 != 0ull && e3 >= tauP) {       // the slab continues above the threshold (rare)
+          const uint4* p = (const uint4*)(f.slab + ((int64_t)w * f.Qpad + q) * 16);
+          for (int c = 2; 2 * c < k; ++c) {
+            const uint4 v = p[c];
+            const uint64_t a = ((uint64_t)v.y << 32) | v.x, bb = ((uint64_t)v.w << 32) | v.z;
+            take(a, tauP);
+            take(bb, tauP);
+            if (bb == 0ull || bb < tauP) break;
+          }
+        }
+      }
+    }
+  }
+  int m = 0;
+#pragma unroll
+  for (int p = 0; p < 16; ++p) m += L[p] != 0ull ? 1 : 0;
+  uint64_t* qb = buf + (int64_t)qi * tpq * 16;
+  if (act && m) {
+    const uint32_t at = atomicAdd(&hdr[qi], (uint32_t)m);   // LDS
+#pragma unroll
+    for (int p = 0; p < 16; ++p)
+      if (p < m) qb[at + p] = L[p];
+  }
+  __syncthreads();
+  if (!act) return;
+  const int n = (int)hdr[qi];
+  int rk[16];
+#pragma unroll
+  for (int p = 0; p < 16; ++p) rk[p] = 0;
+  for (int j = 0; j < n; ++j) {
+    const uint64_t e = qb[j];
+#pragma unroll
+    for (int p = 0; p < 16; ++p) rk[p] += e > L[p] ? 1 : 0;
+  }
+#pragma unroll
+  for (int p = 0; p < 16; ++p)
+    if (p < m && rk[p] < k) {
+      out_s[q * k + rk[p]] = decode_key((uint32_t)(L[p] >> 32), nan_first);
+      out_i[q * k + rk[p]] = index_base + (int64_t)(uint32_t)~(uint32_t)L[p];
+    }
+  for (int r = n + sub; r < k; r += tpq) {             // fewer than k rows in all
+    out_s[q * k + r] = -INFINITY;
+    out_i[q * k + r] = -1;
+  }
+}
+
+
+static inline int64_t qpad(int64_t Q) { return (Q + FQ - 1) / FQ * FQ; }
+static inline size_t al128(size_t b) { return (b + 127) / 128 * 128; }
+
+// in-launch merge workspace: slabs [nwg][Qpad][16] u64, counters [Qpad / 32] u32, gtau [Qpad] u32
+static inline size_t fold_ws_bytes(int64_t nwg, int64_t Q) {
+  const int64_t qp = qpad(Q);
+  return (size_t)(nwg * qp) * 128 + al128((size_t)(qp / FQ) * 4) + al128((size_t)qp * 4);
+}
+
+static inline FoldWs fold_ws(void* ws, int64_t nwg, int64_t Q) {
+  const int64_t qp = qpad(Q);
+  FoldWs f;
+  f.slab = (uint64_t*)ws;
+  f.cnt = (uint32_t*)((char*)ws + (size_t)(nwg * qp) * 128);
+  f.gtau = (uint32_t*)((char*)f.cnt + al128((size_t)(qp / FQ) * 4));
+  f.Qpad = qp;
+  return f;
+}
+
+static inline hipError_t fold_zero(const FoldWs& f, hipStream_t s) {
+  return hipMemsetAsync(f.cnt, 0, (size_t)((char*)(f.gtau + f.Qpad) - (char*)f.cnt), s);
 }
 
 }  // namespace rankk

@@ -92,9 +92,8 @@ __global__ __launch_bounds__(256) void mirror_build_kernel(const void* __restric
 template <int D, bool SPLIT, bool ILV = false, bool PIPE = true, int NB = 8, int PF = 6>
 __global__ __launch_bounds__(256) void rank_mirror_kernel(const uint16_t* __restrict__ mirror, int64_t N,
                                                           const float* __restrict__ queries, int64_t Q, int k,
-                                                          int64_t rows_per_wg, int nan_first,
-                                                          float* __restrict__ ws_s, int64_t* __restrict__ ws_i,
-                                                          int64_t C) {
+                                                          int64_t rows_per_wg, int nan_first, FoldWs f,
+                                                          float* __restrict__ out_s, int64_t* __restrict__ out_i) {
   constexpr int NW = 4, NT = 64 * NW, KC = 16, NCH = D / 64, NS = D / 16;
   constexpr int SLOT = 32 * 128;   // 32 rows x 64 k fp16
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -258,36 +257,8 @@ __global__ __launch_bounds__(256) void rank_mirror_kernel(const uint16_t* __rest
     Li[tid * KC + p] = real ? (int32_t)~(uint32_t)L[p] : INT_MAX;
   }
   __syncthreads();
-  if (tid < MQ && q0 + tid < Q) {
-    int pos[2 * NW];
-#pragma unroll
-    for (int l = 0; l < 2 * NW; ++l) pos[l] = 0;
-    float* os = ws_s + (q0 + tid) * C + (int64_t)RB * k;
-    int64_t* oi = ws_i + (q0 + tid) * C + (int64_t)RB * k;
-    for (int o = 0; o < k; ++o) {
-      uint32_t bk = 0u;
-      int32_t bi = INT_MAX;
-      int bl = 0;
-#pragma unroll
-      for (int l = 0; l < 2 * NW; ++l) {
-        const int src = (l >> 1) * 64 + (l & 1) * 32 + tid;
-        if (pos[l] < KC) {
-          const uint32_t kk = Lk[src * KC + pos[l]];
-          const int32_t ii = Li[src * KC + pos[l]];
-          if (better(kk, ii, bk, bi)) { bk = kk; bi = ii; bl = l; }
-        }
-      }
-#pragma unroll
-      for (int l = 0; l < 2 * NW; ++l) pos[l] += (l == bl) ? 1 : 0;
-      if (bi == INT_MAX) {
-        os[o] = -INFINITY;
-        oi[o] = -1;
-      } else {
-        os[o] = decode_key(bk, nan_first);
-        oi[o] = r_begin + bi;
-      }
-    }
-  }
+  fold_publish<2 * NW>(Lk, Li, KC, q0, Q, k, r_begin, f);
+  fold_reduce<NT>(smem, f, q0, Q, k, nan_first, 0, out_s, out_i);
 }
 
 // ---- exact re-score of each query's kc mirror candidates (one wave per query)
@@ -387,7 +358,7 @@ static int64_t mirror_wgs(int64_t N) {
 
 size_t rank_mirror_workspace_bytes(int64_t N, int64_t Q) {
   const int64_t nwg = N > 0 ? mirror_wgs(N) : 1;
-  return (size_t)(Q * nwg * MIRROR_KC + Q * MIRROR_KC) * (sizeof(float) + sizeof(int64_t));
+  return al128((size_t)(Q * MIRROR_KC) * (sizeof(float) + sizeof(int64_t))) + fold_ws_bytes(nwg, Q);
 }
 
 int rank_mirror_supported(int64_t D) { return D == 512 || D == 768; }
@@ -424,7 +395,7 @@ namespace miclip {
 
 template <int D, bool SPLIT>
 static hipError_t launch_mirror(const uint16_t* mirror, int64_t N, const float* q, int64_t Q, int kc, int nf,
-                                float* ws_s, int64_t* ws_i, int64_t C, int64_t nwg, hipStream_t s) {
+                                void* fws, float* out_s, int64_t* out_i, int64_t nwg, hipStream_t s) {
   const size_t lds = (size_t)4 * 8 * 4096 + MQ * 4;
   const int64_t rpw = ((N + nwg - 1) / nwg + 127) / 128 * 128;   // whole tiles per wave round
   // MICLIP_MIRROR_VAR (A/B): 1 fragments read after the wait (no PIPE), 2 seven chunks in
@@ -441,7 +412,9 @@ static hipError_t launch_mirror(const uint16_t* mirror, int64_t N, const float* 
   hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
   const dim3 grid((unsigned)((Q + MQ - 1) / MQ), (unsigned)nwg);   // (query blocks, row blocks): RB / QB
-  hipLaunchKernelGGL(fn, grid, dim3(256), lds, s, mirror, N, q, Q, kc, rpw, nf, ws_s, ws_i, C);
+  const FoldWs f = fold_ws(fws, nwg, Q);
+  if ((e = fold_zero(f, s)) != hipSuccess) return e;
+  hipLaunchKernelGGL(fn, grid, dim3(256), lds, s, mirror, N, q, Q, kc, rpw, nf, f, out_s, out_i);
   return hipGetLastError();
 }
 
@@ -450,16 +423,13 @@ hipError_t rank_mirror(const uint16_t* mirror, const void* master, int64_t N, in
                        void* ws, hipStream_t s) {
   const int kc = MIRROR_KC;
   const int64_t nwg = mirror_wgs(N);
-  const int64_t C = nwg * kc;
-  float* ws_s = (float*)ws;
-  int64_t* ws_i = (int64_t*)((char*)ws + (size_t)(Q * C) * sizeof(float));
-  float* m_s = (float*)((char*)ws_i + (size_t)(Q * C) * sizeof(int64_t));
-  int64_t* m_i = (int64_t*)((char*)m_s + (size_t)(Q * kc) * sizeof(float));
+  // the mirror's merged top-kc per query, then the in-launch merge's area
+  float* m_s = (float*)ws;
+  int64_t* m_i = (int64_t*)((char*)ws + (size_t)(Q * kc) * sizeof(float));
+  void* fws = (char*)ws + al128((size_t)(Q * kc) * (sizeof(float) + sizeof(int64_t)));
   const bool split = D <= 512;
-  hipError_t e = D == 512 ? launch_mirror<512, true>(mirror, N, q, Q, kc, nan_first, ws_s, ws_i, C, nwg, s)
-                          : launch_mirror<768, false>(mirror, N, q, Q, kc, nan_first, ws_s, ws_i, C, nwg, s);
-  if (e != hipSuccess) return e;
-  e = rank_merge(ws_s, ws_i, Q, C, kc, nan_first, m_s, m_i, s);
+  hipError_t e = D == 512 ? launch_mirror<512, true>(mirror, N, q, Q, kc, nan_first, fws, m_s, m_i, nwg, s)
+                          : launch_mirror<768, false>(mirror, N, q, Q, kc, nan_first, fws, m_s, m_i, nwg, s);
   if (e != hipSuccess) return e;
   float d_rel, d_abs;
   mirror_delta(D, split, d_rel, d_abs);

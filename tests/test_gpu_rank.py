@@ -276,3 +276,59 @@ def test_rank_reg_nine_slot_ring_bit_identical(gpu, monkeypatch, N, Q):
     s9, i9 = retrieval.rank_topk(corpus, q, 10)
     torch.cuda.synchronize()
     assert torch.equal(i8, i9) and torch.equal(s8, s9)
+
+
+@pytest.mark.parametrize("dt", ["bf16", "f16"])
+@pytest.mark.parametrize("N,Q", [(1, 1), (77, 3), (4099, 32), (100003, 33)])
+def test_rank_reg_half_corpus_bit_identical(gpu, monkeypatch, dt, N, Q):
+    """16-bit corpora at D = 512 run rank_reg (64-k ring chunks of bf16 / fp16
+    rows, converted exactly to f32 after the fragment read): candidates bit for
+    bit those of rank_stream (A/B build, MICLIP_RANK_REG=0), which converts in
+    its loads; and the top-k of the oracle's f32 scores of the same values."""
+    import torch
+    from miclip import _native, retrieval, weights
+    from oracle import rank_ref
+    tdt = torch.bfloat16 if dt == "bf16" else torch.float16
+    c32 = weights.normal(31, f"h{N}", (N, 512))
+    c32[N // 2] = 0.0                                                # a zero row: inv_norm's guard
+    c = torch.from_numpy(c32).to(tdt).to(gpu)
+    q = _t(weights.synthetic_corpus(Q, 512, seed=32), gpu)
+    s0, i0 = retrieval.rank_topk(c, q, 10)
+    monkeypatch.setattr(_native, "lib", _native.lib_ab)
+    monkeypatch.setenv("MICLIP_RANK_REG", "0")
+    s1, i1 = retrieval.rank_topk(c, q, 10)
+    torch.cuda.synchronize()
+    assert torch.equal(i0, i1) and torch.equal(s0.view(torch.int32), s1.view(torch.int32))
+    if N <= 5000:
+        S = rank_ref.scores_ref(c.float().cpu().numpy(), q.cpu().numpy())
+        for r in range(Q):
+            rank_ref.assert_topk_equivalent(s0[r].cpu().numpy(), i0[r].cpu().numpy(), S[r], 10)
+
+
+@pytest.mark.parametrize("D", [512, 768])
+@pytest.mark.parametrize("k", [1, 10, 16])
+def test_in_launch_merge_mass_ties(gpu, D, k):
+    """The in-launch merge (last workgroup of each query block reduces every
+    workgroup's top-k above the global k-th-key threshold) under exact ties in
+    every workgroup: 200003 rows drawn from 5 distinct vectors and a zero row
+    (NaN score), 33 queries (two query blocks).  Identical rows score bit for
+    bit alike, so the top-k is the best vector's lowest row indices (NaN rows
+    first under nan_policy="first")."""
+    from miclip import retrieval
+    rng = np.random.default_rng(D + k)
+    base = rng.standard_normal((6, D)).astype(np.float32)
+    base[5] = 0.0
+    N = 200_003
+    pick = rng.integers(0, 6, N)
+    corpus = base[pick]
+    q = rng.standard_normal((33, D)).astype(np.float32)
+    sb = (base[:5].astype(np.float64) / np.linalg.norm(base[:5], axis=1, keepdims=True)) @ q.T.astype(np.float64)
+    for pol in ("first", "last"):
+        s, i = retrieval.rank_topk(_t(corpus, gpu), _t(q, gpu), k, nan_policy=pol)
+        i = i.cpu().numpy()
+        for r in range(33):
+            order = np.argsort(-sb[:, r], kind="stable")
+            ranked = [np.flatnonzero(pick == 5)] if pol == "first" else []
+            ranked += [np.flatnonzero(pick == v) for v in order]
+            want = np.concatenate(ranked)[:k]
+            np.testing.assert_array_equal(i[r], want, err_msg=f"query {r} {pol}")
