@@ -12,6 +12,7 @@
 namespace miclip {
 
 namespace {
+
 // --------------------------------------------------------------- attention
 // One wave per (sequence, head), head dim 64, whole padded sequence (SP rows,
 // multiple of 32) per wave; no workgroup barriers.
@@ -595,6 +596,258 @@ __global__ __launch_bounds__(NW * 64) void attention_res_kernel(const uint16_t* 
   }
 }
 
+// ------------- attention, vision towers: K/V resident in LDS, 32x32x16 MFMAs
+// Same work split and LDS residency as attention_res_kernel, on the 32 x 32
+// MFMA shape, whose 32 cycles hold the SIMD's issue for 8 (the 16 x 16 shape
+// holds 8 of 16), so the softmax VALU of the other wave on the SIMD finds
+// twice the issue slots beside the matrix pipe.  Per wave: query blocks of 32
+// rows (two at a time, sharing every K / V^T fragment read), 64-key chunks.
+//   S^T = K Q^T : K is the A operand (lane: key r, 8 dims of k-step s at
+//     chunk 2s + half), Q^T the B operand held in registers for the block;
+//     the result X[key][query] has the query on the lane (r = lane & 31) and
+//     16 keys per lane half in registers: key (reg & 3) + 8 (reg >> 2) + 4 half;
+//   softmax in the log2 domain with the lazy rescale of the kernels above;
+//     a row's max over 64 keys is 32 in-lane values and one permlane32 swap;
+//   O^T = V^T P^T : X's registers 8s .. 8s + 7, packed to bf16, ARE the B
+//     operand of k-step s (the MFMA's k order inside a step is key
+//     16s + 8(j >> 2) + 4 half + (j & 3) for element j), so P never leaves the
+//     lane; V^T is the A operand, read transposed (ds_read_b64_tr_b16) in that
+//     same key order: two reads of 4 keys x 16 dims per 16-lane group.
+//   K image : 16-byte chunk c of key row r at slot c ^ ((r >> 1) & 7) (a
+//             16-lane group of the A-operand read covers all 64 banks);
+//   V image : chunk c of row r at slot c ^ (((r >> 1) & 1) << 2): the four rows
+//             of a transposed read (r0 .. r0 + 3, r0 % 4 == 0) put their 64
+//             bytes in four disjoint quarter-banks.
+// ABL (A/B timing probes only): 1 = no exponentials, 2 = no K/V DMA, 3 = no softmax VALU
+template <int NW, bool TT2 = true, int ABL = 0>
+__global__ __launch_bounds__(NW * 64) void attention_r32_kernel(const uint16_t* __restrict__ qkv,
+                                                                uint16_t* __restrict__ out, int S, int W, int H,
+                                                                uint8_t* __restrict__ q8, uint8_t* __restrict__ qs,
+                                                                int64_t rows_pad, int stagger_ticks) {
+  extern __shared__ __attribute__((aligned(16))) char r32_lds[];
+  const int spad = (S + 31) & ~31;
+  char* Kimg = r32_lds;
+  char* Vimg = r32_lds + spad * 128;
+  const int item = blockIdx.x;
+  const int bseq = item / H, head = item % H;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t ld = 3 * (int64_t)W;
+  const uint16_t* qb = qkv + (int64_t)bseq * S * ld + head * 64;
+  const uint16_t* kb = qb + W;
+  const uint16_t* vb = qb + 2 * W;
+
+  // ---- K, V -> LDS (one DMA instruction = 8 rows; rows >= S clamped copies)
+  // The first workgroups on the CUs start together and, all taking the same
+  // time, would keep issuing their K/V loads (148 KB each at S = 577) in
+  // chip-wide bursts; a start delay of 0-3 quarters of a workgroup's time on
+  // the first workgroup of each CU spreads them out for the rest of the grid.
+  if (stagger_ticks > 0 && (int)blockIdx.x < 256) {
+    const int ph = (blockIdx.x >> 3) & 3;
+    if (ph) {
+      const uint64_t until = __builtin_amdgcn_s_memrealtime() + (uint64_t)ph * stagger_ticks;
+      while (__builtin_amdgcn_s_memrealtime() < until) __builtin_amdgcn_s_sleep(8);
+    }
+  }
+  const int nch = (S + 63) >> 6;
+  if (ABL != 2) {
+    const int nr8 = spad >> 3;
+    const int slot = lane & 7;
+    for (int i = wave; i < 2 * nr8; i += NW) {
+      const bool isv = i >= nr8;
+      const int i8 = isv ? i - nr8 : i;
+      const int rr = i8 * 8 + (lane >> 3);
+      const int cc = isv ? (slot ^ (((rr >> 1) & 1) << 2)) : (slot ^ ((rr >> 1) & 7));
+      glds16((isv ? vb : kb) + (int64_t)min(rr, S - 1) * ld + cc * 8, (isv ? Vimg : Kimg) + i8 * 1024);
+    }
+  }
+
+  const int r = lane & 31, hh = lane >> 5;
+  const int ksw = (r >> 1) & 7;
+  // transposed V^T reads: lane 4q + p of each 16-lane group gives row q
+  // (key 4 half + q of the 8-key half-step), dims 16 g + 4p .. + 3 of the
+  // 32-dim block
+  const int i16 = lane & 15, gq = (lane >> 4) & 1, tq = i16 >> 2, tp = i16 & 3;
+  const int vrow = (4 * hh + tq) * 128 + 8 * (tp & 1);
+  const int vof0 = vrow + 16 * ((0 + 2 * gq + (tp >> 1)) ^ ((tq >> 1) << 2));
+  const int vof1 = vrow + 16 * ((4 + 2 * gq + (tp >> 1)) ^ ((tq >> 1) << 2));
+  const float sl2 = 0.125f * 1.4426950408889634f;   // head_dim^-0.5 * log2(e)
+  constexpr float RESCALE = 8.0f;
+  const int nqb = (S + 31) >> 5;
+  const int last_keys = S - (nch - 1) * 64;   // 1..64
+  typedef short s16x4 __attribute__((ext_vector_type(4)));
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  auto tr_read = [&](const char* p) -> s16x4 {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(LDS_AS char*)(uintptr_t)(const LDS_AS char*)p);
+  };
+  auto vfrag = [&](const char* p) -> bf16x8 {
+    const s16x4 lo = tr_read(p);
+    const s16x4 hi = tr_read(p + 8 * 128);
+    return __builtin_bit_cast(bf16x8, (s16x8)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+  };
+
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  auto blocks = [&](auto tt_c, int b0, int b1) {
+    constexpr int TT = decltype(tt_c)::value;
+    const int bq[2] = {b0, b1};
+    bf16x8 qf[TT][4];
+#pragma unroll
+    for (int u = 0; u < TT; ++u) {
+      const int qrow = min(bq[u] * 32 + r, S - 1);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) qf[u][s] = *(const bf16x8*)(qb + (int64_t)qrow * ld + 16 * s + 8 * hh);
+    }
+    float m[TT], l[TT];
+    f32x16 o[TT][2];
+#pragma unroll
+    for (int u = 0; u < TT; ++u) {
+      m[u] = -INFINITY;
+      l[u] = 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) o[u][0][i] = o[u][1][i] = 0.f;
+    }
+
+    // one 64-key chunk: NKB valid 32-key blocks, MASK: keys >= S inside them
+    auto chunk = [&](auto nkb_c, auto mask_c, int c) {
+      constexpr int NKB = decltype(nkb_c)::value;
+      constexpr bool MASK = decltype(mask_c)::value;
+      f32x16 x[TT][NKB];
+#pragma unroll
+      for (int kt = 0; kt < NKB; ++kt) {
+        const char* kp = Kimg + (c * 64 + kt * 32 + r) * 128;
+        bf16x8 kf[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) kf[s] = *(const bf16x8*)(kp + 16 * ((2 * s + hh) ^ ksw));
+#pragma unroll
+        for (int u = 0; u < TT; ++u) {
+          f32x16 acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[0], qf[u][0], f32x16{}, 0, 0, 0);
+#pragma unroll
+          for (int s = 1; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[s], qf[u][s], acc, 0, 0, 0);
+          x[u][kt] = acc;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < TT && ABL != 3; ++u) {
+        if (MASK) {
+#pragma unroll
+          for (int kt = 0; kt < NKB; ++kt)
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+              if (c * 64 + kt * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh >= S) x[u][kt][i] = -INFINITY;
+        }
+        float cm = x[u][0][0];
+#pragma unroll
+        for (int kt = 0; kt < NKB; ++kt)
+#pragma unroll
+          for (int i = (kt ? 0 : 1); i < 16; ++i) cm = fmaxf(cm, x[u][kt][i]);
+        {
+          const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(cm), __float_as_uint(cm), false, false);
+          cm = fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+        }
+        const float cmu = cm * sl2;   // finite: chunk 0 holds key 0 for every row
+        if (cmu > m[u] + RESCALE) {
+          const float alpha = __builtin_amdgcn_exp2f(m[u] - cmu);
+          l[u] *= alpha;
+          o[u][0] *= alpha;
+          o[u][1] *= alpha;
+          m[u] = cmu;
+        }
+        float ps = 0.f;
+#pragma unroll
+        for (int kt = 0; kt < NKB; ++kt) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            x[u][kt][i] = ABL == 1 ? fmaf(x[u][kt][i], sl2, -m[u]) : __builtin_amdgcn_exp2f(fmaf(x[u][kt][i], sl2, -m[u]));
+#pragma unroll
+          for (int i = 0; i < 16; i += 4) ps += (x[u][kt][i] + x[u][kt][i + 1]) + (x[u][kt][i + 2] + x[u][kt][i + 3]);
+        }
+        l[u] += ps;
+      }
+#pragma unroll
+      for (int kt = 0; kt < NKB; ++kt)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const char* vp = Vimg + (c * 64 + kt * 32 + 16 * s) * 128;
+          const bf16x8 v0 = vfrag(vp + vof0);
+          const bf16x8 v1 = vfrag(vp + vof1);
+#pragma unroll
+          for (int u = 0; u < TT; ++u) {
+            uint32_t pk[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) pk[j] = pack_bf16x2(x[u][kt][8 * s + 2 * j], x[u][kt][8 * s + 2 * j + 1]);
+            typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+            const bf16x8 pb = __builtin_bit_cast(bf16x8, (u32x4_t){pk[0], pk[1], pk[2], pk[3]});
+            o[u][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(v0, pb, o[u][0], 0, 0, 0);
+            o[u][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(v1, pb, o[u][1], 0, 0, 0);
+          }
+        }
+    };
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using BF = std::integral_constant<bool, false>;
+    using BT = std::integral_constant<bool, true>;
+    for (int c = 0; c < nch - 1; ++c) chunk(I2{}, BF{}, c);
+    if (last_keys > 32) chunk(I2{}, BT{}, nch - 1);
+    else chunk(I1{}, BT{}, nch - 1);
+
+#pragma unroll
+    for (int u = 0; u < TT; ++u) {
+      float lt = l[u];
+      {
+        const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(lt), __float_as_uint(lt), false, false);
+        lt = __uint_as_float(b[0]) + __uint_as_float(b[1]);
+      }
+      const float inv = 1.0f / lt;
+      const int qrow = bq[u] * 32 + r;
+      // o[u][db][i]: query qrow, head dim 32 db + (i & 3) + 8 (i >> 2) + 4 hh
+      if (q8) {   // MX-fp8 output: this head's 64 dims are one 64-k block of out_proj
+        float amax = 0.f;
+#pragma unroll
+        for (int db = 0; db < 2; ++db)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) amax = fmaxf(amax, fabsf(o[u][db][i] * inv));
+        {
+          const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(amax), __float_as_uint(amax), false, false);
+          amax = fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+        }
+        const int X = mx_block_exp(amax);
+        const float scl = ldexpf(1.0f, -X);
+        if (qrow < S) {
+          const int64_t row = (int64_t)bseq * S + qrow;
+          uint8_t* dst = q8 + row * W + head * 64 + 4 * hh;
+#pragma unroll
+          for (int db = 0; db < 2; ++db)
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+              *(uint32_t*)(dst + 32 * db + 8 * t) = mx_pack4(o[u][db][4 * t] * inv, o[u][db][4 * t + 1] * inv,
+                                                             o[u][db][4 * t + 2] * inv, o[u][db][4 * t + 3] * inv, scl);
+          if (hh == 0) qs[mx_scale_index(row, head, rows_pad)] = (uint8_t)(X + 127);
+        }
+        continue;
+      }
+      if (qrow < S) {
+        uint16_t* dst = out + ((int64_t)bseq * S + qrow) * W + head * 64 + 4 * hh;
+#pragma unroll
+        for (int db = 0; db < 2; ++db)
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+            *(uint2*)(dst + 32 * db + 8 * t) = make_uint2(pack_bf16x2(o[u][db][4 * t] * inv, o[u][db][4 * t + 1] * inv),
+                                                          pack_bf16x2(o[u][db][4 * t + 2] * inv, o[u][db][4 * t + 3] * inv));
+      }
+    }
+  };
+  if (TT2) {
+    for (int b = wave; b < nqb; b += 2 * NW) {
+      if (b + NW < nqb) blocks(std::integral_constant<int, 2>{}, b, b + NW);
+      else blocks(std::integral_constant<int, 1>{}, b, b);
+    }
+  } else {
+    for (int b = wave; b < nqb; b += NW) blocks(std::integral_constant<int, 1>{}, b, b);
+  }
+}
+
 }  // namespace
 
 hipError_t attention(const uint16_t* qkv, uint16_t* out, int B, int S, int W, int causal, hipStream_t s, uint8_t* q8,
@@ -622,26 +875,45 @@ hipError_t attention(const uint16_t* qkv, uint16_t* out, int B, int S, int W, in
     const int spad = (S + 31) & ~31;
     const size_t lds = 2 * (size_t)spad * 128;
     // variants: 1 = 8 waves, one query tile at a time (round 2); 2 = 8 waves, two tiles at a
-    // time; 3 = 16 waves (4 per SIMD sharing the K/V image), one tile at a time
+    // time; 3 = 16 waves (4 per SIMD sharing the K/V image), one tile at a time; 4-6 = the
+    // 32x32x16 kernel (attention_r32_kernel): 8 waves two blocks at a time, 16 / 12 waves one
 #if MICLIP_AB
     const char* ve = std::getenv("MICLIP_ATTN_VAR");   // A/B
     int var = ve ? std::atoi(ve) : 0;
 #else
     int var = 0;
 #endif
-    if (var < 1 || var > 3) var = S > 320 ? 2 : 1;
-    const void* fns[4] = {nullptr, (const void*)attention_res_kernel<8, false>, (const void*)attention_res_kernel<8, true>,
-                          (const void*)attention_res_kernel<16, false>};
-    static bool attr_set[4] = {false, false, false, false};
+    if (var < 1 || var > 9) var = S > 320 ? 2 : 1;
+    const void* fns[10] = {nullptr,
+                           (const void*)attention_res_kernel<8, false>,
+                           (const void*)attention_res_kernel<8, true>,
+                           (const void*)attention_res_kernel<16, false>,
+                           (const void*)attention_r32_kernel<8, true>,
+                           (const void*)attention_r32_kernel<12, false>,
+                           (const void*)attention_r32_kernel<12, false>,
+                           (const void*)attention_r32_kernel<12, false>,
+                           (const void*)attention_r32_kernel<12, false, 2>,
+                           (const void*)attention_r32_kernel<12, false, 1>};
+    static bool attr_set[10] = {false, false, false, false, false, false, false, false, false, false};
     if (!attr_set[var]) {
       hipError_t e = hipFuncSetAttribute(fns[var], hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       if (e != hipSuccess) return e;
       attr_set[var] = true;
     }
     const int64_t rp = ((int64_t)B * S + 1) & ~1;
+    // a quarter of one workgroup's time (~8.8 us at S = 577, scaling as S^2) in 100 MHz ticks
+    const int quarter = S * S / 378;
     if (var == 1) hipLaunchKernelGGL((attention_res_kernel<8, false>), grid, dim3(512), lds, s, qkv, out, S, W, H, q8, qs, rp);
     else if (var == 2) hipLaunchKernelGGL((attention_res_kernel<8, true>), grid, dim3(512), lds, s, qkv, out, S, W, H, q8, qs, rp);
-    else hipLaunchKernelGGL((attention_res_kernel<16, false>), grid, dim3(1024), lds, s, qkv, out, S, W, H, q8, qs, rp);
+    else if (var == 3) hipLaunchKernelGGL((attention_res_kernel<16, false>), grid, dim3(1024), lds, s, qkv, out, S, W, H, q8, qs, rp);
+    else if (var == 4) hipLaunchKernelGGL((attention_r32_kernel<8, true>), grid, dim3(512), lds, s, qkv, out, S, W, H, q8, qs, rp, 0);
+    else if (var == 5) hipLaunchKernelGGL((attention_r32_kernel<12, false>), grid, dim3(768), lds, s, qkv, out, S, W, H, q8, qs, rp, 0);
+    else if (var == 6) hipLaunchKernelGGL((attention_r32_kernel<12, false>), grid, dim3(768), lds, s, qkv, out, S, W, H, q8, qs, rp, quarter);
+    else if (var == 7) hipLaunchKernelGGL((attention_r32_kernel<12, false>), grid, dim3(768), lds, s, qkv, out, S, W, H, q8, qs, rp, 2 * quarter);
+#if MICLIP_AB
+    else if (var == 8) hipLaunchKernelGGL((attention_r32_kernel<12, false, 2>), grid, dim3(768), lds, s, qkv, out, S, W, H, q8, qs, rp, 0);
+    else hipLaunchKernelGGL((attention_r32_kernel<12, false, 1>), grid, dim3(768), lds, s, qkv, out, S, W, H, q8, qs, rp, quarter);
+#endif
     return hipGetLastError();
   }
 #if MICLIP_AB

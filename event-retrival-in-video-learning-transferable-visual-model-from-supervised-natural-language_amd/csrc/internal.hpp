@@ -171,6 +171,22 @@ hipError_t mirror_build(const void* master, int64_t N, int64_t D, int dt, uint16
 hipError_t rank_mirror(const uint16_t* mirror, const void* master, int64_t N, int64_t D, int dt, const float* q,
                        int64_t Q, int k, int64_t base, int nan_first, float* out_s, int64_t* out_i, int32_t* cert,
                        void* ws, hipStream_t s);
+// exact re-score + certificate of kc candidates per query (rank_mirror.hip): out = their exact top-k,
+// cert[q] = 1 when no row outside them can reach the top-k (|s_cand - s_exact| <= d_rel |q| + d_abs);
+// unsafe (nullable): a device flag that uncertifies every query when set
+hipError_t rank_rescore(const void* master, int64_t N, int64_t D, int dt, const float* q, int64_t Q, int k, int kc,
+                        const float* m_s, const int64_t* m_i, int64_t base, float d_rel, float d_abs, int norm_mode,
+                        int nan_first, const int32_t* unsafe, float* out_s, int64_t* out_i, int32_t* cert,
+                        hipStream_t s);
+// certified bf16-MFMA ranking pass (rank_cert.hip): f32 / bf16 rows, D = 512, k <= 12, L2 norms
+int64_t rank_cert_min_rows();
+bool rank_cert_eligible(int64_t N, int64_t D, int dt, int k, int norm_mode);
+size_t rank_cert_ws_bytes(int64_t N, int64_t Q);
+void rank_cert_delta(int dt, float& d_rel, float& d_abs);
+// certified queries' results in out; *cert_out = the per-query certificates (in ws) for the gated exact pass
+hipError_t rank_cert_topk(const void* corpus, int64_t N, int dt, const float* q, int64_t Q, int k, int64_t base,
+                          int norm_mode, int nan_first, float* out_s, int64_t* out_i, void* ws, int32_t** cert_out,
+                          hipStream_t s);
 }  // namespace miclip
 
 #include <vector>

@@ -158,6 +158,7 @@ __global__ __launch_bounds__(64 * NW) void rank_stream(const void* __restrict__ 
     const uint32_t thr = own > tq_thr ? own : tq_thr;
     uint64_t c[16];
     bool any = false;
+    uint32_t okm = 0u;
 #pragma unroll
     for (int rg = 0; rg < 16; ++rg) {
       const int rr = (rg & 3) + 8 * (rg >> 2) + 4 * h;
@@ -167,10 +168,10 @@ __global__ __launch_bounds__(64 * NW) void rank_stream(const void* __restrict__ 
       const bool ok = qvalid && lr < nrows && key >= thr;
       c[rg] = ok ? (((uint64_t)key << 32) | (uint32_t)~(uint32_t)lr) : 0ull;
       any |= ok;
+      okm |= ok ? 1u << rg : 0u;
     }
     if (__any(any)) {
-      bitonic_sort16_desc(c);
-      merge16_desc(L, c);
+      list_update16(L, c, okm);
       // publish this list's k-th key (a lower bound of the query's k-th best)
       uint32_t kth = (uint32_t)(L[0] >> 32);
 #pragma unroll
@@ -274,7 +275,11 @@ template <int D, int NB = 8, int PF = 6, bool NOMFMA = false, bool ILV = false, 
 __global__ __launch_bounds__(256) void rank_reg(const void* __restrict__ corpus, int64_t N,
                                                 const float* __restrict__ queries, int64_t Q, int k,
                                                 int64_t rows_per_wg, int norm_mode, int nan_first, int64_t index_base,
-                                                FoldWs f, float* __restrict__ out_s, int64_t* __restrict__ out_i) {
+                                                FoldWs f, float* __restrict__ out_s, int64_t* __restrict__ out_i,
+                                                const int32_t* __restrict__ gate) {
+  // gate (nullable): per-query certificates of the certified pass (rank_cert.hip); a query
+  // block whose queries are all certified already holds its results and exits here, before
+  // any barrier or merge-counter update (uniformly over the block's workgroups).
   // DT 0: f32 rows, a ring chunk = 32 k; DT 1 / 2 (bf16 / fp16 rows): a ring chunk = 64 k, two
   // 32-k MFMA groups, converted to f32 (exactly) after the fragment read — the arithmetic of
   // rank_stream<DT> (load_chunk's conversion, the same k order), so its candidates bit for bit.
@@ -304,6 +309,7 @@ __global__ __launch_bounds__(256) void rank_reg(const void* __restrict__ corpus,
   const int r = lane & 31, h = lane >> 5;
   const int64_t q0 = (int64_t)QB * RQ;
   const bool qvalid = q0 + r < Q;
+  if (gate && __all(!qvalid || gate[q0 + r] != 0)) return;
 
   // queries -> registers (zeros past Q)
   float qv[NQ][16];
@@ -461,6 +467,7 @@ __global__ __launch_bounds__(256) void rank_reg(const void* __restrict__ corpus,
       const uint32_t thr = own > tq_thr ? own : tq_thr;
       uint64_t c[16];
       bool any = false;
+      uint32_t okm = 0u;
 #pragma unroll
       for (int rg = 0; rg < 16; ++rg) {
         const int rr = (rg & 3) + 8 * (rg >> 2) + 4 * h;
@@ -470,10 +477,10 @@ __global__ __launch_bounds__(256) void rank_reg(const void* __restrict__ corpus,
         const bool ok = qvalid && lr < nrows && key >= thr;
         c[rg] = ok ? (((uint64_t)key << 32) | (uint32_t)~(uint32_t)lr) : 0ull;
         any |= ok;
+        okm |= ok ? 1u << rg : 0u;
       }
       if (__any(any)) {
-        bitonic_sort16_desc(c);
-        merge16_desc(L, c);
+        list_update16(L, c, okm);
         uint32_t kth = (uint32_t)(L[0] >> 32);
 #pragma unroll
         for (int p = 1; p < KC; ++p) kth = (p == k - 1) ? (uint32_t)(L[p] >> 32) : kth;
@@ -965,7 +972,10 @@ size_t rank_workspace_bytes(int64_t N, int64_t Q, int k) {
   const int64_t nch = N > 0 ? rank_chunks(N) : 1;
   const size_t lists = (size_t)(Q * nch * k) * (sizeof(float) + sizeof(int64_t));   // rank_stage1 + rank_merge
   const size_t fold = kc_for(k) == 16 ? fold_ws_bytes(nch, Q) : 0;                   // in-launch merge (k <= 16)
-  return lists > fold ? lists : fold;
+  const size_t exact = lists > fold ? lists : fold;
+  // the certified pass (rank_cert.hip) ahead of the gated exact pass: its own area first
+  const bool cert = k <= 12 && N >= rank_cert_min_rows();
+  return cert ? al128(rank_cert_ws_bytes(N, Q)) + exact : exact;
 }
 
 static size_t stage1_lds(int64_t D, int KC) {
@@ -1000,7 +1010,8 @@ hipError_t rank_merge(const float* cs, const int64_t* ci, int64_t Q, int64_t C, 
 
 template <int D, int DT>
 static hipError_t launch_reg(int64_t N, const void* corpus, const float* q, int64_t Q, int k, int nm, int nf,
-                             int64_t base, void* ws, float* out_s, int64_t* out_i, hipStream_t s) {
+                             int64_t base, void* ws, float* out_s, int64_t* out_i, hipStream_t s,
+                             const int32_t* gate = nullptr) {
   // one workgroup per CU (LDS ring 128 KB), rows per workgroup a multiple of 128
   // (one 32-row tile per wave); never more workgroups than rank_chunks (workspace)
   int64_t nwg = rank_chunks(N);
@@ -1038,7 +1049,7 @@ static hipError_t launch_reg(int64_t N, const void* corpus, const float* q, int6
   if (e != hipSuccess) return e;
   if ((e = fold_zero(f, s)) != hipSuccess) return e;
   const dim3 grid((unsigned)((Q + RQ - 1) / RQ), (unsigned)nwg);   // (query blocks, row blocks): RB / QB
-  hipLaunchKernelGGL(fn, grid, dim3(256), lds, s, corpus, N, q, Q, k, rpw, nm, nf, base, f, out_s, out_i);
+  hipLaunchKernelGGL(fn, grid, dim3(256), lds, s, corpus, N, q, Q, k, rpw, nm, nf, base, f, out_s, out_i, gate);
   return hipGetLastError();
 }
 
@@ -1087,6 +1098,16 @@ hipError_t rank_topk(const void* corpus, int64_t N, int64_t D, int dt, const flo
   const size_t lds = qa > la ? qa : la;
   hipError_t e;
   if (KC == 16 && D == 512 && !(legacy && legacy[0] == '1') && !(noreg && noreg[0] == '0')) {
+    if (rank_cert_eligible(N, D, dt, k, norm_mode)) {
+      // certified bf16-MFMA pass + exact re-score of its candidates, then the exact pass for
+      // the query blocks it could not certify (results identical to the exact pass alone)
+      int32_t* cert = nullptr;
+      hipError_t ec = rank_cert_topk(corpus, N, dt, q, Q, k, base, norm_mode, nan_first, out_s, out_i, ws, &cert, s);
+      if (ec != hipSuccess) return ec;
+      void* ws2 = (char*)ws + al128(rank_cert_ws_bytes(N, Q));
+      return dt == 0 ? launch_reg<512, 0>(N, corpus, q, Q, k, norm_mode, nan_first, base, ws2, out_s, out_i, s, cert)
+                     : launch_reg<512, 1>(N, corpus, q, Q, k, norm_mode, nan_first, base, ws2, out_s, out_i, s, cert);
+    }
     // (D = 768 would hold 384 query VGPRs: hipcc spills ~230, so it keeps rank_stream)
     return dt == 0   ? launch_reg<512, 0>(N, corpus, q, Q, k, norm_mode, nan_first, base, ws, out_s, out_i, s)
            : dt == 1 ? launch_reg<512, 1>(N, corpus, q, Q, k, norm_mode, nan_first, base, ws, out_s, out_i, s)

@@ -102,6 +102,33 @@ __device__ __forceinline__ void merge16_desc(uint64_t (&L)[16], const uint64_t (
     }
 }
 
+// A tile's candidates c[0..15] (0 = none; m: the non-empty ones) into the
+// sorted (desc) top-16 list L.  Once the threshold has settled a lane has 0 or
+// 1 candidate per tile, and a full bitonic sort + merge (~1000 instructions of
+// 64-bit compare/select) for that one entry was the per-tile cost that bounded
+// the streaming rank kernels (one wave per SIMD: nothing hides it).  So: while
+// no lane has more than 6, each round inserts every lane's next candidate with
+// one branch-free pass over L (~120 instructions; an empty lane inserts 0, a
+// no-op), for as many rounds as the lane with the most; otherwise sort + merge.
+// Same final list either way: the packed keys are unique.
+__device__ __forceinline__ void list_update16(uint64_t (&L)[16], uint64_t (&c)[16], uint32_t m) {
+  if (__any(__builtin_popcount(m) > 6)) {
+    bitonic_sort16_desc(c);
+    merge16_desc(L, c);
+    return;
+  }
+  while (__any(m != 0u)) {
+    const int i = m ? __builtin_ctz(m) : 16;
+    uint64_t e = 0ull;
+#pragma unroll
+    for (int rg = 0; rg < 16; ++rg) e = rg == i ? c[rg] : e;
+#pragma unroll
+    for (int p = 15; p > 0; --p) L[p] = e > L[p - 1] ? L[p - 1] : (e > L[p] ? e : L[p]);
+    L[0] = e > L[0] ? e : L[0];
+    m &= m - 1u;
+  }
+}
+
 // 16 consecutive elements of a row (f32 / bf16 / f16 storage) as f32
 template <int DT>
 __device__ __forceinline__ void load_chunk(const void* corpus, int64_t row, int64_t D, int k0, float (&v)[16]) {

@@ -224,6 +224,7 @@ __global__ __launch_bounds__(256) void rank_mirror_kernel(const uint16_t* __rest
       const uint32_t thr = own > tq_thr ? own : tq_thr;
       uint64_t c[16];
       bool any = false;
+      uint32_t okm = 0u;
 #pragma unroll
       for (int rg = 0; rg < 16; ++rg) {
         const int rr = (rg & 3) + 8 * (rg >> 2) + 4 * h;
@@ -232,10 +233,10 @@ __global__ __launch_bounds__(256) void rank_mirror_kernel(const uint16_t* __rest
         const bool ok = qvalid && gr < nrows && key >= thr;
         c[rg] = ok ? (((uint64_t)key << 32) | (uint32_t)~(uint32_t)gr) : 0ull;
         any |= ok;
+        okm |= ok ? 1u << rg : 0u;
       }
       if (__any(any)) {
-        bitonic_sort16_desc(c);
-        merge16_desc(L, c);
+        list_update16(L, c, okm);
         uint32_t kth = (uint32_t)(L[0] >> 32);
 #pragma unroll
         for (int p = 1; p < KC; ++p) kth = (p == k - 1) ? (uint32_t)(L[p] >> 32) : kth;
@@ -271,7 +272,8 @@ __global__ __launch_bounds__(64) void mirror_rescore_kernel(const void* __restri
                                                             const float* __restrict__ queries, int k, int kc,
                                                             const float* __restrict__ ms,
                                                             const int64_t* __restrict__ mi, int64_t index_base,
-                                                            float d_rel, float d_abs, int nan_first,
+                                                            float d_rel, float d_abs, int norm_mode, int nan_first,
+                                                            const int32_t* __restrict__ unsafe,
                                                             float* __restrict__ out_s, int64_t* __restrict__ out_i,
                                                             int32_t* __restrict__ cert) {
   constexpr int NCH = D / 32;
@@ -306,7 +308,7 @@ __global__ __launch_bounds__(64) void mirror_rescore_kernel(const void* __restri
       ss = fmaf(row[j][i], row[j][i], ss);
     }
   ss += __shfl_xor(ss, 32, 64);
-  if (h == 0) nrm[r] = inv_norm(ss, 0);
+  if (h == 0) nrm[r] = inv_norm(ss, norm_mode);
   __syncthreads();
   if (r == 0) {
 #pragma unroll
@@ -343,6 +345,7 @@ __global__ __launch_bounds__(64) void mirror_rescore_kernel(const void* __restri
       const float delta = d_rel * sqrtf(qq) + d_abs;
       ok = all_fin && nv >= k && kth > ms[q * kc + kc - 1] + delta;
     }
+    if (unsafe && *unsafe) ok = 0;   // the pass met a row its bound does not cover (rank_cert.hip)
     cert[q] = ok;
   }
 }
@@ -433,18 +436,29 @@ hipError_t rank_mirror(const uint16_t* mirror, const void* master, int64_t N, in
   if (e != hipSuccess) return e;
   float d_rel, d_abs;
   mirror_delta(D, split, d_rel, d_abs);
+  return rank_rescore(master, N, D, dt, q, Q, k, kc, m_s, m_i, base, d_rel, d_abs, 0, nan_first, nullptr, out_s, out_i,
+                      cert, s);
+}
+
+hipError_t rank_rescore(const void* master, int64_t N, int64_t D, int dt, const float* q, int64_t Q, int k, int kc,
+                        const float* m_s, const int64_t* m_i, int64_t base, float d_rel, float d_abs, int norm_mode,
+                        int nan_first, const int32_t* unsafe, float* out_s, int64_t* out_i, int32_t* cert,
+                        hipStream_t s) {
+  if (Q <= 0) return hipSuccess;
   const dim3 grid((unsigned)Q);
 #define MI_RS(DTV, DV)                                                                                                \
   hipLaunchKernelGGL((mirror_rescore_kernel<DTV, DV>), grid, dim3(64), 0, s, master, N, q, k, kc, m_s, m_i, base, \
-                     d_rel, d_abs, nan_first, out_s, out_i, cert)
+                     d_rel, d_abs, norm_mode, nan_first, unsafe, out_s, out_i, cert)
   if (D == 512) {
     if (dt == 0) MI_RS(0, 512);
     else if (dt == 1) MI_RS(1, 512);
     else MI_RS(2, 512);
-  } else {
+  } else if (D == 768) {
     if (dt == 0) MI_RS(0, 768);
     else if (dt == 1) MI_RS(1, 768);
     else MI_RS(2, 768);
+  } else {
+    return hipErrorInvalidValue;
   }
 #undef MI_RS
   return hipGetLastError();

@@ -1,6 +1,7 @@
 """A/B of the fused rank kernel variants in ONE process, interleaved rounds
-(default: rank_reg for f32 D = 512, else rank_stream; MICLIP_RANK_REG=0: rank_stream;
-MICLIP_RANK_STAGE1=1: the one-tile-at-a-time kernel), HIP events on the launch stream.
+(default: the certified pass + gated exact pass for >= 262144 rows at D = 512, else rank_reg
+for D = 512 and rank_stream otherwise; MICLIP_RANK_CERT=0: the exact pass alone;
+MICLIP_RANK_REG=0: rank_stream), HIP events on the launch stream.
 
   python scripts/rank_micro.py [rounds]
 """
@@ -15,16 +16,18 @@ os.environ.setdefault("MICLIP_LIB", "ab")   # A/B build: schedule variants, prob
 import torch  # noqa: E402
 from miclip import retrieval  # noqa: E402
 
-VARIANTS = {"default": {}, "seed0": {"MICLIP_RANK_SEED": "0"}, "pipe0": {"MICLIP_RANK_PIPE": "0"},
-            "ilv1": {"MICLIP_RANK_ILV": "1"}, "stream12": {"MICLIP_RANK_REG": "0", "MICLIP_RANK_NW": "12"},
-            "stage1": {"MICLIP_RANK_STAGE1": "1"}, "nomfma": {"MICLIP_RANK_PROBE": "1"}}
+# default: the certified pass (rank_cert.hip) where eligible (>= 262144 rows, D = 512, k <= 12);
+# exact: MICLIP_RANK_CERT=0, the exact pass alone
+VARIANTS = {"default": {}, "exact": {"MICLIP_RANK_CERT": "0"},
+            "stream12": {"MICLIP_RANK_REG": "0", "MICLIP_RANK_NW": "12", "MICLIP_RANK_CERT": "0"},
+            "nomfma": {"MICLIP_RANK_PROBE": "1", "MICLIP_RANK_CERT": "0"}}
 SHAPES = [(125_000, 512, 32, torch.float32), (1_000_000, 512, 32, torch.float32),
           (1_000_000, 512, 32, torch.bfloat16), (1_000_000, 768, 32, torch.float32), (10_000, 512, 32, torch.float32)]
 
 
 def setenv(v):
     for k in ("MICLIP_RANK_STAGE1", "MICLIP_RANK_NW", "MICLIP_RANK_REG", "MICLIP_RANK_PROBE", "MICLIP_RANK_ILV",
-              "MICLIP_RANK_PIPE", "MICLIP_RANK_SEED"):
+              "MICLIP_RANK_PIPE", "MICLIP_RANK_SEED", "MICLIP_RANK_CERT"):
         os.environ.pop(k, None)
     os.environ.update(VARIANTS[v])
 

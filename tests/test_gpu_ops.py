@@ -243,3 +243,37 @@ def test_attention_res_variants_bit_identical(gpu, monkeypatch, B, S, W, var):
     assert La.mi_op_attention(qkv.data_ptr(), b.data_ptr(), B, S, W, 0, _stream()) == 0, La.mi_last_error()
     torch.cuda.synchronize()
     assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("B,S,W", [(2, 577, 1024), (3, 257, 768), (2, 130, 128), (1, 97, 256), (2, 385, 128),
+                                   (1, 640, 192), (2, 100, 128)])
+@pytest.mark.parametrize("grow", [False, True])
+@pytest.mark.parametrize("var", ["4", "5", "6"])
+def test_attention_r32_kernel(gpu, monkeypatch, B, S, W, grow, var):
+    """attention_r32_kernel (32x32x16 MFMAs, P kept in the lane as the PV B
+    operand, V^T by transposed reads; MICLIP_ATTN_VAR=4 (8 waves, two blocks at
+    a time), 5 (12 waves, one block), 6 (12 waves, staggered start) in the A/B build)
+    against float64, on random rows and on rows whose max grows along the keys
+    (the lazy-rescale branch on every chunk).  Query-block counts 19 / 9 / 5 /
+    4 / 13 / 20 / 4 cover pairs, singles and a last block of one row."""
+    import torch
+    N_ = _lib()
+    g = torch.Generator(device="cpu").manual_seed(S + W + grow)
+    if grow:
+        qkv = torch.randn(B, S, 3, W // 64, 64, generator=g)
+        qkv[:, :, 0] = qkv[:, :, 0].abs() * 0.5 + 0.5
+        qkv[:, :, 1] = qkv[:, :, 1].abs() * torch.linspace(0.05, 4.0, S).reshape(1, S, 1, 1)
+        qkv = qkv.reshape(B * S, 3 * W).bfloat16().to(gpu)
+    else:
+        qkv = (torch.randn(B * S, 3 * W, generator=g) * 1.5).bfloat16().to(gpu)
+    out = torch.empty(B * S, W, dtype=torch.bfloat16, device=gpu)
+    monkeypatch.setenv("MICLIP_ATTN_VAR", var)
+    La = N_.lib_ab()
+    assert La.mi_op_attention(qkv.data_ptr(), out.data_ptr(), B, S, W, 0, _stream()) == 0, La.mi_last_error()
+    torch.cuda.synchronize()
+    H = W // 64
+    x = qkv.double().reshape(B, S, 3, H, 64)
+    q, k, v = (x[:, :, i].transpose(1, 2) for i in range(3))
+    ref = (torch.softmax(q @ k.transpose(-1, -2) * 0.125, -1) @ v).transpose(1, 2).reshape(B * S, W)
+    err = (out.double() - ref).abs().max().item()
+    assert err < 3e-2 * max(1.0, ref.abs().max().item()), err

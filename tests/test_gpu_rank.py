@@ -332,3 +332,78 @@ def test_in_launch_merge_mass_ties(gpu, D, k):
             ranked += [np.flatnonzero(pick == v) for v in order]
             want = np.concatenate(ranked)[:k]
             np.testing.assert_array_equal(i[r], want, err_msg=f"query {r} {pol}")
+
+
+def _ranked_both_ways(monkeypatch, c, q, k, **kw):
+    """mi_rank_topk through the A/B build with the certified pass forced on for
+    every eligible call (MICLIP_RANK_CERT=2) and switched off (0)."""
+    import torch
+    from miclip import _native, retrieval
+    monkeypatch.setattr(_native, "lib", _native.lib_ab)
+    monkeypatch.setenv("MICLIP_RANK_CERT", "2")
+    s1, i1 = retrieval.rank_topk(c, q, k, **kw)
+    monkeypatch.setenv("MICLIP_RANK_CERT", "0")
+    s0, i0 = retrieval.rank_topk(c, q, k, **kw)
+    torch.cuda.synchronize()
+    return (s1, i1), (s0, i0)
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+@pytest.mark.parametrize("N,Q,k", [(1, 1, 1), (15, 3, 10), (16, 2, 12), (17, 5, 12), (1000, 32, 10),
+                                   (40003, 33, 1), (100003, 70, 10)])
+def test_certified_pass_bit_identical(gpu, monkeypatch, dt, N, Q, k):
+    """rank_cert.hip (bf16-MFMA pass over f32 / bf16 rows with q = q1 + q2 and, f32 rows,
+    c = c_hi + c_lo; exact re-score of its top-16; certificates; the exact pass gated by
+    them) gives the exact pass's results bit for bit: L2 and guarded-L2 norms, NaN
+    first / last, fewer rows than candidates, one and three query blocks."""
+    import torch
+    from miclip import weights
+    c32 = weights.normal(41, f"c{N}", (N, 512))
+    c = _t(c32, gpu) if dt == "f32" else torch.from_numpy(c32).to(torch.bfloat16).to(gpu)
+    q = _t(weights.synthetic_corpus(Q, 512, seed=42), gpu)
+    for norm, pol in (("l2", "first"), ("l2_guard", "last")):
+        (s1, i1), (s0, i0) = _ranked_both_ways(monkeypatch, c, q, k, norm=norm, nan_policy=pol)
+        assert torch.equal(i1, i0), (norm, pol)
+        assert torch.equal(s1.view(torch.int32), s0.view(torch.int32)), (norm, pol)
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+def test_certified_pass_ties_and_unsafe_rows_fall_back(gpu, monkeypatch, dt):
+    """Rows the certificate cannot separate or its bound does not cover go to the exact
+    pass: exact duplicates of the best rows (ties across the candidate edge), a row of
+    tiny values (sum of squares below 1e-15) and a zero row (NaN score under L2)."""
+    import torch
+    from miclip import weights
+    N, Q = 50_000, 40
+    c32 = weights.normal(43, "ties", (N, 512))
+    q32 = weights.synthetic_corpus(Q, 512, seed=44)
+    c32[100:140] = c32[7]                       # 41 identical rows: ties at every k
+    c32[-5:] = q32[:5] * 3.0                     # rows parallel to queries 0..4
+    for extra in ("none", "tiny", "zero"):
+        cc = c32.copy()
+        if extra == "tiny":
+            cc[1234] = 1e-9
+        elif extra == "zero":
+            cc[1234] = 0.0
+        c = _t(cc, gpu) if dt == "f32" else torch.from_numpy(cc).to(torch.bfloat16).to(gpu)
+        for pol in ("first", "last"):
+            (s1, i1), (s0, i0) = _ranked_both_ways(monkeypatch, c, _t(q32, gpu), 12, nan_policy=pol)
+            assert torch.equal(i1, i0), (extra, pol)
+            assert torch.equal(s1.view(torch.int32), s0.view(torch.int32)), (extra, pol)
+
+
+def test_certified_pass_product_default_large_corpus(gpu, monkeypatch):
+    """The product library routes f32 / bf16 corpora of >= 262144 rows (D = 512, k <= 12)
+    through the certified pass: identical to the A/B build's exact pass."""
+    import torch
+    from miclip import _native, retrieval, weights
+    c = _t(weights.normal(45, "big", (300_001, 512)), gpu)
+    q = _t(weights.synthetic_corpus(32, 512, seed=46), gpu)
+    for cc in (c, c.bfloat16()):
+        s1, i1 = retrieval.rank_topk(cc, q, 10)
+        monkeypatch.setattr(_native, "lib", _native.lib_ab)
+        monkeypatch.setenv("MICLIP_RANK_CERT", "0")
+        s0, i0 = retrieval.rank_topk(cc, q, 10)
+        monkeypatch.undo()
+        torch.cuda.synchronize()
+        assert torch.equal(i1, i0) and torch.equal(s1.view(torch.int32), s0.view(torch.int32))
