@@ -874,46 +874,48 @@ hipError_t attention(const uint16_t* qkv, uint16_t* out, int B, int S, int W, in
     // vision towers (257 / 577 tokens): K/V resident in LDS, no per-chunk barriers
     const int spad = (S + 31) & ~31;
     const size_t lds = 2 * (size_t)spad * 128;
-    // variants: 1 = 8 waves, one query tile at a time (round 2); 2 = 8 waves, two tiles at a
-    // time; 3 = 16 waves (4 per SIMD sharing the K/V image), one tile at a time; 4-6 = the
-    // 32x32x16 kernel (attention_r32_kernel): 8 waves two blocks at a time, 16 / 12 waves one
+    // Defaults (scripts/attn_micro.py, r03): S <= 320 (L/14, 257 tokens) attention_res_kernel
+    // with 8 waves, one 16-row query tile at a time; S > 320 (L/14@336, 577 tokens) the
+    // 32x32x16 kernel with 12 waves, one 32-row block each (2157 us per 1000-frame chunk
+    // against 2392 for attention_res_kernel).  A/B variants (MICLIP_ATTN_VAR): 1 res 8 waves
+    // x 1 tile, 2 res 8 waves x 2 tiles, 3 res 16 waves, 4 r32 8 waves x 2 blocks, 5 r32
+    // 12 waves, 6 / 7 r32 12 waves with a start stagger of 1 / 2 quarter workgroup times,
+    // 8 / 9 r32 timing probes (no K/V load / no exponentials: wrong results)
 #if MICLIP_AB
     const char* ve = std::getenv("MICLIP_ATTN_VAR");   // A/B
     int var = ve ? std::atoi(ve) : 0;
 #else
     int var = 0;
 #endif
-    if (var < 1 || var > 9) var = S > 320 ? 2 : 1;
-    const void* fns[10] = {nullptr,
-                           (const void*)attention_res_kernel<8, false>,
-                           (const void*)attention_res_kernel<8, true>,
-                           (const void*)attention_res_kernel<16, false>,
-                           (const void*)attention_r32_kernel<8, true>,
-                           (const void*)attention_r32_kernel<12, false>,
-                           (const void*)attention_r32_kernel<12, false>,
-                           (const void*)attention_r32_kernel<12, false>,
-                           (const void*)attention_r32_kernel<12, false, 2>,
-                           (const void*)attention_r32_kernel<12, false, 1>};
-    static bool attr_set[10] = {false, false, false, false, false, false, false, false, false, false};
-    if (!attr_set[var]) {
-      hipError_t e = hipFuncSetAttribute(fns[var], hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      if (e != hipSuccess) return e;
-      attr_set[var] = true;
-    }
+    if (var < 1 || var > 9) var = S > 320 ? 5 : 1;
     const int64_t rp = ((int64_t)B * S + 1) & ~1;
-    // a quarter of one workgroup's time (~8.8 us at S = 577, scaling as S^2) in 100 MHz ticks
-    const int quarter = S * S / 378;
-    if (var == 1) hipLaunchKernelGGL((attention_res_kernel<8, false>), grid, dim3(512), lds, s, qkv, out, S, W, H, q8, qs, rp);
-    else if (var == 2) hipLaunchKernelGGL((attention_res_kernel<8, true>), grid, dim3(512), lds, s, qkv, out, S, W, H, q8, qs, rp);
-    else if (var == 3) hipLaunchKernelGGL((attention_res_kernel<16, false>), grid, dim3(1024), lds, s, qkv, out, S, W, H, q8, qs, rp);
-    else if (var == 4) hipLaunchKernelGGL((attention_r32_kernel<8, true>), grid, dim3(512), lds, s, qkv, out, S, W, H, q8, qs, rp, 0);
-    else if (var == 5) hipLaunchKernelGGL((attention_r32_kernel<12, false>), grid, dim3(768), lds, s, qkv, out, S, W, H, q8, qs, rp, 0);
-    else if (var == 6) hipLaunchKernelGGL((attention_r32_kernel<12, false>), grid, dim3(768), lds, s, qkv, out, S, W, H, q8, qs, rp, quarter);
-    else if (var == 7) hipLaunchKernelGGL((attention_r32_kernel<12, false>), grid, dim3(768), lds, s, qkv, out, S, W, H, q8, qs, rp, 2 * quarter);
+    auto set_lds = [&](const void* fn, int slot) -> hipError_t {
+      static bool attr_set[10] = {false, false, false, false, false, false, false, false, false, false};
+      if (attr_set[slot]) return hipSuccess;
+      hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      if (e == hipSuccess) attr_set[slot] = true;
+      return e;
+    };
+    hipError_t e = hipSuccess;
+#define ATT_LAUNCH(SLOT, KERNEL, THREADS, ...)                                  \
+  {                                                                             \
+    if ((e = set_lds((const void*)KERNEL, SLOT)) != hipSuccess) return e;       \
+    hipLaunchKernelGGL(KERNEL, grid, dim3(THREADS), lds, s, __VA_ARGS__);       \
+  }
+    if (var == 1) ATT_LAUNCH(1, (attention_res_kernel<8, false>), 512, qkv, out, S, W, H, q8, qs, rp)
+    else if (var == 5) ATT_LAUNCH(5, (attention_r32_kernel<12, false>), 768, qkv, out, S, W, H, q8, qs, rp, 0)
 #if MICLIP_AB
-    else if (var == 8) hipLaunchKernelGGL((attention_r32_kernel<12, false, 2>), grid, dim3(768), lds, s, qkv, out, S, W, H, q8, qs, rp, 0);
-    else hipLaunchKernelGGL((attention_r32_kernel<12, false, 1>), grid, dim3(768), lds, s, qkv, out, S, W, H, q8, qs, rp, quarter);
+    else if (var == 2) ATT_LAUNCH(2, (attention_res_kernel<8, true>), 512, qkv, out, S, W, H, q8, qs, rp)
+    else if (var == 3) ATT_LAUNCH(3, (attention_res_kernel<16, false>), 1024, qkv, out, S, W, H, q8, qs, rp)
+    else if (var == 4) ATT_LAUNCH(4, (attention_r32_kernel<8, true>), 512, qkv, out, S, W, H, q8, qs, rp, 0)
+    else if (var == 6 || var == 7)
+      ATT_LAUNCH(var, (attention_r32_kernel<12, false>), 768, qkv, out, S, W, H, q8, qs, rp, (var - 5) * (S * S / 378))
+    else if (var == 8) ATT_LAUNCH(8, (attention_r32_kernel<12, false, 2>), 768, qkv, out, S, W, H, q8, qs, rp, 0)
+    else ATT_LAUNCH(9, (attention_r32_kernel<12, false, 1>), 768, qkv, out, S, W, H, q8, qs, rp, 0)
+#else
+    else return hipErrorNotSupported;
 #endif
+#undef ATT_LAUNCH
     return hipGetLastError();
   }
 #if MICLIP_AB

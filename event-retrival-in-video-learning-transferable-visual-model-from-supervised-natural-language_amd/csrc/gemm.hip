@@ -929,6 +929,7 @@ hipError_t launch_ab(const GemmArgs& a, hipStream_t s) {
     ga.ngroup = v == 131 ? -1 : v - 130;
     return gemm_8q(ga, EPI, s, cu_count(), 0);
   }
+  if (v == 125 && bf16_out && gemm_8q_ok(a)) return gemm_8q(a, EPI, s, cu_count(), 10);   // whole-row epilogue stores
   if (v >= 120 && v <= 124 && bf16_out) {   // 256 x 128 tiles, deferred epilogue (v98 where it does not apply)
     if (gemm_8r_ok(a)) return gemm_8r(a, EPI, s, cu_count(), v - 120);
     v = 98;

@@ -67,6 +67,7 @@ constexpr int BUF = 4 * HALF;         // 64 KB K-tile buffer
 constexpr int H_A0 = 0, H_B0 = 1, H_B1 = 2, H_A1 = 3;
 // flags
 constexpr int F_GLDS = 1;   // flat global_load_lds with per-DMA address math (gemm_8p's) instead of descriptors
+constexpr int F_FULL = 2;   // epilogue stores of 8 whole 128-B rows (lane pairs fr, fr ^ 8 swap halves by DPP)
 
 __device__ __forceinline__ f32x2 quick_gelu2_8q(f32x2 v) {
   const f32x2 t = v * (f32x2){-2.45546696f, -2.45546696f};   // -1.702 * log2(e)
@@ -238,6 +239,11 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
   typedef unsigned int u32x4_8q __attribute__((ext_vector_type(4)));
   const uint32_t voO = (uint32_t)(((wr * 128 + fr) * a.ldo + wc * 64 + (g & 1) * 16 + (g >> 1) * 8) * 2);
   const uint32_t blkO = (uint32_t)(16 * a.ldo * 2);
+  // F_FULL: store 1 covers rows 0-7 of the 16-row block, store 2 rows 8-15, each row's 64
+  // columns whole: lane (fr < 8) keeps its p = 0 piece of row fr and takes the p = 0 piece of
+  // row fr + 8 for store 2; lane (fr >= 8) takes the p = 1 piece of row fr - 8 for store 1
+  const uint32_t voF = (uint32_t)(((wr * 128 + (fr & 7)) * a.ldo + wc * 64 + 8 * ((g & 1) * 2 + (g >> 1)) + 32 * (fr >> 3)) * 2);
+  const uint32_t rows8 = (uint32_t)(8 * a.ldo * 2);
   auto epilogue = [&]() {
     if (ABL == 4) {
 #pragma unroll
@@ -261,6 +267,7 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
         (void*)((uint16_t*)a.out + (int64_t)pm0 * a.ldo + pn0), (short)0, rows * (int)a.ldo * 2, 0x00020000);
 #pragma unroll
     for (int mi = 0; mi < 8; ++mi) {
+      u32x4_8q dp[2];
 #pragma unroll
       for (int p = 0; p < 2; ++p) {
         uint2 pk[2];
@@ -278,9 +285,25 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
         const auto sx = __builtin_amdgcn_permlane16_swap(pk[0].x, pk[1].x, false, false);
         const auto sy = __builtin_amdgcn_permlane16_swap(pk[0].y, pk[1].y, false, false);
         const u32x4_8q d = {sx[0], sy[0], sx[1], sy[1]};
+        dp[p] = d;
+        if (F & F_FULL) continue;
         if (ABL == 10) asm volatile("" ::"v"(d));   // stamp probe without the stores
         else if (p == 0) __builtin_amdgcn_raw_buffer_store_b128(d, rsO, voO + mi * blkO, 0, 0);
         else __builtin_amdgcn_raw_buffer_store_b128(d, rsO, voO + mi * blkO + 64, 0, 0);
+      }
+      if (F & F_FULL) {
+        const bool top = fr < 8;
+        u32x4_8q s1, s2;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          // row_ror:8 inside each 16-lane row: lane fr takes lane fr ^ 8's value
+          const uint32_t r0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)dp[0][e], 0x128, 0xf, 0xf, false);
+          const uint32_t r1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)dp[1][e], 0x128, 0xf, 0xf, false);
+          s1[e] = top ? dp[0][e] : r1;
+          s2[e] = top ? r0 : dp[1][e];
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(s1, rsO, voF + mi * blkO, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(s2, rsO, voF + mi * blkO + rows8, 0, 0);
       }
     }
   };
@@ -446,7 +469,7 @@ int gemm_8q_ok(const GemmArgs& a) {
 }
 
 // mode: 0 = default (descriptors), 2 = no-MFMA probe,
-// 3 = flat global_load_lds addressing, 4 = no-epilogue probe
+// 3 = flat global_load_lds addressing, 4 = no-epilogue probe, 10 = whole-row epilogue stores (F_FULL)
 // Tile order: n-tiles walked in groups of ng over all m-tiles, so each XCD's
 // L2 (4 MB) keeps its group's weight panel (ng x 256 x K bf16) while the
 // activation rows stream through: chosen when the tiles split into >= 6-wide
@@ -476,6 +499,7 @@ hipError_t gemm_8q(const GemmArgs& a0, int epi, hipStream_t s, int cus, int mode
 #if MICLIP_AB   // ablation / stamp probes: A/B build only
 #define L8Q_ALL(E)                   \
   if (mode == 0) L8Q(E, 0, 0);       \
+  else if (mode == 10) L8Q(E, 0, F_FULL); \
   else if (mode == 2) L8Q(E, 2, 0);  \
   else if (mode == 3) L8Q(E, 0, F_GLDS); \
   else if (mode == 4) L8Q(E, 4, 0);  \

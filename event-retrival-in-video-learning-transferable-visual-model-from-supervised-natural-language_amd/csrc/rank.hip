@@ -178,7 +178,7 @@ __global__ __launch_bounds__(64 * NW) void rank_stream(const void* __restrict__ 
       for (int p = 1; p < KC; ++p) kth = (p == k - 1) ? (uint32_t)(L[p] >> 32) : kth;
       const uint32_t other = (uint32_t)__shfl_xor((int)kth, 32, 64);
       kth = kth > other ? kth : other;
-      if (h == 0 && qvalid && kth > tq_thr) atomicMax(&tau[r], kth);
+      if (h == 0 && qvalid && kth > tq_thr) tau_max(&tau[r], kth);
     }
     __builtin_amdgcn_wave_barrier();
     acc = f32x16{};
@@ -265,11 +265,11 @@ __global__ __launch_bounds__(64 * NW) void rank_stream(const void* __restrict__ 
 // instead of sitting between the wait and the MFMAs; the DMA lookahead is then
 // PF - 1 chunks beyond the one being read.
 // Dynamic LDS of rank_reg<.., NB, ..>: the ring [NW = 4][NB][4 KB], the per-wave
-// row norms [4][32] f32 and tau [RQ] u32.  The launcher sizes the allocation
+// row norms [4][32] f32, tau [RQ] u32 and the lead keys [RQ][8].  The launcher sizes the allocation
 // with this same function: a kernel whose ring is larger than the allocation
 // puts its norms (and the last wave's slots) past the end of the workgroup's
 // LDS, where reads return zero — every score comes out 0.
-constexpr size_t rank_reg_lds_bytes(int NB) { return (size_t)4 * NB * (32 * 128) + 4 * 32 * 4 + RQ * 4; }
+constexpr size_t rank_reg_lds_bytes(int NB) { return (size_t)4 * NB * (32 * 128) + 4 * 32 * 4 + RQ * 4 + LEAD_LDS; }
 
 template <int D, int NB = 8, int PF = 6, bool NOMFMA = false, bool ILV = false, bool PIPE = false, int DT = 0>
 __global__ __launch_bounds__(256) void rank_reg(const void* __restrict__ corpus, int64_t N,
@@ -304,6 +304,7 @@ __global__ __launch_bounds__(256) void rank_reg(const void* __restrict__ corpus,
   char* ring = smem;                       // [NW][NB][SLOT]
   float* nrm_all = (float*)(smem + NW * NB * SLOT);
   uint32_t* tau = (uint32_t*)(nrm_all + NW * 32);
+  uint32_t* lead = tau + RQ;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, h = lane >> 5;
@@ -327,6 +328,7 @@ __global__ __launch_bounds__(256) void rank_reg(const void* __restrict__ corpus,
       }
   }
   if (tid < RQ) tau[tid] = 0u;
+  lead[tid] = 0u;   // 256 = 32 x 8
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
@@ -383,6 +385,7 @@ __global__ __launch_bounds__(256) void rank_reg(const void* __restrict__ corpus,
   uint64_t L[KC];
 #pragma unroll
   for (int p = 0; p < KC; ++p) L[p] = 0ull;
+  uint32_t kk = 0u;   // running k-th key of this query's lists (own threshold)
 
   auto read_frag = [&](int slot, float4 (&v)[4]) {
     const char* src = wring + slot * SLOT + rbase;
@@ -463,8 +466,10 @@ __global__ __launch_bounds__(256) void rank_reg(const void* __restrict__ corpus,
       __builtin_amdgcn_wave_barrier();
       const int tr0 = (sid + sstep * ct) * 32;
       const uint32_t tq_thr = tau[r];
-      const uint32_t own = (uint32_t)(L[KC - 1] >> 32);
-      const uint32_t thr = own > tq_thr ? own : tq_thr;
+      const uint32_t own = kk;   // the query's two half-lists' k-th: a lower bound of its k-th
+      const uint32_t thr0 = own > tq_thr ? own : tq_thr;
+      const uint32_t lb = lead_min(lead, r);
+      const uint32_t thr = lb > thr0 ? lb : thr0;
       uint64_t c[16];
       bool any = false;
       uint32_t okm = 0u;
@@ -481,12 +486,14 @@ __global__ __launch_bounds__(256) void rank_reg(const void* __restrict__ corpus,
       }
       if (__any(any)) {
         list_update16(L, c, okm);
+        lead_publish(lead, r, 2 * wave + h, (uint32_t)(L[1] >> 32));
         uint32_t kth = (uint32_t)(L[0] >> 32);
 #pragma unroll
         for (int p = 1; p < KC; ++p) kth = (p == k - 1) ? (uint32_t)(L[p] >> 32) : kth;
         const uint32_t other = (uint32_t)__shfl_xor((int)kth, 32, 64);
         kth = kth > other ? kth : other;
-        if (h == 0 && qvalid && kth > tq_thr) atomicMax(&tau[r], kth);
+        kk = kth;
+        if (h == 0 && qvalid && kth > tq_thr) tau_max(&tau[r], kth);
       }
       __builtin_amdgcn_wave_barrier();
     }

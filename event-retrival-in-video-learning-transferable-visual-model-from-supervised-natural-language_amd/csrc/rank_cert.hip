@@ -59,11 +59,13 @@ constexpr int CKC = 16;   // candidates per query
 __device__ __forceinline__ float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 
-// the ring, per-wave row reciprocals [4][32], tau [32]
+// the ring, per-wave row reciprocals [4][32], tau [32], the lead keys [32][8]
 constexpr int CNB = 8, CPF = 6;
-constexpr size_t cert_lds_bytes() { return (size_t)4 * CNB * 4096 + 4 * 32 * 4 + 32 * 4; }
+constexpr size_t cert_lds_bytes() { return (size_t)4 * CNB * 4096 + 4 * 32 * 4 + 32 * 4 + LEAD_LDS; }
 
-template <int DT>
+// ABL (A/B timing probes, wrong results): 1 = no Gram MFMAs (unit norms), 2 = no MFMAs at
+// all, 3 = no list update
+template <int DT, int ABL = 0>
 __global__ __launch_bounds__(256) void rank_cert_kernel(const void* __restrict__ corpus, int64_t N,
                                                         const float* __restrict__ queries, int64_t Q, int kc,
                                                         int64_t rows_per_wg, int norm_mode, int nan_first, FoldWs f,
@@ -84,6 +86,7 @@ __global__ __launch_bounds__(256) void rank_cert_kernel(const void* __restrict__
   char* ring = smem;
   float* nrm_all = (float*)(smem + NW * NB * SLOT);
   uint32_t* tau = (uint32_t*)(nrm_all + NW * 32);
+  uint32_t* lead = tau + 32;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, h = lane >> 5;
@@ -108,6 +111,7 @@ __global__ __launch_bounds__(256) void rank_cert_kernel(const void* __restrict__
     }
   }
   if (tid < FQ) tau[tid] = 0u;
+  lead[tid] = 0u;   // 256 = 32 x 8
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
@@ -168,6 +172,7 @@ __global__ __launch_bounds__(256) void rank_cert_kernel(const void* __restrict__
   uint64_t L[KC];
 #pragma unroll
   for (int p = 0; p < KC; ++p) L[p] = 0ull;
+  uint32_t kk = 0u;   // running k-th key of this query's lists (own threshold)
   bool bad = false;
 
   if (my_tiles > 0) {
@@ -185,7 +190,8 @@ __global__ __launch_bounds__(256) void rank_cert_kernel(const void* __restrict__
     }
     for (int ct = 0; ct < my_tiles; ++ct) {
       f32x16 acc = f32x16{};
-      f32x16 gram = f32x16{};   // bf16 rows
+      f32x16 gram = ABL == 1 ? f32x16{1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f}
+                             : f32x16{};   // bf16 rows
       float ss = 0.f;           // f32 rows (this lane's half of row r)
 #pragma unroll
       for (int j = 0; j < NCH; ++j) {
@@ -206,11 +212,15 @@ __global__ __launch_bounds__(256) void rank_cert_kernel(const void* __restrict__
 #pragma unroll
           for (int t = 0; t < 4; ++t) {
             const bf16x8 av = __builtin_bit_cast(bf16x8, v[t]);
+            if (ABL == 2) {
+              asm volatile("" ::"v"(av));
+              continue;
+            }
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, q1[4 * j + t], acc, 0, 0, 0);
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, q2[4 * j + t], acc, 0, 0, 0);
             // the tile's Gram matrix: the A fragment is also the B fragment of the
             // transposed rows, so its diagonal is each row's sum of squares
-            gram = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, av, gram, 0, 0, 0);
+            if (ABL != 1) gram = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, av, gram, 0, 0, 0);
           }
         } else {
 #pragma unroll
@@ -263,8 +273,10 @@ __global__ __launch_bounds__(256) void rank_cert_kernel(const void* __restrict__
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_wave_barrier();
       const uint32_t tq_thr = tau[r];
-      const uint32_t own = (uint32_t)(L[KC - 1] >> 32);
-      const uint32_t thr = own > tq_thr ? own : tq_thr;
+      const uint32_t own = kk;   // the query's two half-lists' k-th: a lower bound of its k-th
+      const uint32_t thr0 = own > tq_thr ? own : tq_thr;
+      const uint32_t lb = lead_min(lead, r);
+      const uint32_t thr = lb > thr0 ? lb : thr0;
       uint64_t c[16];
       bool any = false;
       uint32_t okm = 0u;
@@ -283,14 +295,14 @@ __global__ __launch_bounds__(256) void rank_cert_kernel(const void* __restrict__
         okm |= ok ? 1u << rg : 0u;
       }
       bad |= nonfin != 0u;
-      if (__any(any)) {
+      if (ABL != 3 && __any(any)) {
         list_update16(L, c, okm);
-        uint32_t kth = (uint32_t)(L[0] >> 32);
-#pragma unroll
-        for (int p = 1; p < KC; ++p) kth = (p == kc - 1) ? (uint32_t)(L[p] >> 32) : kth;
+        lead_publish(lead, r, 2 * wave + h, (uint32_t)(L[1] >> 32));
+        uint32_t kth = (uint32_t)(L[KC - 1] >> 32);   // k = kc = KC candidates
         const uint32_t other = (uint32_t)__shfl_xor((int)kth, 32, 64);
         kth = kth > other ? kth : other;
-        if (h == 0 && qvalid && kth > tq_thr) atomicMax(&tau[r], kth);
+        kk = kth;
+        if (h == 0 && qvalid && kth > tq_thr) tau_max(&tau[r], kth);
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the norm reads, before the slots are rewritten
       __builtin_amdgcn_wave_barrier();
@@ -368,14 +380,19 @@ hipError_t rank_cert_topk(const void* corpus, int64_t N, int dt, const float* q,
   if ((e = fold_zero(fu, s)) != hipSuccess) return e;
   const size_t lds = cert_lds_bytes();
   const dim3 grid((unsigned)((Q + FQ - 1) / FQ), (unsigned)nwg_used);   // (query blocks, row blocks)
-  const void* fn = dt == 0 ? (const void*)rank_cert_kernel<0> : (const void*)rank_cert_kernel<1>;
-  if ((e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)) != hipSuccess) return e;
-  if (dt == 0)
-    hipLaunchKernelGGL(rank_cert_kernel<0>, grid, dim3(256), lds, s, corpus, N, q, Q, CKC, rpw, norm_mode, nan_first,
-                       fu, unsafe, m_s, m_i);
-  else
-    hipLaunchKernelGGL(rank_cert_kernel<1>, grid, dim3(256), lds, s, corpus, N, q, Q, CKC, rpw, norm_mode, nan_first,
-                       fu, unsafe, m_s, m_i);
+#if MICLIP_AB
+  const char* ab = getenv("MICLIP_RANK_CERT_ABL");   // timing probes (wrong results)
+  const int abl = ab ? atoi(ab) : 0;
+#endif
+  auto fn = dt == 0 ? rank_cert_kernel<0> : rank_cert_kernel<1>;
+#if MICLIP_AB
+  if (abl == 1) fn = dt == 0 ? rank_cert_kernel<0, 1> : rank_cert_kernel<1, 1>;
+  else if (abl == 2) fn = dt == 0 ? rank_cert_kernel<0, 2> : rank_cert_kernel<1, 2>;
+  else if (abl == 3) fn = dt == 0 ? rank_cert_kernel<0, 3> : rank_cert_kernel<1, 3>;
+#endif
+  if ((e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)) != hipSuccess)
+    return e;
+  hipLaunchKernelGGL(fn, grid, dim3(256), lds, s, corpus, N, q, Q, CKC, rpw, norm_mode, nan_first, fu, unsafe, m_s, m_i);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   float d_rel, d_abs;
   rank_cert_delta(dt, d_rel, d_abs);

@@ -102,6 +102,40 @@ __device__ __forceinline__ void merge16_desc(uint64_t (&L)[16], const uint64_t (
     }
 }
 
+// The shared threshold's LDS atomic max, as inline asm: hipcc orders a
+// compiler-visible LDS atomic after every LDS-DMA it cannot prove disjoint, i.e.
+// an s_waitcnt vmcnt(0) ahead of it, and in the streaming kernels that drained
+// the whole DMA ring (PF chunks in flight) each time a wave raised tau.  tau
+// shares no bytes with the ring.
+__device__ __forceinline__ void tau_max(uint32_t* p, uint32_t v) {
+  const uint32_t a = (uint32_t)(uintptr_t)(LDS_AS uint32_t*)p;
+  asm volatile("ds_max_u32 %0, %1" ::"v"(a), "v"(v) : "memory");
+}
+
+// Lead bound, the streaming kernels' second threshold.  A workgroup holds 8
+// lists per query (4 waves x 2 lane halves) over disjoint rows; each publishes
+// its 2nd-best key in lead[q][list].  Then 8 lists x 2 rows = 16 distinct rows
+// score at least the smallest of the 8 keys, a lower bound of the query's
+// 16th-best key (so of its k-th for every k <= 16): far tighter than one list's
+// 16th-best (tau) while each list has seen an eighth of the rows, so fewer
+// candidates reach the list update.  LDS: [32 queries][8] u32, zeroed at entry;
+// inline asm so that hipcc adds no LDS-DMA ordering wait.
+constexpr size_t LEAD_LDS = 32 * 8 * 4;
+__device__ __forceinline__ uint32_t lead_min(const uint32_t* lead, int r) {
+  typedef unsigned int u32x4l __attribute__((ext_vector_type(4)));
+  const uint32_t a = (uint32_t)(uintptr_t)(LDS_AS const uint32_t*)(lead + r * 8);
+  u32x4l x, y;
+  asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:16\n\ts_waitcnt lgkmcnt(0)"
+               : "=&v"(x), "=&v"(y) : "v"(a) : "memory");
+  const uint32_t m0 = min(min(x[0], x[1]), min(x[2], x[3]));
+  const uint32_t m1 = min(min(y[0], y[1]), min(y[2], y[3]));
+  return min(m0, m1);
+}
+__device__ __forceinline__ void lead_publish(uint32_t* lead, int r, int list, uint32_t key) {
+  const uint32_t a = (uint32_t)(uintptr_t)(LDS_AS uint32_t*)(lead + r * 8 + list);
+  asm volatile("ds_write_b32 %0, %1" ::"v"(a), "v"(key) : "memory");
+}
+
 // A tile's candidates c[0..15] (0 = none; m: the non-empty ones) into the
 // sorted (desc) top-16 list L.  Once the threshold has settled a lane has 0 or
 // 1 candidate per tile, and a full bitonic sort + merge (~1000 instructions of
@@ -112,9 +146,19 @@ __device__ __forceinline__ void merge16_desc(uint64_t (&L)[16], const uint64_t (
 // no-op), for as many rounds as the lane with the most; otherwise sort + merge.
 // Same final list either way: the packed keys are unique.
 __device__ __forceinline__ void list_update16(uint64_t (&L)[16], uint64_t (&c)[16], uint32_t m) {
-  if (__any(__builtin_popcount(m) > 6)) {
+  const int pc = __builtin_popcount(m);
+  if (__any(pc > 6)) {
     bitonic_sort16_desc(c);
     merge16_desc(L, c);
+    return;
+  }
+  if (__all(pc <= 1)) {   // the common case: one insertion, the entry is the OR of the slots
+    uint64_t e = 0ull;
+#pragma unroll
+    for (int rg = 0; rg < 16; ++rg) e |= c[rg];
+#pragma unroll
+    for (int p = 15; p > 0; --p) L[p] = e > L[p - 1] ? L[p - 1] : (e > L[p] ? e : L[p]);
+    L[0] = e > L[0] ? e : L[0];
     return;
   }
   while (__any(m != 0u)) {

@@ -99,6 +99,7 @@ __global__ __launch_bounds__(256) void rank_mirror_kernel(const uint16_t* __rest
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* ring = smem;   // [NW][NB][SLOT]
   uint32_t* tau = (uint32_t*)(smem + NW * NB * SLOT);
+  uint32_t* lead = tau + MQ;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, h = lane >> 5;
@@ -123,6 +124,7 @@ __global__ __launch_bounds__(256) void rank_mirror_kernel(const uint16_t* __rest
     }
   }
   if (tid < MQ) tau[tid] = 0u;
+  lead[tid] = 0u;   // 256 = 32 x 8
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
@@ -174,6 +176,7 @@ __global__ __launch_bounds__(256) void rank_mirror_kernel(const uint16_t* __rest
   uint64_t L[KC];
 #pragma unroll
   for (int p = 0; p < KC; ++p) L[p] = 0ull;
+  uint32_t kk = 0u;   // running k-th key of this query's lists (own threshold)
 
   auto read_frag = [&](int slot, f32x4v (&v)[4]) {
     const char* src = wring + slot * SLOT + rbase;
@@ -220,8 +223,10 @@ __global__ __launch_bounds__(256) void rank_mirror_kernel(const uint16_t* __rest
       }
       const int tr0 = (sid + sstep * ct) * 32;
       const uint32_t tq_thr = tau[r];
-      const uint32_t own = (uint32_t)(L[KC - 1] >> 32);
-      const uint32_t thr = own > tq_thr ? own : tq_thr;
+      const uint32_t own = kk;   // the query's two half-lists' k-th: a lower bound of its k-th
+      const uint32_t thr0 = own > tq_thr ? own : tq_thr;
+      const uint32_t lb = lead_min(lead, r);
+      const uint32_t thr = lb > thr0 ? lb : thr0;
       uint64_t c[16];
       bool any = false;
       uint32_t okm = 0u;
@@ -237,12 +242,12 @@ __global__ __launch_bounds__(256) void rank_mirror_kernel(const uint16_t* __rest
       }
       if (__any(any)) {
         list_update16(L, c, okm);
-        uint32_t kth = (uint32_t)(L[0] >> 32);
-#pragma unroll
-        for (int p = 1; p < KC; ++p) kth = (p == k - 1) ? (uint32_t)(L[p] >> 32) : kth;
+        lead_publish(lead, r, 2 * wave + h, (uint32_t)(L[1] >> 32));
+        uint32_t kth = (uint32_t)(L[KC - 1] >> 32);   // k = kc = KC candidates
         const uint32_t other = (uint32_t)__shfl_xor((int)kth, 32, 64);
         kth = kth > other ? kth : other;
-        if (h == 0 && qvalid && kth > tq_thr) atomicMax(&tau[r], kth);
+        kk = kth;
+        if (h == 0 && qvalid && kth > tq_thr) tau_max(&tau[r], kth);
       }
       __builtin_amdgcn_wave_barrier();
     }
@@ -399,7 +404,7 @@ namespace miclip {
 template <int D, bool SPLIT>
 static hipError_t launch_mirror(const uint16_t* mirror, int64_t N, const float* q, int64_t Q, int kc, int nf,
                                 void* fws, float* out_s, int64_t* out_i, int64_t nwg, hipStream_t s) {
-  const size_t lds = (size_t)4 * 8 * 4096 + MQ * 4;
+  const size_t lds = (size_t)4 * 8 * 4096 + MQ * 4 + LEAD_LDS;
   const int64_t rpw = ((N + nwg - 1) / nwg + 127) / 128 * 128;   // whole tiles per wave round
   // MICLIP_MIRROR_VAR (A/B): 1 fragments read after the wait (no PIPE), 2 seven chunks in
   // flight, 3 interleaved tiles

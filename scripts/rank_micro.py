@@ -20,14 +20,17 @@ from miclip import retrieval  # noqa: E402
 # exact: MICLIP_RANK_CERT=0, the exact pass alone
 VARIANTS = {"default": {}, "exact": {"MICLIP_RANK_CERT": "0"},
             "stream12": {"MICLIP_RANK_REG": "0", "MICLIP_RANK_NW": "12", "MICLIP_RANK_CERT": "0"},
-            "nomfma": {"MICLIP_RANK_PROBE": "1", "MICLIP_RANK_CERT": "0"}}
+            "nomfma": {"MICLIP_RANK_PROBE": "1", "MICLIP_RANK_CERT": "0"},
+            # certified-pass timing probes (wrong results): no Gram MFMAs, no MFMAs, no list update
+            "c_nogram": {"MICLIP_RANK_CERT_ABL": "1"}, "c_nomfma": {"MICLIP_RANK_CERT_ABL": "2"},
+            "c_nolist": {"MICLIP_RANK_CERT_ABL": "3"}}
 SHAPES = [(125_000, 512, 32, torch.float32), (1_000_000, 512, 32, torch.float32),
-          (1_000_000, 512, 32, torch.bfloat16), (1_000_000, 768, 32, torch.float32), (10_000, 512, 32, torch.float32)]
+          (1_000_000, 512, 32, torch.bfloat16), (1_000_000, 768, 32, torch.float32)]
 
 
 def setenv(v):
     for k in ("MICLIP_RANK_STAGE1", "MICLIP_RANK_NW", "MICLIP_RANK_REG", "MICLIP_RANK_PROBE", "MICLIP_RANK_ILV",
-              "MICLIP_RANK_PIPE", "MICLIP_RANK_SEED", "MICLIP_RANK_CERT"):
+              "MICLIP_RANK_PIPE", "MICLIP_RANK_SEED", "MICLIP_RANK_CERT", "MICLIP_RANK_CERT_ABL"):
         os.environ.pop(k, None)
     os.environ.update(VARIANTS[v])
 
@@ -47,7 +50,7 @@ def main():
             s, i = retrieval.rank_topk(corpus, q, 10)
             if ref is None:
                 ref = (s.clone(), i.clone())
-            elif "nomfma" not in v:   # timing probe: no scores
+            elif "nomfma" not in v and not v.startswith("c_"):   # timing probes: no scores
                 assert torch.equal(i, ref[1]) and torch.equal(s, ref[0]), (name, v)
         times = {v: [] for v in VARIANTS}
         stream = torch.cuda.current_stream(dev)

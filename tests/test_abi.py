@@ -110,6 +110,32 @@ def test_mirror_certificate_delta_covers_worst_case():
             assert da.value >= np.sqrt(D) * 2.0 ** -25
 
 
+def test_cert_delta_covers_worst_case():
+    """The certified rank pass's per-query bound (rank_cert.hip rank_cert_delta)
+    against the analytic worst case per unit |q| at D = 512: the query split into
+    bf16 q1 + q2 (residual 2^-18) and, f32 rows, the row split c_hi + c_lo plus
+    the dropped c_lo q2 (2^-18 each); the bf16 MFMA path's f32 accumulation of
+    P = 2 D / 3 D products (gamma_P, doubled for internal truncation) and the
+    exact chain's gamma_D; the two sums of squares (gamma_D relatively, halved by
+    the square root) with the sqrt / reciprocal roundings; the subnormal floor."""
+    from miclip import _native
+    L = _native.lib()
+    fn = L.mi_debug_cert_delta
+    fn.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]
+    u, D = 2.0 ** -24, 512
+
+    def gamma(n):
+        return n * u / (1 - n * u)
+
+    for dt, P, split in ((0, 3 * D, 3 * 2.0 ** -18), (1, 2 * D, 2.0 ** -18)):
+        dr, da = ctypes.c_float(), ctypes.c_float()
+        assert fn(dt, ctypes.byref(dr), ctypes.byref(da)) == 0
+        worst = split + 2 * gamma(P) + gamma(D) + gamma(D) + 4 * u + 2 * np.sqrt(D) * 2.0 ** -25
+        assert dr.value >= worst, (dt, dr.value, worst)
+        assert da.value >= np.sqrt(D) * 2.0 ** -25
+    assert fn(2, ctypes.byref(ctypes.c_float()), ctypes.byref(ctypes.c_float())) != 0
+
+
 def test_host_gather_concatenates_pieces():
     """mi_host_gather (host only): pieces of bytes objects, at offsets, in order,
     on 1 and 16 threads, byte ranges split across threads."""
