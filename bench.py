@@ -134,19 +134,24 @@ def kernel_timing(model, cfg, chunk, reps=20):
     return res
 
 
-def pmc_traffic(shape):
+def pmc_traffic(shape, fp8=False):
     """HBM bytes per launch of the GEMM at `shape` [M, N, K] from the newest
     committed PMC summary (profiles/*_gemm_traffic.json, made by
     scripts/gpu_traffic.sh + scripts/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE,
-    the gfx950 corrections of MI355X_MICROARCH.md "HBM"), with the MFMA-busy
-    fraction of the same summary's GRBM/SQ pass.  None if absent."""
+    the gfx950 corrections of MI355X_MICROARCH.md "HBM"; MX-fp8:
+    profiles/*_fp8_gemm_traffic.json from scripts/gpu_fp8_traffic.sh), with the
+    MFMA-busy fraction of the same summary's GRBM/SQ pass.  None if absent."""
     import glob
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_gemm_traffic.json")), reverse=True):
+    pat = "*_fp8_gemm_traffic.json" if fp8 else "*_gemm_traffic.json"
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", pat)), reverse=True):
+        if not fp8 and f.endswith("_fp8_gemm_traffic.json"):
+            continue
         try:
-            for v in json.load(open(f)).values():
+            d = json.load(open(f))
+            for v in ([d] if fp8 else d.values()):
                 if list(v["shape"]) == list(shape):
                     return v["traffic_bytes"], os.path.relpath(f, ROOT), v.get("mfma_busy")
-        except (OSError, ValueError, KeyError):
+        except (OSError, ValueError, KeyError, AttributeError):
             continue
     return None, None, None
 
@@ -548,17 +553,17 @@ def main():
             fl = 2.0 * M * 4 * cfg.vision_width * cfg.vision_width
             ach = fl / (dom["us"] * 1e-6) / 1e12
             shape = [M, 4 * cfg.vision_width, cfg.vision_width]
-            traffic, tsrc, busy = pmc_traffic(shape)
             fp8 = args.weights == "fp8"
+            traffic, tsrc, busy = pmc_traffic(shape, fp8)
             peak = FP8_PEAK_TFLOPS if fp8 else BF16_PEAK_TFLOPS
             eb = 1 if fp8 else 2            # operand element bytes (fp8 adds 1/64 B of scales per element)
             roof = {"bound": "mfma",
                     "kernel": ("gemm_mx_kernel<EPI_GELU_BF16> (mlp.c_fc + QuickGELU, MX-fp8 operands)" if fp8
                                else "gemm_8q_kernel<EPI_GELU_BF16> (8-phase interleaved persistent, 256x256x64, descriptor DMAs; mlp.c_fc + QuickGELU)"),
                     "achieved": round(ach, 1), "peak": peak, "unit": "TFLOP/s",
-                    "frac": round(ach / peak, 4), "traffic": None if fp8 else traffic,
-                    "traffic_source": None if fp8 else tsrc,
-                    "mfma_busy_pmc": None if fp8 else busy,
+                    "frac": round(ach / peak, 4), "traffic": traffic,
+                    "traffic_source": tsrc,
+                    "mfma_busy_pmc": busy,
                     "algorithmic_bytes": int(eb * (1 + fp8 / 64) * (M * cfg.vision_width + 4 * cfg.vision_width ** 2)
                                              + 2 * M * 4 * cfg.vision_width),
                     "flops_per_launch": fl, "launch_shape": [M, 4 * cfg.vision_width, cfg.vision_width],
