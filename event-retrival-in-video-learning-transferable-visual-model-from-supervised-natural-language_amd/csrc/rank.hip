@@ -473,11 +473,15 @@ __global__ __launch_bounds__(256) void rank_reg(const void* __restrict__ corpus,
       uint64_t c[16];
       bool any = false;
       uint32_t okm = 0u;
+      // the 16 rows' reciprocals: rows (rg & 3) + 8 (rg >> 2) + 4 h are four 16-byte runs
+      f32x4 nv[4];
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4) nv[q4] = *(const f32x4*)(nrm + 8 * q4 + 4 * h);
 #pragma unroll
       for (int rg = 0; rg < 16; ++rg) {
         const int rr = (rg & 3) + 8 * (rg >> 2) + 4 * h;
         const int lr = tr0 + rr;
-        const float sc = norm_mode == 2 ? acc[rg] : acc[rg] * nrm[rr];
+        const float sc = norm_mode == 2 ? acc[rg] : acc[rg] * nv[rg >> 2][rg & 3];
         const uint32_t key = score_key(sc, nan_first);
         const bool ok = qvalid && lr < nrows && key >= thr;
         c[rg] = ok ? (((uint64_t)key << 32) | (uint32_t)~(uint32_t)lr) : 0ull;

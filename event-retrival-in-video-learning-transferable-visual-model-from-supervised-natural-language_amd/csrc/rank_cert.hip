@@ -282,10 +282,14 @@ __global__ __launch_bounds__(256) void rank_cert_kernel(const void* __restrict__
       uint32_t okm = 0u;
       const int vrows = (int)min((int64_t)32, nrows - tr0);   // valid rows of this tile
       uint32_t nonfin = 0u;
+      // the 16 rows' reciprocals: rows (rg & 3) + 8 (rg >> 2) + 4 h are four 16-byte runs
+      f32x4c nv[4];
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4) nv[q4] = *(const f32x4c*)(nrm + 8 * q4 + 4 * h);
 #pragma unroll
       for (int rg = 0; rg < 16; ++rg) {
         const int rr = (rg & 3) + 8 * (rg >> 2) + 4 * h;
-        const float sc = acc[rg] * nrm[rr];
+        const float sc = acc[rg] * nv[rg >> 2][rg & 3];
         const bool rowok = qvalid && rr < vrows;
         nonfin |= (rowok && !(__builtin_fabsf(sc) <= 3.4e38f)) ? 1u : 0u;   // NaN / inf, no branch
         const uint32_t key = score_key(sc, nan_first);

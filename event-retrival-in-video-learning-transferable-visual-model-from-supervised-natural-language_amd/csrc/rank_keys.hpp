@@ -21,11 +21,14 @@
 namespace miclip {
 namespace rankk {
 
+// Branch-free (selects only): in the streaming kernels' per-tile score loop an
+// early return here became an exec-masked branch per score, which also split
+// the row-norm LDS reads into 16 serialised read + wait pairs.
 __device__ __forceinline__ uint32_t score_key(float s, int nan_first) {
-  if (s != s) return nan_first ? 0xFFFFFFFFu : 0u;
-  if (s == 0.0f) s = 0.0f;  // -0 == +0
-  const uint32_t u = __float_as_uint(s);
-  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+  const uint32_t u = __float_as_uint(s == 0.0f ? 0.0f : s);   // -0 == +0
+  const uint32_t key = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+  const uint32_t nan_key = nan_first ? 0xFFFFFFFFu : 0u;
+  return s != s ? nan_key : key;
 }
 
 __device__ __forceinline__ float decode_key(uint32_t bk, int nan_first) {
