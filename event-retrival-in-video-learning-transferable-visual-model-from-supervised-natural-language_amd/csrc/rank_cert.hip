@@ -63,8 +63,12 @@ __device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 
 constexpr int CNB = 8, CPF = 6;
 constexpr size_t cert_lds_bytes() { return (size_t)4 * CNB * 4096 + 4 * 32 * 4 + 32 * 4 + LEAD_LDS; }
 
+// per wave (row block y < 256, wave w): tile-epilogue cycles, tiles, tiles with an update, sort-path
+// updates, multi-candidate insertion updates (ABL 5, A/B build; mi_debug_cert_probe)
+__device__ unsigned long long g_cert_probe[256 * 4 * 5];
+
 // ABL (A/B timing probes, wrong results): 1 = no Gram MFMAs (unit norms), 2 = no MFMAs at
-// all, 3 = no list update
+// all, 3 = no list update; 5 = the epilogue stamp probe (correct results)
 template <int DT, int ABL = 0>
 __global__ __launch_bounds__(256) void rank_cert_kernel(const void* __restrict__ corpus, int64_t N,
                                                         const float* __restrict__ queries, int64_t Q, int kc,
@@ -172,6 +176,8 @@ __global__ __launch_bounds__(256) void rank_cert_kernel(const void* __restrict__
   uint64_t L[KC];
 #pragma unroll
   for (int p = 0; p < KC; ++p) L[p] = 0ull;
+  unsigned long long pr_cyc = 0ull, pr_t0 = 0ull;   // ABL 5 probe
+  unsigned pr_n[4] = {0u, 0u, 0u, 0u};
   uint32_t kk = 0u;   // running k-th key of this query's lists (own threshold)
   bool bad = false;
 
@@ -299,6 +305,12 @@ __global__ __launch_bounds__(256) void rank_cert_kernel(const void* __restrict__
         okm |= ok ? 1u << rg : 0u;
       }
       bad |= nonfin != 0u;
+      if (ABL == 5) {   // stamp probe: cycles of the whole tile epilogue below, updates, sort-path updates
+        pr_t0 = __builtin_amdgcn_s_memtime();
+        pr_n[1] += __any(any) ? 1u : 0u;
+        pr_n[2] += __any(__builtin_popcount(okm) > 6) ? 1u : 0u;
+        pr_n[3] += __all(__builtin_popcount(okm) <= 1) ? 0u : 1u;
+      }
       if (ABL != 3 && __any(any)) {
         list_update16(L, c, okm);
         lead_publish(lead, r, 2 * wave + h, (uint32_t)(L[1] >> 32));
@@ -308,9 +320,20 @@ __global__ __launch_bounds__(256) void rank_cert_kernel(const void* __restrict__
         kk = kth;
         if (h == 0 && qvalid && kth > tq_thr) tau_max(&tau[r], kth);
       }
+      if (ABL == 5) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        pr_cyc += __builtin_amdgcn_s_memtime() - pr_t0;
+        pr_n[0] += 1u;
+      }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the norm reads, before the slots are rewritten
       __builtin_amdgcn_wave_barrier();
     }
+  }
+  if (ABL == 5 && lane == 0 && (int)blockIdx.y < 256) {
+    unsigned long long* o = g_cert_probe + ((int)blockIdx.y * 4 + wave) * 5;
+    o[0] = pr_cyc;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[1 + i] = pr_n[i];
   }
   if (__any(bad) && lane == 0) __hip_atomic_store(unsafe, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -393,6 +416,7 @@ hipError_t rank_cert_topk(const void* corpus, int64_t N, int dt, const float* q,
   if (abl == 1) fn = dt == 0 ? rank_cert_kernel<0, 1> : rank_cert_kernel<1, 1>;
   else if (abl == 2) fn = dt == 0 ? rank_cert_kernel<0, 2> : rank_cert_kernel<1, 2>;
   else if (abl == 3) fn = dt == 0 ? rank_cert_kernel<0, 3> : rank_cert_kernel<1, 3>;
+  else if (abl == 5) fn = dt == 0 ? rank_cert_kernel<0, 5> : rank_cert_kernel<1, 5>;
 #endif
   if ((e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)) != hipSuccess)
     return e;
@@ -408,6 +432,18 @@ hipError_t rank_cert_topk(const void* corpus, int64_t N, int dt, const float* q,
 
 // Diagnostics (not part of include/miclip.h): the certificate's delta terms for
 // f32 (dt 0) and bf16 (dt 1) rows at D = 512, for a host test (tests/test_abi.py).
+extern "C" int mi_debug_cert_probe(unsigned long long* host, int n) {
+#if MICLIP_AB
+  if (n > 256 * 4 * 5) n = 256 * 4 * 5;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(miclip::g_cert_probe), n * sizeof(unsigned long long), 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+#else
+  (void)host;
+  (void)n;
+  return -2;   // A/B build only
+#endif
+}
+
 extern "C" int mi_debug_cert_delta(int dt, float* d_rel, float* d_abs) {
   if (!d_rel || !d_abs || (dt != 0 && dt != 1)) return -1;   // MI_ERR_ARG
   miclip::rank_cert_delta(dt, *d_rel, *d_abs);
