@@ -870,6 +870,16 @@ hipError_t attention(const uint16_t* qkv, uint16_t* out, int B, int S, int W, in
   const bool old_flash = (causal >> 9) & 1;   // A/B: the chunk-streaming flash kernel for S > 64
   causal &= 1;
   const dim3 grid(items);
+#if MICLIP_AB
+  // A/B: MICLIP_ATTN_SHORT=1 runs S <= 64 (non-causal) on the resident-K/V kernel with 4 waves
+  const char* se = std::getenv("MICLIP_ATTN_SHORT");
+  if (se && se[0] == '1' && !one_wave && !old_flash && !(causal & 1) && S <= 64) {
+    const size_t lds = 2 * (size_t)((S + 31) & ~31) * 128;
+    hipLaunchKernelGGL((attention_res_kernel<4, false>), dim3(B * (W / 64)), dim3(256), lds, s, qkv, out, S, W, W / 64,
+                       q8, qs, ((int64_t)B * S + 1) & ~1);
+    return hipGetLastError();
+  }
+#endif
   if (!one_wave && !old_flash && !causal && S > 64) {
     // vision towers (257 / 577 tokens): K/V resident in LDS, no per-chunk barriers
     const int spad = (S + 31) & ~31;

@@ -12,7 +12,7 @@ import torch  # noqa: E402
 
 from miclip import _native as N  # noqa: E402
 
-SHAPES = [("B/32", 2000, 50, 768, 0), ("text", 256, 77, 512, 1), ("L/14", 385, 257, 1024, 0),
+SHAPES = [("B/32", 2000, 50, 768, 0), ("B/32c", 10000, 50, 768, 0), ("text", 256, 77, 512, 1), ("L/14", 385, 257, 1024, 0),
           ("L/14@336", 173, 577, 1024, 0),
           # the bench chunks of configs[2] (L/14, 1667 frames) and configs[4] (L/14@336)
           ("L/14c", 1667, 257, 1024, 0), ("L/14@336c", 1000, 577, 1024, 0)]
@@ -29,11 +29,15 @@ def main():
             continue
         qkv = (torch.randn(B * S, 3 * W, device=dev) * 1.5).bfloat16()
         outs = {}
-        for mode in ([0, 0x100] if S <= 96 else [0] + [f"v{i}" for i in (4, 5, 6, 7, 8, 9)]):
+        for mode in ([0, 0x100, "short"] if S <= 96 else [0] + [f"v{i}" for i in (4, 5, 6, 7, 8, 9)]):
             out = torch.empty(B * S, W, dtype=torch.bfloat16, device=dev)
             # resident-K/V kernel variants (attention.hip): v1 8 waves one tile at a time, v2 8 waves
             # two tiles at a time, v3 16 waves one tile at a time
-            if isinstance(mode, str):
+            os.environ.pop("MICLIP_ATTN_SHORT", None)
+            if mode == "short":
+                os.environ["MICLIP_ATTN_SHORT"] = "1"
+                os.environ.pop("MICLIP_ATTN_VAR", None)
+            elif isinstance(mode, str):
                 os.environ["MICLIP_ATTN_VAR"] = mode[1:]
             else:
                 os.environ.pop("MICLIP_ATTN_VAR", None)
@@ -52,7 +56,7 @@ def main():
             fl = 4.0 * B * S * S * W * (0.5 if causal else 1.0)
             by = B * S * 4 * W * 2
             d = (out.float() - outs[0].float()).abs().max().item()
-            kind = {0: "default", "v1": "res 8w x1", "v2": "res 8w x2", "v3": "res 16w x1", "v4": "r32 8w x2", "v5": "r32 12w", "v6": "r32 12w stag1", "v7": "r32 12w stag2", "v8": "r32 12w noload", "v9": "r32 12w st1 noexp", 0x100: "one-wave", 0x200: "flash(chunked)"}[mode]
+            kind = {0: "default", "v1": "res 8w x1", "v2": "res 8w x2", "v3": "res 16w x1", "v4": "r32 8w x2", "v5": "r32 12w", "v6": "r32 12w stag1", "v7": "r32 12w stag2", "v8": "r32 12w noload", "v9": "r32 12w st1 noexp", "short": "res 4w (S<=64)", 0x100: "one-wave", 0x200: "flash(chunked)"}[mode]
             print(f"{name:9s} {kind:16s} B={B} S={S} W={W}: {us:8.1f} us "
                   f"{fl / us / 1e6:6.1f} TFLOP/s {by / us / 1e3:7.1f} GB/s  maxdiff {d:.3g}", flush=True)
 
