@@ -42,6 +42,8 @@
 #include <climits>
 #include <cmath>
 #include <cstdlib>
+#include <type_traits>
+#include <utility>
 
 #include "common.hpp"
 #include "internal.hpp"
@@ -56,32 +58,55 @@ typedef unsigned int u32x4c __attribute__((ext_vector_type(4)));
 constexpr int CD = 512;   // supported D
 constexpr int CKC = 16;   // candidates per query
 
+template <int... Is, typename F>
+__device__ __forceinline__ void static_for_impl(std::integer_sequence<int, Is...>, F&& f) {
+  (f(std::integral_constant<int, Is>{}), ...);
+}
+// f(integral_constant<int, 0>) ... f(integral_constant<int, N - 1>): a loop whose index is a constant expression
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(std::make_integer_sequence<int, N>{}, f);
+}
+
+// a lane's four fragment pieces of the ring slot at byte offset OFF
+template <int OFF>
+__device__ __forceinline__ void read_frag(const uint32_t (&fa)[4], f32x4c (&v)[4]) {
+#pragma unroll
+  for (int t = 0; t < 4; ++t) asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v[t]) : "v"(fa[t]), "n"(OFF) : "memory");
+}
+
 __device__ __forceinline__ float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 
-// the ring, per-wave row reciprocals [4][32], tau [32], the lead keys [32][8]
-constexpr int CNB = 8, CPF = 6;
-constexpr size_t cert_lds_bytes() { return (size_t)4 * CNB * 4096 + 4 * 32 * 4 + 32 * 4 + LEAD_LDS; }
+// the ring, per-wave row reciprocals [4][32], tau [32], the lead keys [32][8], the
+// per-wave candidate buckets [4][CBK][64] u64
+constexpr int CNB = 8, CBK = 12;
+constexpr size_t cert_bucket_off() { return (size_t)4 * CNB * 4096 + 4 * 32 * 4 + 32 * 4 + LEAD_LDS; }
+constexpr size_t cert_lds_bytes() { return cert_bucket_off() + (size_t)4 * CBK * 64 * 8; }
 
-// per wave (row block y < 256, wave w): tile-epilogue cycles, tiles, tiles with an update, sort-path
+// per wave (row block y < 256, wave w): tile-epilogue cycles, tiles, tiles with candidates, bucket flushes,
 // updates, multi-candidate insertion updates (ABL 5, A/B build; mi_debug_cert_probe)
 __device__ unsigned long long g_cert_probe[256 * 4 * 5];
 
 // ABL (A/B timing probes, wrong results): 1 = no Gram MFMAs (unit norms), 2 = no MFMAs at
-// all, 3 = no list update; 5 = the epilogue stamp probe (correct results)
+// all, 3 = no list update, 7 = no bucket writes; 5 = the epilogue stamp probe, 6 = the bucket
+// writes at the tile end instead of spread over the next tile (correct results)
 template <int DT, int ABL = 0>
 __global__ __launch_bounds__(256) void rank_cert_kernel(const void* __restrict__ corpus, int64_t N,
                                                         const float* __restrict__ queries, int64_t Q, int kc,
                                                         int64_t rows_per_wg, int norm_mode, int nan_first, FoldWs f,
                                                         int32_t* __restrict__ unsafe, float* __restrict__ out_s,
                                                         int64_t* __restrict__ out_i) {
-  constexpr int D = CD, NW = 4, NT = 64 * NW, KC = CKC, NB = CNB, PF = CPF;
+  constexpr int D = CD, NW = 4, NT = 64 * NW, KC = CKC, NB = CNB;
+  // chunks in flight: bf16 rows read their fragments one chunk ahead, so a slot is free once
+  // its fragments have arrived (PF = NB); f32 rows read the chunk itself (PF = NB - 1)
+  constexpr int PF = DT ? NB : NB - 1;
   constexpr int ES = DT ? 2 : 4;           // bytes per element
   constexpr int KCH = 128 / ES;            // k per 4-KB chunk (32 rows x 128 B)
   constexpr int NCH = D / KCH;             // chunks per 32-row tile
   constexpr int NS = D / 16;               // bf16 MFMA k-steps
   constexpr int SLOT = 32 * 128;
-  static_assert(NB >= PF + 1, "rank_cert: a refilled ring slot must have been read in an earlier chunk");
+  static_assert(NB >= PF + (DT ? 0 : 1), "rank_cert: a refilled ring slot must have been read in an earlier chunk");
   static_assert(4 * PF <= 63, "rank_cert: vmcnt(4 PF) exceeds the counter");
   static_assert(cert_lds_bytes() <= 160 * 1024, "rank_cert: ring exceeds the LDS");
   static_assert(cert_lds_bytes() >= (size_t)NT * KC * 8, "rank_cert: list merge area exceeds the allocation");
@@ -92,6 +117,9 @@ __global__ __launch_bounds__(256) void rank_cert_kernel(const void* __restrict__
   uint32_t* tau = (uint32_t*)(nrm_all + NW * 32);
   uint32_t* lead = tau + 32;
   const int tid = threadIdx.x, lane = tid & 63;
+  // this lane's candidate bucket: slot j at bkt + 512 j (slot-major, conflict-free)
+  const uint32_t bkt = (uint32_t)(uintptr_t)(LDS_AS char*)(smem + cert_bucket_off()) +
+                       (uint32_t)((tid >> 6) * CBK * 512 + (tid & 63) * 8);
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, h = lane >> 5;
   const int64_t q0 = (int64_t)QB * FQ;
@@ -99,6 +127,7 @@ __global__ __launch_bounds__(256) void rank_cert_kernel(const void* __restrict__
 
   // queries -> bf16 B fragments q1 + q2: step s holds k = 16 s + 8 h + e of query r
   bf16x8 q1[NS], q2[NS];
+  bool qbad = false;
   {
     const float* qp = queries + (qvalid ? (q0 + r) : 0) * D + 8 * h;
 #pragma unroll
@@ -108,6 +137,7 @@ __global__ __launch_bounds__(256) void rank_cert_kernel(const void* __restrict__
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const float xv = qvalid ? x[e] : 0.f;
+        qbad |= !(__builtin_fabsf(xv) <= 1e15f);   // non-finite or huge: scores could overflow
         const __bf16 hi = (__bf16)xv;
         q1[st][e] = hi;
         q2[st][e] = (__bf16)(xv - (float)hi);
@@ -164,22 +194,54 @@ __global__ __launch_bounds__(256) void rank_cert_kernel(const void* __restrict__
   const int sw = (r >> 1) & 7;
   // fragment pieces of this lane in a chunk: bf16 rows, k-step t: piece 2t + h;
   // f32 rows, k-step t: pieces 4t + 2h and 4t + 2h + 1
-  auto read_frag = [&](int slot, f32x4c (&v)[4]) {
-    const char* src = wring + slot * SLOT + rbase;
+  // The 16-row tile takes NCH chunks and NCH is a multiple of NB, so the slot a chunk
+  // reads is a compile-time function of its position in the tile: the slot goes in the
+  // ds_read's immediate offset, and the per-lane part (4 addresses) is fixed for the kernel
+  // (hipcc otherwise kept all 8 x 4 slot addresses live across the tile loop).
+  static_assert(NCH % NB == 0, "rank_cert: the ring slot of a chunk must be static");
+  uint32_t fa[4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int piece = DT ? 2 * t + h : 4 * (t >> 1) + 2 * h + (t & 1);
-      const uint32_t a = (uint32_t)(uintptr_t)(const LDS_AS char*)(src + ((piece ^ sw) << 4));
-      asm volatile("ds_read_b128 %0, %1" : "=v"(v[t]) : "v"(a) : "memory");
-    }
-  };
+  for (int t = 0; t < 4; ++t) {
+    const int piece = DT ? 2 * t + h : 4 * (t >> 1) + 2 * h + (t & 1);
+    fa[t] = (uint32_t)(uintptr_t)(const LDS_AS char*)(wring + rbase + ((piece ^ sw) << 4));
+  }
   uint64_t L[KC];
 #pragma unroll
   for (int p = 0; p < KC; ++p) L[p] = 0ull;
   unsigned long long pr_cyc = 0ull, pr_t0 = 0ull;   // ABL 5 probe
   unsigned pr_n[4] = {0u, 0u, 0u, 0u};
   uint32_t kk = 0u;   // running k-th key of this query's lists (own threshold)
-  bool bad = false;
+  uint32_t bcnt = 0u;  // entries in this lane's bucket
+  bool bad = qbad;
+  // the bucket's entries into L, one insertion round per slot (an entry at a time: the
+  // 64-bit sort of a whole bucket would need registers the query fragments hold)
+  auto flush = [&]() {
+    for (uint32_t j = 0; __any(j < bcnt); ++j) {
+      uint64_t e;
+      asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(e) : "v"(bkt + 512u * j) : "memory");
+      e = j < bcnt ? e : 0ull;
+#pragma unroll
+      for (int p = 15; p > 0; --p) L[p] = e > L[p - 1] ? L[p - 1] : (e > L[p] ? e : L[p]);
+      L[0] = e > L[0] ? e : L[0];
+    }
+    bcnt = 0u;
+  };
+
+  // The previous tile's scores P and candidate mask pokm (rows ptr0 + rr): their bucket
+  // writes are spread over the next tile's chunks (PPC per chunk, after its MFMAs), so
+  // the DMA issue keeps its pace and the writes' VALU issues beside the MFMAs.
+  constexpr int PPC = 16 / NCH;
+  f32x16 P = f32x16{};
+  uint32_t pokm = 0u;
+  int ptr0 = 0;
+  auto put = [&](int rg) {   // candidate rg of the previous tile -> this lane's bucket
+    if ((pokm >> rg) & 1u) {
+      const int rr = (rg & 3) + 8 * (rg >> 2) + 4 * h;
+      const uint64_t e = ((uint64_t)score_key(P[rg], nan_first) << 32) | (uint32_t)~(uint32_t)(ptr0 + rr);
+      asm volatile("ds_write_b64 %0, %1" ::"v"(bkt + 512u * bcnt), "v"(e) : "memory");
+      ++bcnt;
+    }
+  };
 
   if (my_tiles > 0) {
 #pragma unroll
@@ -187,30 +249,32 @@ __global__ __launch_bounds__(256) void rank_cert_kernel(const void* __restrict__
     // bf16 rows: fragments read one chunk ahead (two register buffers, as the mirror pass);
     // f32 rows: one buffer, read after the chunk's wait (the split's temporaries need the VGPRs)
     constexpr bool PIPE = DT != 0;
-    int cslot = 0;
     f32x4c vb[PIPE ? 2 : 1][4];
     if (PIPE) {
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (PF - 1)) : "memory");
-      read_frag(0, vb[0]);
-      cslot = 1;
+      read_frag<0>(fa, vb[0]);
     }
     for (int ct = 0; ct < my_tiles; ++ct) {
-      f32x16 acc = f32x16{};
+      // two accumulators (the q2 terms apart): two independent MFMA chains per chunk
+      f32x16 acc = f32x16{}, acc2 = f32x16{};
       f32x16 gram = ABL == 1 ? f32x16{1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f}
                              : f32x16{};   // bf16 rows
       float ss = 0.f;           // f32 rows (this lane's half of row r)
-#pragma unroll
-      for (int j = 0; j < NCH; ++j) {
+      static_for<NCH>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        // bf16: this chunk's fragments (read in the previous chunk) have arrived before its
+        // slot is refilled with chunk j + PF (PF = NB)
+        if (PIPE) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         issue();
         f32x4c (&v)[4] = vb[PIPE ? (j & 1) : 0];
         if (PIPE) {
-          asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(4 * (PF - 1)) : "memory");
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (PF - 1)) : "memory");
           __builtin_amdgcn_sched_barrier(0);
-          read_frag(cslot, vb[PIPE ? ((j + 1) & 1) : 0]);
+          read_frag<(j + 1) % NB * SLOT>(fa, vb[PIPE ? ((j + 1) & 1) : 0]);
           __builtin_amdgcn_sched_barrier(0);
         } else {
           asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * PF) : "memory");
-          read_frag(cslot, v);
+          read_frag<j % NB * SLOT>(fa, v);
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           __builtin_amdgcn_sched_barrier(0);
         }
@@ -223,7 +287,7 @@ __global__ __launch_bounds__(256) void rank_cert_kernel(const void* __restrict__
               continue;
             }
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, q1[4 * j + t], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, q2[4 * j + t], acc, 0, 0, 0);
+            acc2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, q2[4 * j + t], acc2, 0, 0, 0);
             // the tile's Gram matrix: the A fragment is also the B fragment of the
             // transposed rows, so its diagonal is each row's sum of squares
             if (ABL != 1) gram = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, av, gram, 0, 0, 0);
@@ -242,13 +306,23 @@ __global__ __launch_bounds__(256) void rank_cert_kernel(const void* __restrict__
             const bf16x8 ah = __builtin_bit_cast(bf16x8, (u32x4c){ph[0], ph[1], ph[2], ph[3]});
             const bf16x8 al = __builtin_bit_cast(bf16x8, (u32x4c){pl[0], pl[1], pl[2], pl[3]});
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, q1[2 * j + t], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, q2[2 * j + t], acc, 0, 0, 0);
+            acc2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, q2[2 * j + t], acc2, 0, 0, 0);
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, q1[2 * j + t], acc, 0, 0, 0);
 #pragma unroll
             for (int e = 0; e < 8; ++e) ss = fmaf(x[e], x[e], ss);
+            // pinned here: hipcc sank the whole tile's fmaf chain to the tile end and kept
+            // the 256 row values it needs live (in AGPRs), spilling the query fragments
+            asm volatile("" : "+v"(ss));
           }
         }
-        cslot = cslot == NB - 1 ? 0 : cslot + 1;
+        if (ABL != 3 && ABL != 6 && ABL != 7) {
+#pragma unroll
+          for (int i = 0; i < PPC; ++i) put(PPC * j + i);
+        }
+      });
+      if (ABL == 6) {   // probe: the previous tile's bucket writes here, not spread over the chunks
+#pragma unroll
+        for (int rg = 0; rg < 16; ++rg) put(rg);
       }
       // row r's reciprocal norm (lanes r and r + 32 hold its two halves) -> the wave's
       // LDS slots, read back in the accumulator's row order
@@ -269,6 +343,8 @@ __global__ __launch_bounds__(256) void rank_cert_kernel(const void* __restrict__
       }
       const int tr0 = (wave + NW * ct) * 32;
       const bool rvalid = (int64_t)tr0 + r < nrows;
+      // also the scores' guard: with the sum of squares in range and a finite query of
+      // moderate norm (checked at entry) every score is finite
       bad |= rvalid && !(ss >= 1e-15f && ss <= 1e36f);
       {
         // the lane id recomputed here (v_mbcnt) rather than kept live across the tile:
@@ -278,48 +354,70 @@ __global__ __launch_bounds__(256) void rank_cert_kernel(const void* __restrict__
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_wave_barrier();
+      if (ABL == 5) pr_t0 = __builtin_amdgcn_s_memtime();
       const uint32_t tq_thr = tau[r];
       const uint32_t own = kk;   // the query's two half-lists' k-th: a lower bound of its k-th
       const uint32_t thr0 = own > tq_thr ? own : tq_thr;
       const uint32_t lb = lead_min(lead, r);
       const uint32_t thr = lb > thr0 ? lb : thr0;
-      uint64_t c[16];
-      bool any = false;
-      uint32_t okm = 0u;
+      // the key threshold as a score: score_key is monotone on finite scores (-0 = +0), so
+      // key >= thr <=> s >= tf; keys below key(-inf) admit every finite score
+      const float tf = thr < 0x00800000u ? -INFINITY
+                                         : __uint_as_float((thr & 0x80000000u) ? (thr & 0x7fffffffu) : ~thr);
       const int vrows = (int)min((int64_t)32, nrows - tr0);   // valid rows of this tile
-      uint32_t nonfin = 0u;
       // the 16 rows' reciprocals: rows (rg & 3) + 8 (rg >> 2) + 4 h are four 16-byte runs
       f32x4c nv[4];
 #pragma unroll
       for (int q4 = 0; q4 < 4; ++q4) nv[q4] = *(const f32x4c*)(nrm + 8 * q4 + 4 * h);
+      uint32_t okm = 0u;
 #pragma unroll
       for (int rg = 0; rg < 16; ++rg) {
         const int rr = (rg & 3) + 8 * (rg >> 2) + 4 * h;
-        const float sc = acc[rg] * nv[rg >> 2][rg & 3];
-        const bool rowok = qvalid && rr < vrows;
-        nonfin |= (rowok && !(__builtin_fabsf(sc) <= 3.4e38f)) ? 1u : 0u;   // NaN / inf, no branch
-        const uint32_t key = score_key(sc, nan_first);
-        const bool ok = rowok && key >= thr;
-        c[rg] = ok ? (((uint64_t)key << 32) | (uint32_t)~(uint32_t)(tr0 + rr)) : 0ull;
-        any |= ok;
-        okm |= ok ? 1u << rg : 0u;
+        const float sc = (acc[rg] + acc2[rg]) * nv[rg >> 2][rg & 3];
+        P[rg] = sc;
+        okm |= (qvalid && rr < vrows && sc >= tf) ? 1u << rg : 0u;
       }
-      bad |= nonfin != 0u;
-      if (ABL == 5) {   // stamp probe: cycles of the whole tile epilogue below, updates, sort-path updates
-        pr_t0 = __builtin_amdgcn_s_memtime();
-        pr_n[1] += __any(any) ? 1u : 0u;
-        pr_n[2] += __any(__builtin_popcount(okm) > 6) ? 1u : 0u;
+      ptr0 = tr0;
+      if (ABL == 5) {
+        pr_n[1] += __any(okm != 0u) ? 1u : 0u;
         pr_n[3] += __all(__builtin_popcount(okm) <= 1) ? 0u : 1u;
       }
-      if (ABL != 3 && __any(any)) {
-        list_update16(L, c, okm);
-        lead_publish(lead, r, 2 * wave + h, (uint32_t)(L[1] >> 32));
+      // a bucket that this tile's candidates could overflow: merge it into the lists now and
+      // refresh the thresholds; a tile with more candidates than a bucket holds (the first
+      // ones, before the thresholds rise) is inserted directly, one candidate per round
+      const uint32_t pc = (uint32_t)__builtin_popcount(okm);
+      if (ABL != 3 && __any(bcnt + pc > (uint32_t)CBK)) {
+        if (ABL == 5) pr_n[2] += 1u;
+        if (__any(bcnt != 0u)) flush();
+        if (__any(pc > (uint32_t)CBK)) {
+          uint32_t m = okm;
+          while (__any(m != 0u)) {
+            const int i = m ? __builtin_ctz(m) : 0;
+            float sc = P[0];
+#pragma unroll
+            for (int rg = 1; rg < 16; ++rg) sc = rg == i ? P[rg] : sc;
+            const int rr = (i & 3) + 8 * (i >> 2) + 4 * h;
+            const uint64_t e = m ? (((uint64_t)score_key(sc, nan_first) << 32) | (uint32_t)~(uint32_t)(tr0 + rr)) : 0ull;
+#pragma unroll
+            for (int p = 15; p > 0; --p) L[p] = e > L[p - 1] ? L[p - 1] : (e > L[p] ? e : L[p]);
+            L[0] = e > L[0] ? e : L[0];
+            m &= m - 1u;
+          }
+          okm = 0u;
+        }
+        {
+          // lane id recomputed (v_mbcnt): a live-across-the-tile LDS address gets spilled, and
+          // its reload's vmcnt(0) would drain the ring
+          const int ln = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+          lead_publish(lead, ln & 31, 2 * wave + (ln >> 5), (uint32_t)(L[1] >> 32));
+        }
         uint32_t kth = (uint32_t)(L[KC - 1] >> 32);   // k = kc = KC candidates
         const uint32_t other = (uint32_t)__shfl_xor((int)kth, 32, 64);
         kth = kth > other ? kth : other;
         kk = kth;
         if (h == 0 && qvalid && kth > tq_thr) tau_max(&tau[r], kth);
       }
+      pokm = okm;
       if (ABL == 5) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         pr_cyc += __builtin_amdgcn_s_memtime() - pr_t0;
@@ -329,6 +427,11 @@ __global__ __launch_bounds__(256) void rank_cert_kernel(const void* __restrict__
       __builtin_amdgcn_wave_barrier();
     }
   }
+  if (ABL != 3) {
+#pragma unroll
+    for (int rg = 0; rg < 16; ++rg) put(rg);   // the last tile's candidates
+  }
+  if (ABL != 3 && __any(bcnt != 0u)) flush();
   if (ABL == 5 && lane == 0 && (int)blockIdx.y < 256) {
     unsigned long long* o = g_cert_probe + ((int)blockIdx.y * 4 + wave) * 5;
     o[0] = pr_cyc;
@@ -417,6 +520,8 @@ hipError_t rank_cert_topk(const void* corpus, int64_t N, int dt, const float* q,
   else if (abl == 2) fn = dt == 0 ? rank_cert_kernel<0, 2> : rank_cert_kernel<1, 2>;
   else if (abl == 3) fn = dt == 0 ? rank_cert_kernel<0, 3> : rank_cert_kernel<1, 3>;
   else if (abl == 5) fn = dt == 0 ? rank_cert_kernel<0, 5> : rank_cert_kernel<1, 5>;
+  else if (abl == 6) fn = dt == 0 ? rank_cert_kernel<0, 6> : rank_cert_kernel<1, 6>;
+  else if (abl == 7) fn = dt == 0 ? rank_cert_kernel<0, 7> : rank_cert_kernel<1, 7>;
 #endif
   if ((e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)) != hipSuccess)
     return e;

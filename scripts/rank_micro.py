@@ -23,9 +23,12 @@ VARIANTS = {"default": {}, "exact": {"MICLIP_RANK_CERT": "0"},
             "nomfma": {"MICLIP_RANK_PROBE": "1", "MICLIP_RANK_CERT": "0"},
             # certified-pass timing probes (wrong results): no Gram MFMAs, no MFMAs, no list update
             "c_nogram": {"MICLIP_RANK_CERT_ABL": "1"}, "c_nomfma": {"MICLIP_RANK_CERT_ABL": "2"},
-            "c_nolist": {"MICLIP_RANK_CERT_ABL": "3"}}
+            "c_nolist": {"MICLIP_RANK_CERT_ABL": "3"}, "c_endput": {"MICLIP_RANK_CERT_ABL": "6"},
+            "c_noput": {"MICLIP_RANK_CERT_ABL": "7"}}
 SHAPES = [(125_000, 512, 32, torch.float32), (1_000_000, 512, 32, torch.float32),
           (1_000_000, 512, 32, torch.bfloat16), (1_000_000, 768, 32, torch.float32)]
+if os.environ.get("RANK_MICRO_SHAPES") == "cert":   # the certified pass's shapes only
+    SHAPES = SHAPES[1:3]
 
 
 def setenv(v):
