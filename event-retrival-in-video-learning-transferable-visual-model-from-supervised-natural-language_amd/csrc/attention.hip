@@ -618,8 +618,26 @@ __global__ __launch_bounds__(NW * 64) void attention_res_kernel(const uint16_t* 
 //   V image : chunk c of row r at slot c ^ (((r >> 1) & 1) << 2): the four rows
 //             of a transposed read (r0 .. r0 + 3, r0 % 4 == 0) put their 64
 //             bytes in four disjoint quarter-banks.
-// ABL (A/B timing probes only): 1 = no exponentials, 2 = no K/V DMA, 3 = no softmax VALU
-template <int NW, bool TT2 = true, int ABL = 0>
+// s_waitcnt vmcnt(n) for a wave-uniform n in [0, N] (the count is an immediate)
+template <int N>
+__device__ __forceinline__ void vm_wait_younger(int n) {
+  if constexpr (N > 0) {
+    if (n >= N) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+      return;
+    }
+    vm_wait_younger<N - 1>(n);
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+}
+
+// ABL (A/B timing probes only): 1 = no exponentials, 2 = no K/V DMA, 3 = no softmax VALU.
+// PH2: the K/V load in two phases, keys [0, 64 c0) (c0 = spad / 128 chunks) first; the wave's first query
+// block, its Q loaded ahead of the DMAs, starts on the first phase's keys after one
+// barrier and takes a second barrier (vmcnt(0)) before chunk c0, so the second half of
+// the 148 KB load (S = 577) arrives under the first half's math instead of before it.
+template <int NW, bool TT2 = true, int ABL = 0, bool PH2 = false>
 __global__ __launch_bounds__(NW * 64) void attention_r32_kernel(const uint16_t* __restrict__ qkv,
                                                                 uint16_t* __restrict__ out, int S, int W, int H,
                                                                 uint8_t* __restrict__ q8, uint8_t* __restrict__ qs,
@@ -650,8 +668,37 @@ __global__ __launch_bounds__(NW * 64) void attention_r32_kernel(const uint16_t* 
     }
   }
   const int nch = (S + 63) >> 6;
-  if (ABL != 2) {
-    const int nr8 = spad >> 3;
+  const int nr8 = spad >> 3;
+  const int c0 = PH2 ? max(1, nr8 >> 4) : nch;   // chunks of the first load phase (nr8 >= 12 for S > 64)
+  static_assert(!PH2 || (NW == 12 && !TT2), "attention_r32: the two-phase load's slot count assumes 12 waves");
+  // NI2 (below) x 12 waves >= 2 nr8 for spad <= 640
+  bf16x8 qf0[4];
+  if (PH2) {   // the first block's Q, ahead of the DMAs: waiting for it drains none of them
+    const int qrow = min(wave * 32 + (lane & 31), S - 1);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) qf0[s] = *(const bf16x8*)(qb + (int64_t)qrow * ld + 16 * s + 8 * (lane >> 5));
+  }
+  // PH2: NI2 DMA slots per wave in global order g = wave + 12 k, so each wave issues its
+  // first-phase blocks (g < 2 h0: K then V blocks of keys < 64 c0) before its second-phase
+  // ones; slots past the 2 nr8 blocks re-load the last block (identical bytes, same place)
+  constexpr int NI2 = 14;
+  const int h0 = 8 * c0;
+  if (ABL != 2 && PH2) {
+    const int slot = lane & 7;
+    const int n1 = nr8 - h0;
+#pragma unroll
+    for (int k = 0; k < NI2; ++k) {
+      const int g = min(wave + NW * k, 2 * nr8 - 1);
+      const bool ph = g >= 2 * h0;
+      const int j = ph ? g - 2 * h0 : g, cnt = ph ? n1 : h0;
+      const bool isv = j >= cnt;
+      const int i8 = (ph ? h0 : 0) + (isv ? j - cnt : j);
+      const int rr = i8 * 8 + (lane >> 3);
+      const int cc = isv ? (slot ^ (((rr >> 1) & 1) << 2)) : (slot ^ ((rr >> 1) & 7));
+      glds16((isv ? vb : kb) + (int64_t)min(rr, S - 1) * ld + cc * 8, (isv ? Vimg : Kimg) + i8 * 1024);
+    }
+  }
+  if (ABL != 2 && !PH2) {
     const int slot = lane & 7;
     for (int i = wave; i < 2 * nr8; i += NW) {
       const bool isv = i >= nr8;
@@ -686,10 +733,15 @@ __global__ __launch_bounds__(NW * 64) void attention_r32_kernel(const uint16_t* 
     return __builtin_bit_cast(bf16x8, (s16x8)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
   };
 
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (PH2) {   // this wave's first-phase DMAs (and Q): the NI2 - n0 younger ones may stay in flight
+    const int n0 = 2 * h0 > wave ? (2 * h0 - wave + NW - 1) / NW : 0;
+    vm_wait_younger<NI2>(NI2 - min(n0, NI2));
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   __syncthreads();
 
-  auto blocks = [&](auto tt_c, int b0, int b1) {
+  auto blocks = [&](auto tt_c, int b0, int b1, bool first) {
     constexpr int TT = decltype(tt_c)::value;
     const int bq[2] = {b0, b1};
     bf16x8 qf[TT][4];
@@ -697,7 +749,8 @@ __global__ __launch_bounds__(NW * 64) void attention_r32_kernel(const uint16_t* 
     for (int u = 0; u < TT; ++u) {
       const int qrow = min(bq[u] * 32 + r, S - 1);
 #pragma unroll
-      for (int s = 0; s < 4; ++s) qf[u][s] = *(const bf16x8*)(qb + (int64_t)qrow * ld + 16 * s + 8 * hh);
+      for (int s = 0; s < 4; ++s)
+        qf[u][s] = PH2 && first ? qf0[s] : *(const bf16x8*)(qb + (int64_t)qrow * ld + 16 * s + 8 * hh);
     }
     float m[TT], l[TT];
     f32x16 o[TT][2];
@@ -788,7 +841,17 @@ __global__ __launch_bounds__(NW * 64) void attention_r32_kernel(const uint16_t* 
     using I2 = std::integral_constant<int, 2>;
     using BF = std::integral_constant<bool, false>;
     using BT = std::integral_constant<bool, true>;
-    for (int c = 0; c < nch - 1; ++c) chunk(I2{}, BF{}, c);
+    for (int c = 0; c < nch - 1; ++c) {
+      if (PH2 && first && c == c0) {   // the second load phase (every wave passes here once)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+      }
+      chunk(I2{}, BF{}, c);
+    }
+    if (PH2 && first && c0 >= nch - 1) {   // short sequences: the second phase before the last chunk
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
     if (last_keys > 32) chunk(I2{}, BT{}, nch - 1);
     else chunk(I1{}, BT{}, nch - 1);
 
@@ -840,11 +903,15 @@ __global__ __launch_bounds__(NW * 64) void attention_r32_kernel(const uint16_t* 
   };
   if (TT2) {
     for (int b = wave; b < nqb; b += 2 * NW) {
-      if (b + NW < nqb) blocks(std::integral_constant<int, 2>{}, b, b + NW);
-      else blocks(std::integral_constant<int, 1>{}, b, b);
+      if (b + NW < nqb) blocks(std::integral_constant<int, 2>{}, b, b + NW, false);
+      else blocks(std::integral_constant<int, 1>{}, b, b, false);
     }
   } else {
-    for (int b = wave; b < nqb; b += NW) blocks(std::integral_constant<int, 1>{}, b, b);
+    if (PH2 && wave >= nqb) {   // no block: the second phase's barrier all the same
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+    for (int b = wave; b < nqb; b += NW) blocks(std::integral_constant<int, 1>{}, b, b, b == wave);
   }
 }
 
@@ -890,17 +957,18 @@ hipError_t attention(const uint16_t* qkv, uint16_t* out, int B, int S, int W, in
     // against 2392 for attention_res_kernel).  A/B variants (MICLIP_ATTN_VAR): 1 res 8 waves
     // x 1 tile, 2 res 8 waves x 2 tiles, 3 res 16 waves, 4 r32 8 waves x 2 blocks, 5 r32
     // 12 waves, 6 / 7 r32 12 waves with a start stagger of 1 / 2 quarter workgroup times,
-    // 8 / 9 r32 timing probes (no K/V load / no exponentials: wrong results)
+    // 8 / 9 r32 timing probes (no K/V load / no exponentials: wrong results), 10 r32 12 waves
+    // with the two-phase K/V load
 #if MICLIP_AB
     const char* ve = std::getenv("MICLIP_ATTN_VAR");   // A/B
     int var = ve ? std::atoi(ve) : 0;
 #else
     int var = 0;
 #endif
-    if (var < 1 || var > 9) var = S > 320 ? 5 : 1;
+    if (var < 1 || var > 10) var = S > 320 ? 5 : 1;
     const int64_t rp = ((int64_t)B * S + 1) & ~1;
     auto set_lds = [&](const void* fn, int slot) -> hipError_t {
-      static bool attr_set[10] = {false, false, false, false, false, false, false, false, false, false};
+      static bool attr_set[11] = {false, false, false, false, false, false, false, false, false, false, false};
       if (attr_set[slot]) return hipSuccess;
       hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       if (e == hipSuccess) attr_set[slot] = true;
@@ -921,6 +989,7 @@ hipError_t attention(const uint16_t* qkv, uint16_t* out, int B, int S, int W, in
     else if (var == 6 || var == 7)
       ATT_LAUNCH(var, (attention_r32_kernel<12, false>), 768, qkv, out, S, W, H, q8, qs, rp, (var - 5) * (S * S / 378))
     else if (var == 8) ATT_LAUNCH(8, (attention_r32_kernel<12, false, 2>), 768, qkv, out, S, W, H, q8, qs, rp, 0)
+    else if (var == 10) ATT_LAUNCH(10, (attention_r32_kernel<12, false, 0, true>), 768, qkv, out, S, W, H, q8, qs, rp, 0)
     else ATT_LAUNCH(9, (attention_r32_kernel<12, false, 1>), 768, qkv, out, S, W, H, q8, qs, rp, 0)
 #else
     else return hipErrorNotSupported;

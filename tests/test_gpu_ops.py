@@ -249,11 +249,12 @@ def test_attention_res_variants_bit_identical(gpu, monkeypatch, B, S, W, var):
 @pytest.mark.parametrize("B,S,W", [(2, 577, 1024), (3, 257, 768), (2, 130, 128), (1, 97, 256), (2, 385, 128),
                                    (1, 640, 192), (2, 100, 128)])
 @pytest.mark.parametrize("grow", [False, True])
-@pytest.mark.parametrize("var", ["4", "5", "6"])
+@pytest.mark.parametrize("var", ["4", "5", "6", "10"])
 def test_attention_r32_kernel(gpu, monkeypatch, B, S, W, grow, var):
     """attention_r32_kernel (32x32x16 MFMAs, P kept in the lane as the PV B
     operand, V^T by transposed reads; MICLIP_ATTN_VAR=4 (8 waves, two blocks at
-    a time), 5 (12 waves, one block), 6 (12 waves, staggered start) in the A/B build)
+    a time), 5 (12 waves, one block), 6 (12 waves, staggered start), 10 (12 waves,
+    two-phase K/V load) in the A/B build)
     against float64, on random rows and on rows whose max grows along the keys
     (the lazy-rescale branch on every chunk).  Query-block counts 19 / 9 / 5 /
     4 / 13 / 20 / 4 cover pairs, singles and a last block of one row."""
@@ -278,6 +279,12 @@ def test_attention_r32_kernel(gpu, monkeypatch, B, S, W, grow, var):
     ref = (torch.softmax(q @ k.transpose(-1, -2) * 0.125, -1) @ v).transpose(1, 2).reshape(B * S, W)
     err = (out.double() - ref).abs().max().item()
     assert err < 3e-2 * max(1.0, ref.abs().max().item()), err
+    if var == "10":   # the two-phase K/V load changes no arithmetic: bit-identical to variant 5
+        d = torch.empty_like(out)
+        monkeypatch.setenv("MICLIP_ATTN_VAR", "5")
+        assert La.mi_op_attention(qkv.data_ptr(), d.data_ptr(), B, S, W, 0, _stream()) == 0, La.mi_last_error()
+        torch.cuda.synchronize()
+        assert torch.equal(d, out)
     if var == "5" and S > 320:   # the product default for S > 320 is this kernel
         d = torch.empty_like(out)
         N_.check(N_.lib().mi_op_attention(qkv.data_ptr(), d.data_ptr(), B, S, W, 0, _stream()), "attention")
