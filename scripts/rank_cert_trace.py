@@ -14,7 +14,9 @@ from miclip import retrieval  # noqa: E402
 def main():
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(3)
-    for dt in (torch.float32, torch.bfloat16):
+    dts = {"f32": (torch.float32,), "bf16": (torch.bfloat16,)}.get(os.environ.get("RC_DT", ""),
+                                                                   (torch.float32, torch.bfloat16))
+    for dt in dts:
         corpus = torch.randn(1_000_000, 512, device=dev, generator=g).to(dt)
         q = torch.nn.functional.normalize(torch.randn(32, 512, device=dev, generator=g), dim=1)
         for _ in range(10):
