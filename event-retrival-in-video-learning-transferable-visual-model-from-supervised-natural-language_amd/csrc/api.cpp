@@ -224,6 +224,11 @@ const char* mi_last_error(void) { return g_err.c_str(); }
 
 int64_t mi_clip_weights_numel(const mi_clip_arch* a) {
   if (!a) return -1;
+  // sizes the blob's tensors from the arch: no field may be negative or divide by zero
+  if (a->embed_dim < 1 || a->image_resolution < 1 || a->vision_layers < 0 || a->vision_width < 1 ||
+      a->vision_patch_size < 1 || a->image_resolution % a->vision_patch_size || a->context_length < 1 ||
+      a->vocab_size < 1 || a->text_width < 1 || a->text_heads < 1 || a->text_layers < 0)
+    return -1;
   const int64_t W = a->vision_width, P = a->vision_patch_size, G = a->image_resolution / a->vision_patch_size;
   const int64_t S = G * G + 1, E = a->embed_dim, TW = a->text_width;
   int64_t n = W * 3 * P * P + W + S * W + 2 * W + tower_numel(W, a->vision_layers) + 2 * W + W * E;

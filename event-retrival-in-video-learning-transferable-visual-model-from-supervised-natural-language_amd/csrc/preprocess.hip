@@ -227,6 +227,9 @@ hipError_t get_tables(int H, int W, int n, int mode, Tables& out) {
 int resample_coeffs(int in_size, double in0, double in1, int out_size, int filter, std::vector<int32_t>& kk,
                     std::vector<int32_t>& bounds) {
   if (in_size < 1 || out_size < 1 || (filter != 0 && filter != 1)) return -1;
+  // the box inside the input, as Pillow's resize requires ("box can't exceed original image
+  // size"); outside it the bounds below would run past the row (and NaN edges fail here too)
+  if (!(in0 >= 0.0 && in1 <= (double)in_size && in1 > in0)) return -1;
   double (*fn)(double) = filter == 0 ? bicubic : bilinear;
   const double fsupport = filter == 0 ? 2.0 : 1.0;
   // Pillow precompute_coeffs: the box edges are C floats, their difference is
