@@ -41,10 +41,17 @@ def _pairs(word):
 # ftfy.fix_text (openai/CLIP basic_clean's first step; ftfy 6 default
 # TextFixerConfig) is not installed here.  Restated: the deterministic fixers
 # that apply to well-formed Unicode input, in ftfy's order — terminal escapes,
-# Latin ligatures, character width, curly quotes, line breaks, control
-# characters, NFC.  Mojibake repair (fix_encoding / decode_inconsistent_utf8)
-# is not restated: it needs ftfy's charset tables, and a query typed or
-# translated into the search box is already well-formed.
+# mojibake repair (the common case, below), Latin ligatures, character width,
+# curly quotes, line breaks, control characters, NFC.  Of ftfy's fix_encoding
+# only the whole-string case is restated: UTF-8 bytes that were decoded as
+# Windows-1252 / Latin-1 ("cafÃ©", "âœ”", doubly "Ã¢â‚¬â„¢"), recognised by a
+# UTF-8 lead byte followed by a continuation byte as those codecs render them,
+# undone while the string re-encodes in (sloppy) Windows-1252 and the bytes
+# decode as UTF-8.  A string with any character outside Windows-1252 (Vietnamese
+# ư / ơ / ạ, CJK, emoji) never re-encodes, so well-formed text is left alone.
+# ftfy's badness heuristics for partial and mixed mojibake
+# (decode_inconsistent_utf8, restore_byte_a0, replace_lossy_sequences) are not
+# restated: parity with ftfy itself is unpinned.
 _ANSI = re.compile(r"\x1b\[[\d;]*[@-~]")
 _LIGATURES = {"\u0132": "IJ", "\u0133": "ij", "\u01f1": "DZ", "\u01f2": "Dz", "\u01f3": "dz", "\u01c4": "DŽ",
               "\u01c5": "Dž", "\u01c6": "dž", "\u01c7": "LJ", "\u01c8": "Lj", "\u01c9": "lj", "\u01ca": "NJ",
@@ -60,9 +67,50 @@ _CONTROL = re.compile(r"[\x00-\x08\x0b\x0e-\x1f\x7f\u206a-\u206f\ufff9-\ufffc\uf
                       r"\U0001d173-\U0001d17a\U000e0000-\U000e007f]")
 
 
+# cp1252 renders bytes 0x80-0x9F as these characters (the five bytes it leaves undefined,
+# 0x81 0x8D 0x8F 0x90 0x9D, pass through as U+0081 ... in ftfy's "sloppy-windows-1252")
+_CP1252_HIGH = "€\x81‚ƒ„…†‡ˆ‰Š‹Œ\x8dŽ\x8f\x90‘’“”•–—˜™š›œ\x9džŸ"
+_SLOPPY_1252 = {c: 0x80 + i for i, c in enumerate(_CP1252_HIGH)}
+_SLOPPY_1252.update({chr(b): b for b in range(0xA0, 0x100)})
+# a UTF-8 lead byte (0xC2-0xF4) followed by a continuation byte (0x80-0xBF), as cp1252 shows them
+_MOJIBAKE = re.compile("[\u00c2-\u00f4][" + re.escape(_CP1252_HIGH) + "\u00a0-\u00bf]")
+
+
+def _sloppy_1252_bytes(text):
+    out = bytearray()
+    for c in text:
+        o = ord(c)
+        if o < 0x80:
+            out.append(o)
+        elif c in _SLOPPY_1252:
+            out.append(_SLOPPY_1252[c])
+        else:
+            return None
+    return bytes(out)
+
+
+def fix_encoding_subset(text):
+    """ftfy fix_encoding, whole-string case: re-decode text that is UTF-8 read as cp1252."""
+    for _ in range(4):               # doubly (or triply) encoded text unwinds one layer a pass
+        if not _MOJIBAKE.search(text):
+            break
+        b = _sloppy_1252_bytes(text)
+        if b is None:
+            break
+        try:
+            fixed = b.decode("utf-8")
+        except UnicodeDecodeError:
+            break
+        if fixed == text:
+            break
+        text = fixed
+    return text
+
+
 def fix_text_subset(text):
     import unicodedata
     text = _ANSI.sub("", text)
+    text = fix_encoding_subset(text)
     text = "".join(_LIGATURES.get(c, c) for c in text)
     # fix_character_width: fullwidth / halfwidth forms and the ideographic space, by NFKC of those characters
     text = "".join(unicodedata.normalize("NFKC", c) if ("\uff01" <= c <= "\uffee" or c == "\u3000") else c

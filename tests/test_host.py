@@ -120,3 +120,27 @@ def test_tokenizer_clean_restates_ftfy_subset():
     assert _clean("5\u2032 10\u2033") == "5\u2032 10\u2033"
     # ftfy CONTROL_CHARS includes musical formatting U+1D173-1D17A and tags U+E0000-E007F
     assert _clean("a\U0001d173b\U000e0041c\U000e007fd") == "abcd"
+
+
+def test_tokenizer_mojibake_repair_subset():
+    """ftfy fix_encoding's whole-string case (restated in miclip/tokenizer.py): UTF-8 read as
+    Windows-1252, once or twice, is decoded back; text with any character outside
+    Windows-1252 (the reference's Vietnamese queries), legitimate Latin-1 text and lone
+    lead characters are left alone.  Examples follow ftfy's documentation; parity against
+    ftfy itself is unpinned (not installed)."""
+    from miclip.tokenizer import _clean, fix_encoding_subset
+
+    def as_cp1252(t):   # UTF-8 bytes shown through sloppy Windows-1252
+        hi = "€\x81‚ƒ„…†‡ˆ‰Š‹Œ\x8dŽ\x8f\x90‘’“”•–—˜™š›œ\x9džŸ"
+        return "".join(chr(b) if b < 0x80 or b >= 0xA0 else hi[b - 0x80] for b in t.encode("utf-8"))
+
+    assert fix_encoding_subset("cafÃ©") == "café"
+    assert fix_encoding_subset("âœ” No problems") == "✔ No problems"
+    assert fix_encoding_subset("schÃ¶n Ã‰cole Â£100") == "schön École £100"
+    # doubly encoded, then uncurl_quotes
+    assert _clean("The Mona Lisa doesnÃ¢â‚¬â„¢t have eyebrows.") == "The Mona Lisa doesn't have eyebrows."
+    for t in ["người đi xe đạp trên đường", "cảnh hoàng hôn trên biển", "naïve café", "日本語 🚀", "Ã", "plain"]:
+        assert fix_encoding_subset(t) == t, t                  # well-formed: untouched
+        if any(ord(c) > 0x7F for c in t) and len(t) > 1:
+            assert fix_encoding_subset(as_cp1252(t)) == t, t    # its mojibake: repaired
+            assert fix_encoding_subset(as_cp1252(as_cp1252(t))) == t, t
