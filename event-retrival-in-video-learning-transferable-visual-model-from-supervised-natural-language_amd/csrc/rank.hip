@@ -271,7 +271,12 @@ __global__ __launch_bounds__(64 * NW) void rank_stream(const void* __restrict__ 
 // LDS, where reads return zero — every score comes out 0.
 constexpr size_t rank_reg_lds_bytes(int NB) { return (size_t)4 * NB * (32 * 128) + 4 * 32 * 4 + RQ * 4 + LEAD_LDS; }
 
-template <int D, int NB = 8, int PF = 6, bool NOMFMA = false, bool ILV = false, bool PIPE = false, int DT = 0>
+// STAMP (A/B build, MICLIP_RANK_STAMP=1): s_memrealtime (100 MHz) per workgroup at entry, after the query
+// load, after the stream, after fold_publish and at exit (mi_debug_rank_stamp)
+__device__ unsigned long long g_rank_stamp[256 * 10];
+
+template <int D, int NB = 8, int PF = 6, bool NOMFMA = false, bool ILV = false, bool PIPE = false, int DT = 0,
+          bool STAMP = false>
 __global__ __launch_bounds__(256) void rank_reg(const void* __restrict__ corpus, int64_t N,
                                                 const float* __restrict__ queries, int64_t Q, int k,
                                                 int64_t rows_per_wg, int norm_mode, int nan_first, int64_t index_base,
@@ -311,6 +316,8 @@ __global__ __launch_bounds__(256) void rank_reg(const void* __restrict__ corpus,
   const int64_t q0 = (int64_t)QB * RQ;
   const bool qvalid = q0 + r < Q;
   if (gate && __all(!qvalid || gate[q0 + r] != 0)) return;
+  unsigned long long* stamp = g_rank_stamp + 10 * ((int)RB & 255);
+  if (STAMP && tid == 0) stamp[0] = __builtin_amdgcn_s_memrealtime();
 
   // queries -> registers (zeros past Q)
   float qv[NQ][16];
@@ -331,6 +338,7 @@ __global__ __launch_bounds__(256) void rank_reg(const void* __restrict__ corpus,
   lead[tid] = 0u;   // 256 = 32 x 8
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  if (STAMP && tid == 0) stamp[1] = __builtin_amdgcn_s_memrealtime();
 
   const int G = NRB;
   const int64_t r_begin = ILV ? 0 : (int64_t)RB * rows_per_wg;
@@ -505,6 +513,7 @@ __global__ __launch_bounds__(256) void rank_reg(const void* __restrict__ corpus,
   // trailing (zero-range) DMAs and the pipelined read past the last chunk complete before the ring is reused
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();   // ring free -> lists
+  if (STAMP && tid == 0) stamp[2] = __builtin_amdgcn_s_memrealtime();
   uint32_t* Lk = (uint32_t*)smem;
   int32_t* Li = (int32_t*)(smem + NT * KC * 4);
 #pragma unroll
@@ -515,7 +524,9 @@ __global__ __launch_bounds__(256) void rank_reg(const void* __restrict__ corpus,
   }
   __syncthreads();
   fold_publish<2 * NW>(Lk, Li, KC, q0, Q, k, r_begin, f);
-  fold_reduce<NT>(smem, f, q0, Q, k, nan_first, index_base, out_s, out_i);
+  if (STAMP && tid == 0) stamp[3] = __builtin_amdgcn_s_memrealtime();
+  fold_reduce<NT>(smem, f, q0, Q, k, nan_first, index_base, out_s, out_i, STAMP ? stamp : nullptr);
+  if (STAMP && tid == 0) stamp[4] = __builtin_amdgcn_s_memrealtime();
 }
 
 // stage-1 LDS: queries [32][D+4] f32, per-wave norms [4][32]; the lists
@@ -1048,7 +1059,9 @@ static hipError_t launch_reg(int64_t N, const void* corpus, const float* q, int6
   // within noise: the wait before the MFMAs is not where this kernel loses time)
   const char* pipe = getenv("MICLIP_RANK_PIPE");
   const bool pp = pipe && pipe[0] == '1';
-  auto fn = nb9 ? rank_reg<D, 9, 7, false, false, false, DT>
+  const char* stp = getenv("MICLIP_RANK_STAMP");
+  auto fn = (stp && stp[0] == '1') ? rank_reg<D, 8, 6, false, false, false, DT, true>
+            : nb9 ? rank_reg<D, 9, 7, false, false, false, DT>
             : (probe && probe[0] == '1') ? (il ? rank_reg<D, 8, 6, true, true, false, DT> : rank_reg<D, 8, 6, true, false, false, DT>)
             : il ? (pp ? rank_reg<D, 8, 6, false, true, true, DT> : rank_reg<D, 8, 6, false, true, false, DT>)
                  : (pp ? rank_reg<D, 8, 6, false, false, true, DT> : rank_reg<D, 8, 6, false, false, false, DT>);
@@ -1167,3 +1180,17 @@ hipError_t rank_of_targets(const float* S, int64_t Q, int64_t N, const int64_t* 
 }
 
 }  // namespace miclip
+
+// Diagnostics (A/B build): the rank_reg stamps of the last MICLIP_RANK_STAMP launch, 256 x 10
+extern "C" int mi_debug_rank_stamp(unsigned long long* host, int n) {
+#if MICLIP_AB
+  if (!host || n < 0) return -1;
+  if (n > 256 * 10) n = 256 * 10;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(miclip::g_rank_stamp), n * sizeof(unsigned long long), 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+#else
+  (void)host;
+  (void)n;
+  return -2;   // A/B build only
+#endif
+}

@@ -225,11 +225,20 @@ constexpr int FQ = 32;   // queries per ranking workgroup (MFMA N)
 // are zeroed by a hipMemsetAsync ahead of the launch.
 constexpr size_t fold_lds(int NT) { return 256 + (size_t)NT * 16 * 8; }
 
+// Two levels: workgroups are grouped by FOLD_GS consecutive row blocks; the last arrival of
+// a group merges the group's slabs into a group slab, and the last group to finish merges
+// the group slabs into the result.  One reducer over ~250 slabs read 32 slabs per thread
+// in dependent batches: 60-100 us at the end of every large call (scripts/rank_stamp.py).
+constexpr int FOLD_GS = 32;
+
 struct FoldWs {
   uint64_t* slab;    // [nwg][Qpad][16]
-  uint32_t* cnt;     // [query blocks]
+  uint64_t* gslab;   // [groups][Qpad][16]
+  uint32_t* cnt;     // [query blocks]: groups finished
+  uint32_t* gcnt;    // [query blocks][groups]: workgroups of a group finished
   uint32_t* gtau;    // [Qpad]
   int64_t Qpad;
+  int ngrp;
 };
 
 template <int NL>
@@ -275,24 +284,34 @@ __device__ __forceinline__ void fold_publish(const uint32_t* Lk, const int32_t* 
 template <int NT>
 __device__ __forceinline__ void fold_reduce(char* smem, const FoldWs& f, int64_t q0, int64_t Q, int k, int nan_first,
                                             int64_t index_base, float* __restrict__ out_s,
-                                            int64_t* __restrict__ out_i) {
+                                            int64_t* __restrict__ out_i, unsigned long long* stamp = nullptr) {
   const int tid = threadIdx.x;
   uint32_t* hdr = (uint32_t*)smem;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's slab stores and gtau atomics
-  __syncthreads();
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    hdr[FQ] = __hip_atomic_fetch_add(&f.cnt[QB], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int nwg = NRB, grp = (int)RB / FOLD_GS, g0 = grp * FOLD_GS;
+  const int gsz = nwg - g0 < FOLD_GS ? nwg - g0 : FOLD_GS;
+  // ticket: agent-scope release of this workgroup's stores, counter, and on the last arrival an
+  // acquire of everyone else's (cdna_hip_programming.md §6 G16's counter form)
+  auto last_arrival = [&](uint32_t* counter, uint32_t total) -> bool {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's slab stores and gtau atomics
+    __syncthreads();
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      hdr[FQ] = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    const bool last = hdr[FQ] == total - 1;
+    if (last && tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();   // every thread has read the ticket before hdr is reused
+    return last;
+  };
+  if (!last_arrival(f.gcnt + (int64_t)QB * f.ngrp + grp, (uint32_t)gsz)) {
+    if (stamp && tid == 0) stamp[5] = __builtin_amdgcn_s_memrealtime();
+    return;
   }
-  __syncthreads();
-  if (hdr[FQ] != (uint32_t)NRB - 1) return;            // not the last arrival of this query block
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  if (tid < FQ) hdr[tid] = 0u;
-  __syncthreads();
   uint64_t* buf = (uint64_t*)(smem + 256);
   const int nq = (int)(Q - q0 < FQ ? Q - q0 : FQ);
   int g = 1;
@@ -301,101 +320,148 @@ __device__ __forceinline__ void fold_reduce(char* smem, const FoldWs& f, int64_t
   const int qi = tid / tpq, sub = tid - qi * tpq;
   const bool act = qi < nq;
   const int64_t q = q0 + qi;
-  uint64_t L[16];
+  const int nld = (k + 1) >> 1;                        // 16-byte pieces of a slab line holding k entries
+
+  // merge `count` slab lines (slab w of query q at base[(w Qpad + q) 16]) into the query's top-k:
+  // into gdst's line (sorted packed keys, zeros after) or, final, into out_s / out_i
+  auto reduce = [&](const uint64_t* base, int count, uint64_t* gdst) {
+    if (tid < FQ) hdr[tid] = 0u;
+    __syncthreads();
+    uint64_t L[16];
 #pragma unroll
-  for (int p = 0; p < 16; ++p) L[p] = 0ull;
-  auto take = [&](uint64_t e, uint64_t tauP) {        // into the sorted (desc) top-16
-    if (e < tauP || e <= L[15]) return;
+    for (int p = 0; p < 16; ++p) L[p] = 0ull;
+    auto take = [&](uint64_t e, uint64_t tauP) {        // into the sorted (desc) top-16
+      if (e < tauP || e <= L[15]) return;
 #pragma unroll
-    for (int p = 15; p > 0; --p) L[p] = e > L[p - 1] ? L[p - 1] : (e > L[p] ? e : L[p]);
-    L[0] = e > L[0] ? e : L[0];
-  };
-  if (act) {
-    const uint64_t tauP = (uint64_t)__hip_atomic_fetch_max(&f.gtau[q], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                          << 32;
-    const int nwg = NRB;
-    constexpr int BATCH = 8;
-    for (int w0 = sub; w0 < nwg; w0 += BATCH * tpq) {
-      uint4 h0[BATCH], h1[BATCH];                      // entries 0..3 of BATCH slabs, loads in flight together
+      for (int p = 15; p > 0; --p) L[p] = e > L[p - 1] ? L[p - 1] : (e > L[p] ? e : L[p]);
+      L[0] = e > L[0] ? e : L[0];
+    };
+    if (act) {
+      // after the acquire a plain (atomic) load sees every workgroup's raise; the fetch_max(0) it
+      // replaces was a device-scope RMW per lane, tpq lanes to one address
+      const uint64_t tauP = (uint64_t)__hip_atomic_load(&f.gtau[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) << 32;
+      // whole slab lines, unconditionally, a batch at a time (all pieces in flight together)
+      constexpr int BATCH = 4;
+      for (int w0 = sub; w0 < count; w0 += BATCH * tpq) {
+        uint4 hv[BATCH][8];
 #pragma unroll
-      for (int b = 0; b < BATCH; ++b) {
-        const int w = w0 + b * tpq;
-        const uint4* p = (const uint4*)(f.slab + ((int64_t)(w < nwg ? w : 0) * f.Qpad + q) * 16);
-        h0[b] = p[0];
-        h1[b] = p[1];
-      }
+        for (int b = 0; b < BATCH; ++b) {
+          const int w = w0 + b * tpq;
+          const uint4* p = (const uint4*)(base + ((int64_t)(w < count ? w : 0) * f.Qpad + q) * 16);
 #pragma unroll
-      for (int b = 0; b < BATCH; ++b) {
-        const int w = w0 + b * tpq;
-        if (w >= nwg) continue;
-        take(((uint64_t)h0[b].y << 32) | h0[b].x, tauP);
-        take(((uint64_t)h0[b].w << 32) | h0[b].z, tauP);
-        take(((uint64_t)h1[b].y << 32) | h1[b].x, tauP);
-        const uint64_t e3 = ((uint64_t)h1[b].w << 32) | h1[b].z;
-        take(e3, tauP);
-        if (k > 4 && e3 != 0ull && e3 >= tauP) {       // the slab continues above the threshold (rare)
-          const uint4* p = (const uint4*)(f.slab + ((int64_t)w * f.Qpad + q) * 16);
-          for (int c = 2; 2 * c < k; ++c) {
-            const uint4 v = p[c];
-            const uint64_t a = ((uint64_t)v.y << 32) | v.x, bb = ((uint64_t)v.w << 32) | v.z;
-            take(a, tauP);
-            take(bb, tauP);
-            if (bb == 0ull || bb < tauP) break;
+          for (int c = 0; c < 8; ++c) hv[b][c] = p[c];
+        }
+#pragma unroll
+        for (int b = 0; b < BATCH; ++b) {
+          if (w0 + b * tpq >= count) continue;
+#pragma unroll
+          for (int c = 0; c < 8; ++c) {
+            if (c >= nld) break;
+            take(((uint64_t)hv[b][c].y << 32) | hv[b][c].x, tauP);
+            take(((uint64_t)hv[b][c].w << 32) | hv[b][c].z, tauP);
           }
         }
       }
     }
-  }
-  int m = 0;
+    // cut: the largest k-th key among the query's tpq threads (one of them holds k entries at or
+    // above it, so the query's k-th is too); entries below it cannot rank, so fewer are appended
+    // and counted.  Ties on the key stay in (the cut compares keys only).
+    uint64_t lk = 0ull;
 #pragma unroll
-  for (int p = 0; p < 16; ++p) m += L[p] != 0ull ? 1 : 0;
-  uint64_t* qb = buf + (int64_t)qi * tpq * 16;
-  if (act && m) {
-    const uint32_t at = atomicAdd(&hdr[qi], (uint32_t)m);   // LDS
-#pragma unroll
-    for (int p = 0; p < 16; ++p)
-      if (p < m) qb[at + p] = L[p];
-  }
-  __syncthreads();
-  if (!act) return;
-  const int n = (int)hdr[qi];
-  int rk[16];
-#pragma unroll
-  for (int p = 0; p < 16; ++p) rk[p] = 0;
-  for (int j = 0; j < n; ++j) {
-    const uint64_t e = qb[j];
-#pragma unroll
-    for (int p = 0; p < 16; ++p) rk[p] += e > L[p] ? 1 : 0;
-  }
-#pragma unroll
-  for (int p = 0; p < 16; ++p)
-    if (p < m && rk[p] < k) {
-      out_s[q * k + rk[p]] = decode_key((uint32_t)(L[p] >> 32), nan_first);
-      out_i[q * k + rk[p]] = index_base + (int64_t)(uint32_t)~(uint32_t)L[p];
+    for (int p = 0; p < 16; ++p) lk = p == k - 1 ? L[p] : lk;
+    uint32_t tk = (uint32_t)(lk >> 32);
+    if (tpq <= 64 && (tpq & (tpq - 1)) == 0) {   // the query's threads: an aligned power-of-two lane group
+      for (int off = 1; off < tpq; off <<= 1) {
+        const uint32_t o = (uint32_t)__shfl_xor((int)tk, off, 64);
+        tk = o > tk ? o : tk;
+      }
+    } else {
+      tk = 0u;
     }
-  for (int r = n + sub; r < k; r += tpq) {             // fewer than k rows in all
-    out_s[q * k + r] = -INFINITY;
-    out_i[q * k + r] = -1;
+    const uint64_t cut = (uint64_t)tk << 32;
+    int m = 0;
+#pragma unroll
+    for (int p = 0; p < 16; ++p) m += (L[p] != 0ull && L[p] >= cut) ? 1 : 0;   // a prefix: L is sorted
+    uint64_t* qb = buf + (int64_t)qi * tpq * 16;
+    if (act && m) {
+      const uint32_t at = atomicAdd(&hdr[qi], (uint32_t)m);   // LDS
+#pragma unroll
+      for (int p = 0; p < 16; ++p)
+        if (p < m) qb[at + p] = L[p];
+    }
+    __syncthreads();
+    if (act) {
+      const int n = (int)hdr[qi];
+      int rk[16];
+#pragma unroll
+      for (int p = 0; p < 16; ++p) rk[p] = 0;
+      for (int j = 0; j < n; ++j) {
+        const uint64_t e = qb[j];
+#pragma unroll
+        for (int p = 0; p < 16; ++p) rk[p] += e > L[p] ? 1 : 0;
+      }
+      if (gdst) {   // the group's top-k as a slab line: ranks 0 .. k - 1, zeros after
+        uint64_t* line = gdst + ((int64_t)q) * 16;
+#pragma unroll
+        for (int p = 0; p < 16; ++p)
+          if (p < m && rk[p] < k) line[rk[p]] = L[p];
+        for (int r = (n < k ? n : k) + sub; r < 2 * nld; r += tpq) line[r] = 0ull;
+      } else {
+#pragma unroll
+        for (int p = 0; p < 16; ++p)
+          if (p < m && rk[p] < k) {
+            out_s[q * k + rk[p]] = decode_key((uint32_t)(L[p] >> 32), nan_first);
+            out_i[q * k + rk[p]] = index_base + (int64_t)(uint32_t)~(uint32_t)L[p];
+          }
+        for (int r = n + sub; r < k; r += tpq) {           // fewer than k rows in all
+          out_s[q * k + r] = -INFINITY;
+          out_i[q * k + r] = -1;
+        }
+      }
+    }
+    __syncthreads();
+  };
+
+  if (stamp && tid == 0) stamp[5] = __builtin_amdgcn_s_memrealtime();
+  if (f.ngrp == 1) {                                   // one group: its last arrival writes the result
+    if (stamp && tid == 0) stamp[6] = __builtin_amdgcn_s_memrealtime();
+    reduce(f.slab, nwg, nullptr);
+    if (stamp && tid == 0) stamp[8] = __builtin_amdgcn_s_memrealtime();
+    return;
   }
+  reduce(f.slab + (int64_t)g0 * f.Qpad * 16, gsz, f.gslab + (int64_t)grp * f.Qpad * 16);
+  if (stamp && tid == 0) stamp[6] = __builtin_amdgcn_s_memrealtime();
+  if (!last_arrival(f.cnt + QB, (uint32_t)f.ngrp)) return;
+  if (stamp && tid == 0) stamp[7] = __builtin_amdgcn_s_memrealtime();
+  reduce(f.gslab, f.ngrp, nullptr);
+  if (stamp && tid == 0) stamp[8] = __builtin_amdgcn_s_memrealtime();
 }
 
 
 static inline int64_t qpad(int64_t Q) { return (Q + FQ - 1) / FQ * FQ; }
 static inline size_t al128(size_t b) { return (b + 127) / 128 * 128; }
 
-// in-launch merge workspace: slabs [nwg][Qpad][16] u64, counters [Qpad / 32] u32, gtau [Qpad] u32
+// in-launch merge workspace: slabs [nwg][Qpad][16] u64, group slabs [groups][Qpad][16] u64,
+// counters [Qpad / 32] u32, group counters [Qpad / 32][groups] u32, gtau [Qpad] u32 (the last
+// three contiguous: fold_zero clears them with one memset)
+static inline int64_t fold_groups(int64_t nwg) { return (nwg + FOLD_GS - 1) / FOLD_GS; }
+
 static inline size_t fold_ws_bytes(int64_t nwg, int64_t Q) {
-  const int64_t qp = qpad(Q);
-  return (size_t)(nwg * qp) * 128 + al128((size_t)(qp / FQ) * 4) + al128((size_t)qp * 4);
+  const int64_t qp = qpad(Q), ng = fold_groups(nwg);
+  return (size_t)((nwg + ng) * qp) * 128 + al128((size_t)(qp / FQ) * 4) + al128((size_t)(qp / FQ * ng) * 4) +
+         al128((size_t)qp * 4);
 }
 
 static inline FoldWs fold_ws(void* ws, int64_t nwg, int64_t Q) {
-  const int64_t qp = qpad(Q);
+  const int64_t qp = qpad(Q), ng = fold_groups(nwg);
   FoldWs f;
   f.slab = (uint64_t*)ws;
-  f.cnt = (uint32_t*)((char*)ws + (size_t)(nwg * qp) * 128);
-  f.gtau = (uint32_t*)((char*)f.cnt + al128((size_t)(qp / FQ) * 4));
+  f.gslab = (uint64_t*)((char*)ws + (size_t)(nwg * qp) * 128);
+  f.cnt = (uint32_t*)((char*)f.gslab + (size_t)(ng * qp) * 128);
+  f.gcnt = (uint32_t*)((char*)f.cnt + al128((size_t)(qp / FQ) * 4));
+  f.gtau = (uint32_t*)((char*)f.gcnt + al128((size_t)(qp / FQ * ng) * 4));
   f.Qpad = qp;
+  f.ngrp = (int)ng;
   return f;
 }
 

@@ -17,7 +17,7 @@ def main():
     dts = {"f32": (torch.float32,), "bf16": (torch.bfloat16,)}.get(os.environ.get("RC_DT", ""),
                                                                    (torch.float32, torch.bfloat16))
     for dt in dts:
-        corpus = torch.randn(1_000_000, 512, device=dev, generator=g).to(dt)
+        corpus = torch.randn(int(os.environ.get("RC_N", 1_000_000)), 512, device=dev, generator=g).to(dt)
         q = torch.nn.functional.normalize(torch.randn(32, 512, device=dev, generator=g), dim=1)
         for _ in range(10):
             retrieval.rank_topk(corpus, q, 10)
