@@ -41,7 +41,7 @@ def main():
         last = st[st[:, 6] > st[:, 5]]   # this launch's reducer (older launches' stamps 6-9 linger)
         for row in last:
             r = (row - t0) / 100.0
-            print(f"  group reducer: ticket {r[5]:.1f} group merged {r[6]:.1f}"
+            print(f"  group reducer: ticket {r[5]:.1f} slabs taken {r[9]:.1f} group merged {r[6]:.1f}"
                   + (f" final ticket {r[7]:.1f} final merged {r[8]:.1f}" if row[8] > row[6] else "") + f" exit {r[4]:.1f}")
         del corpus
 
