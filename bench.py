@@ -50,8 +50,12 @@ def parse():
     ap.add_argument("--queries", type=int, default=32)
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--image-chunk", type=int, default=None)
-    ap.add_argument("--weights", choices=["bf16", "fp8"], default="bf16",
-                    help="fp8: vision GEMMs on the MX-fp8 block-scaled MFMA (BASELINE configs[4])")
+    ap.add_argument("--weights", choices=["bf16", "fp8", "fp32"], default="bf16",
+                    help="fp8: vision GEMMs on the MX-fp8 block-scaled MFMA (BASELINE configs[4]); "
+                         "fp32: the parity mode (every GEMM on the exact-f32 MFMA, model.float())")
+    ap.add_argument("--no-parity-mode", action="store_true",
+                    help="skip the fp32-tower (R@K parity mode) measurement beside the bf16 line")
+    ap.add_argument("--parity-steps", type=int, default=3)
     ap.add_argument("--cpu-frames", type=int, default=256,
                     help="CPU baseline sample: frames encoded at batch 64 (secondary figure)")
     ap.add_argument("--cpu-frames-b1", type=int, default=64,
@@ -103,6 +107,20 @@ def kernel_timing(model, cfg, chunk, reps=20):
 
     gemms = [("gemm_qkv", 3 * W, W, 0, outb), ("gemm_out", W, W, 0, outb), ("gemm_fc", 4 * W, W, 1, outb),
              ("gemm_proj", W, 4 * W, 0, outb)]
+    if getattr(model, "weights", "bf16") == "fp32":
+        # the parity mode's exact-f32 MFMA GEMM (precise.hip): f32 operands, epilogue 1 = QuickGELU
+        del A, outb
+        Af = torch.randn(M, 4 * W, device=dev, generator=g) * 0.5
+        Wf = torch.randn(4 * W, 4 * W, device=dev, generator=g) * 0.02
+        outF = torch.empty(M, 4 * W, device=dev)
+        for name, Nn, K, epi, _ in gemms:
+            Ak, Wk = Af[:, :K].contiguous(), Wf[:Nn, :K].contiguous()
+            timed(name, lambda Nn=Nn, K=K, epi=epi, Ak=Ak, Wk=Wk: N.check(
+                L.mi_op_gemm_f32(Ak.data_ptr(), Wk.data_ptr(), bias.data_ptr(), outF.data_ptr(), M, Nn, K, epi, sp),
+                "gemm_f32"), flops=2.0 * M * Nn * K)
+            del Ak, Wk
+        del Af, Wf, outF
+        return res
     if getattr(model, "weights", "bf16") == "fp8":
         # MX-fp8 operands: e4m3 codes + stage-major e8m0 scales (mi_op_quantize_mx)
         def mx(t):
@@ -399,6 +417,48 @@ def mirror_timing(corpus, q, n, exact_us):
             "certified": f"{mc.certified}/{mc.certified + mc.fallbacks}"}
 
 
+def parity_mode(args, dev, pixels, tokens, Q, k, base, chunk):
+    """The R@K parity mode: the same step on the
+    fp32 tower (`weights="fp32"`, openai/CLIP's fp32 arithmetic, every GEMM on
+    the exact-f32 MFMA), timed like the headline over --parity-steps steps,
+    with the roofline of its c_fc GEMM against the 157.3 TF f32 MFMA peak."""
+    import torch
+    from miclip import api, retrieval
+    model, _ = api.load(args.model, device=dev, image_chunk=chunk, weights="fp32")
+    cfg = model.cfg
+
+    def step():
+        emb = model.encode_image(pixels, out_dtype=torch.float32)
+        txt = model.encode_text(tokens, normalize=True, out_dtype=torch.float32)
+        return retrieval.rank_topk(emb, txt, k, index_base=base)
+
+    step()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.parity_steps):
+        step()
+    torch.cuda.synchronize(dev)
+    ms = (time.perf_counter() - t0) / args.parity_steps * 1e3
+    kern = kernel_timing(model, cfg, chunk, reps=5)
+    M = chunk * cfg.vision_tokens
+    fl = 2.0 * M * 4 * cfg.vision_width * cfg.vision_width
+    fc = kern["gemm_fc"]["us"]
+    step_flops = pixels.shape[0] * cfg.image_flops() + Q * cfg.text_flops() + 2.0 * pixels.shape[0] * Q * cfg.embed_dim
+    out = {"weights": "fp32", "value": round(pixels.shape[0] / (ms / 1e3), 1), "unit": "frames/s",
+           "ms_per_step": round(ms, 3), "steps": args.parity_steps,
+           "note": "fp32 tower: the mode whose R@1/5/10 equal the float64 oracle flow (tests/test_gpu_rk_flow.py)",
+           "roofline": {"bound": "mfma", "kernel": "gemm_f32 (precise.hip; mlp.c_fc + QuickGELU, exact-f32 MFMA)",
+                        "achieved": round(fl / (fc * 1e-6) / 1e12, 1), "peak": F32_MFMA_PEAK_TFLOPS,
+                        "unit": "TFLOP/s", "frac": round(fl / (fc * 1e-6) / 1e12 / F32_MFMA_PEAK_TFLOPS, 4),
+                        "traffic": None, "launch_shape": [M, 4 * cfg.vision_width, cfg.vision_width],
+                        "avg_launch_us": fc},
+           "mfma_frac_end_to_end_f32": round(step_flops / (ms / 1e3) / (F32_MFMA_PEAK_TFLOPS * 1e12), 4),
+           "kernels": kern}
+    del model
+    torch.cuda.empty_cache()
+    return out
+
+
 def launch_workers(args):
     """`bench.py --gpus N` without torch.distributed.run: start N worker
     processes (one per GPU) through torch.distributed.run as a CHILD process,
@@ -544,7 +604,7 @@ def main():
         F_frame, F_text = cfg.image_flops(), cfg.text_flops()
         step_flops = Nf * world * F_frame + Q * world * F_text + 2.0 * Nf * world * Q * cfg.embed_dim
         # against the peak of the arithmetic the step's GEMMs run on (fp8 runs: the MX-fp8 peak)
-        step_peak = FP8_PEAK_TFLOPS if args.weights == "fp8" else BF16_PEAK_TFLOPS
+        step_peak = {"fp8": FP8_PEAK_TFLOPS, "fp32": F32_MFMA_PEAK_TFLOPS}.get(args.weights, BF16_PEAK_TFLOPS)
         mfma_frac = step_flops / (ms / 1e3) / (step_peak * 1e12) / world
         dom = kern.get("gemm_fc")
         M = chunk * cfg.vision_tokens
@@ -554,20 +614,25 @@ def main():
             ach = fl / (dom["us"] * 1e-6) / 1e12
             shape = [M, 4 * cfg.vision_width, cfg.vision_width]
             fp8 = args.weights == "fp8"
-            traffic, tsrc, busy = pmc_traffic(shape, fp8)
-            peak = FP8_PEAK_TFLOPS if fp8 else BF16_PEAK_TFLOPS
-            eb = 1 if fp8 else 2            # operand element bytes (fp8 adds 1/64 B of scales per element)
+            f32 = args.weights == "fp32"
+            traffic, tsrc, busy = (None, None, None) if f32 else pmc_traffic(shape, fp8)
+            peak = FP8_PEAK_TFLOPS if fp8 else (F32_MFMA_PEAK_TFLOPS if f32 else BF16_PEAK_TFLOPS)
+            eb = 1 if fp8 else (4 if f32 else 2)   # operand element bytes (fp8 adds 1/64 B of scales per element)
             roof = {"bound": "mfma",
                     "kernel": ("gemm_mx_kernel<EPI_GELU_BF16> (mlp.c_fc + QuickGELU, MX-fp8 operands)" if fp8
+                               else "gemm_f32 (precise.hip; mlp.c_fc + QuickGELU, exact-f32 MFMA)" if f32
                                else "gemm_8q_kernel<EPI_GELU_BF16> (8-phase interleaved persistent, 256x256x64, descriptor DMAs; mlp.c_fc + QuickGELU)"),
                     "achieved": round(ach, 1), "peak": peak, "unit": "TFLOP/s",
                     "frac": round(ach / peak, 4), "traffic": traffic,
                     "traffic_source": tsrc,
                     "mfma_busy_pmc": busy,
                     "algorithmic_bytes": int(eb * (1 + fp8 / 64) * (M * cfg.vision_width + 4 * cfg.vision_width ** 2)
-                                             + 2 * M * 4 * cfg.vision_width),
+                                             + (4 if f32 else 2) * M * 4 * cfg.vision_width),
                     "flops_per_launch": fl, "launch_shape": [M, 4 * cfg.vision_width, cfg.vision_width],
                     "avg_launch_us": dom["us"]}
+        parity = None
+        if not args.no_parity_mode and world == 1 and args.weights == "bf16":
+            parity = parity_mode(args, dev, pixels, tokens, Q, k, base, chunk)
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(cfg, Nf, Q, k, args.cpu_frames_b1, args.cpu_frames)
@@ -585,7 +650,7 @@ def main():
             "value": round(value, 1), "unit": "frames/s", "n_gpus": world, "world_size_seen": seen,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
             "scaling": "strong" if strong else "weak", "vs_baseline": None,
-            "dtype": "bf16" if args.weights == "bf16" else "fp8-e4m3(MX) vision GEMMs, bf16 rest",
+            "dtype": {"bf16": "bf16", "fp32": "f32"}.get(args.weights, "fp8-e4m3(MX) vision GEMMs, bf16 rest"),
             "data": "synthetic (random pixels/tokens, deterministic random-init weights of the real architecture)",
             "config": {"workload": workload, "frames_per_gpu": Nf,
                        "global_frames": args.global_frames if strong else Nf * world, "queries": Q, "k": k,
@@ -593,6 +658,7 @@ def main():
             "roofline": roof,
             "rank_roofline": rank_roof,
             "mfma_frac_end_to_end": round(mfma_frac, 4),
+            "parity_mode": parity,
             "kernels": kern,
             "cpu_baseline": cpu,
         }

@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <mutex>
 #include <string>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -811,6 +812,16 @@ int mi_mirror_build(const void* corpus, int64_t N, int64_t D, int corpus_dtype, 
   return MI_OK;
 }
 
+int mi_normalize_rows_f16(const void* rows, int64_t N, int64_t D, void* out, void* stream) {
+  if (N < 0) return fail(MI_ERR_ARG, "negative size");
+  if (D < 1 || D > 1024) return fail(MI_ERR_UNSUPPORTED, "mi_normalize_rows_f16: D must be in [1, 1024] (got %lld)", (long long)D);
+  if (N == 0) return MI_OK;
+  if (!rows || !out) return fail(MI_ERR_ARG, "mi_normalize_rows_f16: null pointer");
+  if (N > ((int64_t)1 << 40)) return fail(MI_ERR_UNSUPPORTED, "mi_normalize_rows_f16: N too large");
+  HIP_TRY(normalize_rows_f16((const uint16_t*)rows, N, (int)D, (uint16_t*)out, (hipStream_t)stream));
+  return MI_OK;
+}
+
 size_t mi_rank_mirror_workspace_bytes(int64_t N, int64_t Q) {
   if (N < 0 || Q < 0) return 0;
   return rank_mirror_workspace_bytes(N, Q);
@@ -1022,6 +1033,9 @@ int mi_jpeg_decode(const uint8_t* data, int64_t data_bytes, const int64_t* seg_o
 
 int mi_host_gather(void* dst, const void* const* src, const int64_t* len, int64_t n, int32_t threads) {
   if (!dst || n < 0 || (n > 0 && (!src || !len))) return fail(MI_ERR_ARG, "mi_host_gather: bad arguments");
+  // no C++ exception may cross the C ABI (std::bad_alloc, std::system_error from a thread
+  // that cannot be created, e.g. under a tight cgroup pids limit)
+  try {
   std::vector<int64_t> off((size_t)n + 1, 0);
   for (int64_t i = 0; i < n; ++i) {
     if (len[i] < 0 || (len[i] > 0 && !src[i])) return fail(MI_ERR_ARG, "mi_host_gather: bad piece %lld", (long long)i);
@@ -1046,9 +1060,20 @@ int mi_host_gather(void* dst, const void* const* src, const int64_t* len, int64_
   }
   std::vector<std::thread> th;
   th.reserve(T);
-  for (int t = 0; t < T; ++t) th.emplace_back(work, total * t / T, total * (t + 1) / T);
+  int started = 0;
+  for (; started < T; ++started) {
+    try {
+      th.emplace_back(work, total * started / T, total * (started + 1) / T);
+    } catch (const std::system_error&) {
+      break;   // no more threads: the calling thread copies the remaining ranges
+    }
+  }
+  if (started < T) work(total * started / T, total);
   for (auto& x : th) x.join();
   return MI_OK;
+  } catch (const std::exception& ex) {
+    return fail(MI_ERR_STATE, "mi_host_gather: %s", ex.what());
+  }
 }
 
 }  // extern "C"

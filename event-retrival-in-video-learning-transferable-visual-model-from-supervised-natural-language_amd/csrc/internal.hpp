@@ -187,6 +187,17 @@ void rank_cert_delta(int dt, float& d_rel, float& d_abs);
 hipError_t rank_cert_topk(const void* corpus, int64_t N, int dt, const float* q, int64_t Q, int k, int64_t base,
                           int norm_mode, int nan_first, float* out_s, int64_t* out_i, void* ws, int32_t** cert_out,
                           hipStream_t s);
+// float16 corpus rows normalised as NumPy does it in float16 (corpus.hip;
+// embedding_service.py:209-210): the host-planned pairwise-summation tree of
+// the row's squares (leaves <= 128 elements, ops 0 = next leaf, 1 = add)
+struct PairwisePlan {
+  int32_t nleaf, nops;
+  int16_t start[8], len[8];
+  int8_t ops[16];
+};
+PairwisePlan pairwise_plan(int D);
+// out[r] = f16(in[r] / f16 norm(in[r])) per NumPy float16; D in [1, 1024]; in == out allowed
+hipError_t normalize_rows_f16(const uint16_t* in, int64_t N, int D, uint16_t* out, hipStream_t s);
 }  // namespace miclip
 
 #include <vector>

@@ -281,7 +281,8 @@ __global__ __launch_bounds__(64) void jpeg_entropy_kernel(const uint8_t* __restr
                                                           const int64_t* __restrict__ seg_end,
                                                           const JpegHuff* __restrict__ huff,
                                                           const int32_t* __restrict__ huff_idx, int nsets,
-                                                          JpegGeom g, int nframes, int16_t* __restrict__ coef) {
+                                                          JpegGeom g, int nframes, int16_t* __restrict__ coef,
+                                                          int64_t data_bytes, const uint8_t* __restrict__ skip) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   JpegHuff* sh = (JpegHuff*)smem;
   uint8_t* zz = (uint8_t*)smem + (LDS_T ? nsets * 4 * (int)sizeof(JpegHuff) : 0);
@@ -296,8 +297,10 @@ __global__ __launch_bounds__(64) void jpeg_entropy_kernel(const uint8_t* __restr
   const int64_t lane = (int64_t)blockIdx.x * 64 + threadIdx.x;
   if (lane >= (int64_t)nframes * g.nseg) return;
   const int f = (int)(lane / g.nseg), s = (int)(lane % g.nseg);
+  if (skip && skip[f]) return;   // the chunked decode's frames (the fix-up pass takes the others)
   BitReader br;
-  br.init(data + seg_off[lane], data + seg_end[lane]);
+  const int64_t so = min(max(seg_off[lane], (int64_t)0), data_bytes);
+  br.init(data + so, data + min(max(seg_end[lane], so), data_bytes));
   const int set = huff_idx ? huff_idx[f] : f;
   const JpegHuff* T = (LDS_T ? (const JpegHuff*)sh : huff) + (int64_t)set * 4;
   int16_t* out = coef + (int64_t)f * g.blocks_per_frame * 64;
@@ -481,18 +484,54 @@ struct JpChunks {
   const uint32_t* ulen;    // [B] unstuffed bytes of frame f
 };
 
-// chunk layout: T_f = max(1, ceil(raw bytes / JP_CHUNK)) chunks per frame; one workgroup
+// chunk layout: T_f = max(1, ceil(raw bytes / JP_CHUNK)) chunks per frame; one workgroup.
+// The caller's segments are sanitised first (mi_jpeg_decode's contract: disjoint, in
+// frame order, inside [0, data_bytes)): each is clipped to [0, data_bytes), and a frame
+// whose segment starts before the end of an earlier frame's (a repeated or out-of-order
+// frame) gets no chunks -- vf[f] = 0 -- and is decoded afterwards by the serial kernel,
+// which only reads the data.  So sum T_f <= data_bytes / JP_CHUNK + B = the workspace's
+// nmax, and the valid frames' unstuffed streams (at their own byte offsets) never overlap.
 __global__ __launch_bounds__(1024) void jp_layout_kernel(const int64_t* __restrict__ seg_off,
                                                          const int64_t* __restrict__ seg_end, int nframes,
-                                                         int64_t* __restrict__ cbase, int64_t* __restrict__ ubase) {
+                                                         int64_t data_bytes, int64_t* __restrict__ cbase,
+                                                         int64_t* __restrict__ ubase, int64_t* __restrict__ sso,
+                                                         int64_t* __restrict__ sse, uint8_t* __restrict__ vf) {
   __shared__ int64_t part[1024];
   const int tid = threadIdx.x;
   const int per = (nframes + 1023) / 1024;
   const int f0 = tid * per, f1 = min(nframes, f0 + per);
+  auto clip = [&](int f, int64_t& o, int64_t& e) {
+    o = min(max(seg_off[f], (int64_t)0), data_bytes);
+    e = min(max(seg_end[f], o), data_bytes);
+  };
+  // prefix max of the clipped segment ends over all earlier frames
+  int64_t mx = -1;
+  for (int f = f0; f < f1; ++f) {
+    int64_t o, e;
+    clip(f, o, e);
+    mx = max(mx, e);
+  }
+  part[tid] = mx;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {   // inclusive Hillis-Steele max scan
+    const int64_t v = tid >= o ? part[tid - o] : -1;
+    __syncthreads();
+    part[tid] = max(part[tid], v);
+    __syncthreads();
+  }
+  int64_t runmax = tid > 0 ? part[tid - 1] : -1;
+  __syncthreads();
   int64_t sum = 0;
   for (int f = f0; f < f1; ++f) {
-    const int64_t len = seg_end[f] - seg_off[f];
-    sum += len > JP_CHUNK ? (len + JP_CHUNK - 1) / JP_CHUNK : 1;
+    int64_t o, e;
+    clip(f, o, e);
+    const bool ok = o >= runmax;
+    runmax = max(runmax, e);
+    sso[f] = o;
+    sse[f] = ok ? e : o;
+    vf[f] = ok ? 1 : 0;
+    const int64_t len = e - o;
+    sum += ok ? (len > JP_CHUNK ? (len + JP_CHUNK - 1) / JP_CHUNK : 1) : 0;
   }
   part[tid] = sum;
   __syncthreads();
@@ -505,10 +544,10 @@ __global__ __launch_bounds__(1024) void jp_layout_kernel(const int64_t* __restri
   int64_t run = part[tid] - sum;
   for (int f = f0; f < f1; ++f) {
     cbase[f] = run;
-    const int64_t len = seg_end[f] - seg_off[f];
-    run += len > JP_CHUNK ? (len + JP_CHUNK - 1) / JP_CHUNK : 1;
+    const int64_t len = sse[f] - sso[f];
+    run += vf[f] ? (len > JP_CHUNK ? (len + JP_CHUNK - 1) / JP_CHUNK : 1) : 0;
     // unstuffed stream: 4-byte aligned, never past the next frame's start (unstuffed <= raw bytes)
-    ubase[f] = (seg_off[f] + 4 * (int64_t)f + 3) & ~(int64_t)3;
+    ubase[f] = (sso[f] + 4 * (int64_t)f + 3) & ~(int64_t)3;
   }
   if (tid == 1023) cbase[nframes] = part[1023];
 }
@@ -1014,7 +1053,7 @@ __global__ __launch_bounds__(256) void jpeg_color_kernel(const uint8_t* __restri
 struct JpWs {
   size_t bytes;
   size_t o_ustuff, o_cbase, o_ubase, o_ulen, o_cframe, o_cnt, o_coff, o_mk, o_x[2], o_nb[2], o_dc[2], o_ch[2],
-      o_bfirst, o_pred, o_fch;
+      o_bfirst, o_pred, o_fch, o_sso, o_sse, o_vf;
   int64_t nmax;
 };
 
@@ -1041,6 +1080,9 @@ static JpWs jp_layout(int nframes, int64_t data_bytes) {
   w.o_bfirst = carve((size_t)w.nmax * 8);
   w.o_pred = carve((size_t)w.nmax * 12);
   w.o_fch = carve((size_t)(JP_ROUNDS + 1) * B * 4);
+  w.o_sso = carve((size_t)B * 8);
+  w.o_sse = carve((size_t)B * 8);
+  w.o_vf = carve((size_t)B);
   w.bytes = off;
   return w;
 }
@@ -1120,6 +1162,9 @@ hipError_t jpeg_decode(const uint8_t* data, int64_t data_bytes, const int64_t* s
     int64_t* bfirst = (int64_t*)(w + jw.o_bfirst);
     int32_t* pred = (int32_t*)(w + jw.o_pred);
     int32_t* fch = (int32_t*)(w + jw.o_fch);
+    int64_t* sso = (int64_t*)(w + jw.o_sso);
+    int64_t* sse = (int64_t*)(w + jw.o_sse);
+    uint8_t* vf = (uint8_t*)(w + jw.o_vf);
     const int64_t nmax = jw.nmax;
     if ((e = hipMemsetAsync(cframe, 0xFF, (size_t)nmax * 4, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(fch, 0, (size_t)(JP_ROUNDS + 1) * nframes * 4, s)) != hipSuccess) return e;
@@ -1133,15 +1178,16 @@ hipError_t jpeg_decode(const uint8_t* data, int64_t data_bytes, const int64_t* s
           mc.dv[mc.bpm] = (int8_t)bv;
           ++mc.bpm;
         }
-    const dim3 fg((unsigned)((nframes + 255) / 256)), cg((unsigned)((nmax + 255) / 256));
-    hipLaunchKernelGGL(jp_layout_kernel, dim3(1), dim3(1024), 0, s, seg_off, seg_end, nframes, cbase, ubase);
+    const dim3 fg((unsigned)((nframes + 255) / 256)), cg((unsigned)((nmax + 255) / 256)),
+        fg4((unsigned)((nframes + 63) / 64));
+    hipLaunchKernelGGL(jp_layout_kernel, dim3(1), dim3(1024), 0, s, seg_off, seg_end, nframes, data_bytes, cbase, ubase,
+                       sso, sse, vf);
     hipLaunchKernelGGL(jp_chunk_frame_kernel, fg, dim3(256), 0, s, cbase, nframes, cframe);
     const JpChunks ch{cbase, cframe, ubase, ulen};
-    hipLaunchKernelGGL(jp_unstuff_count_kernel, dim3((unsigned)nmax), dim3(256), 0, s, data, seg_off, seg_end, ch, cnt,
-                       mk);
+    hipLaunchKernelGGL(jp_unstuff_count_kernel, dim3((unsigned)nmax), dim3(256), 0, s, data, sso, sse, ch, cnt, mk);
     hipLaunchKernelGGL(jp_unstuff_scan_kernel, fg, dim3(256), 0, s, ch, nframes, cnt, mk, coff, ulen);
-    hipLaunchKernelGGL(jp_unstuff_scatter_kernel, dim3((unsigned)nmax), dim3(256), 0, s, data, seg_off, seg_end, ch, cnt,
-                       coff, ustuff);
+    hipLaunchKernelGGL(jp_unstuff_scatter_kernel, dim3((unsigned)nmax), dim3(256), 0, s, data, sso, sse, ch, cnt, coff,
+                       ustuff);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const size_t tl = lds_t ? nsets * 4 * sizeof(JpegHuff) : 0;
     for (int r = 0; r <= JP_ROUNDS; ++r) {
@@ -1165,15 +1211,20 @@ hipError_t jpeg_decode(const uint8_t* data, int64_t data_bytes, const int64_t* s
       hipLaunchKernelGGL(jp_final_kernel<false>, cg, dim3(256), 80, s, ustuff, ch, nmax, (const JpegHuff*)huff,
                          huff_idx, nsets, g, mc, fin, bfirst, pred, last_changed, coef);
     if ((e = hipGetLastError()) != hipSuccess) return e;
+    // frames outside the chunk layout (repeated / out-of-order segments): the serial decode
+    hipLaunchKernelGGL(jpeg_entropy_kernel<false>, fg4, dim3(64), 80, s, data, seg_off, seg_end, (const JpegHuff*)huff,
+                       huff_idx, nsets, g, nframes, coef, data_bytes, (const uint8_t*)vf);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
   } else {
     const int64_t lanes = (int64_t)nframes * g.nseg;
     const dim3 eg((unsigned)((lanes + 63) / 64));
     if (lds_t)
       hipLaunchKernelGGL(jpeg_entropy_kernel<true>, eg, dim3(64), nsets * 4 * sizeof(JpegHuff) + 80, s, data, seg_off,
-                         seg_end, (const JpegHuff*)huff, huff_idx, nsets, g, nframes, coef);
+                         seg_end, (const JpegHuff*)huff, huff_idx, nsets, g, nframes, coef, data_bytes,
+                         (const uint8_t*)nullptr);
     else
       hipLaunchKernelGGL(jpeg_entropy_kernel<false>, eg, dim3(64), 80, s, data, seg_off, seg_end,
-                         (const JpegHuff*)huff, huff_idx, nsets, g, nframes, coef);
+                         (const JpegHuff*)huff, huff_idx, nsets, g, nframes, coef, data_bytes, (const uint8_t*)nullptr);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
   }

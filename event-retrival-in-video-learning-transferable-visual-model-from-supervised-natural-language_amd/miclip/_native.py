@@ -36,7 +36,7 @@ EXPORTS = (
     "mi_resample_coeffs", "mi_preprocess_workspace_bytes", "mi_preprocess_frames",
     "mi_jpeg_workspace_bytes", "mi_jpeg_decode", "mi_host_gather",
     "mi_op_quantize_mx", "mi_op_gemm_mx",
-    "mi_mirror_build", "mi_rank_mirror_workspace_bytes", "mi_rank_mirror",
+    "mi_mirror_build", "mi_rank_mirror_workspace_bytes", "mi_rank_mirror", "mi_normalize_rows_f16",
 )
 
 
@@ -112,6 +112,7 @@ def _bind(path):
         "mi_rank_merge": (ctypes.c_int, [P, P, I64, I64, I32, ctypes.c_int, P, P, P]),
         "mi_mirror_build": (ctypes.c_int, [P, I64, I64, ctypes.c_int, P, P]),
         "mi_rank_mirror_workspace_bytes": (SZ, [I64, I64]),
+        "mi_normalize_rows_f16": (ctypes.c_int, [P, I64, I64, P, P]),
         "mi_rank_mirror": (ctypes.c_int, [P, P, I64, I64, ctypes.c_int, P, I64, I32, I64, ctypes.c_int, P, P, P, P,
                                           SZ, P]),
         "mi_score_matrix": (ctypes.c_int, [P, I64, I64, ctypes.c_int, P, I64, ctypes.c_int, P, P]),
@@ -134,7 +135,7 @@ def _bind(path):
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
-    if L.mi_abi_version() != 2:
+    if L.mi_abi_version() != 3:
         raise MiClipError("libmiclip ABI version mismatch")
     return L
 

@@ -359,6 +359,66 @@ def _upload(bufs, keep, segl, starts, total, dev, slot=0):
         return d
 
 
+def launch_args(bufs, heads, keep, segl, key, dedupe=True):
+    """mi_jpeg_decode's arguments for the frames ``keep`` of one geometry group
+    ``key`` (their entropy-coded segments ``segl`` concatenated in order):
+    (geom int32[20], huff [nsets, 4] tables, huff_idx int32[B], qtab uint16[B, 4, 64],
+    seg_off / seg_end int64[B * nseg] into the concatenation, starts int64[B + 1]
+    (frame r's bytes at [starts[r], starts[r + 1])), nsets), or None when the
+    frames' table selectors differ."""
+    W, H, nc, samp, ri = key
+    h0 = heads[keep[0]]
+    B = len(keep)
+    lens = np.array([sg[-1][1] - sg[0][0] for sg in segl], np.int64)
+    starts = np.zeros(B + 1, np.int64)
+    np.cumsum(lens, out=starts[1:])
+    if ri:
+        offs = [int(starts[r]) + a - sg[0][0] for r, sg in enumerate(segl) for a, _ in sg]
+        ends = [int(starts[r]) + b - sg[0][0] for r, sg in enumerate(segl) for _, b in sg]
+    else:
+        offs, ends = starts[:-1], starts[1:]
+    # table sets deduplicated: frames of one encoder share one set (and one
+    # cached header object), which the entropy kernel stages in LDS
+    sets, set_of, hidx = [], {}, np.zeros(B, np.int32)
+    qts, qidx, per_head = [], np.zeros(B, np.int64), {}
+    for r, i in enumerate(keep):
+        h = heads[i]
+        e = per_head.get(id(h))
+        if e is None:
+            slots, tabs = [None] * 4, [None] * 4
+            for (tc, th), (bits, vals) in h.huff.items():
+                if th <= 1:
+                    slots[th * 2 + tc], tabs[th * 2 + tc] = _huff_cached(bits, vals)
+            q4 = np.zeros((4, 64), np.uint16)
+            for tq, q in h.qt.items():
+                if tq <= 3:
+                    q4[tq] = q
+            qts.append(q4)
+            e = per_head[id(h)] = (tuple(slots), tabs, len(qts) - 1)
+        k = e[0] if dedupe else r
+        if k not in set_of:
+            set_of[k] = len(sets)
+            sets.append(e[1])
+        hidx[r] = set_of[k]
+        qidx[r] = e[2]
+    qt = np.ascontiguousarray(np.stack(qts)[qidx])
+    nseg = len(segl[0])
+    geom = np.zeros(20, np.int32)
+    geom[:5] = (W, H, nc, ri, nseg)
+    for c in range(nc):
+        geom[5 + 2 * c], geom[6 + 2 * c] = (samp[c] if nc == 3 else (1, 1))
+        geom[11 + c], geom[14 + c], geom[17 + c] = h0.qsel[c], h0.dcsel[c], h0.acsel[c]
+    # per-frame table selectors must agree within the group (they come from the SOS / SOF)
+    if not all(heads[i].qsel == h0.qsel and heads[i].dcsel == h0.dcsel and heads[i].acsel == h0.acsel for i in keep):
+        return None
+    huff = np.zeros((len(sets), 4), dtype=_HUFF_DT)
+    for u, tabs in enumerate(sets):
+        for j, t in enumerate(tabs):
+            if t is not None:
+                huff[u, j] = t
+    return (geom, huff, hidx, qt, np.asarray(offs, np.int64), np.asarray(ends, np.int64), starts, len(sets))
+
+
 def decode_batch(bufs, device="cuda", dedupe=True):
     """Decode JPEG byte strings on the GPU where the geometry allows, Pillow
     otherwise.  Returns a list of uint8 [H, W, 3] device tensors (None for a
@@ -410,59 +470,14 @@ def decode_groups(bufs, device="cuda", dedupe=True, heads=None):
         if not keep:
             continue
         B = len(keep)
-        lens = np.array([sg[-1][1] - sg[0][0] for sg in segl], np.int64)
-        starts = np.zeros(B + 1, np.int64)
-        np.cumsum(lens, out=starts[1:])
-        total = int(starts[-1])
-        if ri:
-            offs = [int(starts[r]) + a - sg[0][0] for r, sg in enumerate(segl) for a, _ in sg]
-            ends = [int(starts[r]) + b - sg[0][0] for r, sg in enumerate(segl) for _, b in sg]
-        else:
-            offs, ends = starts[:-1], starts[1:]
-        # table sets deduplicated: frames of one encoder share one set (and one
-        # cached header object), which the entropy kernel stages in LDS
-        sets, set_of, hidx = [], {}, np.zeros(B, np.int32)
-        qts, qidx, per_head = [], np.zeros(B, np.int64), {}
-        for r, i in enumerate(keep):
-            h = heads[i]
-            e = per_head.get(id(h))
-            if e is None:
-                slots, tabs = [None] * 4, [None] * 4
-                for (tc, th), (bits, vals) in h.huff.items():
-                    if th <= 1:
-                        slots[th * 2 + tc], tabs[th * 2 + tc] = _huff_cached(bits, vals)
-                q4 = np.zeros((4, 64), np.uint16)
-                for tq, q in h.qt.items():
-                    if tq <= 3:
-                        q4[tq] = q
-                qts.append(q4)
-                e = per_head[id(h)] = (tuple(slots), tabs, len(qts) - 1)
-            key = e[0] if dedupe else r
-            if key not in set_of:
-                set_of[key] = len(sets)
-                sets.append(e[1])
-            hidx[r] = set_of[key]
-            qidx[r] = e[2]
-        qt = np.ascontiguousarray(np.stack(qts)[qidx])
-        geom = np.zeros(20, np.int32)
-        geom[:5] = (W, H, nc, ri, nseg)
-        for c in range(nc):
-            geom[5 + 2 * c], geom[6 + 2 * c] = (samp[c] if nc == 3 else (1, 1))
-            geom[11 + c], geom[14 + c], geom[17 + c] = h0.qsel[c], h0.dcsel[c], h0.acsel[c]
-        # per-frame table selectors must agree within the group (they come from the SOS / SOF)
-        sel_ok = [heads[i].qsel == h0.qsel and heads[i].dcsel == h0.dcsel and heads[i].acsel == h0.acsel for i in keep]
-        if not all(sel_ok):
+        args = launch_args(bufs, heads, keep, segl, key, dedupe)
+        if args is None:     # per-frame table selectors differ within the group: the host decoder
             for i in keep:
                 yield _host_group(bufs, i, device)
             continue
-        huff = np.zeros((len(sets), 4), dtype=_HUFF_DT)
-        for u, tabs in enumerate(sets):
-            for j, t in enumerate(tabs):
-                if t is not None:
-                    huff[u, j] = t
+        geom, huff, hidx, qt, offs, ends, starts, nsets = args
+        total = int(starts[-1])
         d_huff = torch.from_numpy(huff.view(np.uint8).reshape(-1)).to(dev)
-        offs = np.asarray(offs, np.int64)
-        ends = np.asarray(ends, np.int64)
         rgb = torch.empty(B, H, W, 3, dtype=torch.uint8, device=dev)
         gp = geom.ctypes.data
         # launches of SUB_FRAMES frames: the host gathers launch j + 1 into the other
@@ -481,7 +496,7 @@ def decode_groups(bufs, device="cuda", dedupe=True, heads=None):
             # without dedupe frame f uses set f: this launch's frames start at set j0
             hp = d_huff.data_ptr() + (0 if dedupe else j0 * 4 * HUFF_BYTES)
             N.check(L.mi_jpeg_decode(d_data.data_ptr(), sub_total, d_off.data_ptr(), d_end.data_ptr(), hp,
-                                     d_hidx.data_ptr() if dedupe else None, len(sets), d_qt.data_ptr(), gp, j1 - j0,
+                                     d_hidx.data_ptr() if dedupe else None, nsets, d_qt.data_ptr(), gp, j1 - j0,
                                      rgb[j0:j1].data_ptr(), ws.data_ptr(), nb, N.stream_ptr(dev)), "mi_jpeg_decode")
             del d_data
         del ws

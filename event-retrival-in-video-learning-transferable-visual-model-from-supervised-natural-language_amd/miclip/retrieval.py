@@ -88,6 +88,25 @@ def rank_topk(corpus, queries, k, index_base=0, norm="l2", nan_policy="first"):
     return out_s[:, :kk], out_i[:, :kk]
 
 
+def normalize_rows_f16(rows, out=None):
+    """``embeddings / np.linalg.norm(embeddings, axis=-1, keepdims=True)`` for a
+    float16 corpus, bit for bit as NumPy evaluates it in float16
+    (Backend/services/embedding_service.py:209-210 on the reference's fp16
+    ``.npy`` files; ``mi_normalize_rows_f16``, csrc/corpus.hip).  ``rows``: device
+    fp16 [N, D]; returns the normalised fp16 rows (``out`` may be ``rows``)."""
+    import torch
+    if not rows.is_cuda or rows.dtype != torch.float16 or rows.dim() != 2:
+        raise N.MiClipError("normalize_rows_f16 takes device float16 [N, D] rows")
+    r = rows.contiguous()
+    o = torch.empty_like(r) if out is None else out
+    if o.shape != r.shape or o.dtype != torch.float16 or not o.is_contiguous():
+        raise N.MiClipError("normalize_rows_f16: out must be contiguous float16 of the rows' shape")
+    with torch.cuda.device(r.device):
+        N.check(N.lib().mi_normalize_rows_f16(r.data_ptr(), r.shape[0], r.shape[1], o.data_ptr(),
+                                              N.stream_ptr(r.device)), "mi_normalize_rows_f16")
+    return o
+
+
 def merge_topk(cand_scores, cand_index, k, nan_policy="first"):
     """Merge [Q, C] candidate lists (index -1 = empty) into the top-k (device)."""
     import torch

@@ -10,7 +10,11 @@ app.py:157-174) work unchanged.  What moves to the device:
   get_text_features      clip.tokenize -> encode_text (+L2 in the kernel)      :151-184
   search_top_frames      np.dot + np.argsort(s)[::-1][:k] -> one fused kernel  :284-344
                          over the HBM-resident corpus (file rows, normalised
-                         in-kernel, as get_embeddings does at load :209-210)
+                         as get_embeddings does at load :209-210: f32 files
+                         in the rank kernel; float16 files -- the reference's
+                         default video_test_3 / image_embeddings.npy -- by
+                         mi_normalize_rows_f16 in NumPy's float16 arithmetic,
+                         then ranked as stored)
   search_top_frames_by_image                                                    :346-392
   extract_and_save_embeddings_from_folder  batches -> encode_image (+L2)      :425-536
 
@@ -27,7 +31,7 @@ import numpy as np
 
 from . import api
 from .preprocess import decode_chunk, load_frames
-from .retrieval import MirroredCorpus, rank_topk
+from .retrieval import MirroredCorpus, normalize_rows_f16, rank_topk
 
 # corpora from this many rows on also get an fp16 ranking mirror (scripts/mirror_micro.py:
 # 1M rows 1.6-1.9x faster than the exact pass, 125k rows slower: fixed merge/re-score cost)
@@ -79,6 +83,9 @@ class FinetunedCLIP:
 
     def __call__(self, images, texts=None, get_embeddings=False):
         import torch
+        if texts is not None and self.classifier is None:
+            # checked before any encode: the reference's CLIPWithClassifier always has the head
+            raise ValueError("this checkpoint has no classifier.* weights: class logits are unavailable")
         image_features = self.clip_model.encode_image(images, normalize=True, out_dtype=torch.float32)
         if texts is None:
             return image_features
@@ -88,8 +95,6 @@ class FinetunedCLIP:
         # (logit_scale * image_features) @ text_features.t()  (:57-58)
         logits_per_image = score_matrix(text_features, image_features * scale, norm="none")
         logits_per_text = logits_per_image.t()
-        if self.classifier is None:
-            raise ValueError("this checkpoint has no classifier.* weights: class logits are unavailable")
         c = self.classifier
         hidden = gemm_f32(image_features, c["0.weight"], c["0.bias"], relu=True)
         class_logits = gemm_f32(hidden, c["3.weight"], c["3.bias"])
@@ -182,8 +187,14 @@ class EmbeddingService:
             return None
 
     def _corpus_on_device(self, video_name):
-        """Raw file rows resident in HBM (fp32 or fp16 as stored); the rank
-        kernel normalises each row in the same pass."""
+        """(rows, norm) resident in HBM for the rank kernel, normalised as
+        get_embeddings normalises the file (embedding_service.py:209-210):
+        f32 rows stay raw and the rank kernel normalises each row in the same
+        pass (norm "l2"); float16 rows -- NumPy normalises those in float16 --
+        are normalised once on the device bit for bit as NumPy does it
+        (``normalize_rows_f16``) and ranked as they are (norm "none"), so
+        search_top_frames ranks exactly the rows extract_query_confidence
+        reads from get_embeddings."""
         import torch
         path = self.path_service.get_embeddings_path(video_name)
         if not os.path.exists(path):
@@ -193,15 +204,19 @@ class EmbeddingService:
         if hit is not None and hit[0] == mtime:
             return hit[1]
         if hit is not None:
-            self._mirrors.pop(id(hit[1]), None)   # the file changed: drop the old rows' mirror
+            self._mirrors.pop(id(hit[1][0]), None)   # the file changed: drop the old rows' mirror
         raw = np.load(path)
         if raw.dtype not in (np.float32, np.float16):
             raw = raw.astype(np.float32)
         t = torch.from_numpy(np.ascontiguousarray(raw)).to(self.original_model.device)
-        self._device_corpus[path] = (mtime, t)
-        if t.shape[0] >= MIRROR_MIN_ROWS and t.shape[1] in (512, 768):
-            self._mirrors[id(t)] = MirroredCorpus(t)
-        return t
+        if t.dtype == torch.float16:
+            entry = (normalize_rows_f16(t, out=t), "none")
+        else:
+            entry = (t, "l2")
+            if t.shape[0] >= MIRROR_MIN_ROWS and t.shape[1] in (512, 768):
+                self._mirrors[id(t)] = MirroredCorpus(t)
+        self._device_corpus[path] = (mtime, entry)
+        return entry
 
     def _frames(self, video_name):
         json_path = self.path_service.get_metadata_path(video_name)
@@ -211,20 +226,22 @@ class EmbeddingService:
             self.cache_service.set_frames_list(json_path, frames)
         return frames
 
-    def _rank(self, corpus, query_vec, top_k):
+    def _rank(self, entry, query_vec, top_k):
         """Top-k (score desc, index asc; NaN first as argsort(s)[::-1]); any
         k up to the corpus size (a full sort when top_k >= N, as the reference's
-        np.argsort(s)[::-1] at embedding_service.py:317-318)."""
+        np.argsort(s)[::-1] at embedding_service.py:317-318).  ``entry`` is
+        ``_corpus_on_device``'s (rows, norm)."""
         import torch
+        corpus, norm = entry
         k = min(int(top_k), corpus.shape[0])
         if k <= 0:
             return np.zeros(0, np.float32), np.zeros(0, np.int64)
         q = torch.as_tensor(np.asarray(query_vec, dtype=np.float32).reshape(1, -1), device=corpus.device)
         mc = self._mirrors.get(id(corpus))
-        if mc is not None and mc.master is corpus and k <= MirroredCorpus.MAX_K:
+        if mc is not None and mc.master is corpus and norm == "l2" and k <= MirroredCorpus.MAX_K:
             s, i = mc.topk(q, k, norm="l2", nan_policy="first")   # certified == the exact pass, bit for bit
         else:
-            s, i = rank_topk(corpus, q, k, norm="l2", nan_policy="first")
+            s, i = rank_topk(corpus, q, k, norm=norm, nan_policy="first")
         return s[0].cpu().numpy(), i[0].cpu().numpy()
 
     # --------------------------------------------------------------- search

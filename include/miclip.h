@@ -35,7 +35,8 @@
 extern "C" {
 #endif
 
-#define MICLIP_ABI_VERSION 2   /* 2: mi_jpeg_workspace_bytes / mi_jpeg_decode take the data size */
+#define MICLIP_ABI_VERSION 3   /* 2: mi_jpeg_workspace_bytes / mi_jpeg_decode take the data size;
+                                  3: mi_normalize_rows_f16 */
 
 enum mi_dtype { MI_F32 = 0, MI_BF16 = 1, MI_F16 = 2, MI_FP8 = 3 /* weights only: MX-fp8 vision GEMMs */ };
 enum mi_status { MI_OK = 0, MI_ERR_ARG = -1, MI_ERR_HIP = -2, MI_ERR_UNSUPPORTED = -3, MI_ERR_STATE = -4 };
@@ -147,6 +148,18 @@ int mi_rank_topk(const void* corpus, int64_t N, int64_t D, int corpus_dtype,
  * embedding_service.py:210).  D = 512 or 768. */
 int mi_mirror_build(const void* corpus, int64_t N, int64_t D, int corpus_dtype, void* mirror_f16, void* stream);
 
+/* Replaces get_embeddings' row normalisation of a float16 `.npy` corpus
+ * (Backend/services/embedding_service.py:209-210,
+ * `embeddings / np.linalg.norm(embeddings, axis=-1, keepdims=True)` evaluated by
+ * NumPy in float16 — the reference's default corpus files video_test_3 /
+ * image_embeddings.npy are float16) bit for bit: f16 squares, NumPy's pairwise
+ * f32 summation of them rounded to f16, f16 sqrt, f16 quotients (csrc/corpus.hip).
+ * A zero row becomes NaN as in the reference.  rows / out: device fp16 [N,D]
+ * (out == rows allowed); 1 <= D <= 1024.  search_top_frames' ranking of such a
+ * file is then mi_rank_topk(out, ..., MI_F16, MI_NORM_NONE, ...) with the f32
+ * query (embedding_service.py:314-320). */
+int mi_normalize_rows_f16(const void* rows, int64_t N, int64_t D, void* out, void* stream);
+
 /* Workspace bytes mi_rank_mirror needs for (N, Q). */
 size_t mi_rank_mirror_workspace_bytes(int64_t N, int64_t Q);
 
@@ -217,7 +230,13 @@ int mi_preprocess_frames(const uint8_t* frames, int64_t B, int32_t H, int32_t W,
  *             readable for 16 bytes past the last segment end (aligned 16-byte reads);
  *             data_bytes = its size (the segments lie in [0, data_bytes))
  *   seg_off / seg_end  [B * nseg] byte offsets of each restart segment (nseg = 1
- *             without restart markers); a segment ends at its RSTn / EOI marker
+ *             without restart markers); a segment ends at its RSTn / EOI marker.
+ *             Contract: frames' segments are disjoint, in frame order and inside
+ *             [0, data_bytes) (miclip/jpeg.py concatenates the frames' scans).  Offsets
+ *             are clipped to [0, data_bytes) on the device; with nseg = 1 a frame whose
+ *             segment starts before an earlier frame's end (a repeated or out-of-order
+ *             frame) is left out of the chunked decode and decoded by the serial
+ *             kernel, so no input layout writes outside the workspace
  *   huff      [nsets][4] decode tables {dc0, ac0, dc1, ac1}, MI_JPEG_HUFF_BYTES each
  *   huff_idx  [B] int32 table set of each frame, in [0, nsets) (frames of one
  *             encoder share a set; up to 11 sets are staged in LDS), or NULL:

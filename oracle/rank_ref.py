@@ -25,6 +25,72 @@ def normalize_rows(E):
         return E / np.linalg.norm(E, axis=-1, keepdims=True)
 
 
+def pairwise_plan(D):
+    """NumPy's pairwise summation tree for a length-D reduction
+    (numpy/_core/src/umath/loops_utils.h.src ``pairwise_sum``): leaves of
+    <= 128 elements as (start, length) and a postfix program (0 = next leaf,
+    1 = add the top two).  csrc/corpus.hip's host plan, restated."""
+    leaves, ops = [], []
+
+    def rec(off, n):
+        if n <= 128:
+            leaves.append((off, n))
+            ops.append(0)
+            return
+        n2 = n // 2
+        n2 -= n2 % 8
+        rec(off, n2)
+        rec(off + n2, n - n2)
+        ops.append(1)
+    rec(0, D)
+    return leaves, ops
+
+
+def normalize_rows_f16(E16):
+    """``E / np.linalg.norm(E, axis=-1, keepdims=True)`` for a float16 array,
+    restated step by step as NumPy evaluates it (embedding_service.py:209-210
+    on the reference's float16 files; the arithmetic csrc/corpus.hip replays):
+    f16 squares, pairwise f32 sum of all D squares from the identity 0 (leaf:
+    n < 8 sequential, else 8 strided accumulators ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7))
+    + sequential tail), f16 round, f32 sqrt -> f16, f16(f32 x / f32 norm).
+    Pinned against NumPy itself by tests/test_oracle.py."""
+    f32 = np.float32
+    X = np.asarray(E16, dtype=np.float16)
+    R, D = X.shape
+    sq = (X * X).astype(f32)                      # HALF_multiply: f16 squares
+    leaves, ops = pairwise_plan(D)
+
+    def leaf(a):
+        n = a.shape[1]
+        if n < 8:
+            r = np.zeros(R, f32)
+            for i in range(n):
+                r = (r + a[:, i]).astype(f32)
+            return r
+        r = [a[:, j].astype(f32) for j in range(8)]
+        body = n - n % 8
+        for i in range(8, body, 8):
+            for j in range(8):
+                r[j] = (r[j] + a[:, i + j]).astype(f32)
+        res = (((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]))).astype(f32)
+        for i in range(body, n):
+            res = (res + a[:, i]).astype(f32)
+        return res
+    sums = [leaf(sq[:, o:o + n]) for o, n in leaves]
+    st, nl = [], 0
+    for op in ops:
+        if op == 0:
+            st.append(sums[nl])
+            nl += 1
+        else:
+            right = st.pop()
+            st[-1] = (st[-1] + right).astype(f32)
+    total = (f32(0) + st[0]).astype(np.float16)
+    with np.errstate(invalid="ignore", divide="ignore", over="ignore"):
+        nrm = np.sqrt(total.astype(f32)).astype(np.float16)
+        return (X.astype(f32) / nrm.astype(f32)[:, None]).astype(np.float16)
+
+
 def normalize_rows_guarded(F):
     """compare_models.py:1166-1171."""
     n = np.linalg.norm(F, axis=1, keepdims=True)

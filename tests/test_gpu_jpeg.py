@@ -240,3 +240,62 @@ def test_load_frames_decode_budget(gpu, monkeypatch):
 def torch_equal(a, b):
     import torch
     return torch.equal(a, b)
+
+
+def _decode_raw(bufs, order, off_fn):
+    """mi_jpeg_decode through the C-ABI on the scans of ``bufs`` concatenated in
+    order, with frame f reading the byte range off_fn(f, starts) -> (seg_off,
+    seg_end) of that concatenation (``order`` maps frames to buffers)."""
+    import torch
+    from miclip import _native as N, jpeg
+    heads = [jpeg.parse(b) for b in bufs]
+    key = jpeg._geom_key(heads[0])
+    segl = [((h.scan_start, len(b)),) for h, b in zip(heads, bufs)]
+    geom, huff, hidx, qt, offs, ends, starts, nsets = jpeg.launch_args(bufs, heads, list(range(len(bufs))), segl, key)
+    data = b"".join(b[h.scan_start:] for h, b in zip(heads, bufs))
+    total = len(data)
+    dev = torch.device("cuda")
+    d_data = torch.frombuffer(bytearray(data + b"\xff\xd9" * 16), dtype=torch.uint8).to(dev)
+    B = len(order)
+    so = np.zeros(B, np.int64)
+    se = np.zeros(B, np.int64)
+    for f in range(B):
+        so[f], se[f] = off_fn(f, order[f], starts)
+    W, H = int(geom[0]), int(geom[1])
+    rgb = torch.empty(B, H, W, 3, dtype=torch.uint8, device=dev)
+    L = N.lib()
+    nb = L.mi_jpeg_workspace_bytes(geom.ctypes.data, B, total)
+    ws = torch.empty(nb, dtype=torch.uint8, device=dev)
+    d_h = torch.from_numpy(huff.view(np.uint8).reshape(-1)).to(dev)
+    d_i = torch.from_numpy(np.ascontiguousarray(hidx[list(order)])).to(dev)
+    d_q = torch.from_numpy(np.ascontiguousarray(qt[list(order)])).to(dev)
+    d_so, d_se = torch.from_numpy(so).to(dev), torch.from_numpy(se).to(dev)     # kept alive over the call
+    N.check(L.mi_jpeg_decode(d_data.data_ptr(), total, d_so.data_ptr(), d_se.data_ptr(), d_h.data_ptr(), d_i.data_ptr(), nsets,
+                             d_q.data_ptr(), geom.ctypes.data, B, rgb.data_ptr(), ws.data_ptr(), nb,
+                             N.stream_ptr(dev)), "mi_jpeg_decode")
+    torch.cuda.synchronize()
+    return rgb.cpu().numpy()
+
+
+def test_segments_outside_the_contract_stay_in_bounds(gpu):
+    """mi_jpeg_decode's segments are meant to be disjoint, in frame order, inside
+    [0, data_bytes).  Callers that break that must not make the
+    chunked decode write past its workspace: the same scan referenced by two
+    frames, frames out of order, and a segment end past data_bytes.  Those frames
+    leave the chunk layout and are decoded by the serial kernel from the data
+    (clipped to data_bytes), so every frame still equals Pillow."""
+    files = sorted(glob.glob(os.path.join(ROOT, "golden", "ref_frames", "*.jpg")))[:3]
+    bufs = [open(f, "rb").read() for f in files]
+    refs = [_pil(b) for b in bufs]
+    rng = lambda i, st: (int(st[i]), int(st[i + 1]))
+    # frame 1 repeats frame 0's bytes; frame 3 re-reads frame 1's (out of order); frame 4 runs past the end
+    order = [0, 0, 1, 1, 2]
+    specs = {0: lambda st: rng(0, st), 1: lambda st: rng(0, st), 2: lambda st: rng(1, st),
+             3: lambda st: rng(1, st), 4: lambda st: (int(st[2]), int(st[3]) + 100_000)}
+    got = _decode_raw(bufs, order, lambda f, b, st: specs[f](st))
+    for f, b in enumerate(order):
+        assert np.array_equal(got[f], refs[b]), f"frame {f}"
+    # reversed order: every frame after the first starts before an earlier end
+    got = _decode_raw(bufs, [2, 1, 0], lambda f, b, st: rng(b, st))
+    for f, b in enumerate([2, 1, 0]):
+        assert np.array_equal(got[f], refs[b]), f"reversed frame {f}"

@@ -45,6 +45,63 @@ def test_topk_half_corpus(gpu, dtype):
         rank_ref.assert_topk_equivalent(s[r].cpu().numpy(), i[r].cpu().numpy(), S[r], 10)
 
 
+@pytest.mark.parametrize("D", [1, 7, 32, 96, 130, 512, 544, 768, 992, 1024])
+def test_normalize_rows_f16_bit_identical_to_numpy(gpu, D):
+    """mi_normalize_rows_f16 == NumPy's float16 `E / np.linalg.norm(E, axis=-1,
+    keepdims=True)` (embedding_service.py:209-210) bit for bit, NaN rows
+    included, out of place and in place."""
+    import torch
+    from miclip import retrieval
+    from test_oracle import _f16_rows
+    X = _f16_rows(np.random.default_rng(100 + D), 3001, D)
+    with np.errstate(all="ignore"):
+        ref = X / np.linalg.norm(X, axis=-1, keepdims=True)
+    t = _t(X, gpu)
+    got = retrieval.normalize_rows_f16(t).cpu().numpy()
+    nan = np.isnan(ref)
+    assert np.array_equal(nan, np.isnan(got))
+    assert np.array_equal(ref.view(np.uint16)[~nan], got.view(np.uint16)[~nan])
+    retrieval.normalize_rows_f16(t, out=t)
+    assert np.array_equal(np.isnan(t.cpu().numpy()), nan)
+    assert np.array_equal(t.cpu().numpy().view(np.uint16)[~nan], ref.view(np.uint16)[~nan])
+    e = torch.zeros(0, D, dtype=torch.float16, device=gpu)
+    assert retrieval.normalize_rows_f16(e).shape == (0, D)
+
+
+def test_reference_fp16_corpus_fixture(gpu):
+    """The app's default corpus, the reference's float16 file
+    Backend/embedding/video_test_3_embeddings.npy (== image_embeddings.npy):
+    rows normalised on the device in NumPy's float16 arithmetic (bit-identical
+    to the fixture's NumPy rows), ranked as stored against f32 text vectors:
+    identical frame lists to the literal search_top_frames restatement for
+    all 200 queries at k = 10 and k = 60 (fixture: make_golden.py --fp16-rank).
+    A query whose literal answer hinges on a float64 gap < 2e-7 between
+    consecutive top scores (the host BLAS's summation order decides those) may
+    swap exactly those two rows; none may differ otherwise."""
+    import torch
+    from miclip import retrieval
+    from oracle import rank_ref
+    g = golden("rank_video_test_3.npz")
+    raw, q = g["corpus"], g["queries"]
+    E = retrieval.normalize_rows_f16(_t(raw, gpu))
+    assert E.dtype == torch.float16
+    assert np.array_equal(E.cpu().numpy().view(np.uint16), g["normalized"].view(np.uint16))
+    S = q.astype(np.float64) @ g["normalized"].astype(np.float64).T
+    swaps = 0
+    for k in (10, 60):
+        s, i = retrieval.rank_topk(E, _t(q, gpu), k, norm="none")
+        i = i.cpu().numpy()
+        ref = g[f"top_index_{k}"]
+        for r in range(q.shape[0]):
+            if np.array_equal(i[r], ref[r]):
+                continue
+            assert g[f"gap_{k}"][r] < 2e-7, (k, r, i[r], ref[r])
+            swaps += rank_ref.assert_topk_equivalent(s[r].cpu().numpy(), i[r], S[r], k, tol=2e-7)
+        exp = np.take_along_axis(S, i, 1)
+        assert np.allclose(s.cpu().numpy(), exp, rtol=0, atol=2e-6)
+    assert swaps <= 2
+
+
 def test_topk_nan_rows_and_ties(gpu):
     from miclip import retrieval
     from oracle import rank_ref

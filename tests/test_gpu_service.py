@@ -260,3 +260,38 @@ def test_large_corpus_ranks_through_mirror(service):
     assert got == [big[j] for j in i[0].cpu().numpy()]
     got40 = svc.search_top_frames_by_image(q, 40, "big")          # k > 12: the exact pass
     assert got40[:10] == got and mc.certified == 1
+
+
+def test_fp16_corpus_file_matches_reference(service, monkeypatch):
+    """search_top_frames / extract_query_confidence / search_top_frames_by_image
+    over the reference's float16 corpus file (video_test_3_embeddings.npy, the
+    app's default corpus; fixture rank_video_test_3.npz): the frame lists equal
+    the literal restatement (get_embeddings normalises in float16,
+    embedding_service.py:209-210, then :314-336), and the confidences the
+    reference's per-frame path computes from get_embeddings' rows
+    (:219-282) agree with the ranking: each returned frame's confidence is its
+    rank score, in non-increasing order."""
+    from conftest import golden
+    svc, frame_dir, names, paths = service
+    g = golden("rank_video_test_3.npz")
+    raw, q = g["corpus"], g["queries"]
+    os.makedirs(os.path.dirname(paths.get_embeddings_path("v3")), exist_ok=True)
+    np.save(paths.get_embeddings_path("v3"), raw)
+    frames = [f"{i}.jpg" for i in range(raw.shape[0])]
+    with open(paths.get_metadata_path("v3"), "w") as f:
+        json.dump([{"frame": x} for x in frames], f)
+    feats = {f"query {r}": q[r:r + 1] for r in range(0, q.shape[0], 7)}
+    monkeypatch.setattr(svc, "get_text_features", lambda query, video_name=None: feats[query])
+    E = svc.get_embeddings("v3")
+    assert E.dtype == np.float16 and np.array_equal(E.view(np.uint16), g["normalized"].view(np.uint16))
+    for text, t in feats.items():
+        r = int(text.split()[1])
+        for k in (10, 60):
+            got = svc.search_top_frames(text, k, "v3")
+            assert got == [frames[j] for j in g[f"top_index_{k}"][r]], (r, k)
+        conf = [svc.extract_query_confidence(fr, text, "v3") for fr in got]
+        assert all(a >= b - 2e-7 for a, b in zip(conf, conf[1:]))
+        exact = [float(E[int(fr.split(".")[0])].astype(np.float64) @ t[0].astype(np.float64)) for fr in got]
+        assert np.allclose(conf, exact, rtol=0, atol=1e-6)
+    got = svc.search_top_frames_by_image(q[3], 10, "v3")
+    assert got == [frames[j] for j in g["top_index_10"][3]]

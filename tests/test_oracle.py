@@ -111,3 +111,67 @@ def test_torch_cpu_restatement_matches_golden(name, fname):
     np.testing.assert_allclose(img, g["image"], rtol=0, atol=5e-5 * np.abs(g["image"]).max())
     np.testing.assert_allclose(txt, g["text"], rtol=0, atol=5e-5 * np.abs(g["text"]).max())
     assert 1 - clip_ref.cosine(img, g["image"]).min() < 1e-8
+
+
+def _f16_rows(rng, R, D):
+    X = (rng.standard_normal((R, D)) * np.exp(rng.uniform(-7, 2.5, (R, D)))).astype(np.float16)
+    X[0] = 0                                         # zero row -> NaN (0/0)
+    X[1, :] = np.float16(6e-8)                        # f16 subnormal squares -> 0
+    X[2, 0] = np.float16(200.0)                       # square overflows f16 -> inf norm -> 0 / NaN
+    X[3, min(5, D - 1)] = np.float16(np.nan)
+    if R > 8:
+        X[8:, 0] = rng.uniform(31, 45, R - 8).astype(np.float16)   # one dominant square: exercises the tree order
+    return X
+
+
+@pytest.mark.parametrize("D", [1, 7, 8, 32, 96, 130, 512, 544, 768, 992, 1024])
+def test_f16_norm_plan_matches_numpy(D):
+    """The float16 row normalisation csrc/corpus.hip replays (oracle
+    rank_ref.normalize_rows_f16) is NumPy's own float16 evaluation of
+    embedding_service.py:209-210, bit for bit (NaN positions included)."""
+    from oracle import rank_ref
+    rng = np.random.default_rng(D)
+    X = _f16_rows(rng, 4000 if D <= 544 else 1500, D)
+    with np.errstate(all="ignore"):
+        ref = X / np.linalg.norm(X, axis=-1, keepdims=True)
+    got = rank_ref.normalize_rows_f16(X)
+    assert ref.dtype == np.float16 and got.dtype == np.float16
+    nan = np.isnan(ref)
+    assert np.array_equal(nan, np.isnan(got))
+    assert np.array_equal(ref.view(np.uint16)[~nan], got.view(np.uint16)[~nan])
+    leaves, _ = rank_ref.pairwise_plan(D)
+    assert len(leaves) <= 8                           # one lane per strided accumulator in the kernel
+
+
+def test_f16_plan_initial_value_is_identity():
+    """The half add-reduce starts from the identity 0 and sums all D squares
+    pairwise (not x_0 + pairwise(x_1..)): rows built so that the two differ."""
+    from oracle import rank_ref
+    rng = np.random.default_rng(1)
+    X = (rng.standard_normal((200000, 512)) * 0.03).astype(np.float16)
+    X[:, 0] = rng.uniform(31, 45, X.shape[0]).astype(np.float16)
+    with np.errstate(all="ignore"):
+        ref = X / np.linalg.norm(X, axis=-1, keepdims=True)
+    assert np.array_equal(ref.view(np.uint16), rank_ref.normalize_rows_f16(X).view(np.uint16))
+
+
+def test_fp16_reference_corpus_fixture():
+    """tests/golden/rank_video_test_3.npz (the reference's float16 default
+    corpus, video_test_3 == image_embeddings.npy byte for byte): the stored
+    normalised rows are NumPy's, the frame lists are the literal
+    search_top_frames restatement, and that literal answer equals the
+    (score desc, index asc) order of the exact scores of those float16 rows."""
+    from oracle import rank_ref
+    g = golden("rank_video_test_3.npz")
+    raw, q = g["corpus"], g["queries"]
+    assert raw.dtype == np.float16 and bool(g["image_embeddings_identical"])
+    E16 = rank_ref.normalize_rows(raw)
+    assert np.array_equal(E16.view(np.uint16), g["normalized"].view(np.uint16))
+    assert np.array_equal(rank_ref.normalize_rows_f16(raw).view(np.uint16), g["normalized"].view(np.uint16))
+    frames = [f"{i}.jpg" for i in range(raw.shape[0])]
+    for r in range(0, q.shape[0], 23):
+        _, idx = rank_ref.search_top_frames_ref(raw, q[r:r + 1], 60, frames)
+        assert np.array_equal(np.asarray(idx[:60]), g["top_index_60"][r])
+    _, exact = rank_ref.topk_ref(E16.astype(np.float64), q, 60, norm="none")
+    assert np.array_equal(exact, g["top_index_60"])
+    assert np.array_equal(exact[:, :10], g["top_index_10"])
