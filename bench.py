@@ -37,6 +37,11 @@ FP8_PEAK_TFLOPS = 5000.0       # dense fp8 / MX-fp8 MFMA (spec, no sparsity)
 F32_MFMA_PEAK_TFLOPS = 157.3
 
 
+def _progress(msg):
+    """A progress line on stderr (stdout carries only the JSON result)."""
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -201,8 +206,10 @@ def jpeg_ingest_timing(dev, n_px, B=8192, threads=16, pil_frames=1024):
     """Frame ingest from JPEG bytes in host memory to preprocessed [B,3,n,n]
     bf16 tensors: the reference's 16 real 1280x720
     frames (tests/golden/ref_frames) repeated to B.  GPU path: header parse +
-    table build on the host, mi_jpeg_decode + mi_preprocess_frames on the
-    device (bit-identical to Pillow, tests/test_gpu_jpeg.py); host path: Pillow
+    table build on the host, mi_jpeg_decode_transform on the device (entropy
+    decode + IDCT, then colour conversion, both resample passes and Normalize
+    fused; bit-identical to Pillow + torchvision, tests/test_gpu_jpeg.py), and
+    the pre-r04 two-step path (decode to RGB + mi_preprocess_frames); host path: Pillow
     decode on `threads` host threads, as the reference decodes, + the same GPU
     preprocessing, timed on the first `pil_frames` frames.  The GPU entropy
     decode runs one lane per 1-KB chunk of a frame's scan (jpeg.hip, chunked
@@ -223,7 +230,10 @@ def jpeg_ingest_timing(dev, n_px, B=8192, threads=16, pil_frames=1024):
     raw = [open(f, "rb").read() for f in files]
     bufs = [raw[i % len(raw)] for i in range(B)]
 
-    def gpu():   # each geometry group's decoded [B,H,W,3] buffer goes straight to the resampler
+    def gpu():   # fused decode + colour + resample + normalise (mi_jpeg_decode_transform), per geometry group
+        return [x for _, x in jpeg.decode_groups(bufs, dev, transform=(n_px, False, torch.bfloat16))]
+
+    def gpu_two_step():   # decode to RGB, then mi_preprocess_frames (the pre-r04 path)
         return [preprocess_frames(rgb, n_px, out_dtype=torch.bfloat16) for _, rgb in jpeg.decode_groups(bufs, dev)]
 
     def pil_one(b):
@@ -237,7 +247,8 @@ def jpeg_ingest_timing(dev, n_px, B=8192, threads=16, pil_frames=1024):
 
     res = {"frames": B, "pil_frames": pil_frames,
            "source": "tests/golden/ref_frames (16 reference frames, 1280x720 4:2:0)", "host_threads": threads}
-    for name, fn, n in (("gpu_decode", gpu, B), ("pil_decode", host, pil_frames)):
+    for name, fn, n in (("gpu_decode", gpu, B), ("gpu_decode_two_step", gpu_two_step, B),
+                        ("pil_decode", host, pil_frames)):
         out = fn()
         torch.cuda.synchronize(dev)
         best = 1e9
@@ -312,7 +323,10 @@ def cpu_baseline(cfg, n_frames_metric, Q, k, b1_frames, b64_frames):
     import torch
     from miclip import weights
     from oracle import clip_ref, clip_torch, rank_ref
-    threads = _usable_cores()
+    # threads: $OMP_NUM_THREADS when set (16 on the GPU box), else the process's usable cores;
+    # BASELINE.md's literal torch.set_num_threads(os.cpu_count()) is timed beside it
+    env_threads = os.environ.get("OMP_NUM_THREADS", "")
+    threads = int(env_threads) if env_threads.isdigit() and int(env_threads) > 0 else _usable_cores()
     torch.set_num_threads(threads)
     sd = weights.make_state_dict(cfg)
     m = clip_torch.TorchCLIP(sd, cfg)
@@ -342,9 +356,13 @@ def cpu_baseline(cfg, n_frames_metric, Q, k, b1_frames, b64_frames):
     def rate(t_img):
         return n_frames_metric / (n_frames_metric * t_img + Q * t_txt + Q * t_rank)
 
+
     return {"value": round(rate(t_b1), 2), "unit": "frames/s", "cores": int(threads), "kind": "port",
             "nproc": os.cpu_count(), "cores_available": _usable_cores(), "cpu_model": _cpu_model(),
             "batch64_value": round(rate(t_b64), 2), "numpy_batch64_value": round(rate(t_np), 2),
+            "threads_policy": "OMP_NUM_THREADS" if env_threads.isdigit() and int(env_threads) > 0
+                              else "min(affinity, cgroup quota)",
+
             "sample": f"torch-CPU fp32 restatement of openai/CLIP (oracle/clip_torch.py), {threads} threads: "
                       f"{b1_frames} frames one per call as Backend/embedding.py:39-52 ({t_b1 * 1e3:.1f} ms/frame; "
                       f"batch 64 over {b64_frames} frames: {t_b64 * 1e3:.1f} ms/frame; numpy oracle batch 64: "
@@ -593,6 +611,7 @@ def main():
     value = total_frames / elapsed
     result = None
     if rank == 0:
+        _progress(f"timed {args.steps} steps: {ms:.2f} ms/step; kernel timings")
         kern = {} if args.no_kernel_timing else kernel_timing(model, cfg, chunk)
         txt = model.encode_text(tokens, normalize=True, out_dtype=torch.float32)
         kern["rank_topk"] = rank_timing(emb, txt, k)
@@ -600,6 +619,7 @@ def main():
         ingest = jpeg_ingest_timing(dev, cfg.image_resolution)
         if ingest:
             kern["jpeg_ingest_720p"] = ingest
+        _progress("rank roofline")
         rank_roof = None if args.no_rank_roofline else rank_roofline(dev)
         F_frame, F_text = cfg.image_flops(), cfg.text_flops()
         step_flops = Nf * world * F_frame + Q * world * F_text + 2.0 * Nf * world * Q * cfg.embed_dim
@@ -631,6 +651,7 @@ def main():
                     "flops_per_launch": fl, "launch_shape": [M, 4 * cfg.vision_width, cfg.vision_width],
                     "avg_launch_us": dom["us"]}
         parity = None
+        _progress("parity mode / cpu baseline")
         if not args.no_parity_mode and world == 1 and args.weights == "bf16":
             parity = parity_mode(args, dev, pixels, tokens, Q, k, base, chunk)
         cpu = None

@@ -62,6 +62,10 @@ struct Layer {
   // MX-fp8 copies (weight_dtype MI_FP8, vision tower): e4m3 codes + stage-major e8m0 scales
   const uint8_t *q_qkv = nullptr, *s_qkv = nullptr, *q_out = nullptr, *s_out = nullptr;
   const uint8_t *q_fc = nullptr, *s_fc = nullptr, *q_proj = nullptr, *s_proj = nullptr;
+  // LayerNorm-folded copies (bf16 vision tower, run_tower_fold): W' = f16(W * gamma) of
+  // in_proj (ln_1) and c_fc (ln_2), their column sums s_n and c_n = b_n + W beta
+  const uint16_t *lw_qkv = nullptr, *lw_fc = nullptr;
+  const float *ls_qkv = nullptr, *lc_qkv = nullptr, *ls_fc = nullptr, *lc_fc = nullptr;
 };
 
 // Device weight image: bf16 GEMM weights and f32 vectors in one allocation.
@@ -140,25 +144,80 @@ struct Builder {
 
 struct LayerOff {
   size_t ln1_g, ln1_b, w_qkv, b_qkv, w_out, b_out, ln2_g, ln2_b, w_fc, b_fc, w_proj, b_proj;
+  // blob positions of the tensors the LayerNorm fold reads
+  int64_t p_ln1_g, p_ln1_b, p_w_qkv, p_b_qkv, p_ln2_g, p_ln2_b, p_w_fc, p_b_fc;
+  size_t lw_qkv = 0, ls_qkv = 0, lc_qkv = 0, lw_fc = 0, ls_fc = 0, lc_fc = 0;   // 0: not folded
 };
 
 void build_tower(Builder& b, int W, int L, std::vector<LayerOff>& out, bool full) {
   out.resize(L);
   for (int i = 0; i < L; ++i) {
     LayerOff& l = out[i];
+    l.p_ln1_g = b.pos;
     l.ln1_g = b.f32(W);
+    l.p_ln1_b = b.pos;
     l.ln1_b = b.f32(W);
+    l.p_w_qkv = b.pos;
     l.w_qkv = b.mat(full, 3 * W, W, W);
+    l.p_b_qkv = b.pos;
     l.b_qkv = b.f32(3 * W);
     l.w_out = b.mat(full, W, W, W);
     l.b_out = b.f32(W);
+    l.p_ln2_g = b.pos;
     l.ln2_g = b.f32(W);
+    l.p_ln2_b = b.pos;
     l.ln2_b = b.f32(W);
+    l.p_w_fc = b.pos;
     l.w_fc = b.mat(full, 4 * W, W, W);
+    l.p_b_fc = b.pos;
     l.b_fc = b.f32(4 * W);
     l.w_proj = b.mat(full, W, 4 * W, 4 * W);
     l.b_proj = b.f32(W);
   }
+}
+
+uint16_t f2h_host(float f) {
+  const _Float16 h = (_Float16)f;
+  uint16_t u;
+  memcpy(&u, &h, 2);
+  return u;
+}
+
+// LayerNorm folded into the following GEMM (ln_1 -> in_proj, ln_2 -> c_fc; gemm_8q.hip EPI_LN_*):
+//   LN(x) W^T + b = rstd * (x W'^T) - rstd * mean * s + c,
+//   W'[n][k] = f16(W[n][k] * gamma[k]),  s_n = sum_k W'[n][k],  c_n = b_n + sum_k beta[k] W[n][k]
+// (s from the rounded W', so that x W'^T - mean s = (x - mean) W'^T exactly; sums in double).
+// Appends W' (f16 [N][K]), s and c (f32 [N]) to the image; returns their offsets.
+void fold_ln(Builder& b, int64_t p_g, int64_t p_beta, int64_t p_w, int64_t p_bias, int N, int K, size_t& ow,
+             size_t& os, size_t& oc) {
+  const float* g = b.src + p_g;
+  const float* be = b.src + p_beta;
+  const float* w = b.src + p_w;
+  const float* bias = b.src + p_bias;
+  ow = b.align();
+  b.img.resize(ow + (size_t)N * K * 2);
+  std::vector<float> sv(N), cv(N);
+  for (int n = 0; n < N; ++n) {
+    uint16_t* d = (uint16_t*)(b.img.data() + ow) + (size_t)n * K;
+    double ss = 0, cc = bias[n];
+    for (int k = 0; k < K; ++k) {
+      const float wv = w[(size_t)n * K + k];
+      const uint16_t h = f2h_host(wv * g[k]);
+      d[k] = h;
+      _Float16 hv;
+      memcpy(&hv, &h, 2);
+      ss += (double)(float)hv;
+      cc += (double)be[k] * (double)wv;
+    }
+    sv[n] = (float)ss;
+    cv[n] = (float)cc;
+  }
+  os = b.align();
+  b.img.resize(os + (size_t)N * 4);
+  memcpy(b.img.data() + os, sv.data(), (size_t)N * 4);
+  oc = b.align();
+  b.img.resize(oc + (size_t)N * 4);
+  memcpy(b.img.data() + oc, cv.data(), (size_t)N * 4);
 }
 
 int64_t tower_numel(int64_t W, int64_t L) { return L * (W * 2 + 3 * W * W + 3 * W + W * W + W + 2 * W + 4 * W * W + 4 * W + 4 * W * W + W); }
@@ -190,6 +249,7 @@ struct mi_clip {
   float* x = nullptr;
   uint16_t *h = nullptr, *qkv = nullptr, *att = nullptr, *mlp = nullptr, *patches = nullptr, *cls_ln = nullptr;
   uint16_t* delta = nullptr;  // bf16 GEMM output added to x by the next residual_ln
+  float* rs = nullptr;        // LayerNorm-folded tower: per-row (rstd, rstd * mean), 256 rows of padding
   float* y = nullptr;
   // MX-fp8 activations (fp8 mode): LN outputs, attention output, QuickGELU(c_fc) + their scales
   uint8_t *hq = nullptr, *hqs = nullptr, *attq = nullptr, *attqs = nullptr, *mlpq = nullptr, *mlpqs = nullptr;
@@ -296,6 +356,14 @@ int mi_clip_create(const mi_clip_arch* arch, const float* weights, int64_t numel
     return fail(MI_ERR_ARG, "weight blob layout mismatch (consumed %lld of %lld)", (long long)b.pos,
                 (long long)numel);
   }
+  // bf16 vision tower: the LayerNorm-folded GEMM weights (run_tower_fold); W % 256 == 0 so
+  // that all four GEMMs take the 8-phase kernel
+  if (weight_dtype == MI_BF16 && W % 256 == 0) {
+    for (LayerOff& l : vlo) {
+      fold_ln(b, l.p_ln1_g, l.p_ln1_b, l.p_w_qkv, l.p_b_qkv, 3 * W, W, l.lw_qkv, l.ls_qkv, l.lc_qkv);
+      fold_ln(b, l.p_ln2_g, l.p_ln2_b, l.p_w_fc, l.p_b_fc, 4 * W, W, l.lw_fc, l.ls_fc, l.lc_fc);
+    }
+  }
   hipError_t e = hipMalloc(&c->wdev, b.img.size());
   if (e == hipSuccess) e = hipMemcpy(c->wdev, b.img.data(), b.img.size(), hipMemcpyHostToDevice);
   if (e != hipSuccess) {
@@ -336,6 +404,14 @@ int mi_clip_create(const mi_clip_arch* arch, const float* weights, int64_t numel
       } else {
         L[i] = Layer{F(o.ln1_g), F(o.ln1_b), F(o.b_qkv), F(o.b_out), F(o.ln2_g), F(o.ln2_b), F(o.b_fc), F(o.b_proj),
                      H(o.w_qkv), H(o.w_out), H(o.w_fc), H(o.w_proj)};
+        if (o.lw_qkv) {
+          L[i].lw_qkv = H(o.lw_qkv);
+          L[i].ls_qkv = F(o.ls_qkv);
+          L[i].lc_qkv = F(o.lc_qkv);
+          L[i].lw_fc = H(o.lw_fc);
+          L[i].ls_fc = F(o.ls_fc);
+          L[i].lc_fc = F(o.lc_fc);
+        }
       }
     }
   };
@@ -415,6 +491,7 @@ static int reserve_locked(mi_clip* c, int64_t ic, int64_t tc) {
   const size_t o_pat = carve((size_t)ic * c->G * c->G * (c->f32 ? c->Kp32 * 4 : c->Kp * 2));
   const size_t o_cls = carve((size_t)rows_max * mx(Wv, Wt) * es);
   const size_t o_y = carve((size_t)rows_max * a.embed_dim * 4);
+  const size_t o_rs = carve((size_t)(Mv + 256) * 8);
   size_t o_hq = 0, o_hqs = 0, o_attq = 0, o_attqs = 0, o_mlpq = 0, o_mlpqs = 0;
   if (c->fp8) {
     const size_t mp = (size_t)((Mv + 1) & ~1);
@@ -442,6 +519,7 @@ static int reserve_locked(mi_clip* c, int64_t ic, int64_t tc) {
   c->patches = (uint16_t*)(ws + o_pat);
   c->cls_ln = (uint16_t*)(ws + o_cls);
   c->y = (float*)(ws + o_y);
+  c->rs = (float*)(ws + o_rs);
   if (c->fp8) {
     c->hq = (uint8_t*)(ws + o_hq);
     c->hqs = (uint8_t*)(ws + o_hqs);
@@ -579,6 +657,43 @@ static int run_tower(mi_clip* c, const std::vector<Layer>& layers, int B, int S,
   return MI_OK;
 }
 
+// LayerNorm folded into the in_proj / c_fc GEMMs (bf16 vision tower): the GEMMs read the fp16
+// residual stream x16 directly (half-slot layout, row stride 2W elements) and apply ln_1 / ln_2
+// in their epilogues from per-row (rstd, rstd * mean) (gemm_8q.hip EPI_LN_*), so the residual
+// adds only write x16 and the statistics (residual_stats: 6 instead of residual_ln's 8 bytes per
+// element, no h buffer).  MICLIP_LNFOLD=0 keeps run_tower (A/B).
+static int lnfold() {
+  const char* e = ab_getenv("MICLIP_LNFOLD");   // read per call (A/B tests switch it within one process)
+  return e ? atoi(e) != 0 : 1;
+}
+
+static GemmArgs ln_args(mi_clip* c, const uint16_t* wf, const float* sv, const float* cv, void* out, int N, int M,
+                        int W) {
+  GemmArgs g = gargs((const uint16_t*)c->x, 2 * W, wf, W, cv, out, N, M, N, W);
+  g.a_f16 = 1;
+  g.rs = c->rs;
+  g.colv = sv;
+  return g;
+}
+
+// x16 / rs hold the embedding output and ln_1's statistics (vision_embed_ln16).  On return x16
+// + delta is the final residual stream (the last c_proj output stays in delta, as run_tower).
+static int run_tower_fold(mi_clip* c, const std::vector<Layer>& layers, int B, int S, int W, hipStream_t s) {
+  const int M = B * S;
+  for (size_t l = 0; l < layers.size(); ++l) {
+    const Layer& L = layers[l];
+    HIP_TRY(gemm_bf16(ln_args(c, L.lw_qkv, L.ls_qkv, L.lc_qkv, c->qkv, 3 * W, M, W), EPI_LN_BF16, s));
+    HIP_TRY(attention(c->qkv, c->att, B, S, W, 0, s));
+    HIP_TRY(gemm_bf16(with_variant(gargs(c->att, W, L.w_out, W, L.b_out, c->delta, W, M, W, W), GV_OUT), EPI_BF16, s));
+    HIP_TRY(residual_stats(c->x, c->delta, c->rs, M, W, s));
+    HIP_TRY(gemm_bf16(ln_args(c, L.lw_fc, L.ls_fc, L.lc_fc, c->mlp, 4 * W, M, W), EPI_LN_GELU_BF16, s));
+    HIP_TRY(gemm_bf16(with_variant(gargs(c->mlp, 4 * W, L.w_proj, 4 * W, L.b_proj, c->delta, W, M, W, 4 * W), GV_PROJ),
+                      EPI_BF16, s));
+    if (l + 1 < layers.size()) HIP_TRY(residual_stats(c->x, c->delta, c->rs, M, W, s));
+  }
+  return MI_OK;
+}
+
 // MX-fp8 GEMM arguments: A / W e4m3 with their stage-major scales
 static GemmArgs margs(const uint8_t* A, const uint8_t* as, const uint8_t* W, const uint8_t* ws, const float* bias,
                       void* out, int64_t ldo, int M, int N, int K) {
@@ -712,13 +827,22 @@ int mi_clip_encode_image(mi_clip* c, const void* pixels, int64_t B, int in_dtype
     pg.gstride = S;
     pg.goffset = 1;
     HIP_TRY(gemm_bf16(pg, EPI_F32, s));
-    const bool fuse_ln1 = !c->fp8 && !c->vl.empty() && embed_ln1();  // the MX tower's first LN writes fp8 itself
-    HIP_TRY(vision_embed_ln(c->x, c->cls, c->vpos, c->ln_pre_g, c->ln_pre_b, nb, S, W, s,
-                            fuse_ln1 ? c->vl[0].ln1_g : nullptr, fuse_ln1 ? c->vl[0].ln1_b : nullptr,
-                            fuse_ln1 ? c->h : nullptr));
-    const int r16 = resid16() && !c->vl.empty();
-    int r = c->fp8 ? run_tower_mx(c, c->vl, nb, S, W, s, r16) : run_tower(c, c->vl, nb, S, W, 0, s, r16, fuse_ln1);
+    // LayerNorm-folded tower: bf16 weights folded at create (W % 256 == 0), whole 256-row tiles
+    const bool fold = !c->fp8 && !c->vl.empty() && c->vl[0].lw_qkv && lnfold() && (int64_t)nb * S >= 256;
+    int r;
+    if (fold) {
+      HIP_TRY(vision_embed_ln16(c->x, c->cls, c->vpos, c->ln_pre_g, c->ln_pre_b, nb, S, W, c->rs, s));
+      r = run_tower_fold(c, c->vl, nb, S, W, s);
+    } else {
+      const bool fuse_ln1 = !c->fp8 && !c->vl.empty() && embed_ln1();  // the MX tower's first LN writes fp8 itself
+      HIP_TRY(vision_embed_ln(c->x, c->cls, c->vpos, c->ln_pre_g, c->ln_pre_b, nb, S, W, s,
+                              fuse_ln1 ? c->vl[0].ln1_g : nullptr, fuse_ln1 ? c->vl[0].ln1_b : nullptr,
+                              fuse_ln1 ? c->h : nullptr));
+      r = c->fp8 ? run_tower_mx(c, c->vl, nb, S, W, s, resid16() && !c->vl.empty())
+                 : run_tower(c, c->vl, nb, S, W, 0, s, resid16() && !c->vl.empty(), fuse_ln1);
+    }
     if (r) return r;
+    const int r16 = fold || (resid16() && !c->vl.empty());
     // ln_post(x[:, 0] + last c_proj delta) over the CLS rows only
     HIP_TRY(residual_ln(c->x, c->delta, (int64_t)S * W, 0, c->ln_post_g, c->ln_post_b, c->cls_ln, nb, W, s, nullptr,
                         nullptr, r16 ? 2 : 0));
@@ -1002,32 +1126,63 @@ size_t mi_jpeg_workspace_bytes(const int32_t* geom, int32_t B, int64_t data_byte
   return jpeg_workspace_bytes(geom, B, data_bytes);
 }
 
-int mi_jpeg_decode(const uint8_t* data, int64_t data_bytes, const int64_t* seg_off, const int64_t* seg_end, const void* huff,
-                   const int32_t* huff_idx, int32_t nsets, const uint16_t* qtab, const int32_t* geom, int32_t B,
-                   uint8_t* out_rgb, void* workspace, size_t workspace_bytes, void* stream) {
-  if (!geom || B < 0 || data_bytes < 0) return fail(MI_ERR_ARG, "mi_jpeg_decode: bad arguments");
-  if (huff_idx && nsets < 1) return fail(MI_ERR_ARG, "mi_jpeg_decode: huff_idx needs nsets >= 1");
+static int check_jpeg_args(const char* fn, const uint8_t* data, int64_t data_bytes, const int64_t* seg_off,
+                           const int64_t* seg_end, const void* huff, const int32_t* huff_idx, int32_t nsets,
+                           const uint16_t* qtab, const int32_t* geom, int32_t B, const void* out, void* workspace,
+                           size_t workspace_bytes) {
+  if (!geom || B < 0 || data_bytes < 0) return fail(MI_ERR_ARG, "%s: bad arguments", fn);
+  if (huff_idx && nsets < 1) return fail(MI_ERR_ARG, "%s: huff_idx needs nsets >= 1", fn);
   if (B == 0) return MI_OK;
-  if (!data || !seg_off || !seg_end || !huff || !qtab || !out_rgb) return fail(MI_ERR_ARG, "mi_jpeg_decode: null pointer");
+  if (!data || !seg_off || !seg_end || !huff || !qtab || !out) return fail(MI_ERR_ARG, "%s: null pointer", fn);
   const int W = geom[0], H = geom[1], nc = geom[2], ri = geom[3], nseg = geom[4];
   if (W < 1 || H < 1 || W > 65535 || H > 65535 || (nc != 1 && nc != 3) || ri < 0 || nseg < 1)
-    return fail(MI_ERR_ARG, "mi_jpeg_decode: bad geometry");
+    return fail(MI_ERR_ARG, "%s: bad geometry", fn);
   if (nc == 3) {
     const int h0 = geom[5], v0 = geom[6];
     const bool luma_ok = (h0 == 1 && v0 == 1) || (h0 == 2 && v0 == 1) || (h0 == 2 && v0 == 2);
     for (int c = 1; c < 3; ++c)
       if (geom[5 + 2 * c] != 1 || geom[6 + 2 * c] != 1 || !luma_ok)
-        return fail(MI_ERR_UNSUPPORTED, "mi_jpeg_decode: sampling must be luma 1x1/2x1/2x2 with chroma 1x1");
+        return fail(MI_ERR_UNSUPPORTED, "%s: sampling must be luma 1x1/2x1/2x2 with chroma 1x1", fn);
   }
   for (int c = 0; c < nc; ++c)
     if (geom[11 + c] < 0 || geom[11 + c] > 3 || geom[14 + c] < 0 || geom[14 + c] > 1 || geom[17 + c] < 0 ||
         geom[17 + c] > 1)
-      return fail(MI_ERR_ARG, "mi_jpeg_decode: bad table selector");
+      return fail(MI_ERR_ARG, "%s: bad table selector", fn);
   const size_t need = jpeg_workspace_bytes(geom, B, data_bytes);
   if (!workspace || workspace_bytes < need)
-    return fail(MI_ERR_ARG, "mi_jpeg_decode: workspace too small (%zu < %zu)", workspace_bytes, need);
+    return fail(MI_ERR_ARG, "%s: workspace too small (%zu < %zu)", fn, workspace_bytes, need);
+  return MI_OK;
+}
+
+int mi_jpeg_decode(const uint8_t* data, int64_t data_bytes, const int64_t* seg_off, const int64_t* seg_end, const void* huff,
+                   const int32_t* huff_idx, int32_t nsets, const uint16_t* qtab, const int32_t* geom, int32_t B,
+                   uint8_t* out_rgb, void* workspace, size_t workspace_bytes, void* stream) {
+  const int r = check_jpeg_args("mi_jpeg_decode", data, data_bytes, seg_off, seg_end, huff, huff_idx, nsets, qtab, geom,
+                                B, out_rgb, workspace, workspace_bytes);
+  if (r || B == 0) return r;
   HIP_TRY(jpeg_decode(data, data_bytes, seg_off, seg_end, huff, huff_idx, nsets, qtab, geom, B, out_rgb, workspace, workspace_bytes,
                       (hipStream_t)stream));
+  return MI_OK;
+}
+
+int mi_jpeg_decode_transform(const uint8_t* data, int64_t data_bytes, const int64_t* seg_off, const int64_t* seg_end,
+                             const void* huff, const int32_t* huff_idx, int32_t nsets, const uint16_t* qtab,
+                             const int32_t* geom, int32_t B, int32_t n, int mode, void* out, int out_dtype,
+                             void* workspace, size_t workspace_bytes, void* stream) {
+  const int r = check_jpeg_args("mi_jpeg_decode_transform", data, data_bytes, seg_off, seg_end, huff, huff_idx, nsets,
+                                qtab, geom, B, out, workspace, workspace_bytes);
+  if (r) return r;
+  if (n < 1 || n > 4096 || (mode != MI_PREP_CLIP && mode != MI_PREP_SQUASH))
+    return fail(MI_ERR_ARG, "mi_jpeg_decode_transform: bad size / mode");
+  if (out_dtype != MI_F32 && out_dtype != MI_BF16) return fail(MI_ERR_ARG, "mi_jpeg_decode_transform: out_dtype must be f32/bf16");
+  if (B == 0) return MI_OK;
+  const JpegXform xf{n, mode, out_dtype == MI_BF16, out};
+  const hipError_t e = jpeg_decode(data, data_bytes, seg_off, seg_end, huff, huff_idx, nsets, qtab, geom, B, nullptr,
+                                   workspace, workspace_bytes, (hipStream_t)stream, &xf);
+  if (e == hipErrorInvalidValue)
+    return fail(MI_ERR_UNSUPPORTED, "mi_jpeg_decode_transform: %dx%d -> %d does not fit one LDS band: use "
+                "mi_jpeg_decode + mi_preprocess_frames", geom[0], geom[1], n);
+  HIP_TRY(e);
   return MI_OK;
 }
 

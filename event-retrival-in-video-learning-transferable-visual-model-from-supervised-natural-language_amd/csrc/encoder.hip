@@ -212,6 +212,91 @@ __global__ __launch_bounds__(256) void vision_embed_ln_kernel(float* __restrict_
   }
 }
 
+// LayerNorm-folded vision tower (gemm_8q.hip EPI_LN_*): the consumer GEMMs read the fp16
+// residual stream itself and apply ln_1 / ln_2 in their epilogues from per-row (rstd, rstd * mean),
+// so no LayerNorm output h is written.  Both kernels describe the STORED fp16 values (what the
+// GEMM reads), with ln_stats' two-pass f32 arithmetic.
+__device__ __forceinline__ void store_row_stats(RowVals& r, int n4, int lane, int W, float* rs, int row) {
+  float mean, rstd;
+  ln_stats(r, n4, lane, W, mean, rstd);
+  if (lane == 0) *(float2*)(rs + 2 * (int64_t)row) = make_float2(rstd, rstd * mean);
+}
+
+// x = ln_pre([CLS | patches] + pos): f32 slot in, fp16 half-slot out (the wave holds the row
+// before it stores), rs = the statistics of the stored values (the first block's ln_1)
+__global__ __launch_bounds__(256) void vision_embed_ln16_kernel(float* __restrict__ x, const float* __restrict__ cls,
+                                                                const float* __restrict__ pos,
+                                                                const float* __restrict__ g,
+                                                                const float* __restrict__ b, int rows, int S, int W,
+                                                                float* __restrict__ rs) {
+  typedef _Float16 h4v __attribute__((ext_vector_type(4)));
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const int t = row % S, n4 = W >> 2;
+  const float4* xr = (const float4*)(x + (int64_t)row * W);
+  h4v* xh = (h4v*)((_Float16*)x + (int64_t)row * W * 2);
+  const float4* src = t == 0 ? (const float4*)cls : xr;
+  const float4* p4 = (const float4*)(pos + (int64_t)t * W);
+  RowVals r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = lane + 64 * i;
+    if (idx < n4) {
+      const float4 sv = src[idx], p = p4[idx];
+      r.v[i] = make_float4(sv.x + p.x, sv.y + p.y, sv.z + p.z, sv.w + p.w);
+    } else {
+      r.v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  float mean, rstd;
+  ln_stats(r, n4, lane, W, mean, rstd);
+  const float4* g4 = (const float4*)g;
+  const float4* b4 = (const float4*)b;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = lane + 64 * i;
+    if (idx < n4) {
+      const float4 gg = g4[idx], bb = b4[idx];
+      const h4v o{(_Float16)((r.v[i].x - mean) * rstd * gg.x + bb.x), (_Float16)((r.v[i].y - mean) * rstd * gg.y + bb.y),
+                  (_Float16)((r.v[i].z - mean) * rstd * gg.z + bb.z), (_Float16)((r.v[i].w - mean) * rstd * gg.w + bb.w)};
+      r.v[i] = make_float4((float)o[0], (float)o[1], (float)o[2], (float)o[3]);
+      xh[idx] = o;
+    }
+  }
+  store_row_stats(r, n4, lane, W, rs, row);
+}
+
+// x16 += delta (the bf16 out_proj / c_proj output, bias included), fp16 half-slot layout,
+// and the statistics of the stored row: residual_ln_kernel<RES_F16> without its LN output
+__global__ __launch_bounds__(256) void residual_stats_kernel(float* __restrict__ x, const uint16_t* __restrict__ delta,
+                                                             float* __restrict__ rs, int rows, int W) {
+  typedef _Float16 h4v __attribute__((ext_vector_type(4)));
+  typedef uint32_t u2v __attribute__((ext_vector_type(2)));
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const int n4 = W >> 2;
+  h4v* xh = (h4v*)((_Float16*)x + (int64_t)row * W * 2);
+  const u2v* dr = (const u2v*)(delta + (int64_t)row * W);
+  RowVals r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = lane + 64 * i;
+    if (idx < n4) {
+      const h4v vh = __builtin_nontemporal_load(&xh[idx]);
+      const u2v d = __builtin_nontemporal_load(&dr[idx]);
+      const h4v o{(_Float16)((float)vh[0] + bf2f((uint16_t)(d[0] & 0xffff))),
+                  (_Float16)((float)vh[1] + bf2f((uint16_t)(d[0] >> 16))),
+                  (_Float16)((float)vh[2] + bf2f((uint16_t)(d[1] & 0xffff))),
+                  (_Float16)((float)vh[3] + bf2f((uint16_t)(d[1] >> 16)))};
+      __builtin_nontemporal_store(o, &xh[idx]);
+      r.v[i] = make_float4((float)o[0], (float)o[1], (float)o[2], (float)o[3]);
+    } else {
+      r.v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  store_row_stats(r, n4, lane, W, rs, row);
+}
+
 __global__ __launch_bounds__(256) void text_embed_kernel(const int32_t* __restrict__ tokens,
                                                          const float* __restrict__ tok_emb,
                                                          const float* __restrict__ pos, float* __restrict__ x,
@@ -385,6 +470,22 @@ hipError_t vision_embed_ln(float* x, const float* cls, const float* pos, const f
   if (W % 4 || W > 1024) return hipErrorInvalidValue;
   hipLaunchKernelGGL(vision_embed_ln_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, x, cls, pos, g, b, rows, S, W,
                      g1, b1, h);
+  return hipGetLastError();
+}
+
+hipError_t vision_embed_ln16(float* x, const float* cls, const float* pos, const float* g, const float* b, int B,
+                             int S, int W, float* rs, hipStream_t s) {
+  const int rows = B * S;
+  if (W % 4 || W > 1024) return hipErrorInvalidValue;
+  if (rows <= 0) return hipSuccess;
+  hipLaunchKernelGGL(vision_embed_ln16_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, x, cls, pos, g, b, rows, S, W, rs);
+  return hipGetLastError();
+}
+
+hipError_t residual_stats(float* x, const uint16_t* delta, float* rs, int rows, int W, hipStream_t s) {
+  if (W % 4 || W > 1024) return hipErrorInvalidValue;
+  if (rows <= 0) return hipSuccess;
+  hipLaunchKernelGGL(residual_stats_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, x, delta, rs, rows, W);
   return hipGetLastError();
 }
 

@@ -103,10 +103,23 @@ struct BoolC {
 };
 
 // ABL (timing probes): 2 = no MFMAs, 4 = no epilogue work (accumulators kept live), 9 = stamps
-template <int EPI, int ABL = 0, int F = 0>
+typedef _Float16 f16x8_8q __attribute__((ext_vector_type(8)));
+
+template <int EPI>
+struct EpiKind8q {
+  static constexpr bool LN = EPI == EPI_LN_BF16 || EPI == EPI_LN_GELU_BF16;   // LayerNorm folded in (fp16 operands)
+  static constexpr bool GELU = EPI == EPI_GELU_BF16 || EPI == EPI_LN_GELU_BF16;
+  // LDS: 2 K-tile buffers, bias [2][BN]; LN: + row statistics [2][BM][2] + column sums [2][BN]
+  static constexpr int LDS = 2 * BUF + 2 * BN * 4 + (LN ? 2 * BM * 8 + 2 * BN * 4 : 0);
+};
+
+template <int EPI, int ABL = 0, int F = 0, bool OPF16 = false>
 __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * BUF + 2 * BN * 4];
+  using EK = EpiKind8q<EPI>;
+  __shared__ __attribute__((aligned(16))) char smem[EK::LDS];
   float* sbias = (float*)(smem + 2 * BUF);
+  float* srs = (float*)(smem + 2 * BUF + 2 * BN * 4);              // LN: [2][BM][2]
+  float* scol = (float*)(smem + 2 * BUF + 2 * BN * 4 + 2 * BM * 8);  // LN: [2][BN]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
@@ -188,6 +201,23 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
     }
   };
 
+  // per-tile vectors into LDS parity `par`: bias (wave 0); LN: column sums (wave 1) and the
+  // tile's 256 rows of (rstd, rstd * mean) (waves 2, 3; rs is readable 256 rows past M)
+  // (buffer-descriptor DMAs: the base is scalar, the lane offset lane * 16 -- no 64-bit
+  // per-lane address kept live across the tile)
+  auto dma_vec = [&](const float* base, float* lds) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 1024, 0x00020000);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (LDS_AS void*)lds, 16, (uint32_t)lane * 16, 0, 0, 0);
+  };
+  auto stage_vectors = [&](int m0, int n0, int par) {
+    if (wave == 0 && a.bias) dma_vec(a.bias + n0, sbias + par * BN);
+    if (EK::LN) {
+      if (wave == 1) dma_vec(a.colv + n0, scol + par * BN);
+      if (wave == 2) dma_vec(a.rs + (int64_t)m0 * 2, srs + par * BM * 2);
+      if (wave == 3) dma_vec(a.rs + (int64_t)(m0 + 128) * 2, srs + par * BM * 2 + 256);
+    }
+  };
+
   // ---- fragment side
   const int fr = lane & 15, fq = lane >> 4, g = fq;
   const int rd0 = fr * 128 + (((0 + fq) ^ (fr >> 1)) << 4);   // k 0..31 of the K-tile
@@ -228,7 +258,7 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
   // previous tile (its epilogue runs in this tile's phases 1-4)
   int pm0 = 0, pn0 = 0, ppar = 0;
   bool has_prev = false;
-  int nxt_n0 = 0, cpar = 0;
+  int nxt_m0 = 0, nxt_n0 = 0, cpar = 0;
   bool has_next = false;
 
   // the previous tile's epilogue: bias (+ QuickGELU), bf16, permlane16-swapped
@@ -262,21 +292,51 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
 #pragma unroll
       for (int ni = 0; ni < 4; ++ni) bias[ni] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
+    // LN: the column sums s_n beside c_n (= bias) and the lane's 8 rows' (rstd, rstd * mean)
+    // LN: the column sums s_n beside c_n (= bias); the lane's rows' (rstd, rstd * mean) are read
+    // per 16-row block below (one block ahead)
+    float4 col[4];
+    // lane offsets recomputed here (a lane constant kept from kernel entry is spilled around the
+    // tile loop, and its reload's vmcnt(0) would drain the DMAs in flight)
+    int ln_ = 0;
+    if (EK::LN) asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln_));
+    // (asm LDS reads: a compiler-visible LDS read waits vmcnt(0) for the LDS-DMAs in flight)
+    const uint32_t rab_a = (uint32_t)(uintptr_t)(const LDS_AS float*)(srs + ppar * BM * 2 + (wr * 128 + (ln_ & 15)) * 2);
+    f32x2 rab_c = (f32x2){0.f, 0.f}, rab_n = (f32x2){0.f, 0.f};
+    if (EK::LN) {
+      const uint32_t ca = (uint32_t)(uintptr_t)(const LDS_AS float*)(scol + ppar * BN + wc * 64 + 4 * (ln_ >> 4));
+      asm volatile("ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:64\n\tds_read_b128 %2, %4 offset:128\n\t"
+                   "ds_read_b128 %3, %4 offset:192\n\ts_waitcnt lgkmcnt(0)"
+                   : "=&v"(col[0]), "=&v"(col[1]), "=&v"(col[2]), "=&v"(col[3]) : "v"(ca) : "memory");
+      asm volatile("ds_read_b64 %0, %1" : "=v"(rab_c) : "v"(rab_a) : "memory");
+    }
     const int rows = min(a.M - pm0, BM);
     const __amdgpu_buffer_rsrc_t rsO = __builtin_amdgcn_make_buffer_rsrc(
         (void*)((uint16_t*)a.out + (int64_t)pm0 * a.ldo + pn0), (short)0, rows * (int)a.ldo * 2, 0x00020000);
 #pragma unroll
     for (int mi = 0; mi < 8; ++mi) {
       u32x4_8q dp[2];
+      if (EK::LN) {   // block mi's row statistics landed; block mi + 1's read goes out
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(rab_c) : : "memory");
+        if (mi < 7) asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(rab_n) : "v"(rab_a), "i"((mi + 1) * 128) : "memory");
+      }
 #pragma unroll
       for (int p = 0; p < 2; ++p) {
         uint2 pk[2];
 #pragma unroll
         for (int qq = 0; qq < 2; ++qq) {
           const int ni = 2 * p + qq;
-          f32x2 lo = (f32x2){acc[mi][ni][0], acc[mi][ni][1]} + (f32x2){bias[ni].x, bias[ni].y};
-          f32x2 hi = (f32x2){acc[mi][ni][2], acc[mi][ni][3]} + (f32x2){bias[ni].z, bias[ni].w};
-          if (EPI == EPI_GELU_BF16) {
+          f32x2 lo = (f32x2){acc[mi][ni][0], acc[mi][ni][1]};
+          f32x2 hi = (f32x2){acc[mi][ni][2], acc[mi][ni][3]};
+          if (EK::LN) {   // rstd * acc + (c_n - rstd * mean * s_n)
+            const f32x2 ar = (f32x2){rab_c.x, rab_c.x}, br = (f32x2){-rab_c.y, -rab_c.y};
+            lo = ar * lo + (br * (f32x2){col[ni].x, col[ni].y} + (f32x2){bias[ni].x, bias[ni].y});
+            hi = ar * hi + (br * (f32x2){col[ni].z, col[ni].w} + (f32x2){bias[ni].z, bias[ni].w});
+          } else {
+            lo = lo + (f32x2){bias[ni].x, bias[ni].y};
+            hi = hi + (f32x2){bias[ni].z, bias[ni].w};
+          }
+          if (EK::GELU) {
             lo = quick_gelu2_8q(lo);
             hi = quick_gelu2_8q(hi);
           }
@@ -305,6 +365,7 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
         __builtin_amdgcn_raw_buffer_store_b128(s1, rsO, voF + mi * blkO, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b128(s2, rsO, voF + mi * blkO + rows8, 0, 0);
       }
+      rab_c = rab_n;
     }
   };
 
@@ -363,8 +424,8 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
     if (P == 8 && FIRST) stamp(4);   // S4: before the first pair's phase-8 wait (the stores must be done)
     if (P == 8) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     if (P == 8 && FIRST) stamp(5);   // S5: after it
-    if (P == 8 && LAST && has_next && wave == 0 && a.bias)   // next tile's bias, older than phase 1's DMAs
-      glds16(a.bias + nxt_n0 + lane * 4, sbias + (cpar ^ 1) * BN);
+    if (P == 8 && LAST && has_next)   // next tile's bias (+ LN vectors), older than phase 1's DMAs
+      stage_vectors(nxt_m0, nxt_n0, cpar ^ 1);
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
@@ -388,9 +449,14 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
           for (int ni = 0; ni < 2; ++ni)
             // a tile's first MFMA into each accumulator (first pair, phases 1-4, k-step 0)
             // takes C = 0 as an inline constant: no zeroing pass between tiles
-            acc[mh * 4 + mi][nh * 2 + ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                fb[ni][ks], fa[mi][ks], (FIRST && P <= 4 && ks == 0) ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[mh * 4 + mi][nh * 2 + ni],
-                0, 0, 0);
+            if (OPF16)   // fp16 operands (the LN-folded GEMMs: x16 rows and W' = f16(W * gamma))
+              acc[mh * 4 + mi][nh * 2 + ni] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
+                  __builtin_bit_cast(f16x8_8q, fb[ni][ks]), __builtin_bit_cast(f16x8_8q, fa[mi][ks]),
+                  (FIRST && P <= 4 && ks == 0) ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[mh * 4 + mi][nh * 2 + ni], 0, 0, 0);
+            else
+              acc[mh * 4 + mi][nh * 2 + ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                  fb[ni][ks], fa[mi][ks], (FIRST && P <= 4 && ks == 0) ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[mh * 4 + mi][nh * 2 + ni],
+                  0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
     barrier();
   };
@@ -416,7 +482,7 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
   {
     int m0, n0;
     coords(blockIdx.x, m0, n0);
-    if (wave == 0 && a.bias) glds16(a.bias + n0 + lane * 4, sbias);
+    stage_vectors(m0, n0, 0);
   }
   issue(H_A0, 0);
   issue(H_B1, 0);
@@ -432,10 +498,7 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
     int cm0, cn0;
     coords(v, cm0, cn0);
     has_next = v + G < ntiles;
-    if (has_next) {
-      int nm0;
-      coords(v + G, nm0, nxt_n0);
-    }
+    if (has_next) coords(v + G, nxt_m0, nxt_n0);
     // (npairs >= 2, gemm_8q_ok: a one-pair instance beside these made hipcc spill ~200 VGPRs)
     pair(BoolC<true>{}, BoolC<false>{});
     for (int pp = 1; pp < npairs - 1; ++pp) pair(BoolC<false>{}, BoolC<false>{});
@@ -495,6 +558,14 @@ hipError_t gemm_8q(const GemmArgs& a0, int epi, hipStream_t s, int cus, int mode
   }
   const int nt = ((a.M + BM - 1) / BM) * (a.N / BN);
   const int grid = nt < cus ? nt : cus;
+  // the LayerNorm-folded GEMMs read fp16 operands; their vectors must be present
+  if (epi == EPI_LN_BF16 || epi == EPI_LN_GELU_BF16) {
+    if (!a.a_f16 || !a.rs || !a.colv || !a.bias || mode) return hipErrorInvalidValue;
+    if (epi == EPI_LN_BF16) hipLaunchKernelGGL((gemm_8q_kernel<EPI_LN_BF16, 0, 0, true>), dim3(grid), dim3(512), 0, s, a);
+    else hipLaunchKernelGGL((gemm_8q_kernel<EPI_LN_GELU_BF16, 0, 0, true>), dim3(grid), dim3(512), 0, s, a);
+    return hipGetLastError();
+  }
+  if (a.a_f16) return hipErrorInvalidValue;
 #define L8Q(E, ABL_, F_) hipLaunchKernelGGL((gemm_8q_kernel<E, ABL_, F_>), dim3(grid), dim3(512), 0, s, a)
 #if MICLIP_AB   // ablation / stamp probes: A/B build only
 #define L8Q_ALL(E)                   \

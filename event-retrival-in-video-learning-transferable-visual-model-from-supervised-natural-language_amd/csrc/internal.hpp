@@ -15,7 +15,12 @@ enum GemmEpi {
   EPI_RESID_F32 = 2,   // out f32 += acc + bias   (residual stream, in place)
   EPI_F32 = 3,         // out f32 = acc (+ bias)
   EPI_GELU_MX = 4,     // MX-fp8 GEMM only: out e4m3 = MX(quick_gelu(acc + bias)), scales -> o_scale
-  EPI_RELU_F32 = 5     // f32 GEMM only: out f32 = max(acc + bias, 0)
+  EPI_RELU_F32 = 5,    // f32 GEMM only: out f32 = max(acc + bias, 0)
+  // LayerNorm folded into the GEMM (gemm_8q.hip, fp16 operands: A = the fp16 residual stream x,
+  // W' = f16(W * gamma)): out bf16 = rstd_r * acc + (c_n - rstd_r * mean_r * s_n), c_n = bias
+  // (= b + W beta), s_n = colv[n] (= sum_k W'[n][k]), (rstd_r, rstd_r * mean_r) = rs[r]
+  EPI_LN_BF16 = 6,
+  EPI_LN_GELU_BF16 = 7     // the same, then QuickGELU
 };
 
 // MX block quantisation shared by the fp8 producers (gemm_mx.hip, encoder.hip):
@@ -62,6 +67,11 @@ struct GemmArgs {
   // persistent 8-phase kernels (gemm_8q.hip): workgroups start (blockIdx / 8) % stagger_phases x
   // stagger_ticks (100 MHz) late, so the CUs' tile epilogues (all 16 stores) do not coincide
   int stagger_phases = 0, stagger_ticks = 0;
+  // EPI_LN_* (gemm_8q.hip): operands are fp16 (f16 MFMA) when a_f16; rs is readable for
+  // 256 rows past M (the tile stages whole tiles' rows)
+  int a_f16 = 0;
+  const float* rs = nullptr;     // [M + 256][2] (rstd, rstd * mean) per row
+  const float* colv = nullptr;   // [N] s_n
 };
 
 // Requirements: K % 64 == 0, N % 128 == 0, A/W 16-byte aligned rows.
@@ -78,9 +88,15 @@ hipError_t gemm_8q(const GemmArgs& a, int epi, hipStream_t s, int cus, int mode 
 hipError_t gemm8q_probe_read(unsigned long long* host, int n);   // ABL 9 stamps (gemm_8q.hip)
 // baseline JPEG decode (jpeg.hip); geom as mi_jpeg_decode
 constexpr int JPEG_LDS_SETS = 4;   // table sets staged in LDS (4 x 3480 B each, <= 64 KB)
+// fused output of jpeg_decode: out [B][3][n][n] (f32 / bf16) = mi_preprocess_frames(decoded RGB, n, mode)
+struct JpegXform {
+  int n, mode, out_bf16;
+  void* out;
+};
 hipError_t jpeg_decode(const uint8_t* data, int64_t data_bytes, const int64_t* seg_off, const int64_t* seg_end,
                        const void* huff, const int32_t* huff_idx, int nsets, const uint16_t* qtab, const int32_t* geom,
-                       int nframes, uint8_t* out_rgb, void* ws, size_t ws_bytes, hipStream_t s);
+                       int nframes, uint8_t* out_rgb, void* ws, size_t ws_bytes, hipStream_t s,
+                       const JpegXform* xf = nullptr);
 size_t jpeg_workspace_bytes(const int32_t* geom, int nframes, int64_t data_bytes);
 // 256 x 128 tiles, deferred (drained) epilogue, three-slot ring (gemm_8r.hip)
 int gemm_8r_ok(const GemmArgs& a);
@@ -107,6 +123,15 @@ hipError_t layernorm_bf16(const float* x, int64_t in_stride, const float* g, con
 hipError_t vision_embed_ln(float* x, const float* cls, const float* pos, const float* g,
                            const float* b, int B, int S, int W, hipStream_t s, const float* g1 = nullptr,
                            const float* b1 = nullptr, uint16_t* h = nullptr);
+// LayerNorm-folded vision tower (EPI_LN_*): x = ln_pre([CLS | patches] + pos) written as fp16
+// into the first half of each f32 row slot (element (r, j) at ((half*)x)[2 r W + j]) and
+// rs[r] = (rstd, rstd * mean) of those fp16 values (the first block's ln_1 statistics)
+hipError_t vision_embed_ln16(float* x, const float* cls, const float* pos, const float* g, const float* b, int B,
+                             int S, int W, float* rs, hipStream_t s);
+// x16[r] = f16(x16[r] + delta[r]) in that half-row layout and rs[r] = (rstd, rstd * mean) of the
+// stored fp16 values: the residual add of residual_ln without its LayerNorm output (the
+// consumer GEMM applies the LayerNorm in its epilogue, EPI_LN_*)
+hipError_t residual_stats(float* x, const uint16_t* delta, float* rs, int rows, int W, hipStream_t s);
 // x[q*S + t] = tok_emb[tokens[q*S + t]] + pos[t]
 hipError_t text_embed(const int32_t* tokens, const float* tok_emb, const float* pos, float* x,
                       int Q, int S, int W, int vocab, hipStream_t s);
@@ -208,6 +233,15 @@ namespace miclip {
 int resample_coeffs(int in_size, double in0, double in1, int out_size, int filter, std::vector<int32_t>& kk,
                     std::vector<int32_t>& bounds);
 size_t preprocess_workspace_bytes(int64_t B, int H, int W, int n, int mode);
+// the device coefficient tables of mi_preprocess_frames' resample (H x W -> n x n crop, mode as
+// there): horizontal kh [n][ksh] / bh [n][2], vertical kv [n][ksv] / bv [n][2] (Pillow's int32
+// coefficients and (first tap, taps)); the crop's source columns [xlo, xlo + xw); bv on the host
+struct ResampleTables {
+  const int32_t *kh = nullptr, *bh = nullptr, *kv = nullptr, *bv = nullptr;
+  int ksh = 0, ksv = 0, xlo = 0, xw = 0;
+  std::vector<int32_t> hbv;
+};
+hipError_t resample_tables(int H, int W, int n, int mode, ResampleTables& t);
 // frames uint8 [B,H,W,3] -> out [B,3,n,n] f32 / bf16; mode 0 CLIP _transform, 1 squash (bilinear)
 hipError_t preprocess_frames(const uint8_t* frames, int64_t B, int H, int W, int n, int mode, void* out,
                              int out_bf16, void* ws, hipStream_t s);

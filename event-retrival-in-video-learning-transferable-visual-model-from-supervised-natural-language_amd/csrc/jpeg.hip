@@ -25,6 +25,7 @@
 #include <cstdint>
 #include <cstdlib>
 
+#include "common.hpp"
 #include "internal.hpp"
 #include "miclip.h"
 
@@ -1047,6 +1048,102 @@ __global__ __launch_bounds__(256) void jpeg_color_kernel(const uint8_t* __restri
   }
 }
 
+// ---- fused colour conversion + Pillow resample + crop + ToTensor/Normalize (mi_jpeg_decode_transform)
+// The RGB frame of jpeg_color_kernel never reaches HBM: one workgroup per (frame, band of
+// output rows) converts the source rows the band's vertical taps need (only the crop's source
+// columns) into LDS a few rows at a time, resamples each horizontally into LDS, then resamples
+// vertically and normalises.  Every step is the same integer arithmetic as color_px and
+// preprocess.hip's resample_h / resample_v kernels, so the output is bit-identical to decode +
+// mi_preprocess_frames (and so to Pillow + torchvision).
+constexpr int XF_PREC = 22;   // Pillow PRECISION_BITS
+constexpr int XF_RPI = 4;     // source rows converted per step
+
+__device__ __forceinline__ uint32_t xf_clip8(int acc) {
+  acc >>= XF_PREC;
+  return acc < 0 ? 0u : (acc > 255 ? 255u : (uint32_t)acc);
+}
+
+// RGB of pixel (x, y) of one frame's planes (color_px without the frame-major index)
+__device__ __forceinline__ uint32_t color_xy(const uint8_t* __restrict__ base, const JpegPlanes& pl, int ncomp,
+                                             int cmode, int cdw, int cdh, int x, int y) {
+  const int Y = base[pl.pbase[0] + (int64_t)y * pl.pstride[0] + x];
+  if (ncomp == 1) return (uint32_t)Y * 0x010101u;
+  const int cb = chroma_at(base + pl.pbase[1], pl.pstride[1], cdw, cdh, x, y, cmode) - 128;
+  const int cr = chroma_at(base + pl.pbase[2], pl.pstride[2], cdw, cdh, x, y, cmode) - 128;
+  const int r = Y + ((91881 * cr + 32768) >> 16);
+  const int gch = Y + ((-22554 * cb + 32768 - 46802 * cr) >> 16);
+  const int b = Y + ((116130 * cb + 32768) >> 16);
+  return (uint32_t)clamp255(r) | ((uint32_t)clamp255(gch) << 8) | ((uint32_t)clamp255(b) << 16);
+}
+
+struct XformK {
+  const int32_t *kh, *bh, *kv, *bv;   // preprocess.hip's tables (ResampleTables)
+  int ksh, ksv, n, xlo, xw;
+  int band, nbands, rows_max;         // output rows per workgroup; LDS rows for the widest band
+  float mean[3], sd[3];
+};
+
+template <bool OUT_BF16>
+__global__ __launch_bounds__(256) void jpeg_transform_kernel(const uint8_t* __restrict__ planes, JpegPlanes pl,
+                                                             int ncomp, int cmode, int cdw, int cdh, XformK xk,
+                                                             void* __restrict__ out) {
+#pragma clang fp contract(off)
+  extern __shared__ __attribute__((aligned(16))) char xsm[];
+  const int f = (int)(blockIdx.x / xk.nbands), band = (int)(blockIdx.x % xk.nbands);
+  const int n = xk.n, xw = xk.xw;
+  const int y0 = band * xk.band, y1 = min(n, y0 + xk.band);
+  const int ra = xk.bv[2 * y0];
+  int rb = ra;
+  for (int y = y0; y < y1; ++y) rb = max(rb, xk.bv[2 * y] + xk.bv[2 * y + 1]);
+  uint32_t* crow = (uint32_t*)xsm;          // [XF_RPI][xw] packed RGB of the source rows
+  uint32_t* hrow = crow + XF_RPI * xw;      // [rb - ra][n] the horizontal pass's rows
+  const uint8_t* base = planes + (int64_t)f * pl.plane_frame_bytes;
+  for (int r0 = ra; r0 < rb; r0 += XF_RPI) {
+    const int nr = min(XF_RPI, rb - r0);
+    for (int i = threadIdx.x; i < nr * xw; i += 256) {
+      const int rr = i / xw, x = i - rr * xw;
+      crow[i] = color_xy(base, pl, ncomp, cmode, cdw, cdh, xk.xlo + x, r0 + rr);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < nr * n; i += 256) {   // resample_h_kernel's sums
+      const int rr = i / n, ox = i - rr * n;
+      const int xb = xk.bh[2 * ox] - xk.xlo, xs = xk.bh[2 * ox + 1];
+      const int32_t* k = xk.kh + (int64_t)ox * xk.ksh;
+      const uint32_t* p = crow + rr * xw + xb;
+      int s0 = 1 << (XF_PREC - 1), s1 = s0, s2 = s0;
+      for (int j = 0; j < xs; ++j) {
+        const uint32_t v = p[j];
+        const int w = k[j];
+        s0 += (int)(v & 255u) * w;
+        s1 += (int)((v >> 8) & 255u) * w;
+        s2 += (int)((v >> 16) & 255u) * w;
+      }
+      hrow[(r0 - ra + rr) * n + ox] = xf_clip8(s0) | (xf_clip8(s1) << 8) | (xf_clip8(s2) << 16);
+    }
+    __syncthreads();
+  }
+  for (int i = threadIdx.x; i < (y1 - y0) * n; i += 256) {   // resample_v_kernel's sums + ToTensor / Normalize
+    const int yy = i / n, x = i - yy * n, y = y0 + yy;
+    const int yb = xk.bv[2 * y] - ra, ys = xk.bv[2 * y + 1];
+    const int32_t* k = xk.kv + (int64_t)y * xk.ksv;
+    int sc[3] = {1 << (XF_PREC - 1), 1 << (XF_PREC - 1), 1 << (XF_PREC - 1)};
+    for (int j = 0; j < ys; ++j) {
+      const uint32_t v = hrow[(yb + j) * n + x];
+      const int w = k[j];
+      sc[0] += (int)(v & 255u) * w;
+      sc[1] += (int)((v >> 8) & 255u) * w;
+      sc[2] += (int)((v >> 16) & 255u) * w;
+    }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const float v = ((float)xf_clip8(sc[c]) / 255.0f - xk.mean[c]) / xk.sd[c];
+      const int64_t o = (((int64_t)f * 3 + c) * n + y) * (int64_t)n + x;
+      if (OUT_BF16) ((uint16_t*)out)[o] = f2bf(v);
+      else ((float*)out)[o] = v;
+    }
+  }
+}
+
 }  // namespace
 
 // Workspace of the chunked entropy decode (after the coefficients and planes).
@@ -1096,10 +1193,52 @@ static bool jp_serial_forced() {
 #endif
 }
 
+// The fused transform's launch shape: output rows per workgroup (band) and LDS bytes -- the
+// widest band's source rows of horizontal output plus XF_RPI converted source rows -- kept
+// within 150 KB by halving the band (tall sources need more rows per output row).
+hipError_t jpeg_xform_plan(int H, int W, int n, int mode, XformK& xk, size_t& lds) {
+  ResampleTables t;
+  const hipError_t e = resample_tables(H, W, n, mode, t);
+  if (e != hipSuccess) return e;
+  xk.kh = t.kh;
+  xk.bh = t.bh;
+  xk.kv = t.kv;
+  xk.bv = t.bv;
+  xk.ksh = t.ksh;
+  xk.ksv = t.ksv;
+  xk.n = n;
+  xk.xlo = t.xlo;
+  xk.xw = t.xw;
+  // torchvision's Normalize constants: Python floats -> float32 (preprocess.hip)
+  const float mean[3] = {(float)0.48145466, (float)0.4578275, (float)0.40821073};
+  const float sd[3] = {(float)0.26862954, (float)0.26130258, (float)0.27577711};
+  for (int c = 0; c < 3; ++c) {
+    xk.mean[c] = mean[c];
+    xk.sd[c] = sd[c];
+  }
+  for (int band = 16; band >= 1; band /= 2) {
+    int rows_max = 0;
+    for (int y0 = 0; y0 < n; y0 += band) {
+      const int y1 = std::min(n, y0 + band);
+      int rb = t.hbv[2 * y0];
+      for (int y = y0; y < y1; ++y) rb = std::max(rb, t.hbv[2 * y] + t.hbv[2 * y + 1]);
+      rows_max = std::max(rows_max, rb - t.hbv[2 * y0]);
+    }
+    lds = ((size_t)XF_RPI * t.xw + (size_t)rows_max * n) * 4;
+    if (lds <= 150 * 1024) {
+      xk.band = band;
+      xk.nbands = (n + band - 1) / band;
+      xk.rows_max = rows_max;
+      return hipSuccess;
+    }
+  }
+  return hipErrorInvalidValue;   // a source too wide / tall for one band in LDS: decode + preprocess instead
+}
+
 // Host launch: see include/miclip.h mi_jpeg_decode for the argument contract.
 hipError_t jpeg_decode(const uint8_t* data, int64_t data_bytes, const int64_t* seg_off, const int64_t* seg_end,
                        const void* huff, const int32_t* huff_idx, int nsets, const uint16_t* qtab, const int32_t* geom,
-                       int nframes, uint8_t* out_rgb, void* ws, size_t ws_bytes, hipStream_t s) {
+                       int nframes, uint8_t* out_rgb, void* ws, size_t ws_bytes, hipStream_t s, const JpegXform* xf) {
   // geom: [W, H, ncomp, ri, nseg, hs0, vs0, hs1, vs1, hs2, vs2, q0, q1, q2, dc0, dc1, dc2, ac0, ac1, ac2]
   const int W = geom[0], H = geom[1], ncomp = geom[2];
   JpegGeom g{};
@@ -1246,6 +1385,25 @@ hipError_t jpeg_decode(const uint8_t* data, int64_t data_bytes, const int64_t* s
     cmode = (hr == 1 && vr == 1) ? 0 : (hr == 2 && vr == 1) ? 1 : 2;
     cdw = (W * g.hs[1] + hmax - 1) / hmax;   // libjpeg downsampled_width
     cdh = (H * g.vs[1] + vmax - 1) / vmax;
+  }
+  if (xf) {   // fused colour + resample + crop + normalise (jpeg_transform_kernel)
+    XformK xk{};
+    size_t lds = 0;
+    if ((e = jpeg_xform_plan(H, W, xf->n, xf->mode, xk, lds)) != hipSuccess) return e;
+    const int64_t per_launch = std::max<int64_t>(1, (int64_t)0x7fffffff / ((int64_t)xk.nbands * 256));
+    for (int64_t f0 = 0; f0 < nframes; f0 += per_launch) {
+      const int nfc = (int)std::min<int64_t>(per_launch, nframes - f0);
+      char* o = (char*)xf->out + f0 * 3 * (int64_t)xf->n * xf->n * (xf->out_bf16 ? 2 : 4);
+      const dim3 grid((unsigned)((int64_t)nfc * xk.nbands));
+      if (xf->out_bf16)
+        hipLaunchKernelGGL(jpeg_transform_kernel<true>, grid, dim3(256), lds, s, planes + f0 * bytes, pl, ncomp, cmode,
+                           cdw, cdh, xk, (void*)o);
+      else
+        hipLaunchKernelGGL(jpeg_transform_kernel<false>, grid, dim3(256), lds, s, planes + f0 * bytes, pl, ncomp, cmode,
+                           cdw, cdh, xk, (void*)o);
+      if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    return hipSuccess;
   }
   const int64_t px = (int64_t)W * H;
   const int64_t fc_px = std::max<int64_t>(1, ((int64_t)1 << 31) / px);

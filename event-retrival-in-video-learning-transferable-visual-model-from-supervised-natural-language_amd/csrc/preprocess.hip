@@ -153,6 +153,8 @@ Geometry geometry(int H, int W, int n, int mode) {
 struct Tables {
   int32_t *kh = nullptr, *bh = nullptr, *kv = nullptr, *bv = nullptr;
   int ksh = 0, ksv = 0, r0 = 0, rows = 0;
+  int xlo = 0, xw = 0;            // source columns the crop's taps read: [xlo, xlo + xw)
+  std::vector<int32_t> hbv;       // host copy of bv (the fused JPEG transform sizes its row bands from it)
 };
 
 std::mutex g_tab_mu;
@@ -201,6 +203,14 @@ hipError_t get_tables(int H, int W, int n, int mode, Tables& out) {
   int hi = 0;
   for (int y = 0; y < n; ++y) hi = std::max(hi, bv[2 * y] + bv[2 * y + 1]);
   t.rows = hi - t.r0;
+  int xlo = W, xhi = 0;
+  for (int x = 0; x < n; ++x) {
+    xlo = std::min(xlo, bh[2 * x]);
+    xhi = std::max(xhi, bh[2 * x] + bh[2 * x + 1]);
+  }
+  t.xlo = xlo;
+  t.xw = xhi - xlo;
+  t.hbv = bv;
   const size_t nb = (kh.size() + bh.size() + kv.size() + bv.size()) * 4;
   char* d = nullptr;
   if ((e = hipMalloc(&d, nb)) != hipSuccess) return e;
@@ -266,6 +276,22 @@ int resample_coeffs(int in_size, double in0, double in1, int out_size, int filte
   for (size_t i = 0; i < pre.size(); ++i)
     kk[i] = pre[i] < 0 ? (int32_t)(-0.5 + pre[i] * (1 << PREC)) : (int32_t)(0.5 + pre[i] * (1 << PREC));
   return ksize;
+}
+
+hipError_t resample_tables(int H, int W, int n, int mode, ResampleTables& r) {
+  Tables t;
+  const hipError_t e = get_tables(H, W, n, mode, t);
+  if (e != hipSuccess) return e;
+  r.kh = t.kh;
+  r.bh = t.bh;
+  r.kv = t.kv;
+  r.bv = t.bv;
+  r.ksh = t.ksh;
+  r.ksv = t.ksv;
+  r.xlo = t.xlo;
+  r.xw = t.xw;
+  r.hbv = t.hbv;
+  return hipSuccess;
 }
 
 size_t preprocess_workspace_bytes(int64_t B, int H, int W, int n, int mode) {

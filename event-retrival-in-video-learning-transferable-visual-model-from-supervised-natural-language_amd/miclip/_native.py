@@ -37,6 +37,7 @@ EXPORTS = (
     "mi_jpeg_workspace_bytes", "mi_jpeg_decode", "mi_host_gather",
     "mi_op_quantize_mx", "mi_op_gemm_mx",
     "mi_mirror_build", "mi_rank_mirror_workspace_bytes", "mi_rank_mirror", "mi_normalize_rows_f16",
+    "mi_jpeg_decode_transform",
 )
 
 
@@ -129,6 +130,8 @@ def _bind(path):
         "mi_preprocess_frames": (ctypes.c_int, [P, I64, I32, I32, I32, ctypes.c_int, P, ctypes.c_int, P, SZ, P]),
         "mi_jpeg_workspace_bytes": (SZ, [P, I32, I64]),
         "mi_jpeg_decode": (ctypes.c_int, [P, I64, P, P, P, P, I32, P, P, I32, P, P, SZ, P]),
+        "mi_jpeg_decode_transform": (ctypes.c_int, [P, I64, P, P, P, P, I32, P, P, I32, I32, ctypes.c_int, P,
+                                                    ctypes.c_int, P, SZ, P]),
         "mi_host_gather": (ctypes.c_int, [P, P, P, I64, I32]),
     }
     for name, (res, args) in sig.items():

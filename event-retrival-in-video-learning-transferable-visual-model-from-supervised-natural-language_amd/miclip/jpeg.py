@@ -324,13 +324,27 @@ _PAD = np.frombuffer(b"\xff\xd9" * 16, np.uint8)
 SUB_FRAMES = 2048                # frames per decode launch: the host gathers launch j + 1 while the GPU decodes j
 
 
+_COPY_STREAMS = {}
+
+
+def _copy_stream(dev):
+    """A side stream per device for the frames' H2D copies, so the copy of launch
+    j + 1 overlaps the decode kernels of launch j on the compute stream."""
+    import torch
+    cs = _COPY_STREAMS.get(dev)
+    if cs is None:
+        cs = _COPY_STREAMS[dev] = torch.cuda.Stream(device=dev)
+    return cs
+
+
 def _upload(bufs, keep, segl, starts, total, dev, slot=0):
     """Entropy-coded bytes of the kept frames gathered straight into pinned
     staging buffer `slot` by 16 native threads (mi_host_gather, no GIL), then
-    an asynchronous DMA to the device on the current stream; 32 bytes of EOI
-    markers as padding.  The buffer is reused only after its previous copy
-    has completed (event), so a caller alternating slots overlaps the next
-    gather with this copy and the kernels that follow it."""
+    an asynchronous DMA to the device on the copy stream, which the current
+    (compute) stream waits for; 32 bytes of EOI markers as padding.  The buffer
+    is reused only after its previous copy has completed (event), so a caller
+    alternating slots overlaps the next gather and copy with the kernels that
+    consume this one."""
     import ctypes
     import torch
     with _STAGE_LOCK:
@@ -351,11 +365,17 @@ def _upload(bufs, keep, segl, starts, total, dev, slot=0):
         N.check(N.lib().mi_host_gather(st.data_ptr(), ptrs.ctypes.data, lens.ctypes.data, n, 16), "mi_host_gather")
         del keepalive
         st.numpy()[total:total + 32] = _PAD
-        d = torch.empty(total + 32, dtype=torch.uint8, device=dev)
-        d.copy_(st[:total + 32], non_blocking=True)
+        cur = torch.cuda.current_stream(dev)
+        cs = _copy_stream(dev)
+        cs.wait_stream(cur)          # the buffer the caching allocator hands out may be in use on the compute stream
+        with torch.cuda.stream(cs):
+            d = torch.empty(total + 32, dtype=torch.uint8, device=dev)
+            d.copy_(st[:total + 32], non_blocking=True)
         ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(dev))
+        ev.record(cs)
         _STAGE_EVT[slot] = ev
+        cur.wait_event(ev)
+        d.record_stream(cur)
         return d
 
 
@@ -433,25 +453,39 @@ def decode_batch(bufs, device="cuda", dedupe=True):
     return out
 
 
-def decode_groups(bufs, device="cuda", dedupe=True, heads=None):
+def decode_groups(bufs, device="cuda", dedupe=True, heads=None, transform=None):
     """``decode_batch`` by launch: yields (indices, uint8 [len(indices), H, W, 3]
     device tensor) per geometry group in one buffer (frames the host decodes
     come one per group; (indices, None) for a file neither path can read), so a
-    consumer can take each group's frames without restacking them."""
+    consumer can take each group's frames without restacking them.
+
+    ``transform=(n, squash, out_dtype)``: yield the preprocessed frames
+    [len(indices), 3, n, n] instead (openai/CLIP ``_transform(n)``, or the
+    squash resize of compare_models.py:387-391), through the fused
+    ``mi_jpeg_decode_transform`` (no RGB frames in HBM; bit-identical to decoding
+    and then ``preprocess.preprocess_frames``); host-decoded frames and sources
+    the fused kernel does not take are decoded and then preprocessed."""
     import torch
     L = N.lib()
     if heads is None:
         heads = [parse(b) for b in bufs]
+
+    def host(i):
+        idx, rgb = _host_group(bufs, i, device)
+        if transform is None or rgb is None:
+            return idx, rgb
+        from .preprocess import preprocess_frames
+        return idx, preprocess_frames(rgb, transform[0], squash=transform[1], out_dtype=transform[2])
+
     groups = {}
     for i, h in enumerate(heads):
         if h.supported:
             groups.setdefault(_geom_key(h), []).append(i)
         else:
-            yield _host_group(bufs, i, device)
+            yield host(i)
     dev = torch.device(device)
     for key, idx in groups.items():
         W, H, nc, samp, ri = key
-        h0 = heads[idx[0]]
         mcux = -(-W // (8 * (max(s[0] for s in samp) if nc == 3 else 1)))
         mcuy = -(-H // (8 * (max(s[1] for s in samp) if nc == 3 else 1)))
         nseg = -(-(mcux * mcuy) // ri) if ri else 1
@@ -461,7 +495,7 @@ def decode_groups(bufs, device="cuda", dedupe=True, heads=None):
             if ri:
                 segs = _segments(bufs[i], h)
                 if len(segs) != nseg:     # restart markers not where DRI says: leave it to the host decoder
-                    yield _host_group(bufs, i, device)
+                    yield host(i)
                     continue
             else:
                 segs = ((h.scan_start, len(bufs[i])),)
@@ -473,34 +507,57 @@ def decode_groups(bufs, device="cuda", dedupe=True, heads=None):
         args = launch_args(bufs, heads, keep, segl, key, dedupe)
         if args is None:     # per-frame table selectors differ within the group: the host decoder
             for i in keep:
-                yield _host_group(bufs, i, device)
+                yield host(i)
             continue
         geom, huff, hidx, qt, offs, ends, starts, nsets = args
-        total = int(starts[-1])
-        d_huff = torch.from_numpy(huff.view(np.uint8).reshape(-1)).to(dev)
-        rgb = torch.empty(B, H, W, 3, dtype=torch.uint8, device=dev)
         gp = geom.ctypes.data
-        # launches of SUB_FRAMES frames: the host gathers launch j + 1 into the other
-        # pinned buffer while the GPU copies and decodes launch j
+        # launches of SUB_FRAMES frames: the host gathers (and the copy stream uploads) launch
+        # j + 1 while the GPU decodes launch j; the per-frame arrays go up once for the group,
+        # each launch's segment offsets relative to its own data
         step = max(1, min(B, SUB_FRAMES))
         subs = [(j0, min(B, j0 + step)) for j0 in range(0, B, step)]
+        rel = offs.copy(), ends.copy()
+        for j0, j1 in subs:
+            rel[0][j0 * nseg:j1 * nseg] -= starts[j0]
+            rel[1][j0 * nseg:j1 * nseg] -= starts[j0]
+        d_huff = torch.from_numpy(huff.view(np.uint8).reshape(-1)).to(dev)
+        d_off = torch.from_numpy(rel[0]).to(dev)
+        d_end = torch.from_numpy(rel[1]).to(dev)
+        d_hidx = torch.from_numpy(np.ascontiguousarray(hidx)).to(dev)
+        d_qt = torch.from_numpy(np.ascontiguousarray(qt)).to(dev)
+        fused = transform is not None
+        if fused:
+            n, squash, odt = transform
+            out = torch.empty(B, 3, n, n, dtype=odt, device=dev)
+            mode = N.MI_PREP_SQUASH if squash else N.MI_PREP_CLIP
+        else:
+            out = torch.empty(B, H, W, 3, dtype=torch.uint8, device=dev)
         nb = max(L.mi_jpeg_workspace_bytes(gp, j1 - j0, int(starts[j1] - starts[j0])) for j0, j1 in subs)
         ws = torch.empty(max(nb, 1), dtype=torch.uint8, device=dev)
         for u, (j0, j1) in enumerate(subs):
             base, sub_total = int(starts[j0]), int(starts[j1] - starts[j0])
             d_data = _upload(bufs, keep[j0:j1], segl[j0:j1], starts[j0:j1 + 1] - base, sub_total, dev, slot=u & 1)
-            d_off = torch.from_numpy(offs[j0 * nseg:j1 * nseg] - base).to(dev, non_blocking=False)
-            d_end = torch.from_numpy(ends[j0 * nseg:j1 * nseg] - base).to(dev, non_blocking=False)
-            d_hidx = torch.from_numpy(np.ascontiguousarray(hidx[j0:j1])).to(dev)
-            d_qt = torch.from_numpy(np.ascontiguousarray(qt[j0:j1])).to(dev)
             # without dedupe frame f uses set f: this launch's frames start at set j0
             hp = d_huff.data_ptr() + (0 if dedupe else j0 * 4 * HUFF_BYTES)
-            N.check(L.mi_jpeg_decode(d_data.data_ptr(), sub_total, d_off.data_ptr(), d_end.data_ptr(), hp,
-                                     d_hidx.data_ptr() if dedupe else None, nsets, d_qt.data_ptr(), gp, j1 - j0,
-                                     rgb[j0:j1].data_ptr(), ws.data_ptr(), nb, N.stream_ptr(dev)), "mi_jpeg_decode")
+            a = (d_data.data_ptr(), sub_total, d_off.data_ptr() + j0 * nseg * 8, d_end.data_ptr() + j0 * nseg * 8, hp,
+                 d_hidx.data_ptr() + j0 * 4 if dedupe else None, nsets, d_qt.data_ptr() + j0 * 4 * 64 * 2, gp, j1 - j0)
+            if fused:
+                rc = L.mi_jpeg_decode_transform(*a, n, mode, out[j0:j1].data_ptr(), N.dtype_code(odt), ws.data_ptr(),
+                                                nb, N.stream_ptr(dev))
+                if rc == -3:     # MI_ERR_UNSUPPORTED: too large for the fused kernel's LDS bands
+                    from .preprocess import preprocess_frames
+                    rgb = torch.empty(j1 - j0, H, W, 3, dtype=torch.uint8, device=dev)
+                    N.check(L.mi_jpeg_decode(*a, rgb.data_ptr(), ws.data_ptr(), nb, N.stream_ptr(dev)),
+                            "mi_jpeg_decode")
+                    out[j0:j1] = preprocess_frames(rgb, n, squash=squash, out_dtype=odt)
+                else:
+                    N.check(rc, "mi_jpeg_decode_transform")
+            else:
+                N.check(L.mi_jpeg_decode(*a, out[j0:j1].data_ptr(), ws.data_ptr(), nb, N.stream_ptr(dev)),
+                        "mi_jpeg_decode")
             del d_data
         del ws
-        yield keep, rgb
+        yield keep, out
 
 
 def _host_group(bufs, i, device):

@@ -167,9 +167,13 @@ def load_frames(paths, n_px: int = 224, device="cuda", squash: bool = False, out
         heads = [jpeg.parse(b) for b in bufs]
         out = torch.zeros(len(paths), 3, n_px, n_px, dtype=out_dtype or torch.float32, device=device)
         failed = []
+        # the fused decode + transform kernel (mi_jpeg_decode_transform: no RGB frames in HBM,
+        # bit-identical to decode + preprocess_frames); $MICLIP_JPEG_FUSED=0 runs the two steps
+        fused = os.environ.get("MICLIP_JPEG_FUSED", "1") != "0"
+        tf = (n_px, squash, out.dtype) if fused else None
         for a, b in _budget_slices([jpeg.decoded_bytes(h) for h in heads], decode_budget()):
             # each geometry group's decoded frames go to the resampler as the decoder's own [B,H,W,3] buffer
-            for idx, rgb in jpeg.decode_groups(bufs[a:b], device, heads=heads[a:b]):
+            for idx, rgb in jpeg.decode_groups(bufs[a:b], device, heads=heads[a:b], transform=tf):
                 idx = [a + i for i in idx]
                 if rgb is None:
                     i = idx[0]
@@ -180,7 +184,7 @@ def load_frames(paths, n_px: int = 224, device="cuda", squash: bool = False, out
                         print(f"Error preprocessing image {paths[i]}: cannot identify or decode image file")
                     failed.append(i)
                     continue
-                res = preprocess_frames(rgb, n_px, squash=squash, out_dtype=out.dtype)
+                res = rgb if fused else preprocess_frames(rgb, n_px, squash=squash, out_dtype=out.dtype)
                 del rgb
                 if idx == list(range(idx[0], idx[0] + len(idx))):
                     out[idx[0]:idx[0] + len(idx)] = res

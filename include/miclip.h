@@ -36,7 +36,7 @@ extern "C" {
 #endif
 
 #define MICLIP_ABI_VERSION 3   /* 2: mi_jpeg_workspace_bytes / mi_jpeg_decode take the data size;
-                                  3: mi_normalize_rows_f16 */
+                                  3: mi_normalize_rows_f16, mi_jpeg_decode_transform */
 
 enum mi_dtype { MI_F32 = 0, MI_BF16 = 1, MI_F16 = 2, MI_FP8 = 3 /* weights only: MX-fp8 vision GEMMs */ };
 enum mi_status { MI_OK = 0, MI_ERR_ARG = -1, MI_ERR_HIP = -2, MI_ERR_UNSUPPORTED = -3, MI_ERR_STATE = -4 };
@@ -257,6 +257,21 @@ size_t mi_jpeg_workspace_bytes(const int32_t* geom, int32_t B, int64_t data_byte
 int mi_jpeg_decode(const uint8_t* data, int64_t data_bytes, const int64_t* seg_off, const int64_t* seg_end, const void* huff,
                    const int32_t* huff_idx, int32_t nsets, const uint16_t* qtab, const int32_t* geom, int32_t B,
                    uint8_t* out_rgb, void* workspace, size_t workspace_bytes, void* stream);
+
+/* mi_jpeg_decode fused with mi_preprocess_frames: the same arguments and workspace
+ * (mi_jpeg_workspace_bytes), and out = device [B,3,n,n] (MI_F32 / MI_BF16) =
+ * mi_preprocess_frames(decoded RGB, n, mode) bit for bit — Pillow decode +
+ * openai/CLIP _transform (mode MI_PREP_CLIP) or compare_models.py's squash
+ * (MI_PREP_SQUASH), i.e. the reference's `preprocess(Image.open(p))`
+ * (Backend/services/embedding_service.py:472-480, Backend/embedding.py:46) — without
+ * the RGB frames: colour conversion, both resample passes and Normalize run in one
+ * kernel over the component planes (csrc/jpeg.hip jpeg_transform_kernel).
+ * MI_ERR_UNSUPPORTED when the source does not fit its LDS bands (then decode +
+ * preprocess separately). */
+int mi_jpeg_decode_transform(const uint8_t* data, int64_t data_bytes, const int64_t* seg_off, const int64_t* seg_end,
+                             const void* huff, const int32_t* huff_idx, int32_t nsets, const uint16_t* qtab,
+                             const int32_t* geom, int32_t B, int32_t n, int mode, void* out, int out_dtype,
+                             void* workspace, size_t workspace_bytes, void* stream);
 
 /* Host-side gather of the frames' entropy-coded bytes into one (pinned) staging
  * buffer before the upload: n pieces src[i] of len[i] bytes concatenated into

@@ -1,0 +1,14 @@
+# r04: LayerNorm-folded tower + fused JPEG transform — parity tests, bench line, kernel trace
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out/prof4c
+true || timeout -k 10 900 python -u -m pytest tests/test_gpu_jpeg.py tests/test_gpu_encode.py tests/test_gpu_flows.py \
+  tests/test_gpu_rk_flow.py tests/test_gpu_ops.py tests/test_gpu_service.py -x -q -rf --timeout 200 \
+  --timeout-method thread > gpurun_out/r4c_pytest.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -5 gpurun_out/r4c_pytest.log
+if [ $rc -ne 0 ]; then exit $rc; fi
+timeout -k 10 600 python bench.py --steps 20 --warmup 3 --no-parity-mode > gpurun_out/r4c_bench.log 2> gpurun_out/r4c_bench.err || exit $?
+tail -1 gpurun_out/r4c_bench.log | cut -c1-300
+tail -1 gpurun_out/r4c_bench.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps(d['kernels']['jpeg_ingest_720p'])); print(d['roofline']['avg_launch_us'], d['kernels']['gemm_qkv'], d['kernels']['gemm_fc'])"
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof4c -o bench -- \
+  python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-rank-roofline --no-parity-mode > gpurun_out/prof4c/stdout.log 2>&1 || exit $?
+find gpurun_out/prof4c -name "*kernel_stats.csv" | head -2

@@ -207,3 +207,30 @@ def test_context_on_two_streams(gpu):
             b = m.encode_image(p2)
         torch.cuda.synchronize()
         assert torch.equal(a, r1) and torch.equal(b, r2)
+
+
+@pytest.mark.parametrize("name,n", [("test-small", 30), ("ViT-B/32", 8), ("ViT-B/32", 1), ("ViT-L/14", 2)])
+def test_lnfold_tower_matches_oracle(gpu, monkeypatch, name, n):
+    """The LayerNorm-folded bf16 vision tower (ln_1 / ln_2 applied in the in_proj / c_fc
+    GEMM epilogues on the fp16 residual stream, W' = f16(W * gamma); api.cpp
+    run_tower_fold, taken for whole 256-row tiles: n * tokens >= 256) against float64,
+    and against the unfolded tower (A/B build, MICLIP_LNFOLD=0): both within the
+    north-star cosine, and the folded one no less accurate than the unfolded one
+    beyond a small margin.  n = 1 (50 rows) runs the unfolded path in both builds."""
+    import torch
+    from miclip import _native, config, weights
+    from oracle import clip_ref
+    from oracle.clip_ref import cosine
+    cfg = config.get_config(name)
+    px = weights.synthetic_pixels(n, cfg.image_resolution, seed=77)
+    ref = clip_ref.encode_image(px, state_dict(name), cfg, np.float64)
+    got = _model(name, gpu, image_chunk=n).encode_image(torch.from_numpy(px)).cpu().numpy()
+    c_fold = _check(got, ref, f"{name} folded")
+    monkeypatch.setattr(_native, "lib", _native.lib_ab)
+    monkeypatch.setenv("MICLIP_LNFOLD", "0")
+    got0 = _model(name, gpu, image_chunk=n).encode_image(torch.from_numpy(px)).cpu().numpy()
+    c_plain = _check(got0, ref, f"{name} unfolded")
+    assert cosine(got, got0).min() > 1 - COS_TOL
+    assert 1 - c_fold <= 1.5 * (1 - c_plain) + 2e-5, (c_fold, c_plain)
+    if n * cfg.vision_tokens < 256:
+        assert np.array_equal(got, got0)     # the same (unfolded) path in both libraries

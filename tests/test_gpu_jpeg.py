@@ -299,3 +299,57 @@ def test_segments_outside_the_contract_stay_in_bounds(gpu):
     got = _decode_raw(bufs, [2, 1, 0], lambda f, b, st: rng(b, st))
     for f, b in enumerate([2, 1, 0]):
         assert np.array_equal(got[f], refs[b]), f"reversed frame {f}"
+
+
+@pytest.mark.parametrize("squash", [False, True])
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_fused_decode_transform_bit_identical(gpu, squash, dtype):
+    """mi_jpeg_decode_transform (colour conversion + both Pillow resample passes +
+    crop + ToTensor/Normalize in one kernel over the component planes, no RGB
+    frames in HBM) == mi_jpeg_decode + mi_preprocess_frames, bit for bit: the
+    reference frames (1280x720 4:2:0), 4:4:4 / 4:2:2 / grayscale / restart
+    markers / odd sizes, sources smaller than the output (upsampling), and 1080p /
+    4K (narrower LDS bands), both transforms, f32 and bf16 outputs."""
+    import torch
+    from miclip import jpeg
+    from miclip.preprocess import preprocess_frames
+    files = sorted(glob.glob(os.path.join(ROOT, "golden", "ref_frames", "*.jpg")))[:4]
+    bufs = [open(f, "rb").read() for f in files]
+    bufs += [_save(_img(h, w, s), quality=q, subsampling=sub) for h, w, s, q, sub in
+             ((481, 641, 1, 90, 0), (333, 500, 2, 75, 1), (720, 1280, 3, 85, 2), (100, 60, 4, 80, 2),
+              (1080, 1920, 5, 90, 2), (2160, 3840, 6, 70, 2))]
+    bufs += [_save(_img(300, 400, 7, "L"), quality=80), _save(_img(256, 320, 8), quality=90, restart_marker_rows=1)]
+    odt = torch.float32 if dtype == "f32" else torch.bfloat16
+    for n in (224, 336):
+        got = {}
+        for idx, x in jpeg.decode_groups(bufs, "cuda", transform=(n, squash, odt)):
+            for r, i in enumerate(idx):
+                got[i] = x[r]
+        for idx, rgb in jpeg.decode_groups(bufs, "cuda"):
+            ref = preprocess_frames(rgb, n, squash=squash, out_dtype=odt)
+            for r, i in enumerate(idx):
+                a, b = got[i], ref[r]
+                assert a.shape == b.shape == (3, n, n)
+                assert torch.equal(a.view(torch.int16) if dtype == "bf16" else a.view(torch.int32),
+                                   b.view(torch.int16) if dtype == "bf16" else b.view(torch.int32)), (n, i)
+
+
+def test_load_frames_fused_matches_two_step(gpu, tmp_path, monkeypatch):
+    """preprocess.load_frames through the fused kernel == the two-step path
+    ($MICLIP_JPEG_FUSED=0), including a PNG and an unreadable file (zero frame)."""
+    import torch
+    from miclip import preprocess
+    paths = []
+    for i, f in enumerate(sorted(glob.glob(os.path.join(ROOT, "golden", "ref_frames", "*.jpg")))[:5]):
+        paths.append(f)
+    png = tmp_path / "x.png"
+    _img(90, 160, 3).save(png)
+    paths.append(str(png))
+    bad = tmp_path / "bad.jpg"
+    bad.write_bytes(b"not a jpeg")
+    paths.append(str(bad))
+    a, fa = preprocess.load_frames(paths, 224, device="cuda", out_dtype=torch.bfloat16)
+    monkeypatch.setenv("MICLIP_JPEG_FUSED", "0")
+    b, fb = preprocess.load_frames(paths, 224, device="cuda", out_dtype=torch.bfloat16)
+    assert fa == fb == [len(paths) - 1]
+    assert torch.equal(a.view(torch.int16), b.view(torch.int16))
