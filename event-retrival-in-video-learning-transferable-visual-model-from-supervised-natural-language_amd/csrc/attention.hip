@@ -380,7 +380,11 @@ __global__ __launch_bounds__(512) void attention_flash_kernel(const uint16_t* __
 //   per 64-key chunk: S^T = K Q^T (8 MFMA), online softmax in the log2
 //   domain with lazy rescale (flash kernel above), P to bf16, 8 PV MFMAs;
 //   the partial last chunk runs only its valid 16-key tiles (NKT template).
-template <int NW, bool TT2 = true>
+// SPLIT (S % 16 small, e.g. L/14's 257 = 16 x 16 + 1): the last, nearly empty query tile
+// would add a third tile to wave 0 while the other waves idle with two; instead every wave
+// runs it over its share of the 16-key tiles (w, w + NW, ...) and wave 0 merges the partial
+// softmax states (m, l, o) of its valid rows through LDS.
+template <int NW, bool TT2 = true, bool SPLIT = false>
 __global__ __launch_bounds__(NW * 64) void attention_res_kernel(const uint16_t* __restrict__ qkv,
                                                                 uint16_t* __restrict__ out, int S, int W, int H,
                                                                 uint8_t* __restrict__ q8, uint8_t* __restrict__ qs,
@@ -587,11 +591,121 @@ __global__ __launch_bounds__(NW * 64) void attention_res_kernel(const uint16_t* 
       }
     }
   };
-  for (int t = wave; t < nqt; t += 2 * NW) {
-    if (TT2 && t + NW < nqt) tiles(std::integral_constant<int, 2>{}, t, t + NW);
+  const int nfull = SPLIT ? nqt - 1 : nqt;   // SPLIT: the last tile is shared out below
+  for (int t = wave; t < nfull; t += 2 * NW) {
+    if (TT2 && t + NW < nfull) tiles(std::integral_constant<int, 2>{}, t, t + NW);
     else {
       tiles(std::integral_constant<int, 1>{}, t, t);
-      if (!TT2 && t + NW < nqt) tiles(std::integral_constant<int, 1>{}, t + NW, t + NW);
+      if (!TT2 && t + NW < nfull) tiles(std::integral_constant<int, 1>{}, t + NW, t + NW);
+    }
+  }
+  if (SPLIT) {
+    // the last query tile (rows 16 (nqt - 1) .. S - 1, vr <= 16 of them) over this wave's
+    // 16-key tiles; the same arithmetic as chunk() per key tile (log2-domain online softmax)
+    const int tl = nqt - 1, vr = S - 16 * tl;
+    const int nkt = (S + 15) / 16;
+    bf16x8 qf[2];
+    {
+      const int qrow = min(tl * 16 + fr, S - 1);
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) qf[s2] = *(const bf16x8*)(qb + (int64_t)qrow * ld + 32 * s2 + 8 * g);
+    }
+    float m = -INFINITY, l = 0.f;
+    f32x4 o[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int kt = wave; kt < nkt; kt += NW) {
+      const int kb = kt * 16;
+      const bf16x8 k0 = *(const bf16x8*)(Kimg + kb * 128 + rk0);
+      const bf16x8 k1 = *(const bf16x8*)(Kimg + kb * 128 + rk1);
+      f32x4 sc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k0, qf[0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      sc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k1, qf[1], sc, 0, 0, 0);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (kb + 4 * g + j >= S) sc[j] = -INFINITY;
+      float cm = fmaxf(fmaxf(sc[0], sc[1]), fmaxf(sc[2], sc[3]));
+      {
+        const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(cm), __float_as_uint(cm), false, false);
+        cm = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+        const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(cm), __float_as_uint(cm), false, false);
+        cm = fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+      }
+      const float cmu = cm * sl2;   // finite: key tile kb < S holds key kb
+      if (cmu > m + RESCALE) {
+        const float alpha = __builtin_amdgcn_exp2f(m - cmu);
+        l *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
+        m = cmu;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) sc[j] = __builtin_amdgcn_exp2f(fmaf(sc[j], sl2, -m));
+      l += (sc[0] + sc[1]) + (sc[2] + sc[3]);
+      bf16x8 pb;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        pb[j] = (__bf16)sc[j];
+        pb[4 + j] = (__bf16)0.f;
+      }
+      const char* vc = Vimg + kb * 128 + rvb;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const s16x4 lo = tr_read(vc + ((dt ^ vx) << 5));
+        const s16x4 hi = tr_read(vc + 16 * 128 + ((dt ^ vx) << 5));
+        typedef short s16x8 __attribute__((ext_vector_type(8)));
+        const s16x8 v8 = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, v8), pb, o[dt], 0, 0, 0);
+      }
+    }
+    float lt = l;
+    {
+      const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(lt), __float_as_uint(lt), false, false);
+      lt = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+      const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(lt), __float_as_uint(lt), false, false);
+      lt = __uint_as_float(b[0]) + __uint_as_float(b[1]);
+    }
+    // partial states of the valid rows: [wave][row][m, l, o 0..63] after the K / V images
+    float* part = (float*)(res_lds + 2 * spad * 128);
+    if (fr < vr) {
+      float* pw = part + (wave * vr + fr) * 68;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) pw[4 + dt * 16 + 4 * g + j] = o[dt][j];
+      if (g == 0) {
+        pw[0] = m;
+        pw[1] = lt;
+      }
+    }
+    __syncthreads();
+    if (wave == 0 && fr < vr) {
+      float M = -INFINITY;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) M = fmaxf(M, part[(w * vr + fr) * 68]);
+      float L = 0.f;
+      f32x4 O[4];
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) O[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int w = 0; w < NW; ++w) {
+        const float* pw = part + (w * vr + fr) * 68;
+        const float sw = pw[0] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(pw[0] - M);
+        L += pw[1] * sw;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) O[dt][j] += pw[4 + dt * 16 + 4 * g + j] * sw;
+      }
+      const float inv = 1.0f / L;
+      const int qrow = tl * 16 + fr;
+      if (q8) {   // never taken: the MX tower's attention runs the 32x32 kernel (SPLIT is bf16 only)
+      } else {
+        uint16_t* dst = out + ((int64_t)bseq * S + qrow) * W + h * 64 + 4 * g;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+          *(uint2*)(dst + dt * 16) = make_uint2(pack_bf16x2(O[dt][0] * inv, O[dt][1] * inv),
+                                                pack_bf16x2(O[dt][2] * inv, O[dt][3] * inv));
+      }
     }
   }
 }
@@ -965,7 +1079,7 @@ hipError_t attention(const uint16_t* qkv, uint16_t* out, int B, int S, int W, in
 #else
     int var = 0;
 #endif
-    if (var < 1 || var > 10) var = S > 320 ? 5 : 1;
+    if (var < 1 || var > 12) var = S > 320 ? 5 : 1;
     const int64_t rp = ((int64_t)B * S + 1) & ~1;
     auto set_lds = [&](const void* fn, int slot) -> hipError_t {
       static bool attr_set[11] = {false, false, false, false, false, false, false, false, false, false, false};
@@ -980,6 +1094,21 @@ hipError_t attention(const uint16_t* qkv, uint16_t* out, int B, int S, int W, in
     if ((e = set_lds((const void*)KERNEL, SLOT)) != hipSuccess) return e;       \
     hipLaunchKernelGGL(KERNEL, grid, dim3(THREADS), lds, s, __VA_ARGS__);       \
   }
+#if MICLIP_AB
+    // A/B variant 12: the nearly empty last query tile (S % 16 in 1..4, bf16 output) split over
+    // the 8 waves' key tiles (attention_res_kernel SPLIT).  Measured at L/14 (scripts/attn_micro.py,
+    // r04): 1074 vs 1031 us per 1667-frame chunk -- the second workgroup on the CU already fills
+    // the idle waves -- so the unsplit kernel stays the default.  Variant 11 = variant 1.
+    const int vr = S - 16 * ((S + 15) / 16 - 1);
+    if (var == 12 && vr <= 4 && !q8) {
+      const size_t lds_s = lds + (size_t)8 * vr * 68 * 4;
+      if ((e = set_lds((const void*)attention_res_kernel<8, false, true>, 0)) != hipSuccess) return e;
+      hipLaunchKernelGGL((attention_res_kernel<8, false, true>), grid, dim3(512), lds_s, s, qkv, out, S, W, H, q8, qs,
+                         rp);
+      return hipGetLastError();
+    }
+#endif
+    if (var == 11 || var == 12) var = 1;
     if (var == 1) ATT_LAUNCH(1, (attention_res_kernel<8, false>), 512, qkv, out, S, W, H, q8, qs, rp)
     else if (var == 5) ATT_LAUNCH(5, (attention_r32_kernel<12, false>), 768, qkv, out, S, W, H, q8, qs, rp, 0)
 #if MICLIP_AB

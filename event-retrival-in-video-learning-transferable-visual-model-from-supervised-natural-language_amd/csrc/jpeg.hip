@@ -413,15 +413,6 @@ struct JpegMcu {
   int8_t comp[16], dh[16], dv[16];
 };
 
-__device__ __forceinline__ int64_t block_addr(const JpegGeom& g, const JpegMcu& mc, int64_t blk) {
-  const int64_t m = blk / mc.bpm;
-  const int bb = (int)(blk - m * mc.bpm);
-  const int c = mc.comp[bb];
-  const int64_t my = m / g.mcux, mx = m - my * g.mcux;
-  const int hs_c = pick3(c, g.hs[0], g.hs[1], g.hs[2]), vs_c = pick3(c, g.vs[0], g.vs[1], g.vs[2]);
-  const int bw_c = pick3(c, g.bw[0], g.bw[1], g.bw[2]), cb_c = pick3(c, g.cbase[0], g.cbase[1], g.cbase[2]);
-  return cb_c + (my * vs_c + mc.dv[bb]) * bw_c + mx * hs_c + mc.dh[bb];
-}
 
 // Decode from the reader's position in state (b, k) until the position reaches
 // `stop` (at a symbol boundary) or, when writing, the frame's last block is
@@ -434,7 +425,21 @@ __device__ __forceinline__ void jp_run(UReader& br, const JpegHuff* __restrict__
                                        const JpegMcu& mc, const uint8_t* __restrict__ zz, int& b, int& k,
                                        uint32_t stop, int64_t blk, int64_t total, int& nblk, int (&dc)[3],
                                        int16_t* __restrict__ out) {
-  int16_t* bp = WRITE ? out + block_addr(g, mc, blk) * 64 : nullptr;
+  // the block's MCU coordinates, advanced per block (block_addr's 64-bit divisions once per
+  // call, not at every block end: in the wave's lockstep some lane ends a block nearly every trip)
+  int mx = 0, my = 0;
+  if (WRITE) {
+    const int64_t m = blk / mc.bpm;
+    my = (int)(m / g.mcux);
+    mx = (int)(m - (int64_t)my * g.mcux);
+  }
+  auto addr = [&](int bb) -> int64_t {
+    const int c = mc.comp[bb];
+    const int hs_c = pick3(c, g.hs[0], g.hs[1], g.hs[2]), vs_c = pick3(c, g.vs[0], g.vs[1], g.vs[2]);
+    const int bw_c = pick3(c, g.bw[0], g.bw[1], g.bw[2]), cb_c = pick3(c, g.cbase[0], g.cbase[1], g.cbase[2]);
+    return cb_c + (int64_t)(my * vs_c + mc.dv[bb]) * bw_c + mx * hs_c + mc.dh[bb];
+  };
+  int16_t* bp = WRITE ? out + addr(b) * 64 : nullptr;
   while (br.pos < stop && (!WRITE || blk < total)) {
     const int c = mc.comp[b];
     const JpegHuff* tp = k ? T + pick3(c, g.acsel[0], g.acsel[1], g.acsel[2]) * 2 + 1
@@ -472,7 +477,13 @@ __device__ __forceinline__ void jp_run(UReader& br, const JpegHuff* __restrict__
       b = b + 1 == mc.bpm ? 0 : b + 1;
       ++nblk;
       ++blk;
-      if (WRITE && blk < total) bp = out + block_addr(g, mc, blk) * 64;
+      if (WRITE) {
+        if (b == 0) {
+          mx = mx + 1 == g.mcux ? 0 : mx + 1;
+          my += mx == 0 ? 1 : 0;
+        }
+        if (blk < total) bp = out + addr(b) * 64;
+      }
     }
   }
 }
@@ -1057,6 +1068,7 @@ __global__ __launch_bounds__(256) void jpeg_color_kernel(const uint8_t* __restri
 // mi_preprocess_frames (and so to Pillow + torchvision).
 constexpr int XF_PREC = 22;   // Pillow PRECISION_BITS
 constexpr int XF_RPI = 4;     // source rows converted per step
+constexpr int XF_NT = 512;    // threads per workgroup (two workgroups per CU at ~70 KB of LDS each)
 
 __device__ __forceinline__ uint32_t xf_clip8(int acc) {
   acc >>= XF_PREC;
@@ -1076,21 +1088,98 @@ __device__ __forceinline__ uint32_t color_xy(const uint8_t* __restrict__ base, c
   return (uint32_t)clamp255(r) | ((uint32_t)clamp255(gch) << 8) | ((uint32_t)clamp255(b) << 16);
 }
 
+// RGB of the 4 pixels x0 .. x0 + 3 of row y (x0 % 4 == 0, 1 <= x0, x0 + 4 < W: no chroma edge
+// column): one dword of Y and one (unaligned) dword per chroma row instead of a byte load per
+// sample; the same fancy-upsampling / colour arithmetic as chroma_at + color_px
+// 4 bytes at any address as one value: the two aligned dwords around them, byte-aligned
+__device__ __forceinline__ uint32_t load4u(const uint8_t* p) {
+  const uintptr_t a = (uintptr_t)p;
+  const uint32_t* q = (const uint32_t*)(a & ~(uintptr_t)3);
+  return __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)(a & 3));
+}
+
+__device__ __forceinline__ void color4(const uint8_t* __restrict__ base, const JpegPlanes& pl, int cmode, int cdh,
+                                       int x0, int y, uint32_t* __restrict__ o) {
+  // planes are 64-byte aligned with row strides of whole blocks: the Y dword is aligned
+  const uint32_t yw = *(const uint32_t*)(base + pl.pbase[0] + (int64_t)y * pl.pstride[0] + x0);
+  int cb[4], cr[4];
+  if (cmode == 0) {
+    const uint32_t bw = *(const uint32_t*)(base + pl.pbase[1] + (int64_t)y * pl.pstride[1] + x0);
+    const uint32_t rw = *(const uint32_t*)(base + pl.pbase[2] + (int64_t)y * pl.pstride[2] + x0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      cb[i] = (int)((bw >> (8 * i)) & 255u);
+      cr[i] = (int)((rw >> (8 * i)) & 255u);
+    }
+  } else {
+    const int c0 = (x0 >> 1) - 1;   // chroma columns c0 .. c0 + 3 serve the 4 pixels
+    int tb[4], tr[4];
+    if (cmode == 1) {
+      const uint32_t bw = load4u(base + pl.pbase[1] + (int64_t)y * pl.pstride[1] + c0);
+      const uint32_t rw = load4u(base + pl.pbase[2] + (int64_t)y * pl.pstride[2] + c0);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        tb[k] = (int)((bw >> (8 * k)) & 255u);
+        tr[k] = (int)((rw >> (8 * k)) & 255u);
+      }
+      // h2v1_fancy_upsample: even pixel (v * 3 + left + 1) >> 2, odd (v * 3 + right + 2) >> 2
+      cb[0] = (tb[1] * 3 + tb[0] + 1) >> 2;
+      cb[1] = (tb[1] * 3 + tb[2] + 2) >> 2;
+      cb[2] = (tb[2] * 3 + tb[1] + 1) >> 2;
+      cb[3] = (tb[2] * 3 + tb[3] + 2) >> 2;
+      cr[0] = (tr[1] * 3 + tr[0] + 1) >> 2;
+      cr[1] = (tr[1] * 3 + tr[2] + 2) >> 2;
+      cr[2] = (tr[2] * 3 + tr[1] + 1) >> 2;
+      cr[3] = (tr[2] * 3 + tr[3] + 2) >> 2;
+    } else {
+      const int r = y >> 1;
+      const int rf = (y & 1) ? min(r + 1, cdh - 1) : max(r - 1, 0);
+      const uint32_t bn = load4u(base + pl.pbase[1] + (int64_t)r * pl.pstride[1] + c0);
+      const uint32_t bf = load4u(base + pl.pbase[1] + (int64_t)rf * pl.pstride[1] + c0);
+      const uint32_t rn = load4u(base + pl.pbase[2] + (int64_t)r * pl.pstride[2] + c0);
+      const uint32_t rfw = load4u(base + pl.pbase[2] + (int64_t)rf * pl.pstride[2] + c0);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        tb[k] = (int)((bn >> (8 * k)) & 255u) * 3 + (int)((bf >> (8 * k)) & 255u);
+        tr[k] = (int)((rn >> (8 * k)) & 255u) * 3 + (int)((rfw >> (8 * k)) & 255u);
+      }
+      // h2v2_fancy_upsample: even pixel (th * 3 + left + 8) >> 4, odd (th * 3 + right + 7) >> 4
+      cb[0] = (tb[1] * 3 + tb[0] + 8) >> 4;
+      cb[1] = (tb[1] * 3 + tb[2] + 7) >> 4;
+      cb[2] = (tb[2] * 3 + tb[1] + 8) >> 4;
+      cb[3] = (tb[2] * 3 + tb[3] + 7) >> 4;
+      cr[0] = (tr[1] * 3 + tr[0] + 8) >> 4;
+      cr[1] = (tr[1] * 3 + tr[2] + 7) >> 4;
+      cr[2] = (tr[2] * 3 + tr[1] + 8) >> 4;
+      cr[3] = (tr[2] * 3 + tr[3] + 7) >> 4;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int Y = (int)((yw >> (8 * i)) & 255u);
+    const int b_ = cb[i] - 128, r_ = cr[i] - 128;
+    const int r = Y + ((91881 * r_ + 32768) >> 16);
+    const int gch = Y + ((-22554 * b_ + 32768 - 46802 * r_) >> 16);
+    const int b = Y + ((116130 * b_ + 32768) >> 16);
+    o[i] = (uint32_t)clamp255(r) | ((uint32_t)clamp255(gch) << 8) | ((uint32_t)clamp255(b) << 16);
+  }
+}
+
 struct XformK {
   const int32_t *kh, *bh, *kv, *bv;   // preprocess.hip's tables (ResampleTables)
-  int ksh, ksv, n, xlo, xw;
+  int ksh, ksv, n, xlo, xw, W;        // xlo % 4 == 0, xw % 4 == 0 (the span rounded out)
   int band, nbands, rows_max;         // output rows per workgroup; LDS rows for the widest band
   float mean[3], sd[3];
 };
 
 template <bool OUT_BF16>
-__global__ __launch_bounds__(256) void jpeg_transform_kernel(const uint8_t* __restrict__ planes, JpegPlanes pl,
+__global__ __launch_bounds__(XF_NT) void jpeg_transform_kernel(const uint8_t* __restrict__ planes, JpegPlanes pl,
                                                              int ncomp, int cmode, int cdw, int cdh, XformK xk,
                                                              void* __restrict__ out) {
 #pragma clang fp contract(off)
   extern __shared__ __attribute__((aligned(16))) char xsm[];
   const int f = (int)(blockIdx.x / xk.nbands), band = (int)(blockIdx.x % xk.nbands);
-  const int n = xk.n, xw = xk.xw;
+  const int n = xk.n, xw = xk.xw;   // xw: the crop's source span rounded out to whole 4-pixel groups
   const int y0 = band * xk.band, y1 = min(n, y0 + xk.band);
   const int ra = xk.bv[2 * y0];
   int rb = ra;
@@ -1100,12 +1189,21 @@ __global__ __launch_bounds__(256) void jpeg_transform_kernel(const uint8_t* __re
   const uint8_t* base = planes + (int64_t)f * pl.plane_frame_bytes;
   for (int r0 = ra; r0 < rb; r0 += XF_RPI) {
     const int nr = min(XF_RPI, rb - r0);
-    for (int i = threadIdx.x; i < nr * xw; i += 256) {
-      const int rr = i / xw, x = i - rr * xw;
-      crow[i] = color_xy(base, pl, ncomp, cmode, cdw, cdh, xk.xlo + x, r0 + rr);
+    const int xq = xw >> 2;
+    for (int i = threadIdx.x; i < nr * xq; i += XF_NT) {   // 4 pixels per thread
+      const int rr = i / xq, x0 = xk.xlo + 4 * (i - rr * xq), y = r0 + rr;
+      uint32_t* o = crow + rr * xw + (x0 - xk.xlo);
+      if (ncomp == 3 && x0 >= 4 && x0 + 8 <= xk.W) {
+        uint32_t c4[4];
+        color4(base, pl, cmode, cdh, x0, y, c4);
+        *(uint4*)o = make_uint4(c4[0], c4[1], c4[2], c4[3]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = x0 + j < xk.W ? color_xy(base, pl, ncomp, cmode, cdw, cdh, x0 + j, y) : 0u;
+      }
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < nr * n; i += 256) {   // resample_h_kernel's sums
+    for (int i = threadIdx.x; i < nr * n; i += XF_NT) {   // resample_h_kernel's sums
       const int rr = i / n, ox = i - rr * n;
       const int xb = xk.bh[2 * ox] - xk.xlo, xs = xk.bh[2 * ox + 1];
       const int32_t* k = xk.kh + (int64_t)ox * xk.ksh;
@@ -1122,7 +1220,7 @@ __global__ __launch_bounds__(256) void jpeg_transform_kernel(const uint8_t* __re
     }
     __syncthreads();
   }
-  for (int i = threadIdx.x; i < (y1 - y0) * n; i += 256) {   // resample_v_kernel's sums + ToTensor / Normalize
+  for (int i = threadIdx.x; i < (y1 - y0) * n; i += XF_NT) {   // resample_v_kernel's sums + ToTensor / Normalize
     const int yy = i / n, x = i - yy * n, y = y0 + yy;
     const int yb = xk.bv[2 * y] - ra, ys = xk.bv[2 * y + 1];
     const int32_t* k = xk.kv + (int64_t)y * xk.ksv;
@@ -1207,8 +1305,9 @@ hipError_t jpeg_xform_plan(int H, int W, int n, int mode, XformK& xk, size_t& ld
   xk.ksh = t.ksh;
   xk.ksv = t.ksv;
   xk.n = n;
-  xk.xlo = t.xlo;
-  xk.xw = t.xw;
+  xk.xlo = t.xlo & ~3;                          // whole 4-pixel groups (color4); columns past W
+  xk.xw = ((t.xlo + t.xw + 3) & ~3) - xk.xlo;   // are never read by the taps
+  xk.W = W;
   // torchvision's Normalize constants: Python floats -> float32 (preprocess.hip)
   const float mean[3] = {(float)0.48145466, (float)0.4578275, (float)0.40821073};
   const float sd[3] = {(float)0.26862954, (float)0.26130258, (float)0.27577711};
@@ -1224,7 +1323,7 @@ hipError_t jpeg_xform_plan(int H, int W, int n, int mode, XformK& xk, size_t& ld
       for (int y = y0; y < y1; ++y) rb = std::max(rb, t.hbv[2 * y] + t.hbv[2 * y + 1]);
       rows_max = std::max(rows_max, rb - t.hbv[2 * y0]);
     }
-    lds = ((size_t)XF_RPI * t.xw + (size_t)rows_max * n) * 4;
+    lds = ((size_t)XF_RPI * xk.xw + (size_t)rows_max * n) * 4;
     if (lds <= 150 * 1024) {
       xk.band = band;
       xk.nbands = (n + band - 1) / band;
@@ -1390,16 +1489,16 @@ hipError_t jpeg_decode(const uint8_t* data, int64_t data_bytes, const int64_t* s
     XformK xk{};
     size_t lds = 0;
     if ((e = jpeg_xform_plan(H, W, xf->n, xf->mode, xk, lds)) != hipSuccess) return e;
-    const int64_t per_launch = std::max<int64_t>(1, (int64_t)0x7fffffff / ((int64_t)xk.nbands * 256));
+    const int64_t per_launch = std::max<int64_t>(1, (int64_t)0x7fffffff / ((int64_t)xk.nbands * XF_NT));
     for (int64_t f0 = 0; f0 < nframes; f0 += per_launch) {
       const int nfc = (int)std::min<int64_t>(per_launch, nframes - f0);
       char* o = (char*)xf->out + f0 * 3 * (int64_t)xf->n * xf->n * (xf->out_bf16 ? 2 : 4);
       const dim3 grid((unsigned)((int64_t)nfc * xk.nbands));
       if (xf->out_bf16)
-        hipLaunchKernelGGL(jpeg_transform_kernel<true>, grid, dim3(256), lds, s, planes + f0 * bytes, pl, ncomp, cmode,
+        hipLaunchKernelGGL(jpeg_transform_kernel<true>, grid, dim3(XF_NT), lds, s, planes + f0 * bytes, pl, ncomp, cmode,
                            cdw, cdh, xk, (void*)o);
       else
-        hipLaunchKernelGGL(jpeg_transform_kernel<false>, grid, dim3(256), lds, s, planes + f0 * bytes, pl, ncomp, cmode,
+        hipLaunchKernelGGL(jpeg_transform_kernel<false>, grid, dim3(XF_NT), lds, s, planes + f0 * bytes, pl, ncomp, cmode,
                            cdw, cdh, xk, (void*)o);
       if ((e = hipGetLastError()) != hipSuccess) return e;
     }

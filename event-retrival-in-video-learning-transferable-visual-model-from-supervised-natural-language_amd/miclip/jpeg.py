@@ -322,6 +322,7 @@ _STAGE_EVT = [None, None]        # the last H2D copy out of each
 _STAGE_LOCK = threading.Lock()
 _PAD = np.frombuffer(b"\xff\xd9" * 16, np.uint8)
 SUB_FRAMES = 2048                # frames per decode launch: the host gathers launch j + 1 while the GPU decodes j
+FIRST_SUB = 512                  # the first launch of a group: the pipeline's unhidden head
 
 
 _COPY_STREAMS = {}
@@ -367,7 +368,9 @@ def _upload(bufs, keep, segl, starts, total, dev, slot=0):
         st.numpy()[total:total + 32] = _PAD
         cur = torch.cuda.current_stream(dev)
         cs = _copy_stream(dev)
-        cs.wait_stream(cur)          # the buffer the caching allocator hands out may be in use on the compute stream
+        # allocated on the copy stream's pool (the caching allocator reuses a block freed after its
+        # record_stream(cur) only once the compute stream's work on it is done): no wait on the
+        # compute stream, so this copy overlaps the previous launch's kernels
         with torch.cuda.stream(cs):
             d = torch.empty(total + 32, dtype=torch.uint8, device=dev)
             d.copy_(st[:total + 32], non_blocking=True)
@@ -514,8 +517,11 @@ def decode_groups(bufs, device="cuda", dedupe=True, heads=None, transform=None):
         # launches of SUB_FRAMES frames: the host gathers (and the copy stream uploads) launch
         # j + 1 while the GPU decodes launch j; the per-frame arrays go up once for the group,
         # each launch's segment offsets relative to its own data
+        # the first launch is short (FIRST_SUB frames), so the GPU starts after a short gather +
+        # copy instead of a whole launch's worth (the rest of the pipeline hides the host side)
         step = max(1, min(B, SUB_FRAMES))
-        subs = [(j0, min(B, j0 + step)) for j0 in range(0, B, step)]
+        first = FIRST_SUB if B > 2 * FIRST_SUB else step
+        subs = [(0, min(B, first))] + [(j0, min(B, j0 + step)) for j0 in range(min(B, first), B, step)]
         rel = offs.copy(), ends.copy()
         for j0, j1 in subs:
             rel[0][j0 * nseg:j1 * nseg] -= starts[j0]

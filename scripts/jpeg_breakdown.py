@@ -1,7 +1,9 @@
 """Where the GPU JPEG ingest's wall time goes (8192 reference frames by
 default): header parse, the pinned staging copy + upload (jpeg._upload), the
-device decode (mi_jpeg_decode, synchronised), the resample, measured by
-wrapping the stages of miclip.jpeg.decode_groups."""
+device decode (mi_jpeg_decode_transform, fused, the default; or mi_jpeg_decode +
+the resample with argument 2 = "two"), each synchronised (so the stages do not
+overlap here as they do in the pipeline), measured by wrapping the stages of
+miclip.jpeg.decode_groups.  usage: python scripts/jpeg_breakdown.py [frames] [fused|two]"""
 import glob
 import json
 import os
@@ -15,6 +17,7 @@ from miclip import _native as N, jpeg  # noqa: E402
 from miclip.preprocess import preprocess_frames  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
+FUSED = (sys.argv[2] if len(sys.argv) > 2 else "fused") == "fused"
 files = sorted(glob.glob(os.path.join(ROOT, "tests", "golden", "ref_frames", "*.jpg")))
 raw = [open(f, "rb").read() for f in files]
 bufs = [raw[i % len(raw)] for i in range(B)]
@@ -36,12 +39,15 @@ def timed(name, fn):
 jpeg._upload = timed("upload (pinned copy + H2D)", jpeg._upload)
 L = N.lib()
 orig_decode = L.mi_jpeg_decode
+orig_xform = L.mi_jpeg_decode_transform
 
 
 class _Wrap:
     def __getattr__(self, n):
         if n == "mi_jpeg_decode":
             return timed("mi_jpeg_decode (device)", orig_decode)
+        if n == "mi_jpeg_decode_transform":
+            return timed("mi_jpeg_decode_transform (device)", orig_xform)
         return getattr(L, n)
 
 
@@ -53,7 +59,11 @@ for rep in range(3):
     heads = [jpeg.parse(b) for b in bufs]
     T["parse"] = time.perf_counter() - t0
     outs = []
-    for idx, rgb in jpeg.decode_groups(bufs, dev, heads=heads):
+    tf = (224, False, torch.bfloat16) if FUSED else None
+    for idx, rgb in jpeg.decode_groups(bufs, dev, heads=heads, transform=tf):
+        if FUSED:
+            outs.append(rgb)
+            continue
         t1 = time.perf_counter()
         outs.append(preprocess_frames(rgb, 224, out_dtype=torch.bfloat16))
         torch.cuda.synchronize(dev)
@@ -64,4 +74,5 @@ for rep in range(3):
     del outs
     T = {k: round(v * 1e3, 1) for k, v in T.items()}
     T["other host"] = round(wall * 1e3 - sum(T.values()), 1)
-    print(json.dumps({"frames": B, "wall_ms": round(wall * 1e3, 1), "frames_per_s": round(B / wall, 1), "ms": T}))
+    print(json.dumps({"frames": B, "path": "fused" if FUSED else "two-step", "wall_ms": round(wall * 1e3, 1),
+                      "frames_per_s": round(B / wall, 1), "ms": T}))
