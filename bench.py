@@ -73,6 +73,12 @@ def parse():
     return ap.parse_args()
 
 
+def lnfold_active(model, cfg):
+    """The bf16 vision tower runs LayerNorm folded into in_proj / c_fc when its width is a
+    multiple of 256 (api.cpp mi_clip_encode_image: `fold`; the product library has no switch)."""
+    return getattr(model, "weights", "bf16") == "bf16" and cfg.vision_width % 256 == 0
+
+
 def kernel_timing(model, cfg, chunk, reps=20):
     """Average duration of each encoder kernel at the bench's chunk shape, timed
     with HIP events on the stream the kernels are launched on."""
@@ -140,6 +146,29 @@ def kernel_timing(model, cfg, chunk, reps=20):
             timed(name, lambda Nn=Nn, K=K, epi=epi, out=out, Aq=Aq, As=As, Wq=Wq, Ws=Ws: N.check(
                 L.mi_op_gemm_mx(Aq.data_ptr(), As.data_ptr(), Wq.data_ptr(), Ws.data_ptr(), bias.data_ptr(),
                                 out.data_ptr(), M, Nn, K, epi, sp), "gemm_mx"), flops=2.0 * M * Nn * K)
+    elif lnfold_active(model, cfg):
+        # the product bf16 tower (W % 256 == 0): in_proj / c_fc are the LayerNorm-folded GEMMs
+        # (gemm_8q_kernel<EPI_LN_*>, fp16 operands of the half-slot residual stream, lda = 2W),
+        # each residual add is residual_stats (api.cpp run_tower_fold)
+        x16 = (torch.rand(M, 2 * W, device=dev, generator=g) * 2 - 1).half()
+        Wh = (torch.randn(4 * W, W, device=dev, generator=g) * 0.02).half()
+        colsum = Wh.float().sum(1)
+        rs = torch.rand(M + 256, 2, device=dev, generator=g) + 0.5
+        for name, Nn, K, epi, out in gemms:
+            if name in ("gemm_qkv", "gemm_fc"):
+                timed(name, lambda Nn=Nn, epi=epi, out=out: N.check(
+                    L.mi_op_gemm_ln(x16.data_ptr(), 2 * W, rs.data_ptr(), Wh.data_ptr(), colsum.data_ptr(),
+                                    bias.data_ptr(), out.data_ptr(), M, Nn, W, epi, sp), "gemm_ln"),
+                      flops=2.0 * M * Nn * W)
+            else:
+                timed(name, lambda Nn=Nn, K=K, epi=epi, out=out: N.check(
+                    L.mi_op_gemm(A.data_ptr(), Wt.data_ptr(), bias.data_ptr(), out.data_ptr(), M, Nn, K, epi, sp),
+                    "gemm"), flops=2.0 * M * Nn * K)
+        dl = torch.randn(M, W, device=dev, generator=g).bfloat16()
+        timed("residual_stats", lambda: N.check(L.mi_op_residual_stats(x16.data_ptr(), dl.data_ptr(), rs.data_ptr(),
+                                                                        M, W, sp), "residual_stats"),
+              nbytes=M * W * 6 + M * 8)
+        del x16, Wh, colsum, rs, dl
     else:
         for name, Nn, K, epi, out in gemms:
             timed(name, lambda Nn=Nn, K=K, epi=epi, out=out: N.check(
@@ -157,13 +186,14 @@ def kernel_timing(model, cfg, chunk, reps=20):
     return res
 
 
-def pmc_traffic(shape, fp8=False):
+def pmc_traffic(shape, fp8=False, epilogue=None):
     """HBM bytes per launch of the GEMM at `shape` [M, N, K] from the newest
     committed PMC summary (profiles/*_gemm_traffic.json, made by
     scripts/gpu_traffic.sh + scripts/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE,
     the gfx950 corrections of MI355X_MICROARCH.md "HBM"; MX-fp8:
     profiles/*_fp8_gemm_traffic.json from scripts/gpu_fp8_traffic.sh), with the
-    MFMA-busy fraction of the same summary's GRBM/SQ pass.  None if absent."""
+    MFMA-busy fraction of the same summary's GRBM/SQ pass.  `epilogue` (gemm_micro's
+    code, 7 = the LayerNorm-folded c_fc) selects the kernel measured.  None if absent."""
     import glob
     pat = "*_fp8_gemm_traffic.json" if fp8 else "*_gemm_traffic.json"
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", pat)), reverse=True):
@@ -172,7 +202,7 @@ def pmc_traffic(shape, fp8=False):
         try:
             d = json.load(open(f))
             for v in ([d] if fp8 else d.values()):
-                if list(v["shape"]) == list(shape):
+                if list(v["shape"]) == list(shape) and (epilogue is None or v.get("epilogue") == epilogue):
                     return v["traffic_bytes"], os.path.relpath(f, ROOT), v.get("mfma_busy")
         except (OSError, ValueError, KeyError, AttributeError):
             continue
@@ -635,19 +665,23 @@ def main():
             shape = [M, 4 * cfg.vision_width, cfg.vision_width]
             fp8 = args.weights == "fp8"
             f32 = args.weights == "fp32"
-            traffic, tsrc, busy = (None, None, None) if f32 else pmc_traffic(shape, fp8)
+            lnf = lnfold_active(model, cfg)
+            traffic, tsrc, busy = (None, None, None) if f32 else pmc_traffic(shape, fp8, 7 if lnf else None)
             peak = FP8_PEAK_TFLOPS if fp8 else (F32_MFMA_PEAK_TFLOPS if f32 else BF16_PEAK_TFLOPS)
             eb = 1 if fp8 else (4 if f32 else 2)   # operand element bytes (fp8 adds 1/64 B of scales per element)
             roof = {"bound": "mfma",
                     "kernel": ("gemm_mx_kernel<EPI_GELU_BF16> (mlp.c_fc + QuickGELU, MX-fp8 operands)" if fp8
                                else "gemm_f32 (precise.hip; mlp.c_fc + QuickGELU, exact-f32 MFMA)" if f32
+                               else "gemm_8q_kernel<EPI_LN_GELU_BF16> (8-phase interleaved persistent, 256x256x64, descriptor DMAs; "
+                               "ln_2 folded into the epilogue, fp16 operands on the f16 MFMA; mlp.c_fc + QuickGELU)" if lnf
                                else "gemm_8q_kernel<EPI_GELU_BF16> (8-phase interleaved persistent, 256x256x64, descriptor DMAs; mlp.c_fc + QuickGELU)"),
                     "achieved": round(ach, 1), "peak": peak, "unit": "TFLOP/s",
                     "frac": round(ach / peak, 4), "traffic": traffic,
                     "traffic_source": tsrc,
                     "mfma_busy_pmc": busy,
                     "algorithmic_bytes": int(eb * (1 + fp8 / 64) * (M * cfg.vision_width + 4 * cfg.vision_width ** 2)
-                                             + (4 if f32 else 2) * M * 4 * cfg.vision_width),
+                                             + (4 if f32 else 2) * M * 4 * cfg.vision_width
+                                             + (8 * M + 8 * 4 * cfg.vision_width if lnf else 0)),
                     "flops_per_launch": fl, "launch_shape": [M, 4 * cfg.vision_width, cfg.vision_width],
                     "avg_launch_us": dom["us"]}
         parity = None

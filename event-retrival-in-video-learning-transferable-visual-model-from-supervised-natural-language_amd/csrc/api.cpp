@@ -1057,6 +1057,29 @@ int mi_op_residual_ln(void* x, const void* delta, const float* g, const float* b
   return MI_OK;
 }
 
+int mi_op_residual_stats(void* x, const void* delta, float* rs, int32_t rows, int32_t W, void* stream) {
+  if (!x || !delta || !rs || rows < 0) return fail(MI_ERR_ARG, "mi_op_residual_stats: bad arguments");
+  if (W % 4 || W > 1024) return fail(MI_ERR_UNSUPPORTED, "mi_op_residual_stats: W must be a multiple of 4, <= 1024");
+  HIP_TRY(residual_stats((float*)x, (const uint16_t*)delta, rs, rows, W, (hipStream_t)stream));
+  return MI_OK;
+}
+
+int mi_op_gemm_ln(const void* x16, int64_t lda, const float* rs, const void* wf, const float* colsum,
+                  const float* colc, void* out, int32_t M, int32_t N, int32_t K, int32_t gelu, void* stream) {
+  if (!x16 || !rs || !wf || !colsum || !colc || !out || M < 0 || (gelu & ~1))
+    return fail(MI_ERR_ARG, "mi_op_gemm_ln: bad arguments");
+  if (M == 0) return MI_OK;
+  GemmArgs g = gargs((const uint16_t*)x16, lda, (const uint16_t*)wf, K, colc, out, N, M, N, K);
+  g.a_f16 = 1;
+  g.rs = rs;
+  g.colv = colsum;
+  if (lda < K || lda % 8 || !gemm_8q_ok(g))
+    return fail(MI_ERR_UNSUPPORTED, "mi_op_gemm_ln: needs N %% 256 == 0, K %% 128 == 0, K >= 256, M >= 256, "
+                                    "lda >= K with lda %% 8 == 0");
+  HIP_TRY(gemm_bf16(g, gelu ? EPI_LN_GELU_BF16 : EPI_LN_BF16, (hipStream_t)stream));
+  return MI_OK;
+}
+
 int mi_op_attention(const void* qkv, void* out, int32_t B, int32_t S, int32_t W, int32_t causal, void* stream) {
   if (!qkv || !out || B < 0 || S < 1) return fail(MI_ERR_ARG, "mi_op_attention: bad arguments");
   if (W % 64 || S > 640 || (causal & ~0x301)) return fail(MI_ERR_UNSUPPORTED, "mi_op_attention: W %% 64 == 0 and S <= 640");

@@ -307,6 +307,21 @@ int mi_op_attention(const void* qkv, void* out, int32_t B, int32_t S, int32_t W,
  *   (the vision tower's residual stream after its first add). */
 int mi_op_residual_ln(void* x, const void* delta, const float* gamma, const float* beta, void* out, int32_t rows,
                       int32_t W, int32_t xmode, void* stream);
+/* The LayerNorm-folded pair of the bf16 vision tower, the same
+ * ResidualAttentionBlock arithmetic with ln_1 / ln_2 moved into the GEMM epilogue:
+ * mi_op_residual_stats: x (fp16 half-slot layout, xmode 2 above) += delta (bf16 [rows,W]);
+ *   rs [rows][2] f32 = (rstd, rstd * mean) of each stored row (LayerNorm eps 1e-5).
+ * mi_op_gemm_ln: out bf16 [M,N] = LN(x) . W^T + b computed as
+ *   rstd * (x . Wf^T) - rstd * mean * colsum + colc, QuickGELU applied when gelu == 1
+ *   (attn.in_proj after ln_1: gelu 0; mlp.c_fc after ln_2: gelu 1).  x16: fp16 rows of
+ *   stride lda elements; rs: as above, READABLE for M + 256 rows (the kernel stages
+ *   whole 256-row tiles; the extra rows are never used); Wf [N,K] fp16 = W * gamma
+ *   (column-scaled nn.Linear weight); colsum [N] = sum_k Wf[n,k];
+ *   colc [N] = b_n + sum_k beta_k W[n,k].  N % 256 == 0, K % 128 == 0, K >= 256,
+ *   M >= 256, lda >= K, lda % 8 == 0. */
+int mi_op_residual_stats(void* x, const void* delta, float* rs, int32_t rows, int32_t W, void* stream);
+int mi_op_gemm_ln(const void* x16, int64_t lda, const float* rs, const void* Wf, const float* colsum,
+                  const float* colc, void* out, int32_t M, int32_t N, int32_t K, int32_t gelu, void* stream);
 
 /* MX-fp8 operator entry points (the "fp8 MFMA weights" configuration,
  * BASELINE.json configs[4]; OCP e4m3 elements with one e8m0 scale per 64

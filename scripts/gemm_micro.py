@@ -35,6 +35,13 @@ SHAPES = {
     "long": (16384, 4096, 4096, 0),
     "qkv20k": (20000, 2304, 768, 0),
     "fc20k": (20000, 3072, 768, 1),
+    # LayerNorm-folded product GEMMs of the bf16 vision tower (epi 6: in_proj after ln_1,
+    # 7: c_fc + QuickGELU after ln_2): fp16 operands in the residual stream's half-slot
+    # layout (lda = 2K), through mi_op_gemm_ln; variants do not apply
+    "lnqkv500": (500000, 2304, 768, 6),
+    "lnfc500": (500000, 3072, 768, 7),
+    "lnqkv250": (250000, 2304, 768, 6),
+    "lnfc250": (250000, 3072, 768, 7),
     # K sweep at the fc shape (per-tile fixed cost = intercept)
     "fcK384": (100000, 3072, 384, 0),
     "fcK768": (100000, 3072, 768, 0),
@@ -46,20 +53,31 @@ SHAPES = {
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
     only = sys.argv[2].split(",") if len(sys.argv) > 2 else list(SHAPES)
-    variants = [int(v) for v in sys.argv[3].split(",")] if len(sys.argv) > 3 else [0]
+    all_variants = [int(v) for v in sys.argv[3].split(",")] if len(sys.argv) > 3 else [0]
     L = N.lib()
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
     sp = torch.cuda.current_stream().cuda_stream
     for name in only:
         M, Nn, K, epi = SHAPES[name]
-        A = (torch.rand(M, K, device=dev, generator=g) * 2 - 1).bfloat16()
-        W = ((torch.rand(Nn, K, device=dev, generator=g) * 2 - 1) * K ** -0.5).bfloat16()
+        ln = epi in (6, 7)
+        dt = torch.float16 if ln else torch.bfloat16
+        # LN shapes: A is the fp16 half-slot stream [M, 2K] (row stride 2K, first half used)
+        A = (torch.rand(M, 2 * K if ln else K, device=dev, generator=g) * 2 - 1).to(dt)
+        W = ((torch.rand(Nn, K, device=dev, generator=g) * 2 - 1) * K ** -0.5).to(dt)
         bias = torch.rand(Nn, device=dev, generator=g)
-        outs = {v: torch.zeros(M, Nn, device=dev, dtype=torch.bfloat16 if epi in (0, 1) else torch.float32)
+        variants = [0] if ln else all_variants
+        if ln:
+            colsum = W.float().sum(1)
+            rs = torch.rand(M + 256, 2, device=dev, generator=g) + 0.5
+        outs = {v: torch.zeros(M, Nn, device=dev, dtype=torch.bfloat16 if epi in (0, 1, 6, 7) else torch.float32)
                 for v in variants}
 
         def run(v):
+            if ln:
+                N.check(L.mi_op_gemm_ln(A.data_ptr(), 2 * K, rs.data_ptr(), W.data_ptr(), colsum.data_ptr(),
+                                        bias.data_ptr(), outs[v].data_ptr(), M, Nn, K, epi - 6, sp), "gemm_ln")
+                return
             N.check(L.mi_op_gemm(A.data_ptr(), W.data_ptr(), bias.data_ptr(), outs[v].data_ptr(), M, Nn, K,
                                  epi | (v << 8), sp), "gemm")
         for v in variants:
@@ -82,6 +100,8 @@ def main():
             print(f"{name:7s} v{v} M={M} N={Nn} K={K} epi={epi}: {us:9.1f} us {2.0 * M * Nn * K / us / 1e6:7.1f} "
                   f"TFLOP/s  maxdiff vs v{variants[0]} {err:.3g}", flush=True)
         del A, W, outs, ref
+        if ln:
+            del rs, colsum
 
 
 if __name__ == "__main__":

@@ -74,6 +74,8 @@ def main():
         fb = 2 * 1024 * sum(f) / len(f)
         wb = 1024 * sum(w) / len(w)
         alg = 2 * (M * K + N * K + M * N)
+        if epi in (6, 7):                 # LayerNorm-folded: + rs (8 B per row) + colsum / colc (8 B per column)
+            alg += 8 * M + 8 * N
         res[name] = {"kernel": fetch[4 * i][0], "shape": [M, N, K], "epilogue": epi,
                      "fetch_bytes": round(fb), "write_bytes": round(wb), "traffic_bytes": round(fb + wb),
                      "algorithmic_bytes": alg, "traffic_over_algorithmic": round((fb + wb) / alg, 3),

@@ -154,6 +154,91 @@ def test_residual_ln(gpu, rows, W, xmode):
     assert err < 2e-2, err
 
 
+def _half_slots(x16):
+    """fp16 rows [rows, W] in the vision tower's half-slot layout: f32 slots [rows, W]
+    whose first halves hold the row (row stride 2W fp16 elements)."""
+    import torch
+    rows, W = x16.shape
+    slot = torch.zeros(rows, W, dtype=torch.float32)
+    slot.view(torch.float16).view(rows, 2 * W)[:, :W] = x16
+    return slot
+
+
+@pytest.mark.parametrize("rows,W", [(1, 128), (1000, 768), (50, 1024), (33, 512)])
+def test_residual_stats(gpu, rows, W):
+    """mi_op_residual_stats: the fp16 residual add is bit-exact (f32 x + bf16 delta rounded to
+    fp16), and rs holds (rstd, rstd * mean) of the STORED fp16 row (LayerNorm eps 1e-5)."""
+    import torch
+    N_ = _lib()
+    g = torch.Generator(device="cpu").manual_seed(rows * 5 + W)
+    x16 = (torch.randn(rows, W, generator=g) * 3 + 1).half()
+    delta = torch.randn(rows, W, generator=g).bfloat16()
+    xd, dd = _half_slots(x16).to(gpu), delta.to(gpu)
+    rs = torch.full((rows, 2), float("nan"), device=gpu)
+    N_.check(N_.lib().mi_op_residual_stats(xd.data_ptr(), dd.data_ptr(), rs.data_ptr(), rows, W, _stream()),
+             "residual_stats")
+    torch.cuda.synchronize()
+    s = (x16.float() + delta.float()).half()
+    assert torch.equal(xd.cpu().view(torch.float16).view(rows, 2 * W)[:, :W], s)
+    sd = s.double()
+    mean = sd.mean(1)
+    rstd = 1 / torch.sqrt(((sd - mean[:, None]) ** 2).mean(1) + 1e-5)
+    np.testing.assert_allclose(rs[:, 0].cpu().double(), rstd, rtol=2e-6)
+    np.testing.assert_allclose(rs[:, 1].cpu().double(), rstd * mean, rtol=2e-6, atol=2e-6)
+
+
+@pytest.mark.parametrize("M,N,K,gelu,half_slot", [(256, 256, 256, 0, True), (1000, 2304, 768, 0, True),
+                                                  (20000, 3072, 768, 1, True), (777, 4096, 1024, 1, True),
+                                                  (513, 768, 768, 0, False), (300, 3072, 768, 1, False)])
+def test_gemm_ln(gpu, M, N, K, gelu, half_slot):
+    """mi_op_gemm_ln (LayerNorm folded into the GEMM: the bf16 vision tower's in_proj after ln_1
+    and c_fc + QuickGELU after ln_2) against float64 LN(x) W^T + b with the UNFOLDED weights:
+    the fold itself (W' = fp16(W * gamma), colsum, colc) is part of what is checked.  Tolerance
+    as the bf16 GEMMs above (2e-2 of max(1, |ref|)); partial last M-tiles, the half-slot
+    operand stride 2K and plain rows."""
+    import torch
+    N_ = _lib()
+    g = torch.Generator(device="cpu").manual_seed(M + N + K + gelu)
+    x16 = (torch.randn(M, K, generator=g) * 2 + 0.5).half()
+    W = torch.randn(N, K, generator=g) * K ** -0.5
+    gamma = 1 + 0.2 * torch.randn(K, generator=g)
+    beta = 0.1 * torch.randn(K, generator=g)
+    bias = 0.1 * torch.randn(N, generator=g)
+    Wf = (W.double() * gamma.double()).half()
+    colsum = Wf.double().sum(1).float()
+    colc = (bias.double() + W.double() @ beta.double()).float()
+    xd = _half_slots(x16).to(gpu) if half_slot else x16.to(gpu)
+    lda = 2 * K if half_slot else K
+    xs = x16.double()
+    mean = xs.mean(1)
+    rstd = 1 / torch.sqrt(((xs - mean[:, None]) ** 2).mean(1) + 1e-5)
+    rs = torch.zeros(M + 256, 2)                  # readable for M + 256 rows (the header's contract)
+    rs[:M, 0], rs[:M, 1] = rstd.float(), (rstd * mean).float()
+    rs, Wd, sd, cd = rs.to(gpu), Wf.to(gpu), colsum.to(gpu), colc.to(gpu)
+    out = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=gpu)
+    N_.check(N_.lib().mi_op_gemm_ln(xd.data_ptr(), lda, rs.data_ptr(), Wd.data_ptr(), sd.data_ptr(), cd.data_ptr(),
+                                    out.data_ptr(), M, N, K, gelu, _stream()), "gemm_ln")
+    torch.cuda.synchronize()
+    ln = torch.nn.functional.layer_norm(xs, (K,), gamma.double(), beta.double(), 1e-5)
+    ref = ln @ W.double().t() + bias.double()
+    if gelu:
+        ref = ref * torch.sigmoid(1.702 * ref)
+    got = out.cpu().double()
+    assert torch.isfinite(got).all()
+    err = (got - ref).abs().max().item()
+    assert err < 2e-2 * max(1.0, ref.abs().max().item()), err
+
+
+def test_gemm_ln_rejects_unsupported_shapes(gpu):
+    import torch
+    N_ = _lib()
+    t = torch.zeros(4096, device=gpu)
+    p = t.data_ptr()
+    for M, N, K, lda in [(256, 200, 256, 256), (256, 256, 192, 192), (100, 256, 256, 256), (256, 256, 256, 128)]:
+        assert N_.lib().mi_op_gemm_ln(p, lda, p, p, p, p, p, M, N, K, 0, _stream()) == -3    # MI_ERR_UNSUPPORTED
+    assert N_.lib().mi_op_gemm_ln(p, 256, p, p, p, p, p, 256, 256, 256, 2, _stream()) == -1  # MI_ERR_ARG (gelu)
+
+
 @pytest.mark.parametrize("B,S,W,causal", [(1, 50, 768, 0), (7, 50, 768, 0), (3, 77, 512, 1), (2, 17, 128, 0),
                                           (2, 10, 256, 1), (1, 257, 1024, 0), (4, 197, 768, 0),
                                           # long-sequence (flash) kernel: L/14@336 = 577 tokens, ragged tails,
