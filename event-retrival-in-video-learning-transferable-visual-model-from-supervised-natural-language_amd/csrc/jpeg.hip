@@ -32,12 +32,15 @@
 namespace miclip {
 namespace {
 
-__constant__ uint8_t kZigzag[80] = {
-    0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,  12, 19, 26, 33, 40, 48,
-    41, 34, 27, 20, 13, 6,  7,  14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23,
-    30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63,
-    // extra entries so a corrupt run past 63 lands in position 63 (libjpeg's jpeg_natural_order + 16)
-    63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63};
+// The coefficient workspace holds each block in ZIGZAG order (coefficient k at slot min(k, 63):
+// a corrupt run past 63 lands in natural position 63 = zigzag slot 63, as libjpeg's
+// jpeg_natural_order + 16).  The entropy passes then write a block's coefficients in increasing
+// slot order, 16-byte windows at a time (jp_run), and the IDCT reads natural position n from
+// slot kIzz[n] (a compile-time register permutation).
+constexpr uint8_t kIzz[64] = {0,  1,  5,  6,  14, 15, 27, 28, 2,  4,  7,  13, 16, 26, 29, 42,
+                              3,  8,  12, 17, 25, 30, 41, 43, 9,  11, 18, 24, 31, 40, 44, 53,
+                              10, 19, 23, 32, 39, 45, 52, 54, 20, 22, 33, 38, 46, 51, 55, 60,
+                              21, 34, 37, 47, 50, 56, 59, 61, 35, 36, 48, 49, 57, 58, 62, 63};
 
 // One decode table (JpegHuff, host-built, libjpeg d_derived_tbl layout):
 //   look[512]: (length << 8) | symbol for codes of <= 9 bits (0: longer code)
@@ -286,14 +289,12 @@ __global__ __launch_bounds__(64) void jpeg_entropy_kernel(const uint8_t* __restr
                                                           int64_t data_bytes, const uint8_t* __restrict__ skip) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   JpegHuff* sh = (JpegHuff*)smem;
-  uint8_t* zz = (uint8_t*)smem + (LDS_T ? nsets * 4 * (int)sizeof(JpegHuff) : 0);
   if (LDS_T) {
     const uint32_t* src = (const uint32_t*)huff;
     uint32_t* dst = (uint32_t*)smem;
     const int nw = nsets * 4 * (int)sizeof(JpegHuff) / 4;
     for (int i = threadIdx.x; i < nw; i += 64) dst[i] = src[i];
   }
-  for (int i = threadIdx.x; i < 80; i += 64) zz[i] = kZigzag[i];
   __syncthreads();
   const int64_t lane = (int64_t)blockIdx.x * 64 + threadIdx.x;
   if (lane >= (int64_t)nframes * g.nseg) return;
@@ -341,7 +342,7 @@ __global__ __launch_bounds__(64) void jpeg_entropy_kernel(const uint8_t* __restr
       endblk = false;
     } else if (sz) {
       k += r;
-      blk[zz[k]] = (int16_t)val;
+      blk[k < 63 ? k : 63] = (int16_t)val;   // zigzag slot (see kIzz)
       ++k;
       endblk = k >= 64;
     } else if (r == 15) {
@@ -422,9 +423,8 @@ typedef BitReaderT<false> UReader;
 
 template <bool WRITE>
 __device__ __forceinline__ void jp_run(UReader& br, const JpegHuff* __restrict__ T, const JpegGeom& g,
-                                       const JpegMcu& mc, const uint8_t* __restrict__ zz, int& b, int& k,
-                                       uint32_t stop, int64_t blk, int64_t total, int& nblk, int (&dc)[3],
-                                       int16_t* __restrict__ out) {
+                                       const JpegMcu& mc, int& b, int& k, uint32_t stop, int64_t blk, int64_t total,
+                                       int& nblk, int (&dc)[3], int16_t* __restrict__ out, bool st = true) {
   // the block's MCU coordinates, advanced per block (block_addr's 64-bit divisions once per
   // call, not at every block end: in the wave's lockstep some lane ends a block nearly every trip)
   int mx = 0, my = 0;
@@ -440,6 +440,47 @@ __device__ __forceinline__ void jp_run(UReader& br, const JpegHuff* __restrict__
     return cb_c + (int64_t)(my * vs_c + mc.dv[bb]) * bw_c + mx * hs_c + mc.dh[bb];
   };
   int16_t* bp = WRITE ? out + addr(b) * 64 : nullptr;
+  // WRITE: coefficients gather in a 16-byte window of 8 zigzag slots (w[4], slot-pair per dword)
+  // that goes out as ONE 16-byte store when the block leaves it -- ~3-4 stores per block instead
+  // of a 2-byte store per coefficient.  The workspace is zeroed, so skipped windows need no store.
+  // A chunk boundary inside a block splits one window between two lanes: the chunk's first
+  // window from slot lo0 (its entry k) and its last from slot ... up to the exit k are written
+  // slot by slot, so neither lane's zeros overwrite the other's coefficients.
+  uint32_t w[4] = {0u, 0u, 0u, 0u};
+  int wk = -1;                                  // window in w (slot >> 3), -1: none
+  int lo0 = WRITE && (k & 7) ? k : -1;          // entry slot inside a window (first block only)
+  auto flush_range = [&](int lo, int hi) {      // slots [lo, hi) of window wk
+    const int s0 = wk * 8;
+    if (lo <= s0 && hi >= s0 + 8) {
+      if (st) {
+        typedef uint32_t u32x4w __attribute__((ext_vector_type(4)));
+        typedef __attribute__((address_space(1))) u32x4w gu4;
+        *(gu4*)(bp + s0) = (u32x4w){w[0], w[1], w[2], w[3]};
+      }
+      return;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (st && s0 + j >= lo && s0 + j < hi) bp[s0 + j] = (int16_t)(w[j >> 1] >> ((j & 1) * 16));
+  };
+  auto flush = [&]() {
+    if (wk < 0) return;
+    flush_range(lo0 >= 0 && wk == (lo0 >> 3) ? lo0 : 0, 64);
+    w[0] = w[1] = w[2] = w[3] = 0u;
+    wk = -1;
+  };
+  auto put = [&](int slot, int v) {
+    const int wi = slot >> 3;
+    if (wi != wk) {
+      flush();
+      wk = wi;
+    }
+    const int d = (slot >> 1) & 3;
+    const uint32_t sh = (uint32_t)(slot & 1) * 16u;
+    const uint32_t m = 0xFFFFu << sh, x = ((uint32_t)v & 0xFFFFu) << sh;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = d == i ? (w[i] & ~m) | x : w[i];   // replace: a corrupt run rewrites 63
+  };
   while (br.pos < stop && (!WRITE || blk < total)) {
     const int c = mc.comp[b];
     const JpegHuff* tp = k ? T + pick3(c, g.acsel[0], g.acsel[1], g.acsel[2]) * 2 + 1
@@ -458,12 +499,12 @@ __device__ __forceinline__ void jp_run(UReader& br, const JpegHuff* __restrict__
       dc[0] = c == 0 ? pv : dc[0];
       dc[1] = c == 1 ? pv : dc[1];
       dc[2] = c == 2 ? pv : dc[2];
-      if (WRITE) bp[0] = (int16_t)pv;
+      if (WRITE) put(0, pv);
       k = 1;
       endblk = false;
     } else if (sz) {
       k += r;
-      if (WRITE) bp[zz[k]] = (int16_t)val;
+      if (WRITE) put(k < 63 ? k : 63, val);
       ++k;
       endblk = k >= 64;
     } else if (r == 15) {
@@ -478,6 +519,8 @@ __device__ __forceinline__ void jp_run(UReader& br, const JpegHuff* __restrict__
       ++nblk;
       ++blk;
       if (WRITE) {
+        flush();
+        lo0 = -1;
         if (b == 0) {
           mx = mx + 1 == g.mcux ? 0 : mx + 1;
           my += mx == 0 ? 1 : 0;
@@ -485,6 +528,10 @@ __device__ __forceinline__ void jp_run(UReader& br, const JpegHuff* __restrict__
         if (blk < total) bp = out + addr(b) * 64;
       }
     }
+  }
+  if (WRITE && wk >= 0) {   // stopped inside a block: the next chunk owns slots from k on
+    const int hi = (k & 7) && wk == (k >> 3) ? k : 64;
+    flush_range(lo0 >= 0 && wk == (lo0 >> 3) ? lo0 : 0, hi);
   }
 }
 
@@ -781,7 +828,7 @@ __global__ __launch_bounds__(256) void jp_sync_kernel(const uint8_t* __restrict_
   int nblk = 0;
   int dc[3] = {0, 0, 0};
   __builtin_amdgcn_s_waitcnt(0);   // nothing in flight entering the loop (see jpeg_entropy_kernel)
-  jp_run<false>(br, T, g, mc, nullptr, b, k, stop, 0, 0, nblk, dc, nullptr);
+  jp_run<false>(br, T, g, mc, b, k, stop, 0, 0, nblk, dc, nullptr);
   const uint64_t x = pack_state(br.pos, b, k);
   dst.x[ci] = x;
   dst.nb[ci] = nblk;
@@ -819,17 +866,15 @@ __global__ __launch_bounds__(256) void jp_final_kernel(const uint8_t* __restrict
                                                        JpegMcu mc, JpState st, const int64_t* __restrict__ bfirst,
                                                        const int32_t* __restrict__ pred,
                                                        const int32_t* __restrict__ frame_changed,
-                                                       int16_t* __restrict__ coef) {
+                                                       int16_t* __restrict__ coef, int abl) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   JpegHuff* sh = (JpegHuff*)smem;
-  uint8_t* zz = (uint8_t*)smem + (LDS_T ? nsets * 4 * (int)sizeof(JpegHuff) : 0);
   if (LDS_T) {
     const uint32_t* s = (const uint32_t*)huff;
     uint32_t* d = (uint32_t*)smem;
     const int nw = nsets * 4 * (int)sizeof(JpegHuff) / 4;
     for (int i = threadIdx.x; i < nw; i += 256) d[i] = s[i];
   }
-  for (int i = threadIdx.x; i < 80; i += 256) zz[i] = kZigzag[i];
   __syncthreads();
   const int64_t ci = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (ci >= nchunks_max) return;
@@ -863,7 +908,8 @@ __global__ __launch_bounds__(256) void jp_final_kernel(const uint8_t* __restrict
   br.init_at(ustuff + ch.ubase[f], L, start);
   int nblk = 0;
   __builtin_amdgcn_s_waitcnt(0);
-  jp_run<true>(br, T, g, mc, zz, b, k, stop, blk, total, nblk, dc, coef + (int64_t)f * g.blocks_per_frame * 64);
+  jp_run<true>(br, T, g, mc, b, k, stop, blk, total, nblk, dc, coef + (int64_t)f * g.blocks_per_frame * 64,
+               !(abl & 1));
 }
 
 // ---- IDCT (jidctint.c jpeg_idct_islow) -----------------------------------
@@ -949,17 +995,19 @@ __global__ __launch_bounds__(256) void jpeg_idct_kernel(const int16_t* __restric
   const uint16_t* q = qtab + ((int64_t)f * 4 + pl.qsel[c]) * 64;
   int32_t ws[64];
   const uint4* cb4 = (const uint4*)(coef + t * 64);
-  int32_t in[64];
+  int32_t zv[64], in[64];   // zv: the block's zigzag slots; in: natural order, dequantised
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const uint4 v = cb4[j];
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      in[8 * j + 2 * e] = (int32_t)(int16_t)(w[e] & 0xFFFF) * (int32_t)q[8 * j + 2 * e];
-      in[8 * j + 2 * e + 1] = (int32_t)(int16_t)(w[e] >> 16) * (int32_t)q[8 * j + 2 * e + 1];
+      zv[8 * j + 2 * e] = (int32_t)(int16_t)(w[e] & 0xFFFF);
+      zv[8 * j + 2 * e + 1] = (int32_t)(int16_t)(w[e] >> 16);
     }
   }
+#pragma unroll
+  for (int n = 0; n < 64; ++n) in[n] = zv[kIzz[n]] * (int32_t)q[n];
   // pass 1: columns -> ws (DC-only columns: libjpeg's shortcut gives the same values)
 #pragma unroll
   for (int col = 0; col < 8; ++col) {
@@ -1282,6 +1330,16 @@ static JpWs jp_layout(int nframes, int64_t data_bytes) {
   return w;
 }
 
+// A/B timing probes (MICLIP_JPEG_ABL): bit 0 = the final pass decodes without storing coefficients
+static int jp_abl() {
+#if MICLIP_AB
+  const char* e = getenv("MICLIP_JPEG_ABL");
+  return e ? atoi(e) : 0;
+#else
+  return 0;
+#endif
+}
+
 static bool jp_serial_forced() {
 #if MICLIP_AB
   const char* e = getenv("MICLIP_JPEG_SERIAL");   // A/B: the lane-per-frame entropy kernel for every scan
@@ -1443,25 +1501,25 @@ hipError_t jpeg_decode(const uint8_t* data, int64_t data_bytes, const int64_t* s
     hipLaunchKernelGGL(jp_prefix_kernel, fg, dim3(256), 0, s, ch, nframes, fin, bfirst, pred);
     const int32_t* last_changed = fch + (int64_t)JP_ROUNDS * nframes;
     if (lds_t)
-      hipLaunchKernelGGL(jp_final_kernel<true>, cg, dim3(256), tl + 80, s, ustuff, ch, nmax, (const JpegHuff*)huff,
-                         huff_idx, nsets, g, mc, fin, bfirst, pred, last_changed, coef);
+      hipLaunchKernelGGL(jp_final_kernel<true>, cg, dim3(256), tl, s, ustuff, ch, nmax, (const JpegHuff*)huff,
+                         huff_idx, nsets, g, mc, fin, bfirst, pred, last_changed, coef, jp_abl());
     else
-      hipLaunchKernelGGL(jp_final_kernel<false>, cg, dim3(256), 80, s, ustuff, ch, nmax, (const JpegHuff*)huff,
-                         huff_idx, nsets, g, mc, fin, bfirst, pred, last_changed, coef);
+      hipLaunchKernelGGL(jp_final_kernel<false>, cg, dim3(256), 0, s, ustuff, ch, nmax, (const JpegHuff*)huff,
+                         huff_idx, nsets, g, mc, fin, bfirst, pred, last_changed, coef, jp_abl());
     if ((e = hipGetLastError()) != hipSuccess) return e;
     // frames outside the chunk layout (repeated / out-of-order segments): the serial decode
-    hipLaunchKernelGGL(jpeg_entropy_kernel<false>, fg4, dim3(64), 80, s, data, seg_off, seg_end, (const JpegHuff*)huff,
+    hipLaunchKernelGGL(jpeg_entropy_kernel<false>, fg4, dim3(64), 0, s, data, seg_off, seg_end, (const JpegHuff*)huff,
                        huff_idx, nsets, g, nframes, coef, data_bytes, (const uint8_t*)vf);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   } else {
     const int64_t lanes = (int64_t)nframes * g.nseg;
     const dim3 eg((unsigned)((lanes + 63) / 64));
     if (lds_t)
-      hipLaunchKernelGGL(jpeg_entropy_kernel<true>, eg, dim3(64), nsets * 4 * sizeof(JpegHuff) + 80, s, data, seg_off,
+      hipLaunchKernelGGL(jpeg_entropy_kernel<true>, eg, dim3(64), nsets * 4 * sizeof(JpegHuff), s, data, seg_off,
                          seg_end, (const JpegHuff*)huff, huff_idx, nsets, g, nframes, coef, data_bytes,
                          (const uint8_t*)nullptr);
     else
-      hipLaunchKernelGGL(jpeg_entropy_kernel<false>, eg, dim3(64), 80, s, data, seg_off, seg_end,
+      hipLaunchKernelGGL(jpeg_entropy_kernel<false>, eg, dim3(64), 0, s, data, seg_off, seg_end,
                          (const JpegHuff*)huff, huff_idx, nsets, g, nframes, coef, data_bytes, (const uint8_t*)nullptr);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
