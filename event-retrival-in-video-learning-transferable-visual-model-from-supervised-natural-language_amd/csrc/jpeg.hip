@@ -415,16 +415,47 @@ struct JpegMcu {
 };
 
 
+// Checkpoints of a chunk's recorded decode path (the sync rounds).  A decode that restarts
+// from a corrected entry state usually joins the recorded path after a few hundred bits
+// (scripts/jpeg_sync_proto.py: median 838 bits on the reference frames); from a shared state
+// (bit position, block within the MCU, coefficient index) on, the two decodes are identical, so
+// the re-decode stops at the first checkpoint where its state equals the recorded one and takes
+// the rest -- exit state, blocks, DC sums -- from the record.  Checkpoint j is the path's first
+// symbol boundary at or past first + JP_CP_FIRST + j * JP_CP_STEP bits; its counts are relative
+// to the start of the path that recorded it, as are the path totals tn / td.
+constexpr int JP_NCP = 8;
+constexpr uint32_t JP_CP_FIRST = 512, JP_CP_STEP = 1024;
+struct JpCps {
+  uint64_t* x;   // [nmax * JP_NCP] packed state, ~0: none
+  int32_t* nb;   // [nmax * JP_NCP] blocks completed from the path's start
+  int32_t* dc;   // [nmax * JP_NCP * 3] DC-difference sums from the path's start
+  int32_t* tn;   // [nmax] the path's blocks, start -> exit
+  int32_t* td;   // [nmax * 3]
+};
+struct JpCpRun {
+  uint32_t first, thr;   // the chunk's first bit; the next checkpoint's position
+  int j;                 // the next checkpoint
+  int hit;               // -1, or the recorded checkpoint this decode joined
+  bool cmp;              // compare with the recorded path (a re-decode) or only record (round 0)
+  int64_t slot;          // ci * JP_NCP
+  JpCps cp;
+};
+
+__device__ __forceinline__ uint64_t pack_state(uint32_t pos, int b, int k) {
+  return ((uint64_t)pos << 16) | ((uint64_t)b << 8) | (uint64_t)k;
+}
+
 // Decode from the reader's position in state (b, k) until the position reaches
 // `stop` (at a symbol boundary) or, when writing, the frame's last block is
 // done.  nblk counts completed blocks; dc[] accumulates DC differences (WRITE:
 // the running predictors, stored as each block's coefficient 0).
 typedef BitReaderT<false> UReader;
 
-template <bool WRITE>
+template <bool WRITE, bool CP = false>
 __device__ __forceinline__ void jp_run(UReader& br, const JpegHuff* __restrict__ T, const JpegGeom& g,
                                        const JpegMcu& mc, int& b, int& k, uint32_t stop, int64_t blk, int64_t total,
-                                       int& nblk, int (&dc)[3], int16_t* __restrict__ out, bool st = true) {
+                                       int& nblk, int (&dc)[3], int16_t* __restrict__ out, bool st = true,
+                                       JpCpRun* cr = nullptr) {
   // the block's MCU coordinates, advanced per block (block_addr's 64-bit divisions once per
   // call, not at every block end: in the wave's lockstep some lane ends a block nearly every trip)
   int mx = 0, my = 0;
@@ -482,6 +513,21 @@ __device__ __forceinline__ void jp_run(UReader& br, const JpegHuff* __restrict__
     for (int i = 0; i < 4; ++i) w[i] = d == i ? (w[i] & ~m) | x : w[i];   // replace: a corrupt run rewrites 63
   };
   while (br.pos < stop && (!WRITE || blk < total)) {
+    if (CP && br.pos >= cr->thr) {   // checkpoint cr->j: join the recorded path, or record this one
+      const uint64_t xs = pack_state(br.pos, b, k);
+      const int64_t sl = cr->slot + cr->j;
+      if (cr->cmp && cr->cp.x[sl] == xs) {
+        cr->hit = cr->j;
+        break;
+      }
+      cr->cp.x[sl] = xs;
+      cr->cp.nb[sl] = nblk;
+      cr->cp.dc[3 * sl] = dc[0];
+      cr->cp.dc[3 * sl + 1] = dc[1];
+      cr->cp.dc[3 * sl + 2] = dc[2];
+      ++cr->j;
+      cr->thr = cr->j < JP_NCP ? cr->first + JP_CP_FIRST + JP_CP_STEP * (uint32_t)cr->j : 0xFFFFFFFFu;
+    }
     const int c = mc.comp[b];
     const JpegHuff* tp = k ? T + pick3(c, g.acsel[0], g.acsel[1], g.acsel[2]) * 2 + 1
                            : T + pick3(c, g.dcsel[0], g.dcsel[1], g.dcsel[2]) * 2;
@@ -767,10 +813,6 @@ struct JpState {        // per chunk, per buffer: exit state, blocks completed, 
   uint8_t* changed;
 };
 
-__device__ __forceinline__ uint64_t pack_state(uint32_t pos, int b, int k) {
-  return ((uint64_t)pos << 16) | ((uint64_t)b << 8) | (uint64_t)k;
-}
-
 // round 0: every chunk from its first bit in the guessed state (block 0, coefficient 0);
 // round r >= 1: chunks whose predecessor's exit changed in round r - 1 re-decode from it
 template <bool LDS_T>
@@ -778,7 +820,8 @@ __global__ __launch_bounds__(256) void jp_sync_kernel(const uint8_t* __restrict_
                                                       int64_t nchunks_max, const JpegHuff* __restrict__ huff,
                                                       const int32_t* __restrict__ huff_idx, int nsets, JpegGeom g,
                                                       JpegMcu mc, int round, JpState src, JpState dst,
-                                                      int32_t* __restrict__ frame_changed /* this round's [B] */) {
+                                                      int32_t* __restrict__ frame_changed /* this round's [B] */,
+                                                      JpCps cps) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   if (LDS_T) {
     const uint32_t* s = (const uint32_t*)huff;
@@ -827,9 +870,41 @@ __global__ __launch_bounds__(256) void jp_sync_kernel(const uint8_t* __restrict_
   br.init_at(ustuff + ch.ubase[f], L, start);
   int nblk = 0;
   int dc[3] = {0, 0, 0};
+  JpCpRun cr{first, first + JP_CP_FIRST, 0, -1, round > 0, ci * JP_NCP, cps};
   __builtin_amdgcn_s_waitcnt(0);   // nothing in flight entering the loop (see jpeg_entropy_kernel)
-  jp_run<false>(br, T, g, mc, b, k, stop, 0, 0, nblk, dc, nullptr);
-  const uint64_t x = pack_state(br.pos, b, k);
+  jp_run<false, true>(br, T, g, mc, b, k, stop, 0, 0, nblk, dc, nullptr, true, &cr);
+  uint64_t x;
+  if (cr.hit >= 0) {
+    // joined the recorded path at checkpoint hit: its exit, and its counts from there on.
+    // Re-base the recorded checkpoints from hit on (and the totals) to this decode's start;
+    // those before hit were just re-recorded by this decode.
+    const int64_t sh = cr.slot + cr.hit;
+    const int dn = nblk - cps.nb[sh];
+    const int d0 = dc[0] - cps.dc[3 * sh], d1 = dc[1] - cps.dc[3 * sh + 1], d2 = dc[2] - cps.dc[3 * sh + 2];
+    for (int jj = cr.hit; jj < JP_NCP; ++jj) {
+      const int64_t sl = cr.slot + jj;
+      cps.nb[sl] += dn;
+      cps.dc[3 * sl] += d0;
+      cps.dc[3 * sl + 1] += d1;
+      cps.dc[3 * sl + 2] += d2;
+    }
+    cps.tn[ci] += dn;
+    cps.td[3 * ci] += d0;
+    cps.td[3 * ci + 1] += d1;
+    cps.td[3 * ci + 2] += d2;
+    x = src.x[ci];
+    nblk = cps.tn[ci];
+    dc[0] = cps.td[3 * ci];
+    dc[1] = cps.td[3 * ci + 1];
+    dc[2] = cps.td[3 * ci + 2];
+  } else {   // decoded to the chunk's end: this path is the record now
+    for (int jj = cr.j; jj < JP_NCP; ++jj) cps.x[cr.slot + jj] = ~0ull;
+    cps.tn[ci] = nblk;
+    cps.td[3 * ci] = dc[0];
+    cps.td[3 * ci + 1] = dc[1];
+    cps.td[3 * ci + 2] = dc[2];
+    x = pack_state(br.pos, b, k);
+  }
   dst.x[ci] = x;
   dst.nb[ci] = nblk;
   dst.dc[3 * ci] = dc[0];
@@ -1296,7 +1371,7 @@ __global__ __launch_bounds__(XF_NT) void jpeg_transform_kernel(const uint8_t* __
 struct JpWs {
   size_t bytes;
   size_t o_ustuff, o_cbase, o_ubase, o_ulen, o_cframe, o_cnt, o_coff, o_mk, o_x[2], o_nb[2], o_dc[2], o_ch[2],
-      o_bfirst, o_pred, o_fch, o_sso, o_sse, o_vf;
+      o_bfirst, o_pred, o_fch, o_sso, o_sse, o_vf, o_cpx, o_cpn, o_cpd, o_tn, o_td;
   int64_t nmax;
 };
 
@@ -1326,6 +1401,11 @@ static JpWs jp_layout(int nframes, int64_t data_bytes) {
   w.o_sso = carve((size_t)B * 8);
   w.o_sse = carve((size_t)B * 8);
   w.o_vf = carve((size_t)B);
+  w.o_cpx = carve((size_t)w.nmax * JP_NCP * 8);
+  w.o_cpn = carve((size_t)w.nmax * JP_NCP * 4);
+  w.o_cpd = carve((size_t)w.nmax * JP_NCP * 12);
+  w.o_tn = carve((size_t)w.nmax * 4);
+  w.o_td = carve((size_t)w.nmax * 12);
   w.bytes = off;
   return w;
 }
@@ -1461,6 +1541,8 @@ hipError_t jpeg_decode(const uint8_t* data, int64_t data_bytes, const int64_t* s
     int64_t* sso = (int64_t*)(w + jw.o_sso);
     int64_t* sse = (int64_t*)(w + jw.o_sse);
     uint8_t* vf = (uint8_t*)(w + jw.o_vf);
+    const JpCps cps{(uint64_t*)(w + jw.o_cpx), (int32_t*)(w + jw.o_cpn), (int32_t*)(w + jw.o_cpd),
+                    (int32_t*)(w + jw.o_tn), (int32_t*)(w + jw.o_td)};
     const int64_t nmax = jw.nmax;
     if ((e = hipMemsetAsync(cframe, 0xFF, (size_t)nmax * 4, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(fch, 0, (size_t)(JP_ROUNDS + 1) * nframes * 4, s)) != hipSuccess) return e;
@@ -1491,10 +1573,10 @@ hipError_t jpeg_decode(const uint8_t* data, int64_t data_bytes, const int64_t* s
       const JpState& dst = st[r & 1];
       if (lds_t)
         hipLaunchKernelGGL(jp_sync_kernel<true>, cg, dim3(256), tl, s, ustuff, ch, nmax, (const JpegHuff*)huff,
-                           huff_idx, nsets, g, mc, r, src, dst, fch + (int64_t)r * nframes);
+                           huff_idx, nsets, g, mc, r, src, dst, fch + (int64_t)r * nframes, cps);
       else
         hipLaunchKernelGGL(jp_sync_kernel<false>, cg, dim3(256), 0, s, ustuff, ch, nmax, (const JpegHuff*)huff,
-                           huff_idx, nsets, g, mc, r, src, dst, fch + (int64_t)r * nframes);
+                           huff_idx, nsets, g, mc, r, src, dst, fch + (int64_t)r * nframes, cps);
       if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     const JpState& fin = st[JP_ROUNDS & 1];
