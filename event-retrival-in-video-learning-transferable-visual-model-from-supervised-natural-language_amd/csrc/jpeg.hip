@@ -1190,8 +1190,10 @@ __global__ __launch_bounds__(256) void jpeg_color_kernel(const uint8_t* __restri
 // preprocess.hip's resample_h / resample_v kernels, so the output is bit-identical to decode +
 // mi_preprocess_frames (and so to Pillow + torchvision).
 constexpr int XF_PREC = 22;   // Pillow PRECISION_BITS
-constexpr int XF_RPI = 4;     // source rows converted per step
-constexpr int XF_NT = 512;    // threads per workgroup (two workgroups per CU at ~70 KB of LDS each)
+constexpr int XF_RPI = 8;     // source rows converted per step
+constexpr int XF_NT = 512;    // threads per workgroup (two workgroups per CU: <= XF_LDS2 bytes of LDS each)
+constexpr int XF_IPT = 3;     // 4-pixel groups per thread whose loads go out together in a conversion step
+constexpr size_t XF_LDS2 = 78 * 1024;
 
 __device__ __forceinline__ uint32_t xf_clip8(int acc) {
   acc >>= XF_PREC;
@@ -1221,29 +1223,54 @@ __device__ __forceinline__ uint32_t load4u(const uint8_t* p) {
   return __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)(a & 3));
 }
 
-__device__ __forceinline__ void color4(const uint8_t* __restrict__ base, const JpegPlanes& pl, int cmode, int cdh,
-                                       int x0, int y, uint32_t* __restrict__ o) {
+// color4 in two halves, so that a thread's loads for several 4-pixel groups are all in
+// flight before the first group's arithmetic waits: the raw dwords (Y, then the chroma words
+// the fancy upsampling reads, by cmode), then the colour conversion from them
+struct Raw4 {
+  uint32_t y, b0, b1, r0, r1;   // cmode 0: b0 / r0; 1: b0 / r0 (c0 .. c0 + 3); 2: near b0 / r0, far b1 / r1
+};
+
+__device__ __forceinline__ Raw4 color4_load(const uint8_t* __restrict__ base, const JpegPlanes& pl, int cmode,
+                                            int cdh, int x0, int y) {
+  Raw4 w;
   // planes are 64-byte aligned with row strides of whole blocks: the Y dword is aligned
-  const uint32_t yw = *(const uint32_t*)(base + pl.pbase[0] + (int64_t)y * pl.pstride[0] + x0);
-  int cb[4], cr[4];
+  w.y = *(const uint32_t*)(base + pl.pbase[0] + (int64_t)y * pl.pstride[0] + x0);
+  w.b1 = w.r1 = 0u;
   if (cmode == 0) {
-    const uint32_t bw = *(const uint32_t*)(base + pl.pbase[1] + (int64_t)y * pl.pstride[1] + x0);
-    const uint32_t rw = *(const uint32_t*)(base + pl.pbase[2] + (int64_t)y * pl.pstride[2] + x0);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      cb[i] = (int)((bw >> (8 * i)) & 255u);
-      cr[i] = (int)((rw >> (8 * i)) & 255u);
-    }
+    w.b0 = *(const uint32_t*)(base + pl.pbase[1] + (int64_t)y * pl.pstride[1] + x0);
+    w.r0 = *(const uint32_t*)(base + pl.pbase[2] + (int64_t)y * pl.pstride[2] + x0);
   } else {
     const int c0 = (x0 >> 1) - 1;   // chroma columns c0 .. c0 + 3 serve the 4 pixels
+    const int r = cmode == 1 ? y : y >> 1;
+    w.b0 = load4u(base + pl.pbase[1] + (int64_t)r * pl.pstride[1] + c0);
+    w.r0 = load4u(base + pl.pbase[2] + (int64_t)r * pl.pstride[2] + c0);
+    if (cmode == 2) {
+      const int rf = (y & 1) ? min(r + 1, cdh - 1) : max(r - 1, 0);
+      w.b1 = load4u(base + pl.pbase[1] + (int64_t)rf * pl.pstride[1] + c0);
+      w.r1 = load4u(base + pl.pbase[2] + (int64_t)rf * pl.pstride[2] + c0);
+    }
+  }
+  return w;
+}
+
+// RGB of the 4 pixels x0 .. x0 + 3 of row y (x0 % 4 == 0, 1 <= x0, x0 + 4 < W: no chroma edge
+// column) from color4_load's words; the same fancy-upsampling / colour arithmetic as
+// chroma_at + color_px
+__device__ __forceinline__ void color4_math(const Raw4& w, int cmode, uint32_t* __restrict__ o) {
+  int cb[4], cr[4];
+  if (cmode == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      cb[i] = (int)((w.b0 >> (8 * i)) & 255u);
+      cr[i] = (int)((w.r0 >> (8 * i)) & 255u);
+    }
+  } else {
     int tb[4], tr[4];
     if (cmode == 1) {
-      const uint32_t bw = load4u(base + pl.pbase[1] + (int64_t)y * pl.pstride[1] + c0);
-      const uint32_t rw = load4u(base + pl.pbase[2] + (int64_t)y * pl.pstride[2] + c0);
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        tb[k] = (int)((bw >> (8 * k)) & 255u);
-        tr[k] = (int)((rw >> (8 * k)) & 255u);
+        tb[k] = (int)((w.b0 >> (8 * k)) & 255u);
+        tr[k] = (int)((w.r0 >> (8 * k)) & 255u);
       }
       // h2v1_fancy_upsample: even pixel (v * 3 + left + 1) >> 2, odd (v * 3 + right + 2) >> 2
       cb[0] = (tb[1] * 3 + tb[0] + 1) >> 2;
@@ -1255,16 +1282,10 @@ __device__ __forceinline__ void color4(const uint8_t* __restrict__ base, const J
       cr[2] = (tr[2] * 3 + tr[1] + 1) >> 2;
       cr[3] = (tr[2] * 3 + tr[3] + 2) >> 2;
     } else {
-      const int r = y >> 1;
-      const int rf = (y & 1) ? min(r + 1, cdh - 1) : max(r - 1, 0);
-      const uint32_t bn = load4u(base + pl.pbase[1] + (int64_t)r * pl.pstride[1] + c0);
-      const uint32_t bf = load4u(base + pl.pbase[1] + (int64_t)rf * pl.pstride[1] + c0);
-      const uint32_t rn = load4u(base + pl.pbase[2] + (int64_t)r * pl.pstride[2] + c0);
-      const uint32_t rfw = load4u(base + pl.pbase[2] + (int64_t)rf * pl.pstride[2] + c0);
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        tb[k] = (int)((bn >> (8 * k)) & 255u) * 3 + (int)((bf >> (8 * k)) & 255u);
-        tr[k] = (int)((rn >> (8 * k)) & 255u) * 3 + (int)((rfw >> (8 * k)) & 255u);
+        tb[k] = (int)((w.b0 >> (8 * k)) & 255u) * 3 + (int)((w.b1 >> (8 * k)) & 255u);
+        tr[k] = (int)((w.r0 >> (8 * k)) & 255u) * 3 + (int)((w.r1 >> (8 * k)) & 255u);
       }
       // h2v2_fancy_upsample: even pixel (th * 3 + left + 8) >> 4, odd (th * 3 + right + 7) >> 4
       cb[0] = (tb[1] * 3 + tb[0] + 8) >> 4;
@@ -1279,7 +1300,7 @@ __device__ __forceinline__ void color4(const uint8_t* __restrict__ base, const J
   }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int Y = (int)((yw >> (8 * i)) & 255u);
+    const int Y = (int)((w.y >> (8 * i)) & 255u);
     const int b_ = cb[i] - 128, r_ = cr[i] - 128;
     const int r = Y + ((91881 * r_ + 32768) >> 16);
     const int gch = Y + ((-22554 * b_ + 32768 - 46802 * r_) >> 16);
@@ -1303,33 +1324,59 @@ __global__ __launch_bounds__(XF_NT) void jpeg_transform_kernel(const uint8_t* __
   extern __shared__ __attribute__((aligned(16))) char xsm[];
   const int f = (int)(blockIdx.x / xk.nbands), band = (int)(blockIdx.x % xk.nbands);
   const int n = xk.n, xw = xk.xw;   // xw: the crop's source span rounded out to whole 4-pixel groups
-  const int y0 = band * xk.band, y1 = min(n, y0 + xk.band);
+  const int y0 = band * xk.band, y1 = min(n, y0 + xk.band), ny = y1 - y0;
   const int ra = xk.bv[2 * y0];
   int rb = ra;
   for (int y = y0; y < y1; ++y) rb = max(rb, xk.bv[2 * y] + xk.bv[2 * y + 1]);
-  uint32_t* crow = (uint32_t*)xsm;          // [XF_RPI][xw] packed RGB of the source rows
-  uint32_t* hrow = crow + XF_RPI * xw;      // [rb - ra][n] the horizontal pass's rows
+  // LDS: the filter tables (the band's rows of the vertical one), then the converted source
+  // rows of one step, then the band's horizontally resampled rows
+  int32_t* skh = (int32_t*)xsm;                      // [n][ksh]
+  int32_t* sbh = skh + n * xk.ksh;                   // [n] xmin - xlo | xsize << 16
+  int32_t* skv = sbh + n;                            // [band][ksv]
+  int32_t* sbv = skv + xk.band * xk.ksv;             // [band] ymin - ra | ysize << 16
+  uint32_t* crow = (uint32_t*)(sbv + xk.band);       // [XF_RPI][xw] packed RGB of the source rows
+  uint32_t* hrow = crow + XF_RPI * xw;               // [rb - ra][n] the horizontal pass's rows
+  for (int i = threadIdx.x; i < n * xk.ksh; i += XF_NT) skh[i] = xk.kh[i];
+  for (int i = threadIdx.x; i < n; i += XF_NT) sbh[i] = (xk.bh[2 * i] - xk.xlo) | (xk.bh[2 * i + 1] << 16);
+  for (int i = threadIdx.x; i < ny * xk.ksv; i += XF_NT) skv[i] = xk.kv[(int64_t)y0 * xk.ksv + i];
+  for (int i = threadIdx.x; i < ny; i += XF_NT) sbv[i] = (xk.bv[2 * (y0 + i)] - ra) | (xk.bv[2 * (y0 + i) + 1] << 16);
   const uint8_t* base = planes + (int64_t)f * pl.plane_frame_bytes;
+  const int xq = xw >> 2;
   for (int r0 = ra; r0 < rb; r0 += XF_RPI) {
-    const int nr = min(XF_RPI, rb - r0);
-    const int xq = xw >> 2;
-    for (int i = threadIdx.x; i < nr * xq; i += XF_NT) {   // 4 pixels per thread
-      const int rr = i / xq, x0 = xk.xlo + 4 * (i - rr * xq), y = r0 + rr;
-      uint32_t* o = crow + rr * xw + (x0 - xk.xlo);
-      if (ncomp == 3 && x0 >= 4 && x0 + 8 <= xk.W) {
-        uint32_t c4[4];
-        color4(base, pl, cmode, cdh, x0, y, c4);
-        *(uint4*)o = make_uint4(c4[0], c4[1], c4[2], c4[3]);
-      } else {
+    const int nr = min(XF_RPI, rb - r0), items = nr * xq;
+    // colour conversion, 4 pixels per item; each thread's XF_IPT items load before any converts
+    for (int i0 = 0; i0 < items; i0 += XF_NT * XF_IPT) {
+      Raw4 raw[XF_IPT];
+      int ix[XF_IPT];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] = x0 + j < xk.W ? color_xy(base, pl, ncomp, cmode, cdw, cdh, x0 + j, y) : 0u;
+      for (int m = 0; m < XF_IPT; ++m) {
+        const int i = i0 + threadIdx.x + m * XF_NT;
+        const int rr = i / xq, x0 = xk.xlo + 4 * (i - rr * xq);
+        ix[m] = i < items ? (ncomp == 3 && x0 >= 4 && x0 + 8 <= xk.W ? 1 : 2) : 0;   // 1 fast, 2 edge
+        if (ix[m] == 1) raw[m] = color4_load(base, pl, cmode, cdh, x0, r0 + rr);
+      }
+#pragma unroll
+      for (int m = 0; m < XF_IPT; ++m) {
+        if (!ix[m]) continue;
+        const int i = i0 + threadIdx.x + m * XF_NT;
+        const int rr = i / xq, x0 = xk.xlo + 4 * (i - rr * xq), y = r0 + rr;
+        uint32_t* o = crow + rr * xw + (x0 - xk.xlo);
+        if (ix[m] == 1) {
+          uint32_t c4[4];
+          color4_math(raw[m], cmode, c4);
+          *(uint4*)o = make_uint4(c4[0], c4[1], c4[2], c4[3]);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            o[j] = x0 + j < xk.W ? color_xy(base, pl, ncomp, cmode, cdw, cdh, x0 + j, y) : 0u;
+        }
       }
     }
     __syncthreads();
     for (int i = threadIdx.x; i < nr * n; i += XF_NT) {   // resample_h_kernel's sums
       const int rr = i / n, ox = i - rr * n;
-      const int xb = xk.bh[2 * ox] - xk.xlo, xs = xk.bh[2 * ox + 1];
-      const int32_t* k = xk.kh + (int64_t)ox * xk.ksh;
+      const int bh = sbh[ox], xb = bh & 0xFFFF, xs = bh >> 16;
+      const int32_t* k = skh + ox * xk.ksh;
       const uint32_t* p = crow + rr * xw + xb;
       int s0 = 1 << (XF_PREC - 1), s1 = s0, s2 = s0;
       for (int j = 0; j < xs; ++j) {
@@ -1343,10 +1390,10 @@ __global__ __launch_bounds__(XF_NT) void jpeg_transform_kernel(const uint8_t* __
     }
     __syncthreads();
   }
-  for (int i = threadIdx.x; i < (y1 - y0) * n; i += XF_NT) {   // resample_v_kernel's sums + ToTensor / Normalize
+  for (int i = threadIdx.x; i < ny * n; i += XF_NT) {   // resample_v_kernel's sums + ToTensor / Normalize
     const int yy = i / n, x = i - yy * n, y = y0 + yy;
-    const int yb = xk.bv[2 * y] - ra, ys = xk.bv[2 * y + 1];
-    const int32_t* k = xk.kv + (int64_t)y * xk.ksv;
+    const int bv = sbv[yy], yb = bv & 0xFFFF, ys = bv >> 16;
+    const int32_t* k = skv + yy * xk.ksv;
     int sc[3] = {1 << (XF_PREC - 1), 1 << (XF_PREC - 1), 1 << (XF_PREC - 1)};
     for (int j = 0; j < ys; ++j) {
       const uint32_t v = hrow[(yb + j) * n + x];
@@ -1430,8 +1477,8 @@ static bool jp_serial_forced() {
 }
 
 // The fused transform's launch shape: output rows per workgroup (band) and LDS bytes -- the
-// widest band's source rows of horizontal output plus XF_RPI converted source rows -- kept
-// within 150 KB by halving the band (tall sources need more rows per output row).
+// filter tables, XF_RPI converted source rows and the widest band's source rows of horizontal
+// output -- the widest band (16, halved) that fits two workgroups per CU, else one.
 hipError_t jpeg_xform_plan(int H, int W, int n, int mode, XformK& xk, size_t& lds) {
   ResampleTables t;
   const hipError_t e = resample_tables(H, W, n, mode, t);
@@ -1453,20 +1500,23 @@ hipError_t jpeg_xform_plan(int H, int W, int n, int mode, XformK& xk, size_t& ld
     xk.mean[c] = mean[c];
     xk.sd[c] = sd[c];
   }
-  for (int band = 16; band >= 1; band /= 2) {
-    int rows_max = 0;
-    for (int y0 = 0; y0 < n; y0 += band) {
-      const int y1 = std::min(n, y0 + band);
-      int rb = t.hbv[2 * y0];
-      for (int y = y0; y < y1; ++y) rb = std::max(rb, t.hbv[2 * y] + t.hbv[2 * y + 1]);
-      rows_max = std::max(rows_max, rb - t.hbv[2 * y0]);
-    }
-    lds = ((size_t)XF_RPI * xk.xw + (size_t)rows_max * n) * 4;
-    if (lds <= 150 * 1024) {
-      xk.band = band;
-      xk.nbands = (n + band - 1) / band;
-      xk.rows_max = rows_max;
-      return hipSuccess;
+  // the widest band that leaves two workgroups per CU (<= XF_LDS2), else one (<= 150 KB)
+  for (const size_t cap : {XF_LDS2, (size_t)150 * 1024}) {
+    for (int band = 16; band >= 1; band /= 2) {
+      int rows_max = 0;
+      for (int y0 = 0; y0 < n; y0 += band) {
+        const int y1 = std::min(n, y0 + band);
+        int rb = t.hbv[2 * y0];
+        for (int y = y0; y < y1; ++y) rb = std::max(rb, t.hbv[2 * y] + t.hbv[2 * y + 1]);
+        rows_max = std::max(rows_max, rb - t.hbv[2 * y0]);
+      }
+      lds = ((size_t)n * (xk.ksh + 1) + (size_t)band * (xk.ksv + 1) + (size_t)XF_RPI * xk.xw + (size_t)rows_max * n) * 4;
+      if (lds <= cap && xk.xw < 65536 && rows_max < 65536) {
+        xk.band = band;
+        xk.nbands = (n + band - 1) / band;
+        xk.rows_max = rows_max;
+        return hipSuccess;
+      }
     }
   }
   return hipErrorInvalidValue;   // a source too wide / tall for one band in LDS: decode + preprocess instead
