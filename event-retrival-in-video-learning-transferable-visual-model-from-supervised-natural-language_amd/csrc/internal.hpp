@@ -202,7 +202,8 @@ hipError_t rank_mirror(const uint16_t* mirror, const void* master, int64_t N, in
 hipError_t rank_rescore(const void* master, int64_t N, int64_t D, int dt, const float* q, int64_t Q, int k, int kc,
                         const float* m_s, const int64_t* m_i, int64_t base, float d_rel, float d_abs, int norm_mode,
                         int nan_first, const int32_t* unsafe, float* out_s, int64_t* out_i, int32_t* cert,
-                        hipStream_t s);
+                        hipStream_t s, uint32_t* zero = nullptr, int64_t zero_words = 0);
+// (zero / zero_words: words the re-score kernel clears for the launch after it)
 // certified bf16-MFMA ranking pass (rank_cert.hip): f32 / bf16 rows, D = 512, k <= 12, L2 norms
 int64_t rank_cert_min_rows();
 bool rank_cert_eligible(int64_t N, int64_t D, int dt, int k, int norm_mode);
@@ -211,7 +212,7 @@ void rank_cert_delta(int dt, float& d_rel, float& d_abs);
 // certified queries' results in out; *cert_out = the per-query certificates (in ws) for the gated exact pass
 hipError_t rank_cert_topk(const void* corpus, int64_t N, int dt, const float* q, int64_t Q, int k, int64_t base,
                           int norm_mode, int nan_first, float* out_s, int64_t* out_i, void* ws, int32_t** cert_out,
-                          hipStream_t s);
+                          hipStream_t s, uint32_t* zero = nullptr, int64_t zero_words = 0);
 // float16 corpus rows normalised as NumPy does it in float16 (corpus.hip;
 // embedding_service.py:209-210): the host-planned pairwise-summation tree of
 // the row's squares (leaves <= 128 elements, ops 0 = next leaf, 1 = add)
@@ -240,6 +241,7 @@ struct ResampleTables {
   const int32_t *kh = nullptr, *bh = nullptr, *kv = nullptr, *bv = nullptr;
   int ksh = 0, ksv = 0, xlo = 0, xw = 0;
   std::vector<int32_t> hbv;
+  int32_t wmax = 0;   // largest |coefficient|
 };
 hipError_t resample_tables(int H, int W, int n, int mode, ResampleTables& t);
 // frames uint8 [B,H,W,3] -> out [B,3,n,n] f32 / bf16; mode 0 CLIP _transform, 1 squash (bilinear)

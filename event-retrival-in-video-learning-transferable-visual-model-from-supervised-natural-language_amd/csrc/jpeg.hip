@@ -1313,10 +1313,19 @@ struct XformK {
   const int32_t *kh, *bh, *kv, *bv;   // preprocess.hip's tables (ResampleTables)
   int ksh, ksv, n, xlo, xw, W;        // xlo % 4 == 0, xw % 4 == 0 (the span rounded out)
   int band, nbands, rows_max;         // output rows per workgroup; LDS rows for the widest band
+  int i24;                            // every |coefficient| < 2^23: 24-bit multiplies are exact
   float mean[3], sd[3];
 };
 
-template <bool OUT_BF16>
+// pixel (0..255) x Pillow coefficient: with |w| < 2^23 both fit 24-bit signed operands and the
+// product 31 bits, so v_mul_i32_i24 (full rate; v_mul_lo_u32 is quarter rate) is exact
+template <bool I24>
+__device__ __forceinline__ int xf_mul(uint32_t pix, int w) {
+  // (w << 8) >> 8 is w itself when it fits 24 bits; it tells the backend so (v_mul_i32_i24 / v_mad_i32_i24)
+  return I24 ? (int)pix * ((w << 8) >> 8) : (int)pix * w;
+}
+
+template <bool OUT_BF16, bool I24>
 __global__ __launch_bounds__(XF_NT) void jpeg_transform_kernel(const uint8_t* __restrict__ planes, JpegPlanes pl,
                                                              int ncomp, int cmode, int cdw, int cdh, XformK xk,
                                                              void* __restrict__ out) {
@@ -1373,8 +1382,10 @@ __global__ __launch_bounds__(XF_NT) void jpeg_transform_kernel(const uint8_t* __
       }
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < nr * n; i += XF_NT) {   // resample_h_kernel's sums
-      const int rr = i / n, ox = i - rr * n;
+    // resample_h_kernel's sums; the step's rows vary fastest across lanes, so the lanes of one
+    // output column read one weight address (broadcast) and rows xw apart (distinct banks)
+    for (int i = threadIdx.x; i < nr * n; i += XF_NT) {
+      const int ox = i / nr, rr = i - ox * nr;
       const int bh = sbh[ox], xb = bh & 0xFFFF, xs = bh >> 16;
       const int32_t* k = skh + ox * xk.ksh;
       const uint32_t* p = crow + rr * xw + xb;
@@ -1382,9 +1393,9 @@ __global__ __launch_bounds__(XF_NT) void jpeg_transform_kernel(const uint8_t* __
       for (int j = 0; j < xs; ++j) {
         const uint32_t v = p[j];
         const int w = k[j];
-        s0 += (int)(v & 255u) * w;
-        s1 += (int)((v >> 8) & 255u) * w;
-        s2 += (int)((v >> 16) & 255u) * w;
+        s0 += xf_mul<I24>(v & 255u, w);
+        s1 += xf_mul<I24>((v >> 8) & 255u, w);
+        s2 += xf_mul<I24>((v >> 16) & 255u, w);
       }
       hrow[(r0 - ra + rr) * n + ox] = xf_clip8(s0) | (xf_clip8(s1) << 8) | (xf_clip8(s2) << 16);
     }
@@ -1398,9 +1409,9 @@ __global__ __launch_bounds__(XF_NT) void jpeg_transform_kernel(const uint8_t* __
     for (int j = 0; j < ys; ++j) {
       const uint32_t v = hrow[(yb + j) * n + x];
       const int w = k[j];
-      sc[0] += (int)(v & 255u) * w;
-      sc[1] += (int)((v >> 8) & 255u) * w;
-      sc[2] += (int)((v >> 16) & 255u) * w;
+      sc[0] += xf_mul<I24>(v & 255u, w);
+      sc[1] += xf_mul<I24>((v >> 8) & 255u, w);
+      sc[2] += xf_mul<I24>((v >> 16) & 255u, w);
     }
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
@@ -1493,6 +1504,7 @@ hipError_t jpeg_xform_plan(int H, int W, int n, int mode, XformK& xk, size_t& ld
   xk.xlo = t.xlo & ~3;                          // whole 4-pixel groups (color4); columns past W
   xk.xw = ((t.xlo + t.xw + 3) & ~3) - xk.xlo;   // are never read by the taps
   xk.W = W;
+  xk.i24 = t.wmax < (1 << 23);
   // torchvision's Normalize constants: Python floats -> float32 (preprocess.hip)
   const float mean[3] = {(float)0.48145466, (float)0.4578275, (float)0.40821073};
   const float sd[3] = {(float)0.26862954, (float)0.26130258, (float)0.27577711};
@@ -1684,12 +1696,17 @@ hipError_t jpeg_decode(const uint8_t* data, int64_t data_bytes, const int64_t* s
       const int nfc = (int)std::min<int64_t>(per_launch, nframes - f0);
       char* o = (char*)xf->out + f0 * 3 * (int64_t)xf->n * xf->n * (xf->out_bf16 ? 2 : 4);
       const dim3 grid((unsigned)((int64_t)nfc * xk.nbands));
-      if (xf->out_bf16)
-        hipLaunchKernelGGL(jpeg_transform_kernel<true>, grid, dim3(XF_NT), lds, s, planes + f0 * bytes, pl, ncomp, cmode,
-                           cdw, cdh, xk, (void*)o);
-      else
-        hipLaunchKernelGGL(jpeg_transform_kernel<false>, grid, dim3(XF_NT), lds, s, planes + f0 * bytes, pl, ncomp, cmode,
-                           cdw, cdh, xk, (void*)o);
+#define XF_LAUNCH(BF, I24_)                                                                                      \
+  hipLaunchKernelGGL((jpeg_transform_kernel<BF, I24_>), grid, dim3(XF_NT), lds, s, planes + f0 * bytes, pl, ncomp, \
+                     cmode, cdw, cdh, xk, (void*)o)
+      if (xf->out_bf16) {
+        if (xk.i24) XF_LAUNCH(true, true);
+        else XF_LAUNCH(true, false);
+      } else {
+        if (xk.i24) XF_LAUNCH(false, true);
+        else XF_LAUNCH(false, false);
+      }
+#undef XF_LAUNCH
       if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     return hipSuccess;

@@ -155,6 +155,7 @@ struct Tables {
   int ksh = 0, ksv = 0, r0 = 0, rows = 0;
   int xlo = 0, xw = 0;            // source columns the crop's taps read: [xlo, xlo + xw)
   std::vector<int32_t> hbv;       // host copy of bv (the fused JPEG transform sizes its row bands from it)
+  int32_t wmax = 0;               // largest |coefficient| of kh / kv (24-bit multiplies apply below 2^23)
 };
 
 std::mutex g_tab_mu;
@@ -211,6 +212,8 @@ hipError_t get_tables(int H, int W, int n, int mode, Tables& out) {
   t.xlo = xlo;
   t.xw = xhi - xlo;
   t.hbv = bv;
+  for (const int32_t w : kh) t.wmax = std::max(t.wmax, w < 0 ? -w : w);
+  for (const int32_t w : kv) t.wmax = std::max(t.wmax, w < 0 ? -w : w);
   const size_t nb = (kh.size() + bh.size() + kv.size() + bv.size()) * 4;
   char* d = nullptr;
   if ((e = hipMalloc(&d, nb)) != hipSuccess) return e;
@@ -291,6 +294,7 @@ hipError_t resample_tables(int H, int W, int n, int mode, ResampleTables& r) {
   r.xlo = t.xlo;
   r.xw = t.xw;
   r.hbv = t.hbv;
+  r.wmax = t.wmax;
   return hipSuccess;
 }
 

@@ -1030,17 +1030,27 @@ hipError_t rank_merge(const float* cs, const int64_t* ci, int64_t Q, int64_t C, 
   return hipGetLastError();
 }
 
-template <int D, int DT>
-static hipError_t launch_reg(int64_t N, const void* corpus, const float* q, int64_t Q, int k, int nm, int nf,
-                             int64_t base, void* ws, float* out_s, int64_t* out_i, hipStream_t s,
-                             const int32_t* gate = nullptr) {
-  // one workgroup per CU (LDS ring 128 KB), rows per workgroup a multiple of 128
-  // (one 32-row tile per wave); never more workgroups than rank_chunks (workspace)
+// rank_reg's workgroups: one per CU (LDS ring 128 KB), rows per workgroup a multiple of 128
+// (one 32-row tile per wave); never more workgroups than rank_chunks (workspace)
+static int64_t reg_rows_per_wg(int64_t N) {
   int64_t nwg = rank_chunks(N);
   if (nwg > 256) nwg = 256;
   if (nwg > (N + 127) / 128) nwg = (N + 127) / 128;
-  const int64_t rpw = ((N + nwg - 1) / nwg + 127) / 128 * 128;
-  nwg = (N + rpw - 1) / rpw;
+  return ((N + nwg - 1) / nwg + 127) / 128 * 128;
+}
+
+static FoldWs reg_fold(int64_t N, int64_t Q, void* ws) {
+  const int64_t rpw = reg_rows_per_wg(N);
+  return fold_ws(ws, (N + rpw - 1) / rpw, Q);
+}
+
+// prezeroed: the merge counters were cleared by the kernel before (the certified route's re-score)
+template <int D, int DT>
+static hipError_t launch_reg(int64_t N, const void* corpus, const float* q, int64_t Q, int k, int nm, int nf,
+                             int64_t base, void* ws, float* out_s, int64_t* out_i, hipStream_t s,
+                             const int32_t* gate = nullptr, bool prezeroed = false) {
+  const int64_t rpw = reg_rows_per_wg(N);
+  const int64_t nwg = (N + rpw - 1) / rpw;
   const FoldWs f = fold_ws(ws, nwg, Q);
   // interleaved tile order: A/B only (MICLIP_RANK_ILV=1).  scripts/rank_micro.py: 1M x 512 494 us
   // against 479 with contiguous row ranges, 1M x 768 729 against 717: not the stream's limit
@@ -1071,7 +1081,7 @@ static hipError_t launch_reg(int64_t N, const void* corpus, const float* q, int6
 #endif
   hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
-  if ((e = fold_zero(f, s)) != hipSuccess) return e;
+  if (!prezeroed && (e = fold_zero(f, s)) != hipSuccess) return e;
   const dim3 grid((unsigned)((Q + RQ - 1) / RQ), (unsigned)nwg);   // (query blocks, row blocks): RB / QB
   hipLaunchKernelGGL(fn, grid, dim3(256), lds, s, corpus, N, q, Q, k, rpw, nm, nf, base, f, out_s, out_i, gate);
   return hipGetLastError();
@@ -1126,11 +1136,13 @@ hipError_t rank_topk(const void* corpus, int64_t N, int64_t D, int dt, const flo
       // certified bf16-MFMA pass + exact re-score of its candidates, then the exact pass for
       // the query blocks it could not certify (results identical to the exact pass alone)
       int32_t* cert = nullptr;
-      hipError_t ec = rank_cert_topk(corpus, N, dt, q, Q, k, base, norm_mode, nan_first, out_s, out_i, ws, &cert, s);
-      if (ec != hipSuccess) return ec;
       void* ws2 = (char*)ws + al128(rank_cert_ws_bytes(N, Q));
-      return dt == 0 ? launch_reg<512, 0>(N, corpus, q, Q, k, norm_mode, nan_first, base, ws2, out_s, out_i, s, cert)
-                     : launch_reg<512, 1>(N, corpus, q, Q, k, norm_mode, nan_first, base, ws2, out_s, out_i, s, cert);
+      const FoldWs f2 = reg_fold(N, Q, ws2);   // the gated exact pass's counters: the re-score clears them
+      hipError_t ec = rank_cert_topk(corpus, N, dt, q, Q, k, base, norm_mode, nan_first, out_s, out_i, ws, &cert, s,
+                                     fold_zero_base(f2), fold_zero_words(f2));
+      if (ec != hipSuccess) return ec;
+      return dt == 0 ? launch_reg<512, 0>(N, corpus, q, Q, k, norm_mode, nan_first, base, ws2, out_s, out_i, s, cert, true)
+                     : launch_reg<512, 1>(N, corpus, q, Q, k, norm_mode, nan_first, base, ws2, out_s, out_i, s, cert, true);
     }
     // (D = 768 would hold 384 query VGPRs: hipcc spills ~230, so it keeps rank_stream)
     return dt == 0   ? launch_reg<512, 0>(N, corpus, q, Q, k, norm_mode, nan_first, base, ws, out_s, out_i, s)

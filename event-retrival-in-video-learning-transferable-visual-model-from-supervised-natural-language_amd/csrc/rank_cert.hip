@@ -494,19 +494,20 @@ void rank_cert_delta(int dt, float& d_rel, float& d_abs) {
 
 hipError_t rank_cert_topk(const void* corpus, int64_t N, int dt, const float* q, int64_t Q, int k, int64_t base,
                           int norm_mode, int nan_first, float* out_s, int64_t* out_i, void* ws, int32_t** cert_out,
-                          hipStream_t s) {
+                          hipStream_t s, uint32_t* zero, int64_t zero_words) {
   const int64_t nwg = cert_wgs(N);
   float* m_s = (float*)ws;
   int64_t* m_i = (int64_t*)((char*)ws + (size_t)(Q * CKC) * sizeof(float));
   int32_t* cert = (int32_t*)((char*)ws + al128((size_t)(Q * CKC) * (sizeof(float) + sizeof(int64_t))));
-  int32_t* unsafe = cert + Q;
   void* fws = (char*)cert + al128((size_t)Q * 4 + 4);
   *cert_out = cert;
   hipError_t e;
-  if ((e = hipMemsetAsync(unsafe, 0, 4, s)) != hipSuccess) return e;
   const int64_t rpw = ((N + nwg - 1) / nwg + 127) / 128 * 128;   // whole tiles per wave round
   const int64_t nwg_used = (N + rpw - 1) / rpw;                  // <= nwg (the workspace's count)
   const FoldWs fu = fold_ws(fws, nwg_used, Q);
+  // one memset for the merge counters, gtau and the unsafe flag (the fold workspace's aux word):
+  // each fill is a ~5 us dispatch of its own at this size (scripts/gpu_r4p.sh trace)
+  int32_t* unsafe = (int32_t*)fu.aux;
   if ((e = fold_zero(fu, s)) != hipSuccess) return e;
   const size_t lds = cert_lds_bytes();
   const dim3 grid((unsigned)((Q + FQ - 1) / FQ), (unsigned)nwg_used);   // (query blocks, row blocks)
@@ -530,7 +531,7 @@ hipError_t rank_cert_topk(const void* corpus, int64_t N, int dt, const float* q,
   float d_rel, d_abs;
   rank_cert_delta(dt, d_rel, d_abs);
   return rank_rescore(corpus, N, CD, dt, q, Q, k, CKC, m_s, m_i, base, d_rel, d_abs, norm_mode, nan_first, unsafe,
-                      out_s, out_i, cert, s);
+                      out_s, out_i, cert, s, zero, zero_words);
 }
 
 }  // namespace miclip

@@ -237,6 +237,7 @@ struct FoldWs {
   uint32_t* cnt;     // [query blocks]: groups finished
   uint32_t* gcnt;    // [query blocks][groups]: workgroups of a group finished
   uint32_t* gtau;    // [Qpad]
+  uint32_t* aux;     // [32] zeroed with the counters (the certified pass's unsafe flag)
   int64_t Qpad;
   int ngrp;
 };
@@ -442,14 +443,15 @@ static inline int64_t qpad(int64_t Q) { return (Q + FQ - 1) / FQ * FQ; }
 static inline size_t al128(size_t b) { return (b + 127) / 128 * 128; }
 
 // in-launch merge workspace: slabs [nwg][Qpad][16] u64, group slabs [groups][Qpad][16] u64,
-// counters [Qpad / 32] u32, group counters [Qpad / 32][groups] u32, gtau [Qpad] u32 (the last
-// three contiguous: fold_zero clears them with one memset)
+// counters [Qpad / 32] u32, group counters [Qpad / 32][groups] u32, gtau [Qpad] u32, aux [32]
+// u32 (the last four contiguous: fold_zero clears them with one memset, or a preceding kernel
+// with fold_zero_words / fold_zero_base)
 static inline int64_t fold_groups(int64_t nwg) { return (nwg + FOLD_GS - 1) / FOLD_GS; }
 
 static inline size_t fold_ws_bytes(int64_t nwg, int64_t Q) {
   const int64_t qp = qpad(Q), ng = fold_groups(nwg);
   return (size_t)((nwg + ng) * qp) * 128 + al128((size_t)(qp / FQ) * 4) + al128((size_t)(qp / FQ * ng) * 4) +
-         al128((size_t)qp * 4);
+         al128((size_t)qp * 4) + 128;
 }
 
 static inline FoldWs fold_ws(void* ws, int64_t nwg, int64_t Q) {
@@ -460,13 +462,17 @@ static inline FoldWs fold_ws(void* ws, int64_t nwg, int64_t Q) {
   f.cnt = (uint32_t*)((char*)f.gslab + (size_t)(ng * qp) * 128);
   f.gcnt = (uint32_t*)((char*)f.cnt + al128((size_t)(qp / FQ) * 4));
   f.gtau = (uint32_t*)((char*)f.gcnt + al128((size_t)(qp / FQ * ng) * 4));
+  f.aux = (uint32_t*)((char*)f.gtau + al128((size_t)qp * 4));
   f.Qpad = qp;
   f.ngrp = (int)ng;
   return f;
 }
 
+static inline int64_t fold_zero_words(const FoldWs& f) { return (int64_t)((f.aux + 32) - f.cnt); }
+static inline uint32_t* fold_zero_base(const FoldWs& f) { return f.cnt; }
+
 static inline hipError_t fold_zero(const FoldWs& f, hipStream_t s) {
-  return hipMemsetAsync(f.cnt, 0, (size_t)((char*)(f.gtau + f.Qpad) - (char*)f.cnt), s);
+  return hipMemsetAsync(f.cnt, 0, (size_t)fold_zero_words(f) * 4, s);
 }
 
 }  // namespace rankk

@@ -280,7 +280,12 @@ __global__ __launch_bounds__(64) void mirror_rescore_kernel(const void* __restri
                                                             float d_rel, float d_abs, int norm_mode, int nan_first,
                                                             const int32_t* __restrict__ unsafe,
                                                             float* __restrict__ out_s, int64_t* __restrict__ out_i,
-                                                            int32_t* __restrict__ cert) {
+                                                            int32_t* __restrict__ cert, uint32_t* __restrict__ zero,
+                                                            int64_t zero_words) {
+  // the next launch's merge counters (the gated exact pass after a certified pass): cleared
+  // here instead of by a memset dispatch of their own
+  if (zero && blockIdx.x == 0)
+    for (int64_t i = threadIdx.x; i < zero_words; i += 64) zero[i] = 0u;
   constexpr int NCH = D / 32;
   __shared__ float Tq[D];
   __shared__ float nrm[32];
@@ -442,18 +447,18 @@ hipError_t rank_mirror(const uint16_t* mirror, const void* master, int64_t N, in
   float d_rel, d_abs;
   mirror_delta(D, split, d_rel, d_abs);
   return rank_rescore(master, N, D, dt, q, Q, k, kc, m_s, m_i, base, d_rel, d_abs, 0, nan_first, nullptr, out_s, out_i,
-                      cert, s);
+                      cert, s, nullptr, 0);
 }
 
 hipError_t rank_rescore(const void* master, int64_t N, int64_t D, int dt, const float* q, int64_t Q, int k, int kc,
                         const float* m_s, const int64_t* m_i, int64_t base, float d_rel, float d_abs, int norm_mode,
                         int nan_first, const int32_t* unsafe, float* out_s, int64_t* out_i, int32_t* cert,
-                        hipStream_t s) {
+                        hipStream_t s, uint32_t* zero, int64_t zero_words) {
   if (Q <= 0) return hipSuccess;
   const dim3 grid((unsigned)Q);
 #define MI_RS(DTV, DV)                                                                                                \
   hipLaunchKernelGGL((mirror_rescore_kernel<DTV, DV>), grid, dim3(64), 0, s, master, N, q, k, kc, m_s, m_i, base, \
-                     d_rel, d_abs, norm_mode, nan_first, unsafe, out_s, out_i, cert)
+                     d_rel, d_abs, norm_mode, nan_first, unsafe, out_s, out_i, cert, zero, zero_words)
   if (D == 512) {
     if (dt == 0) MI_RS(0, 512);
     else if (dt == 1) MI_RS(1, 512);
