@@ -1351,41 +1351,52 @@ __global__ __launch_bounds__(XF_NT) void jpeg_transform_kernel(const uint8_t* __
   for (int i = threadIdx.x; i < ny; i += XF_NT) sbv[i] = (xk.bv[2 * (y0 + i)] - ra) | (xk.bv[2 * (y0 + i) + 1] << 16);
   const uint8_t* base = planes + (int64_t)f * pl.plane_frame_bytes;
   const int xq = xw >> 2;
-  for (int r0 = ra; r0 < rb; r0 += XF_RPI) {
-    const int nr = min(XF_RPI, rb - r0), items = nr * xq;
-    // colour conversion, 4 pixels per item; each thread's XF_IPT items load before any converts
-    for (int i0 = 0; i0 < items; i0 += XF_NT * XF_IPT) {
-      Raw4 raw[XF_IPT];
-      int ix[XF_IPT];
+  // source rows per step: as many as one thread's XF_IPT 4-pixel groups cover (<= XF_RPI, the
+  // LDS rows), so a step's conversion loads go out together, before the previous step's
+  // horizontal pass, which then runs under their latency
+  const int rps = max(1, min(XF_RPI, XF_NT * XF_IPT / xq));
+  Raw4 raw[XF_IPT];
+  int ix[XF_IPT];
+  auto issue = [&](int r0) {
+    const int items = min(rps, rb - r0) * xq;
 #pragma unroll
-      for (int m = 0; m < XF_IPT; ++m) {
-        const int i = i0 + threadIdx.x + m * XF_NT;
-        const int rr = i / xq, x0 = xk.xlo + 4 * (i - rr * xq);
-        ix[m] = i < items ? (ncomp == 3 && x0 >= 4 && x0 + 8 <= xk.W ? 1 : 2) : 0;   // 1 fast, 2 edge
-        if (ix[m] == 1) raw[m] = color4_load(base, pl, cmode, cdh, x0, r0 + rr);
-      }
-#pragma unroll
-      for (int m = 0; m < XF_IPT; ++m) {
-        if (!ix[m]) continue;
-        const int i = i0 + threadIdx.x + m * XF_NT;
-        const int rr = i / xq, x0 = xk.xlo + 4 * (i - rr * xq), y = r0 + rr;
-        uint32_t* o = crow + rr * xw + (x0 - xk.xlo);
-        if (ix[m] == 1) {
-          uint32_t c4[4];
-          color4_math(raw[m], cmode, c4);
-          *(uint4*)o = make_uint4(c4[0], c4[1], c4[2], c4[3]);
-        } else {
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            o[j] = x0 + j < xk.W ? color_xy(base, pl, ncomp, cmode, cdw, cdh, x0 + j, y) : 0u;
-        }
-      }
+    for (int m = 0; m < XF_IPT; ++m) {
+      const int i = threadIdx.x + m * XF_NT;
+      const int rr = i / xq, x0 = xk.xlo + 4 * (i - rr * xq);
+      ix[m] = i < items ? (ncomp == 3 && x0 >= 4 && x0 + 8 <= xk.W ? 1 : 2) : 0;   // 1 fast, 2 edge
+      if (ix[m] == 1) raw[m] = color4_load(base, pl, cmode, cdh, x0, r0 + rr);
     }
+  };
+  auto convert = [&](int r0) {
+#pragma unroll
+    for (int m = 0; m < XF_IPT; ++m) {
+      if (ix[m] != 1) continue;
+      const int i = threadIdx.x + m * XF_NT;
+      const int rr = i / xq, x0 = xk.xlo + 4 * (i - rr * xq);
+      uint32_t c4[4];
+      color4_math(raw[m], cmode, c4);
+      *(uint4*)(crow + rr * xw + (x0 - xk.xlo)) = make_uint4(c4[0], c4[1], c4[2], c4[3]);
+    }
+    // groups at the frame's left / right edge (or one-component frames): pixel by pixel, rolled
+#pragma unroll 1
+    for (int m = 0; m < XF_IPT; ++m) {
+      if (ix[m] != 2) continue;
+      const int i = threadIdx.x + m * XF_NT;
+      const int rr = i / xq, x0 = xk.xlo + 4 * (i - rr * xq), y = r0 + rr;
+      uint32_t* o = crow + rr * xw + (x0 - xk.xlo);
+#pragma unroll 1
+      for (int j = 0; j < 4; ++j)
+        o[j] = x0 + j < xk.W ? color_xy(base, pl, ncomp, cmode, cdw, cdh, x0 + j, y) : 0u;
+    }
+  };
+  issue(ra);
+  for (int r0 = ra; r0 < rb; r0 += rps) {
+    const int nr = min(rps, rb - r0);
+    convert(r0);
     __syncthreads();
-    // resample_h_kernel's sums; the step's rows vary fastest across lanes, so the lanes of one
-    // output column read one weight address (broadcast) and rows xw apart (distinct banks)
-    for (int i = threadIdx.x; i < nr * n; i += XF_NT) {
-      const int ox = i / nr, rr = i - ox * nr;
+    if (r0 + rps < rb) issue(r0 + rps);
+    for (int i = threadIdx.x; i < nr * n; i += XF_NT) {   // resample_h_kernel's sums
+      const int rr = i / n, ox = i - rr * n;
       const int bh = sbh[ox], xb = bh & 0xFFFF, xs = bh >> 16;
       const int32_t* k = skh + ox * xk.ksh;
       const uint32_t* p = crow + rr * xw + xb;
@@ -1505,6 +1516,7 @@ hipError_t jpeg_xform_plan(int H, int W, int n, int mode, XformK& xk, size_t& ld
   xk.xw = ((t.xlo + t.xw + 3) & ~3) - xk.xlo;   // are never read by the taps
   xk.W = W;
   xk.i24 = t.wmax < (1 << 23);
+  if (xk.xw / 4 > XF_NT * XF_IPT) return hipErrorInvalidValue;   // wider than one step's row: decode + preprocess
   // torchvision's Normalize constants: Python floats -> float32 (preprocess.hip)
   const float mean[3] = {(float)0.48145466, (float)0.4578275, (float)0.40821073};
   const float sd[3] = {(float)0.26862954, (float)0.26130258, (float)0.27577711};
