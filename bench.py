@@ -119,18 +119,29 @@ def kernel_timing(model, cfg, chunk, reps=20):
     gemms = [("gemm_qkv", 3 * W, W, 0, outb), ("gemm_out", W, W, 0, outb), ("gemm_fc", 4 * W, W, 1, outb),
              ("gemm_proj", W, 4 * W, 0, outb)]
     if getattr(model, "weights", "bf16") == "fp32":
-        # the parity mode's exact-f32 MFMA GEMM (precise.hip): f32 operands, epilogue 1 = QuickGELU
+        # the parity mode's GEMMs since round 4: split-bf16 operands (mi_op_split6: 3 bf16 terms per
+        # f32 value, the weights' copies built at load) and one bf16 GEMM over K' = 6K with an f32
+        # epilogue (api.cpp run_tower_f32); "tflops" counts the f32 GEMM's useful flops, "bf16_tflops"
+        # the MFMA work executed (6x); "split" times the activation split of that GEMM's input
         del A, outb
         Af = torch.randn(M, 4 * W, device=dev, generator=g) * 0.5
         Wf = torch.randn(4 * W, 4 * W, device=dev, generator=g) * 0.02
-        outF = torch.empty(M, 4 * W, device=dev)
+        outF = torch.zeros(M, 4 * W, device=dev)
+        A6 = torch.empty(M, 6 * 4 * W, dtype=torch.int16, device=dev)
         for name, Nn, K, epi, _ in gemms:
-            Ak, Wk = Af[:, :K].contiguous(), Wf[:Nn, :K].contiguous()
-            timed(name, lambda Nn=Nn, K=K, epi=epi, Ak=Ak, Wk=Wk: N.check(
-                L.mi_op_gemm_f32(Ak.data_ptr(), Wk.data_ptr(), bias.data_ptr(), outF.data_ptr(), M, Nn, K, epi, sp),
-                "gemm_f32"), flops=2.0 * M * Nn * K)
-            del Ak, Wk
-        del Af, Wf, outF
+            W6 = torch.empty(Nn, 6 * K, dtype=torch.int16, device=dev)
+            N.check(L.mi_op_split6(Wf.data_ptr(), 4 * W, Nn, K, 1, 0, W6.data_ptr(), sp), "split6 W")
+            gelu = 1 if name == "gemm_proj" else 0   # c_proj's input: QuickGELU applied in the split
+            timed(name + "_split", lambda K=K, gelu=gelu: N.check(
+                L.mi_op_split6(Af.data_ptr(), 4 * W, M, K, 0, gelu, A6.data_ptr(), sp), "split6 A"),
+                  nbytes=M * K * 4 + M * 6 * K * 2)
+            ep = 2 if name in ("gemm_out", "gemm_proj") else 3   # += into the residual / f32 store
+            timed(name, lambda Nn=Nn, K=K, ep=ep, W6=W6: N.check(
+                L.mi_op_gemm(A6.data_ptr(), W6.data_ptr(), bias.data_ptr(), outF.data_ptr(), M, Nn, 6 * K, ep, sp),
+                "gemm split-bf16"), flops=2.0 * M * Nn * K)
+            res[name]["bf16_tflops"] = round(res[name]["tflops"] * 6, 1)
+            del W6
+        del Af, Wf, outF, A6
         return res
     if getattr(model, "weights", "bf16") == "fp8":
         # MX-fp8 operands: e4m3 codes + stage-major e8m0 scales (mi_op_quantize_mx)
@@ -494,11 +505,16 @@ def parity_mode(args, dev, pixels, tokens, Q, k, base, chunk):
     step_flops = pixels.shape[0] * cfg.image_flops() + Q * cfg.text_flops() + 2.0 * pixels.shape[0] * Q * cfg.embed_dim
     out = {"weights": "fp32", "value": round(pixels.shape[0] / (ms / 1e3), 1), "unit": "frames/s",
            "ms_per_step": round(ms, 3), "steps": args.parity_steps,
-           "note": "fp32 tower: the mode whose R@1/5/10 equal the float64 oracle flow (tests/test_gpu_rk_flow.py)",
-           "roofline": {"bound": "mfma", "kernel": "gemm_f32 (precise.hip; mlp.c_fc + QuickGELU, exact-f32 MFMA)",
-                        "achieved": round(fl / (fc * 1e-6) / 1e12, 1), "peak": F32_MFMA_PEAK_TFLOPS,
-                        "unit": "TFLOP/s", "frac": round(fl / (fc * 1e-6) / 1e12 / F32_MFMA_PEAK_TFLOPS, 4),
-                        "traffic": None, "launch_shape": [M, 4 * cfg.vision_width, cfg.vision_width],
+           "note": "fp32 tower (split-bf16 GEMMs, f32-grade): the mode whose R@1/5/10 equal the float64 oracle "
+                   "flow (tests/test_gpu_rk_flow.py)",
+           "roofline": {"bound": "mfma",
+                        "kernel": "gemm_pp_kernel<EPI_F32> over split-bf16 operands, K' = 6K (mlp.c_fc pre-activation; "
+                                  "QuickGELU in c_proj's operand split)",
+                        "achieved": round(6 * fl / (fc * 1e-6) / 1e12, 1), "peak": BF16_PEAK_TFLOPS,
+                        "unit": "TFLOP/s", "frac": round(6 * fl / (fc * 1e-6) / 1e12 / BF16_PEAK_TFLOPS, 4),
+                        "f32_equivalent_tflops": round(fl / (fc * 1e-6) / 1e12, 1),
+                        "f32_mfma_peak": F32_MFMA_PEAK_TFLOPS,
+                        "traffic": None, "launch_shape": [M, 4 * cfg.vision_width, 6 * cfg.vision_width],
                         "avg_launch_us": fc},
            "mfma_frac_end_to_end_f32": round(step_flops / (ms / 1e3) / (F32_MFMA_PEAK_TFLOPS * 1e12), 4),
            "kernels": kern}

@@ -46,6 +46,12 @@ int fail(int code, const char* fmt, ...) {
                                       __FILE__, __LINE__);                                      \
   } while (0)
 
+#define MI_TRY(expr)      \
+  do {                    \
+    const int r_ = (expr); \
+    if (r_) return r_;    \
+  } while (0)
+
 uint16_t f2bf_host(float f) {
   uint32_t u;
   memcpy(&u, &f, 4);
@@ -59,6 +65,8 @@ struct Layer {
   const uint16_t *w_qkv, *w_out, *w_fc, *w_proj;
   // f32 GEMM weights (weight_dtype MI_F32): the same [N][K] matrices kept in f32
   const float *f_qkv = nullptr, *f_out = nullptr, *f_fc = nullptr, *f_proj = nullptr;
+  // ... and split into three bf16 terms, [N][6K] (split6_rows role 1): the split-bf16 GEMMs
+  const uint16_t *s6_qkv = nullptr, *s6_out = nullptr, *s6_fc = nullptr, *s6_proj = nullptr;
   // MX-fp8 copies (weight_dtype MI_FP8, vision tower): e4m3 codes + stage-major e8m0 scales
   const uint8_t *q_qkv = nullptr, *s_qkv = nullptr, *q_out = nullptr, *s_out = nullptr;
   const uint8_t *q_fc = nullptr, *s_fc = nullptr, *q_proj = nullptr, *s_proj = nullptr;
@@ -234,6 +242,8 @@ struct mi_clip {
   int Kp32 = 0;           // f32 mode: conv1 K padded to the f32 GEMM's 32-k stage
   const float *conv_f = nullptr, *vproj_f = nullptr, *tproj_f = nullptr;
   char* wq = nullptr;     // MX-fp8 weight copies
+  char* w6 = nullptr;     // f32 mode: split-bf16 weight copies (Layer::s6_*)
+  uint16_t* a6 = nullptr; // f32 mode: split-bf16 activations of one GEMM, [M][6K] (workspace)
   // vision
   const uint16_t* conv_w = nullptr;
   const float *cls = nullptr, *vpos = nullptr, *ln_pre_g = nullptr, *ln_pre_b = nullptr, *ln_post_g = nullptr,
@@ -417,6 +427,38 @@ int mi_clip_create(const mi_clip_arch* arch, const float* weights, int64_t numel
   };
   conv_layers(vlo, c->vl);
   conv_layers(tlo, c->tl);
+  if (full) {
+    // split-bf16 copies of every tower GEMM weight (run_tower_f32): [N][6K] bf16, 144 W^2 bytes
+    // per layer; they need N % 128 == 0 and 6K % 64 == 0 (gemm_bf16), true for W % 128 == 0
+    const int64_t Wv = a.vision_width, Wt = a.text_width;
+    if (Wv % 128 == 0 && Wt % 128 == 0) {
+      const size_t bytes = (size_t)(144 * Wv * Wv * (int64_t)c->vl.size() + 144 * Wt * Wt * (int64_t)c->tl.size());
+      hipError_t e6 = hipMalloc(&c->w6, bytes);
+      char* p6 = c->w6;
+      auto split = [&](const float* w, int64_t N, int64_t K) -> const uint16_t* {
+        uint16_t* o = (uint16_t*)p6;
+        p6 += (size_t)N * 6 * K * 2;
+        if (e6 == hipSuccess) e6 = split6_rows(w, K, N, (int)K, 1, 0, o, nullptr);
+        return o;
+      };
+      for (int t = 0; t < 2 && e6 == hipSuccess; ++t) {
+        const int64_t W = t ? Wt : Wv;
+        for (Layer& L : t ? c->tl : c->vl) {
+          L.s6_qkv = split(L.f_qkv, 3 * W, W);
+          L.s6_out = split(L.f_out, W, W);
+          L.s6_fc = split(L.f_fc, 4 * W, W);
+          L.s6_proj = split(L.f_proj, W, 4 * W);
+        }
+      }
+      if (e6 == hipSuccess) e6 = hipDeviceSynchronize();
+      if (e6 != hipSuccess) {
+        if (c->w6) (void)hipFree(c->w6);
+        (void)hipFree(c->wdev);
+        delete c;
+        return fail(MI_ERR_HIP, "split-bf16 weights: %s", hipGetErrorString(e6));
+      }
+    }
+  }
   if (weight_dtype == MI_FP8) {
     // MX-fp8 copies of the vision tower GEMM weights, quantised on the device
     // from the bf16 image (the text tower and the projections stay bf16)
@@ -463,6 +505,7 @@ int mi_clip_destroy(mi_clip* c) {
     if (c->ws) (void)hipFree(c->ws);
     if (c->wdev) (void)hipFree(c->wdev);
     if (c->wq) (void)hipFree(c->wq);
+    if (c->w6) (void)hipFree(c->w6);
     if (c->ws_evt) (void)hipEventDestroy(c->ws_evt);
   }
   delete c;
@@ -492,6 +535,8 @@ static int reserve_locked(mi_clip* c, int64_t ic, int64_t tc) {
   const size_t o_cls = carve((size_t)rows_max * mx(Wv, Wt) * es);
   const size_t o_y = carve((size_t)rows_max * a.embed_dim * 4);
   const size_t o_rs = carve((size_t)(Mv + 256) * 8);
+  // f32 mode, split-bf16 GEMMs: the widest A operand, c_proj's [M][6 * 4W]
+  const size_t o_a6 = c->w6 ? carve((size_t)mx(Mv * Wv, Mt * Wt) * 24 * 2) : carve(0);
   size_t o_hq = 0, o_hqs = 0, o_attq = 0, o_attqs = 0, o_mlpq = 0, o_mlpqs = 0;
   if (c->fp8) {
     const size_t mp = (size_t)((Mv + 1) & ~1);
@@ -520,6 +565,7 @@ static int reserve_locked(mi_clip* c, int64_t ic, int64_t tc) {
   c->cls_ln = (uint16_t*)(ws + o_cls);
   c->y = (float*)(ws + o_y);
   c->rs = (float*)(ws + o_rs);
+  c->a6 = c->w6 ? (uint16_t*)(ws + o_a6) : nullptr;
   if (c->fp8) {
     c->hq = (uint8_t*)(ws + o_hq);
     c->hqs = (uint8_t*)(ws + o_hqs);
@@ -729,6 +775,13 @@ static int run_tower_mx(mi_clip* c, const std::vector<Layer>& layers, int B, int
 
 static size_t dtype_size(int dt) { return dt == MI_F32 ? 4 : 2; }
 
+// fp32 tower GEMMs as split-bf16 GEMMs (the default); MICLIP_F32_SPLIT=0 (A/B build) runs
+// precise.hip's exact-f32 MFMA GEMM instead
+static bool split6_on() {
+  const char* e = ab_getenv("MICLIP_F32_SPLIT");
+  return e ? atoi(e) != 0 : true;
+}
+
 // The fp32 tower (weight_dtype MI_F32; kernels in precise.hip).  openai/CLIP
 // ResidualAttentionBlock with every tensor f32, the residual adds in the
 // out_proj / c_proj GEMM epilogues:
@@ -741,6 +794,27 @@ static int run_tower_f32(mi_clip* c, const std::vector<Layer>& layers, int B, in
   float* qkv = (float*)c->qkv;
   float* att = (float*)c->att;
   float* mlp = (float*)c->mlp;
+  if (c->a6 && layers.size() && layers[0].s6_qkv && split6_on()) {
+    // split-bf16 GEMMs (split6_rows): one bf16 GEMM over K' = 6K per linear layer, every product
+    // term to 2^-16 relative, f32 accumulation -- f32-grade results at bf16 MFMA rates
+    uint16_t* a6 = c->a6;
+    auto lin = [&](const float* in, int K, const uint16_t* w6, const float* b, float* out, int N, int epi,
+                   int gelu) -> int {
+      HIP_TRY(split6_rows(in, K, M, K, 0, gelu, a6, s));
+      HIP_TRY(gemm_bf16(gargs(a6, 6 * K, w6, 6 * K, b, out, N, M, N, 6 * K), epi, s));
+      return MI_OK;
+    };
+    for (const Layer& L : layers) {
+      HIP_TRY(layernorm_f32(c->x, W, L.ln1_g, L.ln1_b, h, W, M, W, s));
+      MI_TRY(lin(h, W, L.s6_qkv, L.b_qkv, qkv, 3 * W, EPI_F32, 0));
+      HIP_TRY(attention_f32(qkv, att, B, S, W, causal, s));
+      MI_TRY(lin(att, W, L.s6_out, L.b_out, c->x, W, EPI_RESID_F32, 0));
+      HIP_TRY(layernorm_f32(c->x, W, L.ln2_g, L.ln2_b, h, W, M, W, s));
+      MI_TRY(lin(h, W, L.s6_fc, L.b_fc, mlp, 4 * W, EPI_F32, 0));   // pre-activation: the split applies QuickGELU
+      MI_TRY(lin(mlp, 4 * W, L.s6_proj, L.b_proj, c->x, W, EPI_RESID_F32, 1));
+    }
+    return MI_OK;
+  }
   for (const Layer& L : layers) {
     HIP_TRY(layernorm_f32(c->x, W, L.ln1_g, L.ln1_b, h, W, M, W, s));
     HIP_TRY(gemm_f32(h, W, L.f_qkv, W, L.b_qkv, qkv, 3 * W, M, 3 * W, W, EPI_F32, s));
@@ -1054,6 +1128,14 @@ int mi_op_residual_ln(void* x, const void* delta, const float* g, const float* b
   if (xmode < 0 || xmode > 2) return fail(MI_ERR_ARG, "mi_op_residual_ln: xmode must be 0, 1 or 2");
   HIP_TRY(residual_ln((float*)x, (const uint16_t*)delta, W, 1, g, b, (uint16_t*)out, rows, W, (hipStream_t)stream,
                       nullptr, nullptr, xmode));
+  return MI_OK;
+}
+
+int mi_op_split6(const float* x, int64_t ldx, int64_t rows, int32_t K, int32_t role, int32_t gelu, void* out,
+                 void* stream) {
+  if (!x || !out || rows < 0 || (role & ~1) || (gelu & ~1)) return fail(MI_ERR_ARG, "mi_op_split6: bad arguments");
+  if (K < 4 || K % 4 || ldx < K || ldx % 4) return fail(MI_ERR_UNSUPPORTED, "mi_op_split6: K %% 4 == 0, ldx >= K, ldx %% 4 == 0");
+  HIP_TRY(split6_rows(x, ldx, rows, K, role, gelu, (uint16_t*)out, (hipStream_t)stream));
   return MI_OK;
 }
 

@@ -169,6 +169,14 @@ hipError_t layernorm_f32(const float* x, int64_t in_stride, const float* g, cons
 hipError_t attention_f32(const float* qkv, float* out, int B, int S, int W, int causal, hipStream_t s);
 // pixels [B,3,R,R] (f32 / bf16) -> patches f32 [B*G*G, Kp]
 hipError_t im2col_f32(const void* pixels, int in_bf16, float* out, int B, int R, int P, int Kp, hipStream_t s);
+// Split-bf16 operands of the fp32 tower's GEMMs (precise.hip): each f32 value x = x1 + x2 + x3
+// + O(2^-24 |x|) with x1 = bf16(x), x2 = bf16(x - x1), x3 = bf16(x - x1 - x2); a row of K values
+// becomes 6K bf16 in six K-blocks, activations (role 0) as [x1 x2 x3 x1 x2 x1] and weights
+// (role 1) as [w1 w1 w1 w2 w2 w3], so ONE bf16 GEMM over K' = 6K sums a1w1 + a2w1 + a3w1 +
+// a1w2 + a2w2 + a1w3: every product term down to 2^-16 relative, f32 accumulation.
+// gelu: QuickGELU (the fp32 epilogue's expf form) applied to x first (c_proj's input).
+hipError_t split6_rows(const float* x, int64_t ldx, int64_t rows, int K, int role, int gelu, uint16_t* out,
+                       hipStream_t s);
 
 }  // namespace miclip
 

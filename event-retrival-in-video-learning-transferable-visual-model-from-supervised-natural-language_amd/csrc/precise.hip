@@ -122,6 +122,50 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
   }
 }
 
+// ------------------------------------------------------------- split-bf16 operands
+// (internal.hpp split6_rows) one thread per 4 consecutive values of a row
+__device__ __forceinline__ void split3(float x, u16& x1, u16& x2, u16& x3) {
+  x1 = f2bf(x);
+  if (!__builtin_isfinite(x)) {   // inf / NaN: carried by x1 alone (x - x1 would be NaN)
+    x2 = x3 = 0;
+    return;
+  }
+  if ((x1 & 0x7fffu) == 0x7f80u) x1 = (u16)((x1 & 0x8000u) | 0x7f7fu);   // finite x past bf16's range: largest bf16
+  const float r1 = x - bf2f(x1);    // exact: x1 holds x's leading 8 significand bits
+  x2 = f2bf(r1);
+  x3 = f2bf(r1 - bf2f(x2));
+}
+
+__global__ __launch_bounds__(256) void split6_kernel(const float* __restrict__ x, int64_t ldx, int64_t rows, int K,
+                                                     int role, int gelu, uint16_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int k4 = K >> 2;
+  if (i >= rows * k4) return;
+  const int64_t r = i / k4;
+  const int c = (int)(i - r * k4) * 4;
+  float4 v = *(const float4*)(x + r * ldx + c);
+  if (gelu) {
+    v.x = v.x * (1.0f / (1.0f + expf(-1.702f * v.x)));
+    v.y = v.y * (1.0f / (1.0f + expf(-1.702f * v.y)));
+    v.z = v.z * (1.0f / (1.0f + expf(-1.702f * v.z)));
+    v.w = v.w * (1.0f / (1.0f + expf(-1.702f * v.w)));
+  }
+  u16 p[3][4];
+  split3(v.x, p[0][0], p[1][0], p[2][0]);
+  split3(v.y, p[0][1], p[1][1], p[2][1]);
+  split3(v.z, p[0][2], p[1][2], p[2][2]);
+  split3(v.w, p[0][3], p[1][3], p[2][3]);
+  // K-block j holds term t_a[j] (activations) or t_w[j] (weights)
+  constexpr int t_a[6] = {0, 1, 2, 0, 1, 0}, t_w[6] = {0, 0, 0, 1, 1, 2};
+  uint16_t* o = out + r * 6 * (int64_t)K + c;
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    const int t = role ? t_w[j] : t_a[j];
+    const uint2 w = make_uint2((uint32_t)p[t][0] | ((uint32_t)p[t][1] << 16), (uint32_t)p[t][2] | ((uint32_t)p[t][3] << 16));
+    *(uint2*)(o + (int64_t)j * K) = w;
+  }
+}
+
 // ------------------------------------------------------------- LayerNorm
 // One wave per row, W <= 1024, two-pass mean / variance in f32 (torch's
 // LayerNorm on fp32).  tokens != nullptr: row q of the output is the row
@@ -283,6 +327,15 @@ hipError_t gemm_f32(const float* A, int64_t lda, const float* W, int64_t ldw, co
                        group, gstride, goffset);
   else
     return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+hipError_t split6_rows(const float* x, int64_t ldx, int64_t rows, int K, int role, int gelu, uint16_t* out,
+                       hipStream_t s) {
+  if (rows <= 0) return hipSuccess;
+  if (K % 4 || ldx % 4 || K < 4) return hipErrorInvalidValue;
+  const int64_t n = rows * (K / 4);
+  hipLaunchKernelGGL(split6_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, ldx, rows, K, role, gelu, out);
   return hipGetLastError();
 }
 

@@ -320,6 +320,16 @@ int mi_op_residual_ln(void* x, const void* delta, const float* gamma, const floa
  *   colc [N] = b_n + sum_k beta_k W[n,k].  N % 256 == 0, K % 128 == 0, K >= 256,
  *   M >= 256, lda >= K, lda % 8 == 0. */
 int mi_op_residual_stats(void* x, const void* delta, float* rs, int32_t rows, int32_t W, void* stream);
+/* mi_op_split6: the split-bf16 operands of the fp32 tower's GEMMs (weight_dtype MI_F32,
+ *   DESIGN.md §4.7).  Each f32 value x = x1 + x2 + x3 + O(2^-24 |x|), x1 = bf16(x),
+ *   x2 = bf16(x - x1), x3 = bf16(x - x1 - x2) (round to nearest even; inf / NaN: x2 = x3 = 0;
+ *   a finite x that rounds past bf16's range takes x1 = the largest bf16 of its sign);
+ *   row r of x [rows][K] (stride ldx floats) becomes out[r] = 6K bf16 in six K-blocks:
+ *   role 0 (activations) [x1 x2 x3 x1 x2 x1], role 1 (weights, [N][K]) [x1 x1 x1 x2 x2 x3].
+ *   mi_op_gemm (epilogue 2 or 3) over K' = 6K then sums a1w1 + a2w1 + a3w1 + a1w2 + a2w2 +
+ *   a1w3 in f32.  gelu 1 applies QuickGELU (x * 1 / (1 + exp(-1.702 x))) first. */
+int mi_op_split6(const float* x, int64_t ldx, int64_t rows, int32_t K, int32_t role, int32_t gelu, void* out,
+                 void* stream);
 int mi_op_gemm_ln(const void* x16, int64_t lda, const float* rs, const void* Wf, const float* colsum,
                   const float* colc, void* out, int32_t M, int32_t N, int32_t K, int32_t gelu, void* stream);
 

@@ -411,3 +411,121 @@ def test_attention_split_last_tile(gpu, monkeypatch, B, S, W):
     assert err < 3e-2 * max(1.0, ref.abs().max().item()), err
     err_b = (b.double() - ref)[~full].abs().max().item()
     assert (a.double() - ref)[~full].abs().max().item() <= 2 * err_b + 2e-3
+
+
+@pytest.mark.parametrize("M,N,K,epi", [(1, 64, 32, 0), (100, 128, 64, 1), (513, 384, 768, 2), (3000, 3072, 768, 1),
+                                       (777, 768, 3072, 2), (50, 512, 768, 3), (20000, 2304, 768, 0)])
+def test_gemm_f32(gpu, M, N, K, epi):
+    """mi_op_gemm_f32 (the fp32 tower's exact-f32 MFMA GEMM) against float64, within f32
+    rounding (1e-5 of max(1, |ref|)); epilogues 0 store, 1 QuickGELU, 2 +=, 3 ReLU."""
+    import torch
+    N_ = _lib()
+    g = torch.Generator(device="cpu").manual_seed(M * 3 + N + K + epi)
+    A = (torch.randn(M, K, generator=g) * 0.5).to(gpu)
+    W = (torch.randn(N, K, generator=g) * K ** -0.5).to(gpu)
+    bias = torch.randn(N, generator=g).to(gpu)
+    base = torch.randn(M, N, generator=g).to(gpu)
+    out = base.clone() if epi == 2 else torch.full((M, N), float("nan"), device=gpu)
+    N_.check(N_.lib().mi_op_gemm_f32(A.data_ptr(), W.data_ptr(), bias.data_ptr(), out.data_ptr(), M, N, K, epi,
+                                     _stream()), "gemm_f32")
+    torch.cuda.synchronize()
+    ref = A.double() @ W.double().t() + bias.double()
+    if epi == 1:
+        ref = ref * torch.sigmoid(1.702 * ref)
+    elif epi == 2:
+        ref = ref + base.double()
+    elif epi == 3:
+        ref = ref.clamp_min(0)
+    err = (out.double() - ref).abs().max().item()
+    assert err < 1e-5 * max(1.0, ref.abs().max().item()), err
+
+
+def _bf16_rne(x):
+    """float32 -> bf16 bits, round to nearest even (NaN stays NaN), as the kernels' f2bf."""
+    u = np.asarray(x, np.float32).view(np.uint32).astype(np.uint64)
+    nan = ((u & 0x7F800000) == 0x7F800000) & ((u & 0x007FFFFF) != 0)
+    r = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16).astype(np.uint16)
+    return np.where(nan, ((u >> 16) | 0x40).astype(np.uint16), r)
+
+
+def _split6_ref(x, role, gelu):
+    x = np.asarray(x, np.float32)
+    if gelu:
+        x = (x * (np.float32(1) / (np.float32(1) + np.exp(np.float32(-1.702) * x)))).astype(np.float32)
+    b2f = lambda h: (h.astype(np.uint32) << 16).view(np.float32)
+    x1 = _bf16_rne(x)
+    fin = np.isfinite(x)
+    x1 = np.where(fin & ((x1 & 0x7FFF) == 0x7F80), (x1 & 0x8000) | 0x7F7F, x1).astype(np.uint16)
+    with np.errstate(invalid="ignore"):
+        r1 = (x - b2f(x1)).astype(np.float32)
+        x2 = np.where(fin, _bf16_rne(r1), 0).astype(np.uint16)
+        x3 = np.where(fin, _bf16_rne((r1 - b2f(x2)).astype(np.float32)), 0).astype(np.uint16)
+    t = (x1, x2, x3)
+    order = (0, 0, 0, 1, 1, 2) if role else (0, 1, 2, 0, 1, 0)
+    return np.concatenate([t[o] for o in order], axis=1)
+
+
+@pytest.mark.parametrize("role,gelu", [(0, 0), (1, 0), (0, 1)])
+def test_split6_bit_exact(gpu, role, gelu):
+    """mi_op_split6 (the fp32 tower's split-bf16 operands) against its numpy restatement, bit
+    for bit, with inf / NaN / subnormal / zero / past-bf16-range (3.4e38) entries; and x1 + x2 + x3 = x to 2^-24 relative
+    (2^-133 absolute below the normal range).
+    (gelu: only the finite-row comparison -- expf and numpy's exp may differ in the last bit.)"""
+    import torch
+    N_ = _lib()
+    rng = np.random.default_rng(7 + role + 2 * gelu)
+    rows, K = 300, 768
+    x = (rng.standard_normal((rows, K)) * np.exp(rng.uniform(-20, 20, (rows, K)))).astype(np.float32)
+    if not gelu:
+        x[0, :8] = [np.inf, -np.inf, np.nan, 0.0, -0.0, 1e-40, -3e-39, 3.4e38]
+    xd = torch.from_numpy(x).to(gpu)
+    out = torch.zeros(rows, 6 * K, dtype=torch.int16, device=gpu)
+    N_.check(N_.lib().mi_op_split6(xd.data_ptr(), K, rows, K, role, gelu, out.data_ptr(), _stream()), "split6")
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(np.uint16)
+    if gelu:
+        xg = torch.from_numpy(x).to(gpu)
+        xg = (xg * (1.0 / (1.0 + torch.exp(-1.702 * xg)))).cpu().numpy()   # the device's value, then split
+        ref = _split6_ref(xg, role, 0)
+        ok = np.isfinite(xg).all(axis=1)
+        close = (got[ok] == ref[ok]).mean()
+        assert close > 0.999, close
+        return
+    ref = _split6_ref(x, role, 0)
+    assert np.array_equal(got, ref)
+    b2f = lambda h: (h.astype(np.uint32) << 16).view(np.float32).astype(np.float64)
+    t = [got[:, j * K:(j + 1) * K] for j in range(6)]
+    x1, x2, x3 = (t[0], t[1], t[2]) if role == 0 else (t[0], t[3], t[5])
+    fin = np.isfinite(x)
+    s = b2f(x1) + b2f(x2) + b2f(x3)
+    err = np.abs(s[fin] - x[fin].astype(np.float64))
+    # relative 2^-24, and the bf16 terms' subnormal spacing (2^-133) for f32-subnormal inputs
+    assert (err <= 2.0 ** -24 * np.abs(x[fin].astype(np.float64)) + 2.0 ** -133).all()
+
+
+@pytest.mark.parametrize("M,N,K,epi", [(513, 384, 768, 3), (3000, 768, 3072, 2), (20000, 2304, 768, 3)])
+def test_split6_gemm_f32_grade(gpu, M, N, K, epi):
+    """The fp32 tower's GEMM as run since round 4: split-bf16 operands (mi_op_split6) and one
+    bf16 GEMM over K' = 6K with an f32 epilogue (mi_op_gemm 3 = store, 2 = +=), against float64
+    within f32-GEMM error (1e-5 of max(1, |ref|), as test_gemm_f32)."""
+    import torch
+    N_ = _lib()
+    g = torch.Generator(device="cpu").manual_seed(M + N + K + epi)
+    A = (torch.randn(M, K, generator=g) * 0.5).to(gpu)
+    W = (torch.randn(N, K, generator=g) * K ** -0.5).to(gpu)
+    bias = torch.randn(N, generator=g).to(gpu)
+    base = torch.randn(M, N, generator=g).to(gpu)
+    A6 = torch.empty(M, 6 * K, dtype=torch.int16, device=gpu)
+    W6 = torch.empty(N, 6 * K, dtype=torch.int16, device=gpu)
+    L = N_.lib()
+    N_.check(L.mi_op_split6(A.data_ptr(), K, M, K, 0, 0, A6.data_ptr(), _stream()), "split6 A")
+    N_.check(L.mi_op_split6(W.data_ptr(), K, N, K, 1, 0, W6.data_ptr(), _stream()), "split6 W")
+    out = base.clone() if epi == 2 else torch.full((M, N), float("nan"), device=gpu)
+    N_.check(L.mi_op_gemm(A6.data_ptr(), W6.data_ptr(), bias.data_ptr(), out.data_ptr(), M, N, 6 * K, epi, _stream()),
+             "gemm")
+    torch.cuda.synchronize()
+    ref = A.double() @ W.double().t() + bias.double()
+    if epi == 2:
+        ref = ref + base.double()
+    err = (out.double() - ref).abs().max().item()
+    assert err < 1e-5 * max(1.0, ref.abs().max().item()), err
