@@ -708,9 +708,12 @@ static int run_tower(mi_clip* c, const std::vector<Layer>& layers, int B, int S,
 // in their epilogues from per-row (rstd, rstd * mean) (gemm_8q.hip EPI_LN_*), so the residual
 // adds only write x16 and the statistics (residual_stats: 6 instead of residual_ln's 8 bytes per
 // element, no h buffer).  MICLIP_LNFOLD=0 keeps run_tower (A/B).
-static int lnfold() {
+// Default: folded for W <= 768 (B/32: 101.9k -> 103.6k frames/s); at W = 1024 (L/14) the folded
+// c_fc / qkv run 10 % / 5 % slower than the plain GEMMs (K = 1024 amortises the plain epilogue
+// better) and the fold did not pay (configs[2] 16.25 -> 16.32 s per step, profiles/r04_v_config2.json)
+static int lnfold(int W) {
   const char* e = ab_getenv("MICLIP_LNFOLD");   // read per call (A/B tests switch it within one process)
-  return e ? atoi(e) != 0 : 1;
+  return e ? atoi(e) != 0 : W <= 768;
 }
 
 static GemmArgs ln_args(mi_clip* c, const uint16_t* wf, const float* sv, const float* cv, void* out, int N, int M,
@@ -902,7 +905,7 @@ int mi_clip_encode_image(mi_clip* c, const void* pixels, int64_t B, int in_dtype
     pg.goffset = 1;
     HIP_TRY(gemm_bf16(pg, EPI_F32, s));
     // LayerNorm-folded tower: bf16 weights folded at create (W % 256 == 0), whole 256-row tiles
-    const bool fold = !c->fp8 && !c->vl.empty() && c->vl[0].lw_qkv && lnfold() && (int64_t)nb * S >= 256;
+    const bool fold = !c->fp8 && !c->vl.empty() && c->vl[0].lw_qkv && lnfold(W) && (int64_t)nb * S >= 256;
     int r;
     if (fold) {
       HIP_TRY(vision_embed_ln16(c->x, c->cls, c->vpos, c->ln_pre_g, c->ln_pre_b, nb, S, W, c->rs, s));
