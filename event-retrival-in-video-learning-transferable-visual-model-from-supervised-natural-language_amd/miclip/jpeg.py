@@ -126,21 +126,35 @@ def _scan_start(buf):
     return None
 
 
+_HEAD_MRU = []   # (header bytes, parsed header) of the most recently seen encoders
+
+
 def parse(buf: bytes) -> JpegHeader:
     """Marker walk up to the first SOS; sets ``supported`` False (with ``why``)
     for anything the device decoder does not restate.  Frames of one encoder
     share their header bytes, so the parsed header is cached by those bytes
     (everything before the entropy-coded data); only the end-of-image check is
-    per file."""
-    ss = _scan_start(buf)
-    if ss is None:
-        return _parse(buf)
-    key = bytes(buf[:ss])
-    h = _HEAD_CACHE.get(key)
+    per file.  A buffer that starts with a recently seen header's bytes IS that
+    header (the bytes end at the scan start), so the marker walk -- 7 us of
+    Python per frame, most of a batch's host time before the first launch -- is
+    skipped for it."""
+    h = None
+    for key, hh in _HEAD_MRU:
+        if buf.startswith(key):
+            h = hh
+            break
     if h is None:
-        if len(_HEAD_CACHE) > 1024:
-            _HEAD_CACHE.clear()
-        h = _HEAD_CACHE[key] = _parse(buf, check_eoi=False)
+        ss = _scan_start(buf)
+        if ss is None:
+            return _parse(buf)
+        key = bytes(buf[:ss])
+        h = _HEAD_CACHE.get(key)
+        if h is None:
+            if len(_HEAD_CACHE) > 1024:
+                _HEAD_CACHE.clear()
+            h = _HEAD_CACHE[key] = _parse(buf, check_eoi=False)
+        _HEAD_MRU.insert(0, (key, h))
+        del _HEAD_MRU[8:]
     if h.supported and buf.rfind(b"\xff\xd9") <= h.scan_start:   # truncated: Pillow raises; let it
         t = JpegHeader()
         for f in JpegHeader.__slots__:
@@ -321,6 +335,15 @@ _STAGE = [None, None]            # two pinned staging buffers (double-buffered u
 _STAGE_EVT = [None, None]        # the last H2D copy out of each
 _STAGE_LOCK = threading.Lock()
 _PAD = np.frombuffer(b"\xff\xd9" * 16, np.uint8)
+
+
+def _bytes_data_off():
+    import ctypes
+    b = bytes(b"jpeg-probe")
+    return ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p).value - id(b)
+
+
+_BYTES_DATA_OFF = _bytes_data_off()
 SUB_FRAMES = 2048                # frames per decode launch: the host gathers launch j + 1 while the GPU decodes j
 FIRST_SUB = 512                  # the first launch of a group: the pipeline's unhidden head
 
@@ -356,12 +379,12 @@ def _upload(bufs, keep, segl, starts, total, dev, slot=0):
             st = torch.empty(max(total + 32, 1 << 26), dtype=torch.uint8, pin_memory=True)
             _STAGE[slot] = st
         n = len(keep)
-        ptrs = np.empty(n, np.uint64)
-        lens = np.empty(n, np.int64)
-        for r in range(n):
-            b = bufs[keep[r]]
-            ptrs[r] = ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p).value + segl[r][0][0]
-            lens[r] = starts[r + 1] - starts[r]
+        # a bytes object's data sits at a fixed offset from its address (CPython), measured once;
+        # any other object type takes the ctypes path
+        ptrs = np.fromiter((id(bufs[i]) + _BYTES_DATA_OFF + sg[0][0] if type(bufs[i]) is bytes
+                            else ctypes.cast(ctypes.c_char_p(bufs[i]), ctypes.c_void_p).value + sg[0][0]
+                            for i, sg in zip(keep, segl)), np.uint64, n)
+        lens = np.diff(np.asarray(starts, np.int64))
         keepalive = [bufs[i] for i in keep]
         N.check(N.lib().mi_host_gather(st.data_ptr(), ptrs.ctypes.data, lens.ctypes.data, n, 16), "mi_host_gather")
         del keepalive
@@ -402,29 +425,40 @@ def launch_args(bufs, heads, keep, segl, key, dedupe=True):
         offs, ends = starts[:-1], starts[1:]
     # table sets deduplicated: frames of one encoder share one set (and one
     # cached header object), which the entropy kernel stages in LDS
-    sets, set_of, hidx = [], {}, np.zeros(B, np.int32)
-    qts, qidx, per_head = [], np.zeros(B, np.int64), {}
-    for r, i in enumerate(keep):
-        h = heads[i]
-        e = per_head.get(id(h))
-        if e is None:
-            slots, tabs = [None] * 4, [None] * 4
-            for (tc, th), (bits, vals) in h.huff.items():
-                if th <= 1:
-                    slots[th * 2 + tc], tabs[th * 2 + tc] = _huff_cached(bits, vals)
-            q4 = np.zeros((4, 64), np.uint16)
-            for tq, q in h.qt.items():
-                if tq <= 3:
-                    q4[tq] = q
-            qts.append(q4)
-            e = per_head[id(h)] = (tuple(slots), tabs, len(qts) - 1)
-        k = e[0] if dedupe else r
-        if k not in set_of:
-            set_of[k] = len(sets)
-            sets.append(e[1])
-        hidx[r] = set_of[k]
-        qidx[r] = e[2]
-    qt = np.ascontiguousarray(np.stack(qts)[qidx])
+    # (per distinct header object, then mapped to the frames: a per-frame Python loop over numpy
+    # scalars cost ~1.4 us a frame before the first launch)
+    hobj = [heads[i] for i in keep]
+    uniq = {}
+    for h in hobj:
+        uniq.setdefault(id(h), h)
+    first_of = list(uniq.values())
+    index_of = {k: u for u, k in enumerate(uniq)}
+    hid = np.fromiter((index_of[id(h)] for h in hobj), np.int64, B)
+    per_head, qts = [], []
+    for h in first_of:
+        slots, tabs = [None] * 4, [None] * 4
+        for (tc, th), (bits, vals) in h.huff.items():
+            if th <= 1:
+                slots[th * 2 + tc], tabs[th * 2 + tc] = _huff_cached(bits, vals)
+        q4 = np.zeros((4, 64), np.uint16)
+        for tq, q in h.qt.items():
+            if tq <= 3:
+                q4[tq] = q
+        qts.append(q4)
+        per_head.append((tuple(slots), tabs))
+    sets, set_of = [], {}
+    if dedupe:
+        hset = np.zeros(len(per_head), np.int32)
+        for u, (slots, tabs) in enumerate(per_head):
+            if slots not in set_of:
+                set_of[slots] = len(sets)
+                sets.append(tabs)
+            hset[u] = set_of[slots]
+        hidx = hset[hid]
+    else:
+        sets = [per_head[u][1] for u in hid]
+        hidx = np.arange(B, dtype=np.int32)
+    qt = np.ascontiguousarray(np.stack(qts)[hid])
     nseg = len(segl[0])
     geom = np.zeros(20, np.int32)
     geom[:5] = (W, H, nc, ri, nseg)
@@ -432,7 +466,7 @@ def launch_args(bufs, heads, keep, segl, key, dedupe=True):
         geom[5 + 2 * c], geom[6 + 2 * c] = (samp[c] if nc == 3 else (1, 1))
         geom[11 + c], geom[14 + c], geom[17 + c] = h0.qsel[c], h0.dcsel[c], h0.acsel[c]
     # per-frame table selectors must agree within the group (they come from the SOS / SOF)
-    if not all(heads[i].qsel == h0.qsel and heads[i].dcsel == h0.dcsel and heads[i].acsel == h0.acsel for i in keep):
+    if not all(h.qsel == h0.qsel and h.dcsel == h0.dcsel and h.acsel == h0.acsel for h in first_of):
         return None
     huff = np.zeros((len(sets), 4), dtype=_HUFF_DT)
     for u, tabs in enumerate(sets):
@@ -480,10 +514,13 @@ def decode_groups(bufs, device="cuda", dedupe=True, heads=None, transform=None):
         from .preprocess import preprocess_frames
         return idx, preprocess_frames(rgb, transform[0], squash=transform[1], out_dtype=transform[2])
 
-    groups = {}
+    groups, gkey = {}, {}
     for i, h in enumerate(heads):
         if h.supported:
-            groups.setdefault(_geom_key(h), []).append(i)
+            k = gkey.get(id(h))
+            if k is None:
+                k = gkey[id(h)] = _geom_key(h)
+            groups.setdefault(k, []).append(i)
         else:
             yield host(i)
     dev = torch.device(device)
