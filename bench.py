@@ -161,26 +161,27 @@ def kernel_timing(model, cfg, chunk, reps=20):
     elif lnfold_active(model, cfg):
         # the product bf16 tower (W % 256 == 0): in_proj / c_fc are the LayerNorm-folded GEMMs
         # (gemm_8q_kernel<EPI_LN_*>, fp16 operands of the half-slot residual stream, lda = 2W),
-        # each residual add is residual_stats (api.cpp run_tower_fold)
+        # out_proj / c_proj add into that stream in their epilogues and store row partial
+        # statistics, then residual_finalize (mi_op_gemm_residual; api.cpp run_tower_fold)
         x16 = (torch.rand(M, 2 * W, device=dev, generator=g) * 2 - 1).half()
+        x16r = x16.clone()            # the fused GEMMs' in-place stream (keeps x16's values bounded)
         Wh = (torch.randn(4 * W, W, device=dev, generator=g) * 0.02).half()
         colsum = Wh.float().sum(1)
         rs = torch.rand(M + 256, 2, device=dev, generator=g) + 0.5
+        rs2 = torch.empty(M, 2, device=dev)
+        ps = torch.empty(M, W // 64, 2, device=dev)
         for name, Nn, K, epi, out in gemms:
             if name in ("gemm_qkv", "gemm_fc"):
                 timed(name, lambda Nn=Nn, epi=epi, out=out: N.check(
                     L.mi_op_gemm_ln(x16.data_ptr(), 2 * W, rs.data_ptr(), Wh.data_ptr(), colsum.data_ptr(),
                                     bias.data_ptr(), out.data_ptr(), M, Nn, W, epi, sp), "gemm_ln"),
                       flops=2.0 * M * Nn * W)
-            else:
-                timed(name, lambda Nn=Nn, K=K, epi=epi, out=out: N.check(
-                    L.mi_op_gemm(A.data_ptr(), Wt.data_ptr(), bias.data_ptr(), out.data_ptr(), M, Nn, K, epi, sp),
-                    "gemm"), flops=2.0 * M * Nn * K)
-        dl = torch.randn(M, W, device=dev, generator=g).bfloat16()
-        timed("residual_stats", lambda: N.check(L.mi_op_residual_stats(x16.data_ptr(), dl.data_ptr(), rs.data_ptr(),
-                                                                        M, W, sp), "residual_stats"),
-              nbytes=M * W * 6 + M * 8)
-        del x16, Wh, colsum, rs, dl
+            else:   # the residual add fused: x16 read + written, partials, then residual_finalize
+                timed(name, lambda K=K: N.check(
+                    L.mi_op_gemm_residual(x16r.data_ptr(), 2 * W, A.data_ptr(), K, Wt.data_ptr(), bias.data_ptr(),
+                                          ps.data_ptr(), rs2.data_ptr(), M, W, K, sp), "gemm_residual"),
+                      flops=2.0 * M * W * K)
+        del x16, x16r, Wh, colsum, rs, rs2, ps
     else:
         for name, Nn, K, epi, out in gemms:
             timed(name, lambda Nn=Nn, K=K, epi=epi, out=out: N.check(

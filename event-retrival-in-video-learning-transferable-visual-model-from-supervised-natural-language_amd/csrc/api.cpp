@@ -725,20 +725,51 @@ static GemmArgs ln_args(mi_clip* c, const uint16_t* wf, const float* sv, const f
   return g;
 }
 
+// Residual add fused into out_proj / c_proj (gemm_8q EPI_RES16_BF16): the GEMM epilogue adds its
+// bf16 output into x16 in place and stores per-row partial statistics of each 64 columns; the
+// tiny residual_finalize pass turns them into rs.  The GEMM reads and writes x16 (4 B per
+// element) instead of writing delta and residual_stats re-reading it (8 B).  The partials live
+// in the h buffer, which the folded tower does not otherwise use.  MICLIP_RESFUSE=0 keeps the
+// separate residual_stats pass (A/B).
+static int resfuse() {
+  const char* e = ab_getenv("MICLIP_RESFUSE");   // read per call (A/B tests switch it within one process)
+  return e ? atoi(e) != 0 : 1;
+}
+
+// out_proj / c_proj with the residual add fused: x16 += bf16(A W^T + b), partials into c->h
+static int gemm_residual(mi_clip* c, const uint16_t* A, int64_t lda, const uint16_t* w, const float* b, int M, int W,
+                         int K, hipStream_t s) {
+  GemmArgs g = gargs(A, lda, w, K, b, c->x, 2 * W, M, W, K);
+  g.ps = (float*)c->h;
+  HIP_TRY(gemm_bf16(g, EPI_RES16_BF16, s));
+  HIP_TRY(residual_finalize((const float*)c->h, c->rs, M, W, s));
+  return MI_OK;
+}
+
 // x16 / rs hold the embedding output and ln_1's statistics (vision_embed_ln16).  On return x16
 // + delta is the final residual stream (the last c_proj output stays in delta, as run_tower).
 static int run_tower_fold(mi_clip* c, const std::vector<Layer>& layers, int B, int S, int W, hipStream_t s) {
   const int M = B * S;
+  const bool fuse = resfuse() && !gemm_variant_for(GV_OUT) && !gemm_variant_for(GV_PROJ) && !gemm_variant();
   for (size_t l = 0; l < layers.size(); ++l) {
     const Layer& L = layers[l];
+    const bool last = l + 1 == layers.size();
     HIP_TRY(gemm_bf16(ln_args(c, L.lw_qkv, L.ls_qkv, L.lc_qkv, c->qkv, 3 * W, M, W), EPI_LN_BF16, s));
     HIP_TRY(attention(c->qkv, c->att, B, S, W, 0, s));
-    HIP_TRY(gemm_bf16(with_variant(gargs(c->att, W, L.w_out, W, L.b_out, c->delta, W, M, W, W), GV_OUT), EPI_BF16, s));
-    HIP_TRY(residual_stats(c->x, c->delta, c->rs, M, W, s));
+    if (fuse) {
+      MI_TRY(gemm_residual(c, c->att, W, L.w_out, L.b_out, M, W, W, s));
+    } else {
+      HIP_TRY(gemm_bf16(with_variant(gargs(c->att, W, L.w_out, W, L.b_out, c->delta, W, M, W, W), GV_OUT), EPI_BF16, s));
+      HIP_TRY(residual_stats(c->x, c->delta, c->rs, M, W, s));
+    }
     HIP_TRY(gemm_bf16(ln_args(c, L.lw_fc, L.ls_fc, L.lc_fc, c->mlp, 4 * W, M, W), EPI_LN_GELU_BF16, s));
-    HIP_TRY(gemm_bf16(with_variant(gargs(c->mlp, 4 * W, L.w_proj, 4 * W, L.b_proj, c->delta, W, M, W, 4 * W), GV_PROJ),
-                      EPI_BF16, s));
-    if (l + 1 < layers.size()) HIP_TRY(residual_stats(c->x, c->delta, c->rs, M, W, s));
+    if (fuse && !last) {
+      MI_TRY(gemm_residual(c, c->mlp, 4 * W, L.w_proj, L.b_proj, M, W, 4 * W, s));
+    } else {
+      HIP_TRY(gemm_bf16(with_variant(gargs(c->mlp, 4 * W, L.w_proj, 4 * W, L.b_proj, c->delta, W, M, W, 4 * W), GV_PROJ),
+                        EPI_BF16, s));
+      if (!last) HIP_TRY(residual_stats(c->x, c->delta, c->rs, M, W, s));
+    }
   }
   return MI_OK;
 }
@@ -1162,6 +1193,20 @@ int mi_op_gemm_ln(const void* x16, int64_t lda, const float* rs, const void* wf,
     return fail(MI_ERR_UNSUPPORTED, "mi_op_gemm_ln: needs N %% 256 == 0, K %% 128 == 0, K >= 256, M >= 256, "
                                     "lda >= K with lda %% 8 == 0");
   HIP_TRY(gemm_bf16(g, gelu ? EPI_LN_GELU_BF16 : EPI_LN_BF16, (hipStream_t)stream));
+  return MI_OK;
+}
+
+int mi_op_gemm_residual(void* x16, int64_t ldx, const void* A, int64_t lda, const void* w, const float* bias,
+                        float* ps, float* rs, int32_t M, int32_t W, int32_t K, void* stream) {
+  if (!x16 || !A || !w || !ps || !rs || M < 0) return fail(MI_ERR_ARG, "mi_op_gemm_residual: bad arguments");
+  if (M == 0) return MI_OK;
+  GemmArgs g = gargs((const uint16_t*)A, lda, (const uint16_t*)w, K, bias, x16, ldx, M, W, K);
+  g.ps = ps;
+  if (lda < K || lda % 8 || ldx < W || ldx % 8 || W > 1024 || ((uintptr_t)x16 & 15) || !gemm_8q_ok(g))
+    return fail(MI_ERR_UNSUPPORTED, "mi_op_gemm_residual: needs W %% 256 == 0, W <= 1024, K %% 128 == 0, K >= 256, "
+                                    "M >= 256, lda >= K and ldx >= W multiples of 8, x16 16-byte aligned");
+  HIP_TRY(gemm_bf16(g, EPI_RES16_BF16, (hipStream_t)stream));
+  HIP_TRY(residual_finalize(ps, rs, M, W, (hipStream_t)stream));
   return MI_OK;
 }
 

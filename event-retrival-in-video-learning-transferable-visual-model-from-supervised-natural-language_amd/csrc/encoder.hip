@@ -297,6 +297,42 @@ __global__ __launch_bounds__(256) void residual_stats_kernel(float* __restrict__
   store_row_stats(r, n4, lane, W, rs, row);
 }
 
+// rs[r] from the W / 64 partials (sum_j, M2_j) that gemm_8q's EPI_RES16 epilogue stored for row r
+// (each over 64 stored fp16 values): mean = sum / W, M2 = sum_j M2_j + 64 (mean_j - mean)^2
+// (Chan et al.'s pairwise update for equal-count groups), var = M2 / W — the two-pass
+// statistics of residual_stats_kernel up to f32 rounding.  One thread per row; W <= 1024.
+__global__ __launch_bounds__(256) void residual_finalize_kernel(const float* __restrict__ ps, float* __restrict__ rs,
+                                                                int rows, int W) {
+  const int row = blockIdx.x * 256 + threadIdx.x;
+  if (row >= rows) return;
+  const int np = W >> 6;
+  const float4* p4 = (const float4*)(ps + (int64_t)row * np * 2);
+  float s[16], m2[16];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+    if (2 * i < np) {
+      const float4 v = p4[i];
+      s[2 * i] = v.x;
+      m2[2 * i] = v.y;
+      s[2 * i + 1] = v.z;
+      m2[2 * i + 1] = v.w;
+    }
+  float tot = 0.f;
+#pragma unroll
+  for (int j = 0; j < 16; ++j)
+    if (j < np) tot += s[j];
+  const float mean = tot / (float)W;
+  float acc = 0.f;
+#pragma unroll
+  for (int j = 0; j < 16; ++j)
+    if (j < np) {
+      const float dm = s[j] * (1.0f / 64.0f) - mean;
+      acc += m2[j] + 64.0f * dm * dm;
+    }
+  const float rstd = 1.0f / sqrtf(acc / (float)W + LN_EPS);
+  *(float2*)(rs + 2 * (int64_t)row) = make_float2(rstd, rstd * mean);
+}
+
 __global__ __launch_bounds__(256) void text_embed_kernel(const int32_t* __restrict__ tokens,
                                                          const float* __restrict__ tok_emb,
                                                          const float* __restrict__ pos, float* __restrict__ x,
@@ -486,6 +522,13 @@ hipError_t residual_stats(float* x, const uint16_t* delta, float* rs, int rows, 
   if (W % 4 || W > 1024) return hipErrorInvalidValue;
   if (rows <= 0) return hipSuccess;
   hipLaunchKernelGGL(residual_stats_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, x, delta, rs, rows, W);
+  return hipGetLastError();
+}
+
+hipError_t residual_finalize(const float* ps, float* rs, int rows, int W, hipStream_t s) {
+  if (W % 128 || W > 1024 || W <= 0) return hipErrorInvalidValue;   // pairs of partials per float4 read
+  if (rows <= 0) return hipSuccess;
+  hipLaunchKernelGGL(residual_finalize_kernel, dim3((rows + 255) / 256), dim3(256), 0, s, ps, rs, rows, W);
   return hipGetLastError();
 }
 

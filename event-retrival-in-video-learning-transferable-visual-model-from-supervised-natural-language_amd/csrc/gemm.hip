@@ -1100,6 +1100,7 @@ hipError_t gemm_bf16(const GemmArgs& a, int epi, hipStream_t s) {
     case EPI_F32: return launch<EPI_F32>(a, s);
     case EPI_LN_BF16:
     case EPI_LN_GELU_BF16:   // LayerNorm-folded vision tower: the 8-phase kernel only
+    case EPI_RES16_BF16:
       if (!gemm_8q_ok(a) || a.variant != 0) return hipErrorInvalidValue;
       return gemm_8q(a, epi, s, cu_count(), 0);
     default: return hipErrorInvalidValue;

@@ -68,6 +68,7 @@ constexpr int H_A0 = 0, H_B0 = 1, H_B1 = 2, H_A1 = 3;
 // flags
 constexpr int F_GLDS = 1;   // flat global_load_lds with per-DMA address math (gemm_8p's) instead of descriptors
 constexpr int F_FULL = 2;   // epilogue stores of 8 whole 128-B rows (lane pairs fr, fr ^ 8 swap halves by DPP)
+constexpr int F_VOREC = 4;  // epilogue store offsets recomputed from the lane id (EPI_RES16 always)
 
 __device__ __forceinline__ f32x2 quick_gelu2_8q(f32x2 v) {
   const f32x2 t = v * (f32x2){-2.45546696f, -2.45546696f};   // -1.702 * log2(e)
@@ -109,6 +110,7 @@ template <int EPI>
 struct EpiKind8q {
   static constexpr bool LN = EPI == EPI_LN_BF16 || EPI == EPI_LN_GELU_BF16;   // LayerNorm folded in (fp16 operands)
   static constexpr bool GELU = EPI == EPI_GELU_BF16 || EPI == EPI_LN_GELU_BF16;
+  static constexpr bool RES = EPI == EPI_RES16_BF16;   // residual add + row partial statistics fused
   // LDS: 2 K-tile buffers, bias [2][BN]; LN: + row statistics [2][BM][2] + column sums [2][BN]
   static constexpr int LDS = 2 * BUF + 2 * BN * 4 + (LN ? 2 * BM * 8 + 2 * BN * 4 : 0);
 };
@@ -274,7 +276,49 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
   // row fr + 8 for store 2; lane (fr >= 8) takes the p = 1 piece of row fr - 8 for store 1
   const uint32_t voF = (uint32_t)(((wr * 128 + (fr & 7)) * a.ldo + wc * 64 + 8 * ((g & 1) * 2 + (g >> 1)) + 32 * (fr >> 3)) * 2);
   const uint32_t rows8 = (uint32_t)(8 * a.ldo * 2);
-  auto epilogue = [&]() {
+  auto out_rsrc = [&]() {
+    const int rows = min(a.M - pm0, BM);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)((uint16_t*)a.out + (int64_t)pm0 * a.ldo + pn0), (short)0,
+                                             rows * (int)a.ldo * 2, 0x00020000);
+  };
+  // EPI_RES16: the previous tile's x16 blocks (the 16-byte pieces its stores overwrite), four
+  // 16-row blocks in flight.  Blocks 0-3 are loaded at the head of the next tile's phase 1,
+  // AHEAD of that phase's DMAs, so waiting for them needs only DMAs issued a phase earlier (and
+  // the registers are the fragment registers, dead until phase 1's reads); block mi + 4 goes out
+  // as block mi is consumed.  Rows past M read zeros (descriptor range) and are not stored.
+  typedef _Float16 h2_8q __attribute__((ext_vector_type(2)));
+  u32x4_8q xin[4][2];
+  // lane id from an opaque asm, so offsets derived from it are computed where used (the 16
+  // store offsets voO + mi * blkO, derived from a kernel-scope constant, are otherwise hoisted
+  // out of the tile loop and held in 16 VGPRs for the kernel's life)
+  auto lane_id = [&]() {
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+  };
+  auto vo_out = [&](int l) {
+    return (uint32_t)(((wr * 128 + (l & 15)) * a.ldo + wc * 64 + ((l >> 4) & 1) * 16 + (l >> 5) * 8) * 2);
+  };
+  auto res_load = [&](const __amdgpu_buffer_rsrc_t& r, uint32_t vo, int mi) {
+    xin[mi & 3][0] = __builtin_bit_cast(u32x4_8q, __builtin_amdgcn_raw_buffer_load_b128(r, vo + mi * blkO, 0, 0));
+    xin[mi & 3][1] = __builtin_bit_cast(u32x4_8q, __builtin_amdgcn_raw_buffer_load_b128(r, vo + mi * blkO + 64, 0, 0));
+  };
+  auto res_prefetch = [&]() {
+    if (!EK::RES) return;
+    const __amdgpu_buffer_rsrc_t r = out_rsrc();
+    const uint32_t vo = vo_out(lane_id());
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) res_load(r, vo, mi);
+  };
+  // sum across the four lanes (fr + 16 g) that hold one row's 64 columns: every lane gets the
+  // same value (each level adds one commutative pair)
+  auto row_sum4 = [](float x) {
+    const auto a2 = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    x = __uint_as_float(a2[0]) + __uint_as_float(a2[1]);
+    const auto b2 = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return __uint_as_float(b2[0]) + __uint_as_float(b2[1]);
+  };
+  auto epilogue = [&]() __attribute__((always_inline)) {
     if (ABL == 4) {
 #pragma unroll
       for (int mi = 0; mi < 8; ++mi)
@@ -298,8 +342,11 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
     float4 col[4];
     // lane offsets recomputed here (a lane constant kept from kernel entry is spilled around the
     // tile loop, and its reload's vmcnt(0) would drain the DMAs in flight)
+    constexpr bool VOREC = EK::RES || (F & F_VOREC);
     int ln_ = 0;
-    if (EK::LN) asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln_));
+    if (EK::LN || VOREC) asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln_));
+    uint32_t vo = voO;
+    if constexpr (VOREC) vo = vo_out(ln_);
     // (asm LDS reads: a compiler-visible LDS read waits vmcnt(0) for the LDS-DMAs in flight)
     const uint32_t rab_a = (uint32_t)(uintptr_t)(const LDS_AS float*)(srs + ppar * BM * 2 + (wr * 128 + (ln_ & 15)) * 2);
     f32x2 rab_c = (f32x2){0.f, 0.f}, rab_n = (f32x2){0.f, 0.f};
@@ -310,9 +357,18 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
                    : "=&v"(col[0]), "=&v"(col[1]), "=&v"(col[2]), "=&v"(col[3]) : "v"(ca) : "memory");
       asm volatile("ds_read_b64 %0, %1" : "=v"(rab_c) : "v"(rab_a) : "memory");
     }
-    const int rows = min(a.M - pm0, BM);
-    const __amdgpu_buffer_rsrc_t rsO = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)((uint16_t*)a.out + (int64_t)pm0 * a.ldo + pn0), (short)0, rows * (int)a.ldo * 2, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsO = out_rsrc();
+    // EPI_RES16 partials: ps row stride pstr bytes, the wave's 64 columns at entry pn0 / 64 + wc;
+    // lanes g != 0 hold copies of their row's partial and store out of range (dropped)
+    const int pstr = (a.N / 64) * 8;
+    __amdgpu_buffer_rsrc_t rsP;
+    uint32_t voP = 0;
+    if (EK::RES) {
+      const int rows = min(a.M - pm0, BM);
+      rsP = __builtin_amdgcn_make_buffer_rsrc((void*)(a.ps + ((int64_t)pm0 * (a.N / 64) + pn0 / 64) * 2), (short)0,
+                                              (rows - 1) * pstr + 32, 0x00020000);
+      voP = (ln_ >> 4) ? 0x7ff00000u : (uint32_t)((wr * 128 + (ln_ & 15)) * pstr + wc * 8);
+    }
 #pragma unroll
     for (int mi = 0; mi < 8; ++mi) {
       u32x4_8q dp[2];
@@ -344,12 +400,26 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
         }
         const auto sx = __builtin_amdgcn_permlane16_swap(pk[0].x, pk[1].x, false, false);
         const auto sy = __builtin_amdgcn_permlane16_swap(pk[0].y, pk[1].y, false, false);
-        const u32x4_8q d = {sx[0], sy[0], sx[1], sy[1]};
+        u32x4_8q d = {sx[0], sy[0], sx[1], sy[1]};
+        if (EK::RES) {   // x16 = f16(x16 + bf16 delta), as residual_stats_kernel
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const uint32_t dv = d[e];
+            // (vector elements are copied out before __builtin_bit_cast: on an element lvalue,
+            // this hipcc reads element 0 whatever the index)
+            const uint32_t xv = xin[mi & 3][p][e];
+            const h2_8q xh = __builtin_bit_cast(h2_8q, xv);
+            const f32x2 sm = (f32x2){(float)xh.x, (float)xh.y} +
+                             (f32x2){__uint_as_float(dv << 16), __uint_as_float(dv & 0xffff0000u)};
+            const h2_8q oh = {(_Float16)sm.x, (_Float16)sm.y};
+            d[e] = __builtin_bit_cast(uint32_t, oh);
+          }
+        }
         dp[p] = d;
         if (F & F_FULL) continue;
         if (ABL == 10) asm volatile("" ::"v"(d));   // stamp probe without the stores
-        else if (p == 0) __builtin_amdgcn_raw_buffer_store_b128(d, rsO, voO + mi * blkO, 0, 0);
-        else __builtin_amdgcn_raw_buffer_store_b128(d, rsO, voO + mi * blkO + 64, 0, 0);
+        else if (p == 0) __builtin_amdgcn_raw_buffer_store_b128(d, rsO, vo + mi * blkO, 0, 0);
+        else __builtin_amdgcn_raw_buffer_store_b128(d, rsO, vo + mi * blkO + 64, 0, 0);
       }
       if (F & F_FULL) {
         const bool top = fr < 8;
@@ -364,6 +434,29 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
         }
         __builtin_amdgcn_raw_buffer_store_b128(s1, rsO, voF + mi * blkO, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b128(s2, rsO, voF + mi * blkO + rows8, 0, 0);
+      }
+      if (EK::RES) {   // the row's 64-column partial: sum, then squared deviations from its mean
+        // (the stored values re-read from dp in each pass: 16 f32 kept live across the passes spill)
+        auto val = [&](int k) {
+          const uint32_t w = dp[k >> 2][k & 3];
+          const h2_8q h = __builtin_bit_cast(h2_8q, w);
+          return (f32x2){(float)h.x, (float)h.y};
+        };
+        const f32x2 t = ((val(0) + val(1)) + (val(2) + val(3))) + ((val(4) + val(5)) + (val(6) + val(7)));
+        const float s = row_sum4(t.x + t.y);
+        const f32x2 mu = (f32x2){s * (1.0f / 64.0f), s * (1.0f / 64.0f)};
+        f32x2 q = (f32x2){0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const f32x2 dv = val(k) - mu;
+          q = dv * dv + q;
+        }
+        const float m2 = row_sum4(q.x + q.y);
+        typedef unsigned int u32x2_8q __attribute__((ext_vector_type(2)));
+        __builtin_amdgcn_raw_buffer_store_b64((u32x2_8q){__float_as_uint(s), __float_as_uint(m2)}, rsP,
+                                              voP + (uint32_t)(mi * 16 * pstr), 0, 0);
+        if (mi + 4 < 8) res_load(rsO, vo, mi + 4);
+        __builtin_amdgcn_sched_barrier(0);
       }
       rab_c = rab_n;
     }
@@ -380,7 +473,7 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
       stamp(0);   // S0: tile start
       if ((ABL == 9 || ABL == 10) && ti == 2) st[7] = __builtin_amdgcn_s_memrealtime();
     }
-    if (P == 1) {
+    if (P == 1 && !(EK::RES && FIRST)) {
       issue(H_A1, 1);
       // a tile's first pair restages the odd B_n0 here too, ahead of the
       // previous tile's stores: the last pair did not re-read it in phase 8
@@ -393,6 +486,23 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
         __builtin_amdgcn_sched_barrier(0);
       }
       if (FIRST) stamp(1);   // S1: epilogue issued
+    }
+    if (P == 1 && EK::RES && FIRST) {
+      if (has_prev) {
+        // the previous tile's x16 blocks 0-3 ahead of the phase's DMAs (one conditional block
+        // from the loads to the epilogue: split across two, the loads' registers spilled)
+        res_prefetch();
+        __builtin_amdgcn_sched_barrier(0);
+        issue(H_A1, 1);
+        issue(H_B0, 1);
+        __builtin_amdgcn_sched_barrier(0);
+        epilogue();
+        __builtin_amdgcn_sched_barrier(0);
+      } else {
+        issue(H_A1, 1);
+        issue(H_B0, 1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
     if (q == 0) {
       read_a(rbuf + H_A0 * HALF);
@@ -417,7 +527,10 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
     // first pair the previous tile's 16 epilogue stores are younger as well
     // (they then have until phase 8 to complete)
     if (P == 4) {
-      if (FIRST && has_prev && ABL != 10) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+      // (EPI_RES16: 16 stores, 8 partial stores and the x16 loads of blocks 4-7 are younger;
+      // the epilogue's wait for block 7 already retired the odd buffer)
+      if (FIRST && has_prev && EK::RES) asm volatile("s_waitcnt vmcnt(36)" ::: "memory");
+      else if (FIRST && has_prev && ABL != 10) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
       if (FIRST) stamp(3);   // S3: first pair's phase-4 wait passed
     }
@@ -514,6 +627,7 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
   }
   // the last tile's epilogue
   if (wr == 0) barrier();   // the M-groups' barrier counts meet
+  res_prefetch();
   epilogue();
   if ((ABL == 9 || ABL == 10) && lane == 0 && (wave & 3) == 0 && blockIdx.x < 1024) {
 #pragma unroll
@@ -566,6 +680,11 @@ hipError_t gemm_8q(const GemmArgs& a0, int epi, hipStream_t s, int cus, int mode
     return hipGetLastError();
   }
   if (a.a_f16) return hipErrorInvalidValue;
+  if (epi == EPI_RES16_BF16) {   // fused residual add: out = x16 (fp16), ps = row partial statistics
+    if (!a.ps || mode || a.N % 64 || (a.ldo % 8)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((gemm_8q_kernel<EPI_RES16_BF16, 0, 0>), dim3(grid), dim3(512), 0, s, a);
+    return hipGetLastError();
+  }
 #define L8Q(E, ABL_, F_) hipLaunchKernelGGL((gemm_8q_kernel<E, ABL_, F_>), dim3(grid), dim3(512), 0, s, a)
 #if MICLIP_AB   // ablation / stamp probes: A/B build only
 #define L8Q_ALL(E)                   \

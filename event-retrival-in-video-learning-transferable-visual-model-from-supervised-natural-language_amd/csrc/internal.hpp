@@ -20,7 +20,12 @@ enum GemmEpi {
   // W' = f16(W * gamma)): out bf16 = rstd_r * acc + (c_n - rstd_r * mean_r * s_n), c_n = bias
   // (= b + W beta), s_n = colv[n] (= sum_k W'[n][k]), (rstd_r, rstd_r * mean_r) = rs[r]
   EPI_LN_BF16 = 6,
-  EPI_LN_GELU_BF16 = 7     // the same, then QuickGELU
+  EPI_LN_GELU_BF16 = 7,    // the same, then QuickGELU
+  // residual add fused (gemm_8q.hip, bf16 operands): out is the fp16 residual stream x16 (row
+  // stride ldo), x16 = f16(x16 + bf16(acc + bias)) — residual_stats' arithmetic — and ps[r][n / 64]
+  // = (sum, sum of squared deviations from that sum's mean) of the 64 stored values of row r,
+  // columns n .. n + 63; residual_finalize turns a row's N / 64 partials into rs
+  EPI_RES16_BF16 = 8
 };
 
 // MX block quantisation shared by the fp8 producers (gemm_mx.hip, encoder.hip):
@@ -72,6 +77,7 @@ struct GemmArgs {
   int a_f16 = 0;
   const float* rs = nullptr;     // [M + 256][2] (rstd, rstd * mean) per row
   const float* colv = nullptr;   // [N] s_n
+  float* ps = nullptr;           // EPI_RES16_BF16: [M][N / 64][2] row partial statistics
 };
 
 // Requirements: K % 64 == 0, N % 128 == 0, A/W 16-byte aligned rows.
@@ -132,6 +138,9 @@ hipError_t vision_embed_ln16(float* x, const float* cls, const float* pos, const
 // stored fp16 values: the residual add of residual_ln without its LayerNorm output (the
 // consumer GEMM applies the LayerNorm in its epilogue, EPI_LN_*)
 hipError_t residual_stats(float* x, const uint16_t* delta, float* rs, int rows, int W, hipStream_t s);
+// rs[r] = (rstd, rstd * mean) from the W / 64 partials ps[r][j] = (sum, M2) of EPI_RES16_BF16
+// (Chan's pairwise combination of equal-count groups), W % 128 == 0, W <= 1024
+hipError_t residual_finalize(const float* ps, float* rs, int rows, int W, hipStream_t s);
 // x[q*S + t] = tok_emb[tokens[q*S + t]] + pos[t]
 hipError_t text_embed(const int32_t* tokens, const float* tok_emb, const float* pos, float* x,
                       int Q, int S, int W, int vocab, hipStream_t s);

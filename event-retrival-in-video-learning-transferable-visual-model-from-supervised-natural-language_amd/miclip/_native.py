@@ -33,7 +33,7 @@ EXPORTS = (
     "mi_clip_reserve", "mi_clip_encode_image", "mi_clip_encode_text", "mi_rank_workspace_bytes",
     "mi_rank_topk", "mi_rank_merge", "mi_score_matrix", "mi_rank_of_targets",
     "mi_op_gemm", "mi_op_gemm_f32", "mi_op_layernorm", "mi_op_attention", "mi_op_residual_ln",
-    "mi_op_residual_stats", "mi_op_gemm_ln", "mi_op_split6",
+    "mi_op_residual_stats", "mi_op_gemm_ln", "mi_op_gemm_residual", "mi_op_split6",
     "mi_resample_coeffs", "mi_preprocess_workspace_bytes", "mi_preprocess_frames",
     "mi_jpeg_workspace_bytes", "mi_jpeg_decode", "mi_host_gather",
     "mi_op_quantize_mx", "mi_op_gemm_mx",
@@ -126,6 +126,7 @@ def _bind(path):
         "mi_op_residual_ln": (ctypes.c_int, [P, P, P, P, P, I32, I32, I32, P]),
         "mi_op_residual_stats": (ctypes.c_int, [P, P, P, I32, I32, P]),
         "mi_op_gemm_ln": (ctypes.c_int, [P, I64, P, P, P, P, P, I32, I32, I32, I32, P]),
+        "mi_op_gemm_residual": (ctypes.c_int, [P, I64, P, I64, P, P, P, P, I32, I32, I32, P]),
         "mi_op_split6": (ctypes.c_int, [P, I64, I64, I32, I32, I32, P, P]),
         "mi_op_quantize_mx": (ctypes.c_int, [P, P, P, I32, I32, P]),
         "mi_op_gemm_mx": (ctypes.c_int, [P, P, P, P, P, P, I32, I32, I32, I32, P]),

@@ -332,6 +332,17 @@ int mi_op_split6(const float* x, int64_t ldx, int64_t rows, int32_t K, int32_t r
                  void* stream);
 int mi_op_gemm_ln(const void* x16, int64_t lda, const float* rs, const void* Wf, const float* colsum,
                   const float* colc, void* out, int32_t M, int32_t N, int32_t K, int32_t gelu, void* stream);
+/* mi_op_gemm_residual: attn.out_proj / mlp.c_proj with the residual add fused (replaces
+ *   mi_gemm + mi_op_residual_stats in the folded tower):
+ *   x16 [M][W] fp16 (row stride ldx elements) = f16(x16 + bf16(A . W^T + bias)) — exactly
+ *   mi_op_residual_stats' stored values — and rs [M][2] = (rstd, rstd * mean) of the stored
+ *   rows, combined from per-64-column partials (sum, sum of squared deviations) that the GEMM
+ *   epilogue writes to ps [M][W / 64][2] f32 (scratch).  A [M][K] bf16 (stride lda), W [W][K]
+ *   bf16, bias [W] f32 or NULL.  W % 256 == 0, W <= 1024, K % 128 == 0, K >= 256, M >= 256,
+ *   lda >= K, ldx >= W, both multiples of 8, x16 16-byte aligned.  Replaces
+ *   openai/CLIP model.py ResidualAttentionBlock's "x = x + attn(...)" / "x = x + mlp(...)". */
+int mi_op_gemm_residual(void* x16, int64_t ldx, const void* A, int64_t lda, const void* W, const float* bias,
+                        float* ps, float* rs, int32_t M, int32_t Wd, int32_t K, void* stream);
 
 /* MX-fp8 operator entry points (the "fp8 MFMA weights" configuration,
  * BASELINE.json configs[4]; OCP e4m3 elements with one e8m0 scale per 64

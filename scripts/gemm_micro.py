@@ -42,6 +42,11 @@ SHAPES = {
     "lnfc500": (500000, 3072, 768, 7),
     "lnqkv250": (250000, 2304, 768, 6),
     "lnfc250": (250000, 3072, 768, 7),
+    # residual add fused into out_proj / c_proj (epi 8, mi_op_gemm_residual: x16 half-slot stream
+    # read + written in the epilogue, row partials, residual_finalize); variant 1 = the unfused
+    # pair it replaces (mi_op_gemm bf16 out, then mi_op_residual_stats)
+    "resout500": (500000, 768, 768, 8),
+    "resproj500": (500000, 768, 3072, 8),
     # K sweep at the fc shape (per-tile fixed cost = intercept)
     "fcK384": (100000, 3072, 384, 0),
     "fcK768": (100000, 3072, 768, 0),
@@ -72,14 +77,30 @@ def main():
             A, W = A.bfloat16().float(), W.bfloat16().float()
         A, W = A.to(dt), W.to(dt)
         bias = torch.rand(Nn, device=dev, generator=g)
-        variants = [0] if ln else all_variants
+        res = epi == 8
+        variants = [0] if ln else ([0, 1] if res else all_variants)
+        if res:
+            x16 = (torch.rand(M, 2 * Nn, device=dev, generator=g) * 2 - 1).half()
+            ps = torch.empty(M, Nn // 64, 2, device=dev)
+            rs2 = torch.empty(M, 2, device=dev)
         if ln:
             colsum = W.float().sum(1)
             rs = torch.rand(M + 256, 2, device=dev, generator=g) + 0.5
-        outs = {v: torch.zeros(M, Nn, device=dev, dtype=torch.bfloat16 if epi in (0, 1, 6, 7) else torch.float32)
+        outs = {v: torch.zeros(M, Nn, device=dev, dtype=torch.bfloat16 if epi in (0, 1, 6, 7, 8) else torch.float32)
                 for v in variants}
 
         def run(v):
+            if res:   # (x16 grows by the GEMM output each call: timing only, outputs not compared)
+                if v == 0:
+                    N.check(L.mi_op_gemm_residual(x16.data_ptr(), 2 * Nn, A.data_ptr(), K, W.data_ptr(),
+                                                  bias.data_ptr(), ps.data_ptr(), rs2.data_ptr(), M, Nn, K, sp),
+                            "gemm_residual")
+                else:
+                    N.check(L.mi_op_gemm(A.data_ptr(), W.data_ptr(), bias.data_ptr(), outs[v].data_ptr(), M, Nn, K,
+                                         0, sp), "gemm")
+                    N.check(L.mi_op_residual_stats(x16.data_ptr(), outs[v].data_ptr(), rs2.data_ptr(), M, Nn, sp),
+                            "residual_stats")
+                return
             if ln:
                 N.check(L.mi_op_gemm_ln(A.data_ptr(), 2 * K, rs.data_ptr(), W.data_ptr(), colsum.data_ptr(),
                                         bias.data_ptr(), outs[v].data_ptr(), M, Nn, K, epi - 6, sp), "gemm_ln")

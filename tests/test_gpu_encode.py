@@ -229,6 +229,14 @@ def test_lnfold_tower_matches_oracle(gpu, monkeypatch, name, n):
     monkeypatch.setenv("MICLIP_LNFOLD", "1")           # folded at every width (the product: W <= 768)
     got = _model(name, gpu, image_chunk=n).encode_image(torch.from_numpy(px)).cpu().numpy()
     c_fold = _check(got, ref, f"{name} folded")
+    # the residual add fused into out_proj / c_proj (the default) against the separate
+    # residual_stats pass: the same stored residual stream, statistics combined from partials
+    monkeypatch.setenv("MICLIP_RESFUSE", "0")
+    got_sep = _model(name, gpu, image_chunk=n).encode_image(torch.from_numpy(px)).cpu().numpy()
+    c_sep = _check(got_sep, ref, f"{name} folded, separate residual_stats")
+    assert cosine(got, got_sep).min() > 1 - 1e-4
+    assert 1 - c_fold <= 1.5 * (1 - c_sep) + 2e-5, (c_fold, c_sep)
+    monkeypatch.delenv("MICLIP_RESFUSE")
     monkeypatch.setenv("MICLIP_LNFOLD", "0")
     got0 = _model(name, gpu, image_chunk=n).encode_image(torch.from_numpy(px)).cpu().numpy()
     c_plain = _check(got0, ref, f"{name} unfolded")

@@ -229,6 +229,61 @@ def test_gemm_ln(gpu, M, N, K, gelu, half_slot):
     assert err < 2e-2 * max(1.0, ref.abs().max().item()), err
 
 
+@pytest.mark.parametrize("M,W,K,half_slot", [(256, 256, 256, True), (1000, 768, 768, True), (777, 768, 3072, True),
+                                             (20000, 768, 768, True), (300, 1024, 4096, False),
+                                             (513, 512, 1024, False)])
+def test_gemm_residual(gpu, M, W, K, half_slot):
+    """mi_op_gemm_residual (out_proj / c_proj with the residual add fused into the epilogue)
+    against the unfused pair it replaces: mi_op_gemm (bf16 out) then mi_op_residual_stats.
+    The stored fp16 residual stream must be bit-identical; rs (combined from per-64-column
+    partials) within 2e-6 relative of the float64 statistics of the stored rows, as
+    test_residual_stats.  Partial last M-tiles, multi-tile persistent walks, K = 4W."""
+    import torch
+    N_ = _lib()
+    g = torch.Generator(device="cpu").manual_seed(M + 3 * W + K)
+    x16 = (torch.randn(M, W, generator=g) * 3 + 1).half()
+    A = (torch.randn(M, K, generator=g) * 0.5).bfloat16()
+    Wt = (torch.randn(W, K, generator=g) * K ** -0.5).bfloat16()
+    bias = torch.randn(W, generator=g).float()
+    Ad, Wd, bd = A.to(gpu), Wt.to(gpu), bias.to(gpu)
+    delta = torch.empty(M, W, dtype=torch.bfloat16, device=gpu)
+    N_.check(N_.lib().mi_op_gemm(Ad.data_ptr(), Wd.data_ptr(), bd.data_ptr(), delta.data_ptr(), M, W, K, 0,
+                                 _stream()), "gemm")
+    xd = _half_slots(x16).to(gpu) if half_slot else x16.to(gpu)
+    ldx = 2 * W if half_slot else W
+    ps = torch.full((M, W // 64, 2), float("nan"), device=gpu)
+    rs = torch.full((M, 2), float("nan"), device=gpu)
+    N_.check(N_.lib().mi_op_gemm_residual(xd.data_ptr(), ldx, Ad.data_ptr(), K, Wd.data_ptr(), bd.data_ptr(),
+                                          ps.data_ptr(), rs.data_ptr(), M, W, K, _stream()), "gemm_residual")
+    torch.cuda.synchronize()
+    s = (x16.float() + delta.cpu().float()).half()
+    got = xd.cpu().view(torch.float16).view(M, 2 * W)[:, :W] if half_slot else xd.cpu()
+    assert torch.equal(got, s)
+    sd = s.double()
+    mean = sd.mean(1)
+    rstd = 1 / torch.sqrt(((sd - mean[:, None]) ** 2).mean(1) + 1e-5)
+    np.testing.assert_allclose(rs[:, 0].cpu().double(), rstd, rtol=2e-6)
+    np.testing.assert_allclose(rs[:, 1].cpu().double(), rstd * mean, rtol=2e-6, atol=2e-6)
+    # the partials themselves: per 64 columns, the sum and the squared deviations from its mean
+    blk = sd.view(M, W // 64, 64)
+    psum = blk.sum(2)
+    pm2 = ((blk - psum[..., None] / 64) ** 2).sum(2)
+    np.testing.assert_allclose(ps[..., 0].cpu().double(), psum, rtol=1e-5, atol=1e-3)
+    np.testing.assert_allclose(ps[..., 1].cpu().double(), pm2, rtol=1e-5, atol=1e-3)
+
+
+def test_gemm_residual_rejects_unsupported_shapes(gpu):
+    import torch
+    N_ = _lib()
+    t = torch.zeros(4096, device=gpu)
+    p = t.data_ptr()
+    # W not a multiple of 256, K not a multiple of 128, M < 256, lda < K, ldx < W, W > 1024
+    for M, W, K, lda, ldx in [(256, 200, 256, 256, 200), (256, 256, 192, 192, 256), (100, 256, 256, 256, 256),
+                              (256, 256, 256, 128, 256), (256, 256, 256, 256, 128), (256, 1280, 256, 256, 1280)]:
+        assert N_.lib().mi_op_gemm_residual(p, ldx, p, lda, p, p, p, p, M, W, K, _stream()) == -3
+    assert N_.lib().mi_op_gemm_residual(0, 256, p, 256, p, p, p, p, 256, 256, 256, _stream()) == -1
+
+
 def test_gemm_ln_rejects_unsupported_shapes(gpu):
     import torch
     N_ = _lib()
