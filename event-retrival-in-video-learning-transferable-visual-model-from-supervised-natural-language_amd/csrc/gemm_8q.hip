@@ -55,6 +55,8 @@
 //    not a chip-wide write burst; scripts/gemm_probe8q.py stamps).
 // Result (scripts/gemm_micro.py, M = 500k, interleaved with v98 in one process):
 // fc -4..-7 %, qkv -3..-4 %, proj -6 %, out +-3 %; bit-identical to gemm_8p.
+#include <cstdlib>
+
 #include "common.hpp"
 #include "internal.hpp"
 
@@ -286,6 +288,12 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
   // AHEAD of that phase's DMAs, so waiting for them needs only DMAs issued a phase earlier (and
   // the registers are the fragment registers, dead until phase 1's reads); block mi + 4 goes out
   // as block mi is consumed.  Rows past M read zeros (descriptor range) and are not stored.
+  // Measured alternatives (scripts/gemm_micro.py resout500 / resproj500, profiles/r04_a[cde]_*):
+  // blocks 0-1 loaded three phases earlier, in the tile's last pair (729 vs 724 us), and all
+  // eight blocks ahead of phase 1's DMAs (711 / 1890 vs 724 / 1881 us): no faster, so the x16
+  // loads' ~90 us per launch at M = 500k are not exposed latency.  The statistics, partial
+  // stores and residual_finalize cost ~50 us (probe ABL 11) — against the 380 us residual_stats
+  // pass and the delta write they remove.
   typedef _Float16 h2_8q __attribute__((ext_vector_type(2)));
   u32x4_8q xin[4][2];
   // lane id from an opaque asm, so offsets derived from it are computed where used (the 16
@@ -304,7 +312,7 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
     xin[mi & 3][1] = __builtin_bit_cast(u32x4_8q, __builtin_amdgcn_raw_buffer_load_b128(r, vo + mi * blkO + 64, 0, 0));
   };
   auto res_prefetch = [&]() {
-    if (!EK::RES) return;
+    if (!EK::RES || ABL == 12) return;
     const __amdgpu_buffer_rsrc_t r = out_rsrc();
     const uint32_t vo = vo_out(lane_id());
 #pragma unroll
@@ -407,7 +415,7 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
             const uint32_t dv = d[e];
             // (vector elements are copied out before __builtin_bit_cast: on an element lvalue,
             // this hipcc reads element 0 whatever the index)
-            const uint32_t xv = xin[mi & 3][p][e];
+            const uint32_t xv = ABL == 12 ? 0u : xin[mi & 3][p][e];   // ABL 12: x16 loads ablated
             const h2_8q xh = __builtin_bit_cast(h2_8q, xv);
             const f32x2 sm = (f32x2){(float)xh.x, (float)xh.y} +
                              (f32x2){__uint_as_float(dv << 16), __uint_as_float(dv & 0xffff0000u)};
@@ -435,7 +443,10 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
         __builtin_amdgcn_raw_buffer_store_b128(s1, rsO, voF + mi * blkO, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b128(s2, rsO, voF + mi * blkO + rows8, 0, 0);
       }
-      if (EK::RES) {   // the row's 64-column partial: sum, then squared deviations from its mean
+      if (EK::RES && ABL == 11) {   // timing probe: no statistics, no partial stores
+        if (mi + 4 < 8) res_load(rsO, vo, mi + 4);
+        __builtin_amdgcn_sched_barrier(0);
+      } else if (EK::RES) {   // the row's 64-column partial: sum, then squared deviations from its mean
         // (the stored values re-read from dp in each pass: 16 f32 kept live across the passes spill)
         auto val = [&](int k) {
           const uint32_t w = dp[k >> 2][k & 3];
@@ -455,7 +466,7 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
         typedef unsigned int u32x2_8q __attribute__((ext_vector_type(2)));
         __builtin_amdgcn_raw_buffer_store_b64((u32x2_8q){__float_as_uint(s), __float_as_uint(m2)}, rsP,
                                               voP + (uint32_t)(mi * 16 * pstr), 0, 0);
-        if (mi + 4 < 8) res_load(rsO, vo, mi + 4);
+        if (mi + 4 < 8 && ABL != 12) res_load(rsO, vo, mi + 4);
         __builtin_amdgcn_sched_barrier(0);
       }
       rab_c = rab_n;
@@ -529,7 +540,7 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
     if (P == 4) {
       // (EPI_RES16: 16 stores, 8 partial stores and the x16 loads of blocks 4-7 are younger;
       // the epilogue's wait for block 7 already retired the odd buffer)
-      if (FIRST && has_prev && EK::RES) asm volatile("s_waitcnt vmcnt(36)" ::: "memory");
+      if (FIRST && has_prev && EK::RES) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(ABL == 11 ? 28 : ABL == 12 ? 28 : 36) : "memory");
       else if (FIRST && has_prev && ABL != 10) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
       if (FIRST) stamp(3);   // S3: first pair's phase-4 wait passed
@@ -682,6 +693,13 @@ hipError_t gemm_8q(const GemmArgs& a0, int epi, hipStream_t s, int cus, int mode
   if (a.a_f16) return hipErrorInvalidValue;
   if (epi == EPI_RES16_BF16) {   // fused residual add: out = x16 (fp16), ps = row partial statistics
     if (!a.ps || mode || a.N % 64 || (a.ldo % 8)) return hipErrorInvalidValue;
+#if MICLIP_AB   // timing probes (scripts/gemm_micro.py resout500 / resproj500): 11 no statistics, 12 no x16 loads
+    const char* ab = std::getenv("MICLIP_RES_ABL");
+    const int abl = ab ? std::atoi(ab) : 0;
+    if (abl == 11) hipLaunchKernelGGL((gemm_8q_kernel<EPI_RES16_BF16, 11, 0>), dim3(grid), dim3(512), 0, s, a);
+    else if (abl == 12) hipLaunchKernelGGL((gemm_8q_kernel<EPI_RES16_BF16, 12, 0>), dim3(grid), dim3(512), 0, s, a);
+    else
+#endif
     hipLaunchKernelGGL((gemm_8q_kernel<EPI_RES16_BF16, 0, 0>), dim3(grid), dim3(512), 0, s, a);
     return hipGetLastError();
   }

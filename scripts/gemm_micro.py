@@ -44,7 +44,8 @@ SHAPES = {
     "lnfc250": (250000, 3072, 768, 7),
     # residual add fused into out_proj / c_proj (epi 8, mi_op_gemm_residual: x16 half-slot stream
     # read + written in the epilogue, row partials, residual_finalize); variant 1 = the unfused
-    # pair it replaces (mi_op_gemm bf16 out, then mi_op_residual_stats)
+    # pair it replaces (mi_op_gemm bf16 out, then mi_op_residual_stats); v2 / v3 probes (no
+    # statistics / no x16 loads; A/B build, MICLIP_RES_ABL)
     "resout500": (500000, 768, 768, 8),
     "resproj500": (500000, 768, 3072, 8),
     # K sweep at the fc shape (per-tile fixed cost = intercept)
@@ -78,7 +79,7 @@ def main():
         A, W = A.to(dt), W.to(dt)
         bias = torch.rand(Nn, device=dev, generator=g)
         res = epi == 8
-        variants = [0] if ln else ([0, 1] if res else all_variants)
+        variants = [0] if ln else ([0, 1, 2, 3] if res else all_variants)
         if res:
             x16 = (torch.rand(M, 2 * Nn, device=dev, generator=g) * 2 - 1).half()
             ps = torch.empty(M, Nn // 64, 2, device=dev)
@@ -91,7 +92,9 @@ def main():
 
         def run(v):
             if res:   # (x16 grows by the GEMM output each call: timing only, outputs not compared)
-                if v == 0:
+                # v2 / v3: timing probes of the fused kernel without statistics / without x16 loads
+                os.environ["MICLIP_RES_ABL"] = {2: "11", 3: "12"}.get(v, "0")
+                if v != 1:
                     N.check(L.mi_op_gemm_residual(x16.data_ptr(), 2 * Nn, A.data_ptr(), K, W.data_ptr(),
                                                   bias.data_ptr(), ps.data_ptr(), rs2.data_ptr(), M, Nn, K, sp),
                             "gemm_residual")
