@@ -80,6 +80,8 @@ def main():
         bias = torch.rand(Nn, device=dev, generator=g)
         res = epi == 8
         variants = [0] if ln else ([0, 1, 2, 3] if res else all_variants)
+        if os.environ.get("GEMM_MICRO_V0"):   # PMC passes (scripts/pmc_traffic.py): the product kernel only
+            variants = [0]
         if res:
             x16 = (torch.rand(M, 2 * Nn, device=dev, generator=g) * 2 - 1).half()
             ps = torch.empty(M, Nn // 64, 2, device=dev)

@@ -27,7 +27,9 @@ from gemm_micro import SHAPES  # noqa: E402
 def per_dispatch(path):
     rows = {}
     for r in csv.DictReader(open(path)):
-        if "miclip" not in r["Kernel_Name"]:
+        # the GEMMs only: mi_op_gemm_residual's residual_finalize pass (M x W / 8 bytes read,
+        # M x 8 written) is not part of the GEMM launch counted here
+        if "miclip" not in r["Kernel_Name"] or "gemm" not in r["Kernel_Name"]:
             continue
         d = int(r["Dispatch_Id"])
         rows.setdefault(d, [r["Kernel_Name"].split("(")[0], 0.0])
@@ -42,7 +44,7 @@ def mfma_pass(root):
         return None
     per = {}
     for r in csv.DictReader(open(cnt)):
-        if "miclip" not in r["Kernel_Name"]:
+        if "miclip" not in r["Kernel_Name"] or "gemm" not in r["Kernel_Name"]:
             continue
         c = per.setdefault(int(r["Dispatch_Id"]), {})
         c[r["Counter_Name"]] = c.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
@@ -76,6 +78,8 @@ def main():
         alg = 2 * (M * K + N * K + M * N)
         if epi in (6, 7):                 # LayerNorm-folded: + rs (8 B per row) + colsum / colc (8 B per column)
             alg += 8 * M + 8 * N
+        if epi == 8:                      # residual fused: + the x16 read (2 B) + row partials (8 B per 64 columns)
+            alg += 2 * M * N + M * N // 8
         res[name] = {"kernel": fetch[4 * i][0], "shape": [M, N, K], "epilogue": epi,
                      "fetch_bytes": round(fb), "write_bytes": round(wb), "traffic_bytes": round(fb + wb),
                      "algorithmic_bytes": alg, "traffic_over_algorithmic": round((fb + wb) / alg, 3),
