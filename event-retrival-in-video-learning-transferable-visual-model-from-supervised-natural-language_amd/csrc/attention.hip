@@ -158,18 +158,22 @@ __global__ __launch_bounds__(64) void attention_kernel(const uint16_t* __restric
 // NW = blockDim / 64 waves (8, or 4 for the single-slot S <= 64 instance);
 // PP = 16-byte staging pieces of K (and of V) per thread per chunk (1 for 8
 // waves, 2 for 4).
-template <int NT, int PP, int SLOTS = 2>
-__global__ __launch_bounds__(512) void attention_flash_kernel(const uint16_t* __restrict__ qkv,
-                                                                uint16_t* __restrict__ out, int S, int W, int H,
-                                                                int causal, uint8_t* __restrict__ q8,
-                                                                uint8_t* __restrict__ qs, int64_t rows_pad) {
+// HP heads per workgroup (A/B: 2 = adjacent heads of one sequence, their 128-byte row segments
+// read together as 256 bytes), each on its own NW waves and LDS slots.
+template <int NT, int PP, int SLOTS, int HP = 1>
+__device__ __forceinline__ void attention_flash_body(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ out,
+                                                     int S, int W, int H, int causal, uint8_t* __restrict__ q8,
+                                                     uint8_t* __restrict__ qs, int64_t rows_pad) {
   constexpr int KS = 72, VS = 68;  // LDS row strides (bf16)
-  const int NW = PP == 1 ? 8 : (int)(blockDim.x >> 6);  // PP = 1 is launched with 8 waves
-  __shared__ __attribute__((aligned(16))) uint16_t Ks[SLOTS][64 * KS];
-  __shared__ __attribute__((aligned(16))) uint16_t Vs[SLOTS][64 * VS];
+  const int NW = PP == 1 ? 8 : (int)(blockDim.x >> 6) / HP;  // PP = 1 is launched with 8 waves
+  __shared__ __attribute__((aligned(16))) uint16_t Ksh[HP][SLOTS][64 * KS];
+  __shared__ __attribute__((aligned(16))) uint16_t Vsh[HP][SLOTS][64 * VS];
+  const int hh = HP == 1 ? 0 : (int)(threadIdx.x >> 6) / NW;   // this thread's head of the workgroup's HP
+  uint16_t(*Ks)[64 * KS] = Ksh[hh];
+  uint16_t(*Vs)[64 * VS] = Vsh[hh];
   const int item = blockIdx.x;
-  const int bseq = item / H, h = item % H;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int bseq = item / (H / HP), h = (item % (H / HP)) * HP + hh;
+  const int tid = threadIdx.x - hh * 64 * NW, lane = tid & 63, wave = tid >> 6;
   const int64_t ld = 3 * (int64_t)W;
   const uint16_t* qb = qkv + (int64_t)bseq * S * ld + h * 64;
   const uint16_t* kb = qb + W;
@@ -360,6 +364,32 @@ __global__ __launch_bounds__(512) void attention_flash_kernel(const uint16_t* __
     }
   }
 }
+
+template <int NT, int PP, int SLOTS = 2>
+__global__ __launch_bounds__(512) void attention_flash_kernel(const uint16_t* __restrict__ qkv,
+                                                                uint16_t* __restrict__ out, int S, int W, int H,
+                                                                int causal, uint8_t* __restrict__ q8,
+                                                                uint8_t* __restrict__ qs, int64_t rows_pad) {
+  attention_flash_body<NT, PP, SLOTS>(qkv, out, S, W, H, causal, q8, qs, rows_pad);
+}
+
+// S <= 64 (B/32's 50 tokens): 4 waves, one slot.  An occupancy target of 6 waves per SIMD holds
+// the register allocation to 72 VGPRs (162 without it: the scheduler hoists the K / V^T fragment
+// reads of the whole chunk), so 7 workgroups share a CU instead of 3 — this case is bound by the
+// qkv reads, and more workgroups keep more of them in flight.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void attention_short_kernel(
+    const uint16_t* __restrict__ qkv, uint16_t* __restrict__ out, int S, int W, int H, int causal,
+    uint8_t* __restrict__ q8, uint8_t* __restrict__ qs, int64_t rows_pad) {
+  attention_flash_body<1, 2, 1>(qkv, out, S, W, H, causal, q8, qs, rows_pad);
+}
+
+#if MICLIP_AB   // A/B (MICLIP_ATTN_SHORT=2): two adjacent heads per workgroup, 8 waves
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6))) void attention_short2_kernel(
+    const uint16_t* __restrict__ qkv, uint16_t* __restrict__ out, int S, int W, int H, int causal,
+    uint8_t* __restrict__ q8, uint8_t* __restrict__ qs, int64_t rows_pad) {
+  attention_flash_body<1, 2, 1, 2>(qkv, out, S, W, H, causal, q8, qs, rows_pad);
+}
+#endif
 
 
 // ----------------------------- attention, vision towers: K/V resident in LDS
@@ -1054,6 +1084,11 @@ hipError_t attention(const uint16_t* qkv, uint16_t* out, int B, int S, int W, in
 #if MICLIP_AB
   // A/B: MICLIP_ATTN_SHORT=1 runs S <= 64 (non-causal) on the resident-K/V kernel with 4 waves
   const char* se = std::getenv("MICLIP_ATTN_SHORT");
+  if (se && se[0] == '2' && !one_wave && !old_flash && S <= 64 && H % 2 == 0) {
+    hipLaunchKernelGGL(attention_short2_kernel, dim3(items / 2), dim3(512), 0, s, qkv, out, S, W, H, causal & 1, q8, qs,
+                       ((int64_t)B * S + 1) & ~1);
+    return hipGetLastError();
+  }
   if (se && se[0] == '1' && !one_wave && !old_flash && !(causal & 1) && S <= 64) {
     const size_t lds = 2 * (size_t)((S + 31) & ~31) * 128;
     hipLaunchKernelGGL((attention_res_kernel<4, false>), dim3(B * (W / 64)), dim3(256), lds, s, qkv, out, S, W, W / 64,
@@ -1144,7 +1179,7 @@ hipError_t attention(const uint16_t* qkv, uint16_t* out, int B, int S, int W, in
 #define FLASH(T) \
   hipLaunchKernelGGL((attention_flash_kernel<T, 1>), grid, dim3(512), 0, s, qkv, out, S, W, H, causal, q8, qs, rp)
   if (nqt <= 4)
-    hipLaunchKernelGGL((attention_flash_kernel<1, 2, 1>), grid, dim3(256), 0, s, qkv, out, S, W, H, causal, q8, qs, rp);
+    hipLaunchKernelGGL(attention_short_kernel, grid, dim3(256), 0, s, qkv, out, S, W, H, causal, q8, qs, rp);
   else if (nqt <= 8) FLASH(1);
   else if (nqt <= 16) FLASH(2);
   else if (nqt <= 24) FLASH(3);

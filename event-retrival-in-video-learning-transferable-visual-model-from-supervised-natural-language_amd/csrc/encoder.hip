@@ -300,17 +300,28 @@ __global__ __launch_bounds__(256) void residual_stats_kernel(float* __restrict__
 // rs[r] from the W / 64 partials (sum_j, M2_j) that gemm_8q's EPI_RES16 epilogue stored for row r
 // (each over 64 stored fp16 values): mean = sum / W, M2 = sum_j M2_j + 64 (mean_j - mean)^2
 // (Chan et al.'s pairwise update for equal-count groups), var = M2 / W — the two-pass
-// statistics of residual_stats_kernel up to f32 rounding.  One thread per row; W <= 1024.
+// statistics of residual_stats_kernel up to f32 rounding.  One thread per row, W <= 1024; the
+// block's 256 rows of partials are staged through LDS with consecutive lanes reading consecutive
+// 16-byte pieces (a thread reading its own row's 96 bytes directly ran at 1.6 TB/s).
 __global__ __launch_bounds__(256) void residual_finalize_kernel(const float* __restrict__ ps, float* __restrict__ rs,
                                                                 int rows, int W) {
-  const int row = blockIdx.x * 256 + threadIdx.x;
+  __shared__ float4 sp[256 * 8 + 256 / 4];   // rows of np / 2 float4, one pad float4 every 4 rows
+  const int np = W >> 6, nq = np >> 1;
+  const int r0 = blockIdx.x * 256;
+  const int nrow = min(256, rows - r0);
+  const float4* src = (const float4*)(ps + (int64_t)r0 * np * 2);
+  for (int i = threadIdx.x; i < nrow * nq; i += 256) {
+    const int r = i / nq;
+    sp[i + (r >> 2)] = src[i];
+  }
+  __syncthreads();
+  const int row = r0 + threadIdx.x;
   if (row >= rows) return;
-  const int np = W >> 6;
-  const float4* p4 = (const float4*)(ps + (int64_t)row * np * 2);
+  const float4* p4 = sp + threadIdx.x * nq + (threadIdx.x >> 2);
   float s[16], m2[16];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
-    if (2 * i < np) {
+    if (i < nq) {
       const float4 v = p4[i];
       s[2 * i] = v.x;
       m2[2 * i] = v.y;

@@ -71,12 +71,33 @@ constexpr int H_A0 = 0, H_B0 = 1, H_B1 = 2, H_A1 = 3;
 constexpr int F_GLDS = 1;   // flat global_load_lds with per-DMA address math (gemm_8p's) instead of descriptors
 constexpr int F_FULL = 2;   // epilogue stores of 8 whole 128-B rows (lane pairs fr, fr ^ 8 swap halves by DPP)
 constexpr int F_VOREC = 4;  // epilogue store offsets recomputed from the lane id (EPI_RES16 always)
+constexpr int F_GSTAGE = 8; // QuickGELU over a store's 8 values in stage order (quick_gelu8_8q)
 
 __device__ __forceinline__ f32x2 quick_gelu2_8q(f32x2 v) {
   const f32x2 t = v * (f32x2){-2.45546696f, -2.45546696f};   // -1.702 * log2(e)
   f32x2 e = {__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)};
   e = e + 1.0f;
   return v * (f32x2){__builtin_amdgcn_rcpf(e.x), __builtin_amdgcn_rcpf(e.y)};
+}
+
+// QuickGELU of 8 values in stage order (all multiplies, all exponentials, all adds, all
+// reciprocals, all products), so consecutive transcendental ops are independent (F_GSTAGE)
+__device__ __forceinline__ void quick_gelu8_8q(f32x2 (&v)[4]) {
+  float e[8];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const f32x2 t = v[k] * (f32x2){-2.45546696f, -2.45546696f};
+    e[2 * k] = t.x;
+    e[2 * k + 1] = t.y;
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) e[k] = __builtin_amdgcn_exp2f(e[k]);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) e[k] = e[k] + 1.0f;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) e[k] = __builtin_amdgcn_rcpf(e[k]);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) v[k] = v[k] * (f32x2){e[2 * k], e[2 * k + 1]};
 }
 
 __device__ __forceinline__ void tile_coords_8q(int t, int tiles_m, int tiles_n, int ng, int& mb, int& nb) {
@@ -387,6 +408,7 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
 #pragma unroll
       for (int p = 0; p < 2; ++p) {
         uint2 pk[2];
+        f32x2 gv[4];   // F_GSTAGE: the 8 values of this p, QuickGELU in stage order
 #pragma unroll
         for (int qq = 0; qq < 2; ++qq) {
           const int ni = 2 * p + qq;
@@ -400,11 +422,21 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
             lo = lo + (f32x2){bias[ni].x, bias[ni].y};
             hi = hi + (f32x2){bias[ni].z, bias[ni].w};
           }
+          if (EK::GELU && (F & F_GSTAGE)) {
+            gv[2 * qq] = lo;
+            gv[2 * qq + 1] = hi;
+            continue;
+          }
           if (EK::GELU) {
             lo = quick_gelu2_8q(lo);
             hi = quick_gelu2_8q(hi);
           }
           pk[qq] = make_uint2(pack_bf16x2(lo), pack_bf16x2(hi));
+        }
+        if (EK::GELU && (F & F_GSTAGE)) {
+          quick_gelu8_8q(gv);
+#pragma unroll
+          for (int qq = 0; qq < 2; ++qq) pk[qq] = make_uint2(pack_bf16x2(gv[2 * qq]), pack_bf16x2(gv[2 * qq + 1]));
         }
         const auto sx = __builtin_amdgcn_permlane16_swap(pk[0].x, pk[1].x, false, false);
         const auto sy = __builtin_amdgcn_permlane16_swap(pk[0].y, pk[1].y, false, false);
@@ -686,6 +718,21 @@ hipError_t gemm_8q(const GemmArgs& a0, int epi, hipStream_t s, int cus, int mode
   // the LayerNorm-folded GEMMs read fp16 operands; their vectors must be present
   if (epi == EPI_LN_BF16 || epi == EPI_LN_GELU_BF16) {
     if (!a.a_f16 || !a.rs || !a.colv || !a.bias || mode) return hipErrorInvalidValue;
+#if MICLIP_AB   // A/B (MICLIP_8Q_F): epilogue flags F_VOREC (4) / F_GSTAGE (8) / both (12)
+    const char* fe = std::getenv("MICLIP_8Q_F");
+    const int ff = fe ? std::atoi(fe) : 0;
+    if (ff == 4 || ff == 8 || ff == 12) {
+#define LNF(E, FL) hipLaunchKernelGGL((gemm_8q_kernel<E, 0, FL, true>), dim3(grid), dim3(512), 0, s, a)
+      if (epi == EPI_LN_BF16) {
+        if (ff == 4) LNF(EPI_LN_BF16, F_VOREC);
+        else LNF(EPI_LN_BF16, F_VOREC);   // (no GELU: F_GSTAGE has nothing to reorder)
+      } else if (ff == 4) LNF(EPI_LN_GELU_BF16, F_VOREC);
+      else if (ff == 8) LNF(EPI_LN_GELU_BF16, F_GSTAGE);
+      else LNF(EPI_LN_GELU_BF16, F_GSTAGE | F_VOREC);
+#undef LNF
+      return hipGetLastError();
+    }
+#endif
     if (epi == EPI_LN_BF16) hipLaunchKernelGGL((gemm_8q_kernel<EPI_LN_BF16, 0, 0, true>), dim3(grid), dim3(512), 0, s, a);
     else hipLaunchKernelGGL((gemm_8q_kernel<EPI_LN_GELU_BF16, 0, 0, true>), dim3(grid), dim3(512), 0, s, a);
     return hipGetLastError();

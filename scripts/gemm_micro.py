@@ -79,7 +79,7 @@ def main():
         A, W = A.to(dt), W.to(dt)
         bias = torch.rand(Nn, device=dev, generator=g)
         res = epi == 8
-        variants = [0] if ln else ([0, 1, 2, 3] if res else all_variants)
+        variants = (all_variants if os.environ.get("LN_FLAGS") else [0]) if ln else ([0, 1, 2, 3] if res else all_variants)
         if os.environ.get("GEMM_MICRO_V0"):   # PMC passes (scripts/pmc_traffic.py): the product kernel only
             variants = [0]
         if res:
@@ -106,7 +106,8 @@ def main():
                     N.check(L.mi_op_residual_stats(x16.data_ptr(), outs[v].data_ptr(), rs2.data_ptr(), M, Nn, sp),
                             "residual_stats")
                 return
-            if ln:
+            if ln:   # LN_FLAGS=1: variant v = gemm_8q epilogue flags (MICLIP_8Q_F, A/B build)
+                os.environ["MICLIP_8Q_F"] = str(v)
                 N.check(L.mi_op_gemm_ln(A.data_ptr(), 2 * K, rs.data_ptr(), W.data_ptr(), colsum.data_ptr(),
                                         bias.data_ptr(), outs[v].data_ptr(), M, Nn, K, epi - 6, sp), "gemm_ln")
                 return
