@@ -373,17 +373,18 @@ __global__ __launch_bounds__(512) void attention_flash_kernel(const uint16_t* __
   attention_flash_body<NT, PP, SLOTS>(qkv, out, S, W, H, causal, q8, qs, rows_pad);
 }
 
-// S <= 64 (B/32's 50 tokens): 4 waves, one slot.  An occupancy target of 6 waves per SIMD holds
-// the register allocation to 72 VGPRs (162 without it: the scheduler hoists the K / V^T fragment
-// reads of the whole chunk), so 7 workgroups share a CU instead of 3 — this case is bound by the
-// qkv reads, and more workgroups keep more of them in flight.
+#if MICLIP_AB
+// A/B variants of the S <= 64 case (B/32's 50 tokens; the default is attention_flash_kernel<1, 2, 1>
+// on 4 waves).  Timed in interleaved rounds at 10k frames (scripts/attn_micro.py,
+// profiles/r04_ai_attn_micro.log), all bit-identical: default 603 us; an occupancy target of 6 waves
+// per SIMD (72 instead of 74 VGPRs, MICLIP_ATTN_SHORT=3) 604 us; two adjacent heads per 8-wave
+// workgroup, their 128-byte qkv / output row segments together (=2) 616 us.
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void attention_short_kernel(
     const uint16_t* __restrict__ qkv, uint16_t* __restrict__ out, int S, int W, int H, int causal,
     uint8_t* __restrict__ q8, uint8_t* __restrict__ qs, int64_t rows_pad) {
   attention_flash_body<1, 2, 1>(qkv, out, S, W, H, causal, q8, qs, rows_pad);
 }
 
-#if MICLIP_AB   // A/B (MICLIP_ATTN_SHORT=2): two adjacent heads per workgroup, 8 waves
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6))) void attention_short2_kernel(
     const uint16_t* __restrict__ qkv, uint16_t* __restrict__ out, int S, int W, int H, int causal,
     uint8_t* __restrict__ q8, uint8_t* __restrict__ qs, int64_t rows_pad) {
@@ -1084,9 +1085,14 @@ hipError_t attention(const uint16_t* qkv, uint16_t* out, int B, int S, int W, in
 #if MICLIP_AB
   // A/B: MICLIP_ATTN_SHORT=1 runs S <= 64 (non-causal) on the resident-K/V kernel with 4 waves
   const char* se = std::getenv("MICLIP_ATTN_SHORT");
-  if (se && se[0] == '2' && !one_wave && !old_flash && S <= 64 && H % 2 == 0) {
-    hipLaunchKernelGGL(attention_short2_kernel, dim3(items / 2), dim3(512), 0, s, qkv, out, S, W, H, causal & 1, q8, qs,
-                       ((int64_t)B * S + 1) & ~1);
+  // 2: two heads per workgroup; 3: the occupancy-targeted single-head kernel
+  if (se && (se[0] == '2' || se[0] == '3') && !one_wave && !old_flash && S <= 64) {
+    if (se[0] == '2' && H % 2 == 0)
+      hipLaunchKernelGGL(attention_short2_kernel, dim3(items / 2), dim3(512), 0, s, qkv, out, S, W, H, causal, q8, qs,
+                         ((int64_t)B * S + 1) & ~1);
+    else
+      hipLaunchKernelGGL(attention_short_kernel, grid, dim3(256), 0, s, qkv, out, S, W, H, causal, q8, qs,
+                         ((int64_t)B * S + 1) & ~1);
     return hipGetLastError();
   }
   if (se && se[0] == '1' && !one_wave && !old_flash && !(causal & 1) && S <= 64) {
@@ -1179,7 +1185,7 @@ hipError_t attention(const uint16_t* qkv, uint16_t* out, int B, int S, int W, in
 #define FLASH(T) \
   hipLaunchKernelGGL((attention_flash_kernel<T, 1>), grid, dim3(512), 0, s, qkv, out, S, W, H, causal, q8, qs, rp)
   if (nqt <= 4)
-    hipLaunchKernelGGL(attention_short_kernel, grid, dim3(256), 0, s, qkv, out, S, W, H, causal, q8, qs, rp);
+    hipLaunchKernelGGL((attention_flash_kernel<1, 2, 1>), grid, dim3(256), 0, s, qkv, out, S, W, H, causal, q8, qs, rp);
   else if (nqt <= 8) FLASH(1);
   else if (nqt <= 16) FLASH(2);
   else if (nqt <= 24) FLASH(3);

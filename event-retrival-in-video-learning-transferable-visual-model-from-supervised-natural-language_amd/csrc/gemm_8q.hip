@@ -718,9 +718,13 @@ hipError_t gemm_8q(const GemmArgs& a0, int epi, hipStream_t s, int cus, int mode
   // the LayerNorm-folded GEMMs read fp16 operands; their vectors must be present
   if (epi == EPI_LN_BF16 || epi == EPI_LN_GELU_BF16) {
     if (!a.a_f16 || !a.rs || !a.colv || !a.bias || mode) return hipErrorInvalidValue;
-#if MICLIP_AB   // A/B (MICLIP_8Q_F): epilogue flags F_VOREC (4) / F_GSTAGE (8) / both (12)
+#if MICLIP_AB   // A/B (MICLIP_8Q_F): epilogue flags F_VOREC (4) / F_GSTAGE (8) / both (12); 1 = none
     const char* fe = std::getenv("MICLIP_8Q_F");
     const int ff = fe ? std::atoi(fe) : 0;
+    if (ff == 1 && epi == EPI_LN_GELU_BF16) {
+      hipLaunchKernelGGL((gemm_8q_kernel<EPI_LN_GELU_BF16, 0, 0, true>), dim3(grid), dim3(512), 0, s, a);
+      return hipGetLastError();
+    }
     if (ff == 4 || ff == 8 || ff == 12) {
 #define LNF(E, FL) hipLaunchKernelGGL((gemm_8q_kernel<E, 0, FL, true>), dim3(grid), dim3(512), 0, s, a)
       if (epi == EPI_LN_BF16) {
@@ -733,8 +737,10 @@ hipError_t gemm_8q(const GemmArgs& a0, int epi, hipStream_t s, int cus, int mode
       return hipGetLastError();
     }
 #endif
+    // c_fc: QuickGELU in stage order + store offsets from the lane id (bit-identical; lnfc500
+    // 2281 vs 2318 us, profiles/r04_ag_lnflags.log); in_proj: no difference, kept as it was
     if (epi == EPI_LN_BF16) hipLaunchKernelGGL((gemm_8q_kernel<EPI_LN_BF16, 0, 0, true>), dim3(grid), dim3(512), 0, s, a);
-    else hipLaunchKernelGGL((gemm_8q_kernel<EPI_LN_GELU_BF16, 0, 0, true>), dim3(grid), dim3(512), 0, s, a);
+    else hipLaunchKernelGGL((gemm_8q_kernel<EPI_LN_GELU_BF16, 0, F_GSTAGE | F_VOREC, true>), dim3(grid), dim3(512), 0, s, a);
     return hipGetLastError();
   }
   if (a.a_f16) return hipErrorInvalidValue;
@@ -765,6 +771,22 @@ hipError_t gemm_8q(const GemmArgs& a0, int epi, hipStream_t s, int cus, int mode
 #define L8Q_ALL(E)                   \
   if (mode == 0) L8Q(E, 0, 0);       \
   else return hipErrorNotSupported;
+#endif
+#if MICLIP_AB
+  {   // A/B (MICLIP_8Q_F): epilogue flags on the plain GELU kernel (text tower / unfolded c_fc)
+    const char* fe = std::getenv("MICLIP_8Q_F");
+    const int ff = fe ? std::atoi(fe) : 0;
+    if (mode == 0 && epi == EPI_GELU_BF16 && (ff == 4 || ff == 8 || ff == 12)) {
+      if (ff == 4) L8Q(EPI_GELU_BF16, 0, F_VOREC);
+      else if (ff == 8) L8Q(EPI_GELU_BF16, 0, F_GSTAGE);
+      else L8Q(EPI_GELU_BF16, 0, F_GSTAGE | F_VOREC);
+      return hipGetLastError();
+    }
+    if (mode == 0 && epi == EPI_BF16 && ff == 4) {
+      L8Q(EPI_BF16, 0, F_VOREC);
+      return hipGetLastError();
+    }
+  }
 #endif
   if (epi == EPI_GELU_BF16) {
     L8Q_ALL(EPI_GELU_BF16)

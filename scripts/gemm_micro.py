@@ -79,7 +79,7 @@ def main():
         A, W = A.to(dt), W.to(dt)
         bias = torch.rand(Nn, device=dev, generator=g)
         res = epi == 8
-        variants = (all_variants if os.environ.get("LN_FLAGS") else [0]) if ln else ([0, 1, 2, 3] if res else all_variants)
+        variants = (all_variants if os.environ.get("LN_FLAGS") else [0]) if ln else ([0, 1, 2, 3, 4] if res else all_variants)
         if os.environ.get("GEMM_MICRO_V0"):   # PMC passes (scripts/pmc_traffic.py): the product kernel only
             variants = [0]
         if res:
@@ -95,7 +95,7 @@ def main():
         def run(v):
             if res:   # (x16 grows by the GEMM output each call: timing only, outputs not compared)
                 # v2 / v3: timing probes of the fused kernel without statistics / without x16 loads
-                os.environ["MICLIP_RES_ABL"] = {2: "11", 3: "12"}.get(v, "0")
+                os.environ["MICLIP_RES_ABL"] = {2: "11", 3: "12", 4: "16"}.get(v, "0")   # v4: one-pass statistics
                 if v != 1:
                     N.check(L.mi_op_gemm_residual(x16.data_ptr(), 2 * Nn, A.data_ptr(), K, W.data_ptr(),
                                                   bias.data_ptr(), ps.data_ptr(), rs2.data_ptr(), M, Nn, K, sp),
@@ -111,8 +111,12 @@ def main():
                 N.check(L.mi_op_gemm_ln(A.data_ptr(), 2 * K, rs.data_ptr(), W.data_ptr(), colsum.data_ptr(),
                                         bias.data_ptr(), outs[v].data_ptr(), M, Nn, K, epi - 6, sp), "gemm_ln")
                 return
+            sched = v
+            if os.environ.get("LN_FLAGS"):   # variant v = gemm_8q epilogue flags (MICLIP_8Q_F)
+                os.environ["MICLIP_8Q_F"] = str(v)
+                sched = 0
             N.check(L.mi_op_gemm(A.data_ptr(), W.data_ptr(), bias.data_ptr(), outs[v].data_ptr(), M, Nn, K,
-                                 epi | (v << 8), sp), "gemm")
+                                 epi | (sched << 8), sp), "gemm")
         for v in variants:
             run(v)
         torch.cuda.synchronize()

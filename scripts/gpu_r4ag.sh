@@ -15,3 +15,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun
 grep -h "finalize\|residual_stats" gpurun_out/prof4ag/micro_kernel_stats.csv | cut -c1-200
 LN_FLAGS=1 timeout -k 10 300 python -u scripts/gemm_micro.py 10 lnfc500,lnqkv500 0,4,8,12 > gpurun_out/r4ag_lnflags.log 2>&1 || exit $?
 cat gpurun_out/r4ag_lnflags.log
+LN_FLAGS=1 timeout -k 10 300 python -u scripts/gemm_micro.py 10 fc500,qkv500 0,4,8,12 > gpurun_out/r4ag_plainflags.log 2>&1 || exit $?
+cat gpurun_out/r4ag_plainflags.log
