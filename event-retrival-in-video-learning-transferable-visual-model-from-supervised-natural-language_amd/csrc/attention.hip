@@ -3,6 +3,7 @@
 // tower), restated in oracle/clip_ref.py::_mha.  Built with -fno-honor-nans
 // (Makefile): the softmax max/sum chains then compile to v_max3 without NaN
 // canonicalisation; -inf masking is unaffected.
+#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 
@@ -160,10 +161,14 @@ __global__ __launch_bounds__(64) void attention_kernel(const uint16_t* __restric
 // waves, 2 for 4).
 // HP heads per workgroup (A/B: 2 = adjacent heads of one sequence, their 128-byte row segments
 // read together as 256 bytes), each on its own NW waves and LDS slots.
-template <int NT, int PP, int SLOTS, int HP = 1>
+// PIPE (S <= 64: NT = 1, SLOTS = 1, HP = 1): persistent workgroups walk items blockIdx.x,
+// + gridDim.x, ... and load the next item's Q fragments and K / V pieces into registers before
+// computing the current one, so a workgroup always has an item's qkv reads in flight.
+template <int NT, int PP, int SLOTS, int HP = 1, bool PIPE = false>
 __device__ __forceinline__ void attention_flash_body(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ out,
                                                      int S, int W, int H, int causal, uint8_t* __restrict__ q8,
-                                                     uint8_t* __restrict__ qs, int64_t rows_pad) {
+                                                     uint8_t* __restrict__ qs, int64_t rows_pad, int items = 0) {
+  static_assert(!PIPE || (NT == 1 && SLOTS == 1 && HP == 1), "PIPE: the single-chunk instance only");
   constexpr int KS = 72, VS = 68;  // LDS row strides (bf16)
   const int NW = PP == 1 ? 8 : (int)(blockDim.x >> 6) / HP;  // PP = 1 is launched with 8 waves
   __shared__ __attribute__((aligned(16))) uint16_t Ksh[HP][SLOTS][64 * KS];
@@ -171,10 +176,14 @@ __device__ __forceinline__ void attention_flash_body(const uint16_t* __restrict_
   const int hh = HP == 1 ? 0 : (int)(threadIdx.x >> 6) / NW;   // this thread's head of the workgroup's HP
   uint16_t(*Ks)[64 * KS] = Ksh[hh];
   uint16_t(*Vs)[64 * VS] = Vsh[hh];
-  const int item = blockIdx.x;
-  const int bseq = item / (H / HP), h = (item % (H / HP)) * HP + hh;
   const int tid = threadIdx.x - hh * 64 * NW, lane = tid & 63, wave = tid >> 6;
   const int64_t ld = 3 * (int64_t)W;
+  int item = blockIdx.x;
+  bool first = true;
+  uint4 kr_n[PP], vr_n[PP];   // PIPE: the next item's K / V pieces and Q fragments
+  bf16x8 qf_n[2];
+  for (;;) {
+  const int bseq = item / (H / HP), h = (item % (H / HP)) * HP + hh;
   const uint16_t* qb = qkv + (int64_t)bseq * S * ld + h * 64;
   const uint16_t* kb = qb + W;
   const uint16_t* vb = qb + 2 * W;
@@ -211,15 +220,41 @@ __device__ __forceinline__ void attention_flash_body(const uint16_t* __restrict_
   for (int t = 0; t < NT; ++t) {
     const int qrow = min((wave + NW * t) * 16 + fr, S - 1);
 #pragma unroll
-    for (int s = 0; s < 2; ++s) qf[t][s] = *(const bf16x8*)(qb + (int64_t)qrow * ld + 32 * s + fk);
+    for (int s = 0; s < 2; ++s) qf[t][s] = (!PIPE || first) ? *(const bf16x8*)(qb + (int64_t)qrow * ld + 32 * s + fk) : qf_n[s];
     m[t] = -INFINITY;
     l[t] = 0.f;
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) o[t][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  FA_STAGE_LOAD(0);
+  if (!PIPE || first) {
+    FA_STAGE_LOAD(0);
+  } else {
+#pragma unroll
+    for (int i = 0; i < PP; ++i) {
+      kr[i] = kr_n[i];
+      vr[i] = vr_n[i];
+    }
+  }
+  // (PIPE: the previous item's LDS reads ended at the chunk loop's closing barrier)
   FA_STAGE_WRITE(0);
   __syncthreads();
+  if (PIPE && item + (int)gridDim.x < items) {   // the next item's operands, in flight during this one
+    const int nx = item + (int)gridDim.x;
+    const uint16_t* nq = qkv + (int64_t)(nx / H) * S * ld + (nx % H) * 64;
+    const int qrow = min(wave * 16 + fr, S - 1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) qf_n[s] = *(const bf16x8*)(nq + (int64_t)qrow * ld + 32 * s + fk);
+#pragma unroll
+    for (int i = 0; i < PP; ++i) {
+      const int p_ = tid + i * 64 * NW, r_ = p_ >> 3, ch_ = p_ & 7;
+      kr_n[i] = make_uint4(0, 0, 0, 0);
+      vr_n[i] = make_uint4(0, 0, 0, 0);
+      if ((PP == 1 || p_ < 512) && r_ < S) {
+        kr_n[i] = *(const uint4*)(nq + W + (int64_t)r_ * ld + ch_ * 8);
+        vr_n[i] = *(const uint4*)(nq + 2 * W + (int64_t)r_ * ld + ch_ * 8);
+      }
+    }
+  }
 
   for (int c = 0; c < nch; ++c) {
     const int slot = SLOTS == 1 ? 0 : (c & 1);
@@ -363,6 +398,11 @@ __device__ __forceinline__ void attention_flash_body(const uint16_t* __restrict_
                                               pack_bf16x2(o[t][dt][2] * inv, o[t][dt][3] * inv));
     }
   }
+  if (!PIPE) break;
+  item += (int)gridDim.x;
+  if (item >= items) break;
+  first = false;
+  }   // items
 }
 
 template <int NT, int PP, int SLOTS = 2>
@@ -383,6 +423,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void a
     const uint16_t* __restrict__ qkv, uint16_t* __restrict__ out, int S, int W, int H, int causal,
     uint8_t* __restrict__ q8, uint8_t* __restrict__ qs, int64_t rows_pad) {
   attention_flash_body<1, 2, 1>(qkv, out, S, W, H, causal, q8, qs, rows_pad);
+}
+
+__global__ __launch_bounds__(256) void attention_pipe_kernel(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ out,
+                                                             int S, int W, int H, int causal, uint8_t* __restrict__ q8,
+                                                             uint8_t* __restrict__ qs, int64_t rows_pad, int items) {
+  attention_flash_body<1, 2, 1, 1, true>(qkv, out, S, W, H, causal, q8, qs, rows_pad, items);
 }
 
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6))) void attention_short2_kernel(
@@ -1085,6 +1131,15 @@ hipError_t attention(const uint16_t* qkv, uint16_t* out, int B, int S, int W, in
 #if MICLIP_AB
   // A/B: MICLIP_ATTN_SHORT=1 runs S <= 64 (non-causal) on the resident-K/V kernel with 4 waves
   const char* se = std::getenv("MICLIP_ATTN_SHORT");
+  // 5x: persistent workgroups with the next item's operands prefetched, x workgroups per CU (default 4:
+  // 128 VGPRs)
+  if (se && se[0] == '5' && !one_wave && !old_flash && S <= 64) {
+    const int per = se[1] ? std::atoi(se + 1) : 4;
+    const int gp = std::min(items, cu_count() * (per > 0 ? per : 5));
+    hipLaunchKernelGGL(attention_pipe_kernel, dim3(gp), dim3(256), 0, s, qkv, out, S, W, H, causal, q8, qs,
+                       ((int64_t)B * S + 1) & ~1, items);
+    return hipGetLastError();
+  }
   // 2: two heads per workgroup; 3: the occupancy-targeted single-head kernel
   if (se && (se[0] == '2' || se[0] == '3') && !one_wave && !old_flash && S <= 64) {
     if (se[0] == '2' && H % 2 == 0)
