@@ -75,9 +75,9 @@ def parse():
 
 def lnfold_active(model, cfg):
     """The bf16 vision tower runs LayerNorm folded into in_proj / c_fc when its width is a
-    multiple of 256 and at most 768 (api.cpp lnfold / mi_clip_encode_image `fold`; the product
+    multiple of 256 and at most 1024 (api.cpp lnfold / mi_clip_encode_image `fold`; the product
     library has no switch)."""
-    return getattr(model, "weights", "bf16") == "bf16" and cfg.vision_width % 256 == 0 and cfg.vision_width <= 768
+    return getattr(model, "weights", "bf16") == "bf16" and cfg.vision_width % 256 == 0 and cfg.vision_width <= 1024
 
 
 def kernel_timing(model, cfg, chunk, reps=20):

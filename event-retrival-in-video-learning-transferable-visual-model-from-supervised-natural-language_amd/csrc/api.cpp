@@ -708,12 +708,15 @@ static int run_tower(mi_clip* c, const std::vector<Layer>& layers, int B, int S,
 // in their epilogues from per-row (rstd, rstd * mean) (gemm_8q.hip EPI_LN_*), so the residual
 // adds only write x16 and the statistics (residual_stats: 6 instead of residual_ln's 8 bytes per
 // element, no h buffer).  MICLIP_LNFOLD=0 keeps run_tower (A/B).
-// Default: folded for W <= 768 (B/32: 101.9k -> 103.6k frames/s); at W = 1024 (L/14) the folded
-// c_fc / qkv run 10 % / 5 % slower than the plain GEMMs (K = 1024 amortises the plain epilogue
-// better) and the fold did not pay (configs[2] 16.25 -> 16.32 s per step, profiles/r04_v_config2.json)
+// Default: folded for W <= 1024.  Before the residual add moved into the out_proj / c_proj
+// epilogues the fold only paid for W <= 768 (B/32: 101.9k -> 103.6k frames/s; at W = 1024 the
+// folded c_fc / qkv run 10 % / 5 % slower than the plain GEMMs, and residual_stats did not make that
+// up: configs[2] 16.25 -> 16.32 s per step, profiles/r04_v_config2.json).  With the fused residual
+// it pays at L/14 too: 6566 frames/s against 6160 unfolded and 6107 folded without the fusion
+// (10k frames x 256 queries, profiles/r04_al_l14_fold.log).
 static int lnfold(int W) {
   const char* e = ab_getenv("MICLIP_LNFOLD");   // read per call (A/B tests switch it within one process)
-  return e ? atoi(e) != 0 : W <= 768;
+  return e ? atoi(e) != 0 : W <= 1024;
 }
 
 static GemmArgs ln_args(mi_clip* c, const uint16_t* wf, const float* sv, const float* cv, void* out, int N, int M,

@@ -226,7 +226,7 @@ def test_lnfold_tower_matches_oracle(gpu, monkeypatch, name, n):
     ref = clip_ref.encode_image(px, state_dict(name), cfg, np.float64)
     prod = _model(name, gpu, image_chunk=n).encode_image(torch.from_numpy(px)).cpu().numpy()
     monkeypatch.setattr(_native, "lib", _native.lib_ab)
-    monkeypatch.setenv("MICLIP_LNFOLD", "1")           # folded at every width (the product: W <= 768)
+    monkeypatch.setenv("MICLIP_LNFOLD", "1")           # folded at every width (the product: W <= 1024)
     got = _model(name, gpu, image_chunk=n).encode_image(torch.from_numpy(px)).cpu().numpy()
     c_fold = _check(got, ref, f"{name} folded")
     # the residual add fused into out_proj / c_proj (the default) against the separate
@@ -242,7 +242,7 @@ def test_lnfold_tower_matches_oracle(gpu, monkeypatch, name, n):
     c_plain = _check(got0, ref, f"{name} unfolded")
     assert cosine(got, got0).min() > 1 - COS_TOL
     assert 1 - c_fold <= 1.5 * (1 - c_plain) + 2e-5, (c_fold, c_plain)
-    # the product library's default is one of the two, bit for bit: folded for W <= 768
-    assert np.array_equal(prod, got if cfg.vision_width <= 768 else got0)
+    # the product library's default is one of the two, bit for bit: folded for W <= 1024
+    assert np.array_equal(prod, got if cfg.vision_width <= 1024 else got0)
     if n * cfg.vision_tokens < 256:
         assert np.array_equal(got, got0)     # the same (unfolded) path in both libraries
