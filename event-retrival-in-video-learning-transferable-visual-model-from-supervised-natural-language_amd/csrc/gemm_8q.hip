@@ -329,8 +329,9 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
     return (uint32_t)(((wr * 128 + (l & 15)) * a.ldo + wc * 64 + ((l >> 4) & 1) * 16 + (l >> 5) * 8) * 2);
   };
   auto res_load = [&](const __amdgpu_buffer_rsrc_t& r, uint32_t vo, int mi) {
-    xin[mi & 3][0] = __builtin_bit_cast(u32x4_8q, __builtin_amdgcn_raw_buffer_load_b128(r, vo + mi * blkO, 0, 0));
-    xin[mi & 3][1] = __builtin_bit_cast(u32x4_8q, __builtin_amdgcn_raw_buffer_load_b128(r, vo + mi * blkO + 64, 0, 0));
+    // (ABL 13: non-temporal x16 loads and stores, probe of L2 pollution)
+    xin[mi & 3][0] = __builtin_bit_cast(u32x4_8q, __builtin_amdgcn_raw_buffer_load_b128(r, vo + mi * blkO, 0, ABL == 13 ? 2 : 0));
+    xin[mi & 3][1] = __builtin_bit_cast(u32x4_8q, __builtin_amdgcn_raw_buffer_load_b128(r, vo + mi * blkO + 64, 0, ABL == 13 ? 2 : 0));
   };
   auto res_prefetch = [&]() {
     if (!EK::RES || ABL == 12) return;
@@ -458,8 +459,8 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
         dp[p] = d;
         if (F & F_FULL) continue;
         if (ABL == 10) asm volatile("" ::"v"(d));   // stamp probe without the stores
-        else if (p == 0) __builtin_amdgcn_raw_buffer_store_b128(d, rsO, vo + mi * blkO, 0, 0);
-        else __builtin_amdgcn_raw_buffer_store_b128(d, rsO, vo + mi * blkO + 64, 0, 0);
+        else if (p == 0) __builtin_amdgcn_raw_buffer_store_b128(d, rsO, vo + mi * blkO, 0, ABL == 13 ? 2 : 0);
+        else __builtin_amdgcn_raw_buffer_store_b128(d, rsO, vo + mi * blkO + 64, 0, ABL == 13 ? 2 : 0);
       }
       if (F & F_FULL) {
         const bool top = fr < 8;
@@ -751,6 +752,7 @@ hipError_t gemm_8q(const GemmArgs& a0, int epi, hipStream_t s, int cus, int mode
     const int abl = ab ? std::atoi(ab) : 0;
     if (abl == 11) hipLaunchKernelGGL((gemm_8q_kernel<EPI_RES16_BF16, 11, 0>), dim3(grid), dim3(512), 0, s, a);
     else if (abl == 12) hipLaunchKernelGGL((gemm_8q_kernel<EPI_RES16_BF16, 12, 0>), dim3(grid), dim3(512), 0, s, a);
+    else if (abl == 13) hipLaunchKernelGGL((gemm_8q_kernel<EPI_RES16_BF16, 13, 0>), dim3(grid), dim3(512), 0, s, a);
     else
 #endif
     hipLaunchKernelGGL((gemm_8q_kernel<EPI_RES16_BF16, 0, 0>), dim3(grid), dim3(512), 0, s, a);

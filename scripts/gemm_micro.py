@@ -79,7 +79,7 @@ def main():
         A, W = A.to(dt), W.to(dt)
         bias = torch.rand(Nn, device=dev, generator=g)
         res = epi == 8
-        variants = (all_variants if os.environ.get("LN_FLAGS") else [0]) if ln else ([0, 1, 2, 3, 4] if res else all_variants)
+        variants = (all_variants if os.environ.get("LN_FLAGS") else [0]) if ln else ([0, 1, 2, 3, 5] if res else all_variants)
         if os.environ.get("GEMM_MICRO_V0"):   # PMC passes (scripts/pmc_traffic.py): the product kernel only
             variants = [0]
         if res:
@@ -95,7 +95,7 @@ def main():
         def run(v):
             if res:   # (x16 grows by the GEMM output each call: timing only, outputs not compared)
                 # v2 / v3: timing probes of the fused kernel without statistics / without x16 loads
-                os.environ["MICLIP_RES_ABL"] = {2: "11", 3: "12", 4: "16"}.get(v, "0")   # v4: one-pass statistics
+                os.environ["MICLIP_RES_ABL"] = {2: "11", 3: "12", 5: "13"}.get(v, "0")   # v5: non-temporal x16 loads / stores
                 if v != 1:
                     N.check(L.mi_op_gemm_residual(x16.data_ptr(), 2 * Nn, A.data_ptr(), K, W.data_ptr(),
                                                   bias.data_ptr(), ps.data_ptr(), rs2.data_ptr(), M, Nn, K, sp),
