@@ -299,24 +299,26 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
   // row fr + 8 for store 2; lane (fr >= 8) takes the p = 1 piece of row fr - 8 for store 1
   const uint32_t voF = (uint32_t)(((wr * 128 + (fr & 7)) * a.ldo + wc * 64 + 8 * ((g & 1) * 2 + (g >> 1)) + 32 * (fr >> 3)) * 2);
   const uint32_t rows8 = (uint32_t)(8 * a.ldo * 2);
-  auto out_rsrc = [&]() {
-    const int rows = min(a.M - pm0, BM);
-    return __builtin_amdgcn_make_buffer_rsrc((void*)((uint16_t*)a.out + (int64_t)pm0 * a.ldo + pn0), (short)0,
+  auto out_rsrc_at = [&](int m0, int n0) {
+    const int rows = min(a.M - m0, BM);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)((uint16_t*)a.out + (int64_t)m0 * a.ldo + n0), (short)0,
                                              rows * (int)a.ldo * 2, 0x00020000);
   };
-  // EPI_RES16: the previous tile's x16 blocks (the 16-byte pieces its stores overwrite), four
-  // 16-row blocks in flight.  Blocks 0-3 are loaded at the head of the next tile's phase 1,
-  // AHEAD of that phase's DMAs, so waiting for them needs only DMAs issued a phase earlier (and
-  // the registers are the fragment registers, dead until phase 1's reads); block mi + 4 goes out
-  // as block mi is consumed.  Rows past M read zeros (descriptor range) and are not stored.
-  // Measured alternatives (scripts/gemm_micro.py resout500 / resproj500, profiles/r04_a[cde]_*):
-  // blocks 0-1 loaded three phases earlier, in the tile's last pair (729 vs 724 us), and all
-  // eight blocks ahead of phase 1's DMAs (711 / 1890 vs 724 / 1881 us): no faster, so the x16
-  // loads' ~90 us per launch at M = 500k are not exposed latency.  The statistics, partial
-  // stores and residual_finalize cost ~50 us (probe ABL 11) — against the 380 us residual_stats
-  // pass and the delta write they remove.
+  auto out_rsrc = [&]() { return out_rsrc_at(pm0, pn0); };
+  int cur_m0 = 0, cur_n0 = 0;   // the tile in the main loop (EPI_RES16: its x16 blocks 0-1 load in its last pair)
+  // EPI_RES16: the x16 pieces a tile's epilogue stores over (16 bytes per lane and 16-row block),
+  // loaded ahead so that no wait for them also waits for a DMA issued just before: blocks 0-1 at
+  // the head of the tile's LAST pair's phase 6 (16 VGPRs live across phases 6-8), blocks 2-7 at
+  // the head of the next tile's phase 1, AHEAD of that phase's DMAs (the fragment registers are
+  // dead until phase 1's reads).  Rows past M read zeros (descriptor range) and are not stored.
+  // Measured (scripts/gemm_micro.py resout500 / resproj500, profiles/r04_a[cdeq]_*): this order
+  // 684 / 1833 us; blocks 0-3 before phase 1's DMAs and 4-7 behind them (each of those waits then
+  // also waited for phase 1's DMAs) 702-724 / 1867-1890 us; all eight before phase 1's DMAs 711 /
+  // 1890 us; blocks 0-1 in phase 6 with 4-7 behind the DMAs 729 us.  Non-temporal x16 accesses
+  // (probe ABL 13) 742-760 / 1888-1935 us.  The statistics, partial stores and residual_finalize
+  // cost ~30-50 us (probe ABL 11).
   typedef _Float16 h2_8q __attribute__((ext_vector_type(2)));
-  u32x4_8q xin[4][2];
+  u32x4_8q xin[8][2];
   // lane id from an opaque asm, so offsets derived from it are computed where used (the 16
   // store offsets voO + mi * blkO, derived from a kernel-scope constant, are otherwise hoisted
   // out of the tile loop and held in 16 VGPRs for the kernel's life)
@@ -330,15 +332,15 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
   };
   auto res_load = [&](const __amdgpu_buffer_rsrc_t& r, uint32_t vo, int mi) {
     // (ABL 13: non-temporal x16 loads and stores, probe of L2 pollution)
-    xin[mi & 3][0] = __builtin_bit_cast(u32x4_8q, __builtin_amdgcn_raw_buffer_load_b128(r, vo + mi * blkO, 0, ABL == 13 ? 2 : 0));
-    xin[mi & 3][1] = __builtin_bit_cast(u32x4_8q, __builtin_amdgcn_raw_buffer_load_b128(r, vo + mi * blkO + 64, 0, ABL == 13 ? 2 : 0));
+    xin[mi][0] = __builtin_bit_cast(u32x4_8q, __builtin_amdgcn_raw_buffer_load_b128(r, vo + mi * blkO, 0, ABL == 13 ? 2 : 0));
+    xin[mi][1] = __builtin_bit_cast(u32x4_8q, __builtin_amdgcn_raw_buffer_load_b128(r, vo + mi * blkO + 64, 0, ABL == 13 ? 2 : 0));
   };
-  auto res_prefetch = [&]() {
+  auto res_prefetch = [&](int mlo, int mhi, int m0, int n0) {
     if (!EK::RES || ABL == 12) return;
-    const __amdgpu_buffer_rsrc_t r = out_rsrc();
+    const __amdgpu_buffer_rsrc_t r = out_rsrc_at(m0, n0);
     const uint32_t vo = vo_out(lane_id());
 #pragma unroll
-    for (int mi = 0; mi < 4; ++mi) res_load(r, vo, mi);
+    for (int mi = mlo; mi < mhi; ++mi) res_load(r, vo, mi);
   };
   // sum across the four lanes (fr + 16 g) that hold one row's 64 columns: every lane gets the
   // same value (each level adds one commutative pair)
@@ -448,7 +450,7 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
             const uint32_t dv = d[e];
             // (vector elements are copied out before __builtin_bit_cast: on an element lvalue,
             // this hipcc reads element 0 whatever the index)
-            const uint32_t xv = ABL == 12 ? 0u : xin[mi & 3][p][e];   // ABL 12: x16 loads ablated
+            const uint32_t xv = ABL == 12 ? 0u : xin[mi][p][e];   // ABL 12: x16 loads ablated
             const h2_8q xh = __builtin_bit_cast(h2_8q, xv);
             const f32x2 sm = (f32x2){(float)xh.x, (float)xh.y} +
                              (f32x2){__uint_as_float(dv << 16), __uint_as_float(dv & 0xffff0000u)};
@@ -477,7 +479,6 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
         __builtin_amdgcn_raw_buffer_store_b128(s2, rsO, voF + mi * blkO + rows8, 0, 0);
       }
       if (EK::RES && ABL == 11) {   // timing probe: no statistics, no partial stores
-        if (mi + 4 < 8) res_load(rsO, vo, mi + 4);
         __builtin_amdgcn_sched_barrier(0);
       } else if (EK::RES) {   // the row's 64-column partial: sum, then squared deviations from its mean
         // (the stored values re-read from dp in each pass: 16 f32 kept live across the passes spill)
@@ -499,7 +500,6 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
         typedef unsigned int u32x2_8q __attribute__((ext_vector_type(2)));
         __builtin_amdgcn_raw_buffer_store_b64((u32x2_8q){__float_as_uint(s), __float_as_uint(m2)}, rsP,
                                               voP + (uint32_t)(mi * 16 * pstr), 0, 0);
-        if (mi + 4 < 8 && ABL != 12) res_load(rsO, vo, mi + 4);
         __builtin_amdgcn_sched_barrier(0);
       }
       rab_c = rab_n;
@@ -535,7 +535,7 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
       if (has_prev) {
         // the previous tile's x16 blocks 0-3 ahead of the phase's DMAs (one conditional block
         // from the loads to the epilogue: split across two, the loads' registers spilled)
-        res_prefetch();
+        res_prefetch(2, 8, pm0, pn0);
         __builtin_amdgcn_sched_barrier(0);
         issue(H_A1, 1);
         issue(H_B0, 1);
@@ -547,6 +547,10 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
         issue(H_B0, 1);
         __builtin_amdgcn_sched_barrier(0);
       }
+    }
+    if (P == 6 && LAST && EK::RES) {   // this tile's x16 blocks 0-1, ahead of the phase's DMA
+      res_prefetch(0, 2, cur_m0, cur_n0);
+      __builtin_amdgcn_sched_barrier(0);
     }
     if (q == 0) {
       read_a(rbuf + H_A0 * HALF);
@@ -573,7 +577,7 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
     if (P == 4) {
       // (EPI_RES16: 16 stores, 8 partial stores and the x16 loads of blocks 4-7 are younger;
       // the epilogue's wait for block 7 already retired the odd buffer)
-      if (FIRST && has_prev && EK::RES) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(ABL == 11 ? 28 : ABL == 12 ? 28 : 36) : "memory");
+      if (FIRST && has_prev && EK::RES) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(ABL == 11 ? 20 : 28) : "memory");
       else if (FIRST && has_prev && ABL != 10) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
       if (FIRST) stamp(3);   // S3: first pair's phase-4 wait passed
@@ -654,6 +658,8 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
   for (int v = blockIdx.x; v < ntiles; v += G) {
     int cm0, cn0;
     coords(v, cm0, cn0);
+    cur_m0 = cm0;
+    cur_n0 = cn0;
     has_next = v + G < ntiles;
     if (has_next) coords(v + G, nxt_m0, nxt_n0);
     // (npairs >= 2, gemm_8q_ok: a one-pair instance beside these made hipcc spill ~200 VGPRs)
@@ -671,7 +677,7 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
   }
   // the last tile's epilogue
   if (wr == 0) barrier();   // the M-groups' barrier counts meet
-  res_prefetch();
+  res_prefetch(2, 8, pm0, pn0);
   epilogue();
   if ((ABL == 9 || ABL == 10) && lane == 0 && (wave & 3) == 0 && blockIdx.x < 1024) {
 #pragma unroll
