@@ -72,6 +72,7 @@ constexpr int F_GLDS = 1;   // flat global_load_lds with per-DMA address math (g
 constexpr int F_FULL = 2;   // epilogue stores of 8 whole 128-B rows (lane pairs fr, fr ^ 8 swap halves by DPP)
 constexpr int F_VOREC = 4;  // epilogue store offsets recomputed from the lane id (EPI_RES16 always)
 constexpr int F_GSTAGE = 8; // QuickGELU over a store's 8 values in stage order (quick_gelu8_8q)
+constexpr int F_GSTAGE16 = 32;   // the same over a 16-row block's 16 values (A/B)
 
 __device__ __forceinline__ f32x2 quick_gelu2_8q(f32x2 v) {
   const f32x2 t = v * (f32x2){-2.45546696f, -2.45546696f};   // -1.702 * log2(e)
@@ -82,23 +83,25 @@ __device__ __forceinline__ f32x2 quick_gelu2_8q(f32x2 v) {
 
 // QuickGELU of 8 values in stage order (all multiplies, all exponentials, all adds, all
 // reciprocals, all products), so consecutive transcendental ops are independent (F_GSTAGE)
-__device__ __forceinline__ void quick_gelu8_8q(f32x2 (&v)[4]) {
-  float e[8];
+template <int NP>
+__device__ __forceinline__ void quick_gelu_stage_8q(f32x2 (&v)[NP]) {
+  float e[2 * NP];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
+  for (int k = 0; k < NP; ++k) {
     const f32x2 t = v[k] * (f32x2){-2.45546696f, -2.45546696f};
     e[2 * k] = t.x;
     e[2 * k + 1] = t.y;
   }
 #pragma unroll
-  for (int k = 0; k < 8; ++k) e[k] = __builtin_amdgcn_exp2f(e[k]);
+  for (int k = 0; k < 2 * NP; ++k) e[k] = __builtin_amdgcn_exp2f(e[k]);
 #pragma unroll
-  for (int k = 0; k < 8; ++k) e[k] = e[k] + 1.0f;
+  for (int k = 0; k < 2 * NP; ++k) e[k] = e[k] + 1.0f;
 #pragma unroll
-  for (int k = 0; k < 8; ++k) e[k] = __builtin_amdgcn_rcpf(e[k]);
+  for (int k = 0; k < 2 * NP; ++k) e[k] = __builtin_amdgcn_rcpf(e[k]);
 #pragma unroll
-  for (int k = 0; k < 4; ++k) v[k] = v[k] * (f32x2){e[2 * k], e[2 * k + 1]};
+  for (int k = 0; k < NP; ++k) v[k] = v[k] * (f32x2){e[2 * k], e[2 * k + 1]};
 }
+__device__ __forceinline__ void quick_gelu8_8q(f32x2 (&v)[4]) { quick_gelu_stage_8q<4>(v); }
 
 __device__ __forceinline__ void tile_coords_8q(int t, int tiles_m, int tiles_n, int ng, int& mb, int& nb) {
   if (ng <= 0 || ng >= tiles_n) {
@@ -408,6 +411,28 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
         asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(rab_c) : : "memory");
         if (mi < 7) asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(rab_n) : "v"(rab_a), "i"((mi + 1) * 128) : "memory");
       }
+      uint2 pkb[2][2];   // F_GSTAGE16: the block's 16 values through QuickGELU in one stage order
+      if (EK::GELU && (F & F_GSTAGE16)) {
+        f32x2 gw[8];
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+          f32x2 lo = (f32x2){acc[mi][ni][0], acc[mi][ni][1]};
+          f32x2 hi = (f32x2){acc[mi][ni][2], acc[mi][ni][3]};
+          if (EK::LN) {
+            const f32x2 ar = (f32x2){rab_c.x, rab_c.x}, br = (f32x2){-rab_c.y, -rab_c.y};
+            lo = ar * lo + (br * (f32x2){col[ni].x, col[ni].y} + (f32x2){bias[ni].x, bias[ni].y});
+            hi = ar * hi + (br * (f32x2){col[ni].z, col[ni].w} + (f32x2){bias[ni].z, bias[ni].w});
+          } else {
+            lo = lo + (f32x2){bias[ni].x, bias[ni].y};
+            hi = hi + (f32x2){bias[ni].z, bias[ni].w};
+          }
+          gw[2 * ni] = lo;
+          gw[2 * ni + 1] = hi;
+        }
+        quick_gelu_stage_8q<8>(gw);
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) pkb[ni >> 1][ni & 1] = make_uint2(pack_bf16x2(gw[2 * ni]), pack_bf16x2(gw[2 * ni + 1]));
+      }
 #pragma unroll
       for (int p = 0; p < 2; ++p) {
         uint2 pk[2];
@@ -415,6 +440,10 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
 #pragma unroll
         for (int qq = 0; qq < 2; ++qq) {
           const int ni = 2 * p + qq;
+          if (EK::GELU && (F & F_GSTAGE16)) {
+            pk[qq] = pkb[p][qq];
+            continue;
+          }
           f32x2 lo = (f32x2){acc[mi][ni][0], acc[mi][ni][1]};
           f32x2 hi = (f32x2){acc[mi][ni][2], acc[mi][ni][3]};
           if (EK::LN) {   // rstd * acc + (c_n - rstd * mean * s_n)
@@ -425,7 +454,7 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
             lo = lo + (f32x2){bias[ni].x, bias[ni].y};
             hi = hi + (f32x2){bias[ni].z, bias[ni].w};
           }
-          if (EK::GELU && (F & F_GSTAGE)) {
+          if (EK::GELU && (F & F_GSTAGE) && !(F & F_GSTAGE16)) {
             gv[2 * qq] = lo;
             gv[2 * qq + 1] = hi;
             continue;
@@ -436,7 +465,7 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
           }
           pk[qq] = make_uint2(pack_bf16x2(lo), pack_bf16x2(hi));
         }
-        if (EK::GELU && (F & F_GSTAGE)) {
+        if (EK::GELU && (F & F_GSTAGE) && !(F & F_GSTAGE16)) {
           quick_gelu8_8q(gv);
 #pragma unroll
           for (int qq = 0; qq < 2; ++qq) pk[qq] = make_uint2(pack_bf16x2(gv[2 * qq]), pack_bf16x2(gv[2 * qq + 1]));
@@ -732,13 +761,14 @@ hipError_t gemm_8q(const GemmArgs& a0, int epi, hipStream_t s, int cus, int mode
       hipLaunchKernelGGL((gemm_8q_kernel<EPI_LN_GELU_BF16, 0, 0, true>), dim3(grid), dim3(512), 0, s, a);
       return hipGetLastError();
     }
-    if (ff == 4 || ff == 8 || ff == 12) {
+    if (ff == 4 || ff == 8 || ff == 12 || ff == 44) {
 #define LNF(E, FL) hipLaunchKernelGGL((gemm_8q_kernel<E, 0, FL, true>), dim3(grid), dim3(512), 0, s, a)
       if (epi == EPI_LN_BF16) {
         if (ff == 4) LNF(EPI_LN_BF16, F_VOREC);
         else LNF(EPI_LN_BF16, F_VOREC);   // (no GELU: F_GSTAGE has nothing to reorder)
       } else if (ff == 4) LNF(EPI_LN_GELU_BF16, F_VOREC);
       else if (ff == 8) LNF(EPI_LN_GELU_BF16, F_GSTAGE);
+      else if (ff == 44) LNF(EPI_LN_GELU_BF16, F_GSTAGE16 | F_GSTAGE | F_VOREC);
       else LNF(EPI_LN_GELU_BF16, F_GSTAGE | F_VOREC);
 #undef LNF
       return hipGetLastError();
