@@ -57,7 +57,9 @@ def parse():
     ap.add_argument("--image-chunk", type=int, default=None)
     ap.add_argument("--weights", choices=["bf16", "fp8", "fp32"], default="bf16",
                     help="fp8: vision GEMMs on the MX-fp8 block-scaled MFMA (BASELINE configs[4]); "
-                         "fp32: the parity mode (every GEMM on the exact-f32 MFMA, model.float())")
+                         "fp32: the parity mode (model.float(): f32 activations and residual stream, every "
+                         "tower GEMM at f32-GEMM accuracy through split operands on the 16-bit MFMA; the "
+                         "exact-f32 MFMA GEMM is the A/B alternative, MICLIP_F32_SPLIT=0)")
     ap.add_argument("--no-parity-mode", action="store_true",
                     help="skip the fp32-tower (R@K parity mode) measurement beside the bf16 line")
     ap.add_argument("--parity-steps", type=int, default=3)
@@ -480,9 +482,11 @@ def mirror_timing(corpus, q, n, exact_us):
 
 def parity_mode(args, dev, pixels, tokens, Q, k, base, chunk):
     """The R@K parity mode: the same step on the
-    fp32 tower (`weights="fp32"`, openai/CLIP's fp32 arithmetic, every GEMM on
-    the exact-f32 MFMA), timed like the headline over --parity-steps steps,
-    with the roofline of its c_fc GEMM against the 157.3 TF f32 MFMA peak."""
+    fp32 tower (`weights="fp32"`, openai/CLIP's fp32 arithmetic: f32 activations
+    and residual stream, each tower GEMM as ONE 16-bit MFMA GEMM over split
+    operands with f32 accumulation, at f32-GEMM accuracy; the exact-f32 MFMA GEMM
+    is the A/B alternative), timed like the headline over --parity-steps steps,
+    with the roofline of its c_fc GEMM against the 16-bit MFMA peak it runs on."""
     import torch
     from miclip import api, retrieval
     model, _ = api.load(args.model, device=dev, image_chunk=chunk, weights="fp32")

@@ -9,6 +9,7 @@
 // ln_final at argmax(tokens) -> text_projection GEMM.
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstdarg>
 #include <cstdlib>
 #include <cstdio>
@@ -196,7 +197,9 @@ uint16_t f2h_host(float f) {
 //   W'[n][k] = f16(W[n][k] * gamma[k]),  s_n = sum_k W'[n][k],  c_n = b_n + sum_k beta[k] W[n][k]
 // (s from the rounded W', so that x W'^T - mean s = (x - mean) W'^T exactly; sums in double).
 // Appends W' (f16 [N][K]), s and c (f32 [N]) to the image; returns their offsets.
-void fold_ln(Builder& b, int64_t p_g, int64_t p_beta, int64_t p_w, int64_t p_bias, int N, int K, size_t& ow,
+// Returns false when a product W * gamma leaves the fp16 range (|W'| > 65504 rounds to inf) or a
+// column sum / constant is not finite: the caller then keeps the unfolded tower.
+bool fold_ln(Builder& b, int64_t p_g, int64_t p_beta, int64_t p_w, int64_t p_bias, int N, int K, size_t& ow,
              size_t& os, size_t& oc) {
   const float* g = b.src + p_g;
   const float* be = b.src + p_beta;
@@ -205,6 +208,7 @@ void fold_ln(Builder& b, int64_t p_g, int64_t p_beta, int64_t p_w, int64_t p_bia
   ow = b.align();
   b.img.resize(ow + (size_t)N * K * 2);
   std::vector<float> sv(N), cv(N);
+  bool finite = true;
   for (int n = 0; n < N; ++n) {
     uint16_t* d = (uint16_t*)(b.img.data() + ow) + (size_t)n * K;
     double ss = 0, cc = bias[n];
@@ -214,11 +218,13 @@ void fold_ln(Builder& b, int64_t p_g, int64_t p_beta, int64_t p_w, int64_t p_bia
       d[k] = h;
       _Float16 hv;
       memcpy(&hv, &h, 2);
+      finite = finite && std::isfinite((float)hv);
       ss += (double)(float)hv;
       cc += (double)be[k] * (double)wv;
     }
     sv[n] = (float)ss;
     cv[n] = (float)cc;
+    finite = finite && std::isfinite(sv[n]) && std::isfinite(cv[n]);
   }
   os = b.align();
   b.img.resize(os + (size_t)N * 4);
@@ -226,6 +232,7 @@ void fold_ln(Builder& b, int64_t p_g, int64_t p_beta, int64_t p_w, int64_t p_bia
   oc = b.align();
   b.img.resize(oc + (size_t)N * 4);
   memcpy(b.img.data() + oc, cv.data(), (size_t)N * 4);
+  return finite;
 }
 
 int64_t tower_numel(int64_t W, int64_t L) { return L * (W * 2 + 3 * W * W + 3 * W + W * W + W + 2 * W + 4 * W * W + 4 * W + 4 * W * W + W); }
@@ -368,10 +375,18 @@ int mi_clip_create(const mi_clip_arch* arch, const float* weights, int64_t numel
   }
   // bf16 vision tower: the LayerNorm-folded GEMM weights (run_tower_fold); W % 256 == 0 so
   // that all four GEMMs take the 8-phase kernel
+  // (all layers or none: a product W * gamma outside fp16's range, or a non-finite column sum,
+  // keeps the whole tower unfolded, run_tower)
   if (weight_dtype == MI_BF16 && W % 256 == 0) {
+    const size_t img0 = b.img.size();
+    bool ok = true;
     for (LayerOff& l : vlo) {
-      fold_ln(b, l.p_ln1_g, l.p_ln1_b, l.p_w_qkv, l.p_b_qkv, 3 * W, W, l.lw_qkv, l.ls_qkv, l.lc_qkv);
-      fold_ln(b, l.p_ln2_g, l.p_ln2_b, l.p_w_fc, l.p_b_fc, 4 * W, W, l.lw_fc, l.ls_fc, l.lc_fc);
+      ok = fold_ln(b, l.p_ln1_g, l.p_ln1_b, l.p_w_qkv, l.p_b_qkv, 3 * W, W, l.lw_qkv, l.ls_qkv, l.lc_qkv) && ok;
+      ok = fold_ln(b, l.p_ln2_g, l.p_ln2_b, l.p_w_fc, l.p_b_fc, 4 * W, W, l.lw_fc, l.ls_fc, l.lc_fc) && ok;
+    }
+    if (!ok) {
+      for (LayerOff& l : vlo) l.lw_qkv = l.ls_qkv = l.lc_qkv = l.lw_fc = l.ls_fc = l.lc_fc = 0;
+      b.img.resize(img0);
     }
   }
   hipError_t e = hipMalloc(&c->wdev, b.img.size());
@@ -452,10 +467,15 @@ int mi_clip_create(const mi_clip_arch* arch, const float* weights, int64_t numel
       }
       if (e6 == hipSuccess) e6 = hipDeviceSynchronize();
       if (e6 != hipSuccess) {
+        // no room (or no split): the exact-f32 GEMMs need none of these copies (run_tower_f32
+        // takes them when layers[0].s6_qkv is null), so the context is still usable
+        (void)hipGetLastError();
         if (c->w6) (void)hipFree(c->w6);
-        (void)hipFree(c->wdev);
-        delete c;
-        return fail(MI_ERR_HIP, "split-bf16 weights: %s", hipGetErrorString(e6));
+        c->w6 = nullptr;
+        for (int t = 0; t < 2; ++t)
+          for (Layer& L : t ? c->tl : c->vl) L.s6_qkv = L.s6_out = L.s6_fc = L.s6_proj = nullptr;
+        fprintf(stderr, "miclip: split-bf16 weights unavailable (%s); fp32 tower on the exact-f32 GEMM\n",
+                hipGetErrorString(e6));
       }
     }
   }
@@ -722,6 +742,7 @@ static int lnfold(int W) {
 static GemmArgs ln_args(mi_clip* c, const uint16_t* wf, const float* sv, const float* cv, void* out, int N, int M,
                         int W) {
   GemmArgs g = gargs((const uint16_t*)c->x, 2 * W, wf, W, cv, out, N, M, N, W);
+  g.variant = 0;   // the folded GEMMs have one schedule (gemm_bf16 rejects EPI_LN_* with a variant)
   g.a_f16 = 1;
   g.rs = c->rs;
   g.colv = sv;
@@ -1189,6 +1210,7 @@ int mi_op_gemm_ln(const void* x16, int64_t lda, const float* rs, const void* wf,
     return fail(MI_ERR_ARG, "mi_op_gemm_ln: bad arguments");
   if (M == 0) return MI_OK;
   GemmArgs g = gargs((const uint16_t*)x16, lda, (const uint16_t*)wf, K, colc, out, N, M, N, K);
+  g.variant = 0;   // one schedule for the folded GEMMs (an A/B MICLIP_GEMM_VARIANT does not apply)
   g.a_f16 = 1;
   g.rs = rs;
   g.colv = colsum;
@@ -1332,13 +1354,14 @@ int mi_jpeg_decode_transform(const uint8_t* data, int64_t data_bytes, const int6
     return fail(MI_ERR_ARG, "mi_jpeg_decode_transform: bad size / mode");
   if (out_dtype != MI_F32 && out_dtype != MI_BF16) return fail(MI_ERR_ARG, "mi_jpeg_decode_transform: out_dtype must be f32/bf16");
   if (B == 0) return MI_OK;
-  const JpegXform xf{n, mode, out_dtype == MI_BF16, out};
-  const hipError_t e = jpeg_decode(data, data_bytes, seg_off, seg_end, huff, huff_idx, nsets, qtab, geom, B, nullptr,
-                                   workspace, workspace_bytes, (hipStream_t)stream, &xf);
-  if (e == hipErrorInvalidValue)
+  // the fit check comes first, so no decode work is queued for a geometry the fused transform
+  // cannot take; every error after it is a HIP error
+  if (!jpeg_xform_fits(geom[1], geom[0], n, mode))
     return fail(MI_ERR_UNSUPPORTED, "mi_jpeg_decode_transform: %dx%d -> %d does not fit one LDS band: use "
                 "mi_jpeg_decode + mi_preprocess_frames", geom[0], geom[1], n);
-  HIP_TRY(e);
+  const JpegXform xf{n, mode, out_dtype == MI_BF16, out};
+  HIP_TRY(jpeg_decode(data, data_bytes, seg_off, seg_end, huff, huff_idx, nsets, qtab, geom, B, nullptr, workspace,
+                      workspace_bytes, (hipStream_t)stream, &xf));
   return MI_OK;
 }
 

@@ -73,6 +73,8 @@ constexpr int F_FULL = 2;   // epilogue stores of 8 whole 128-B rows (lane pairs
 constexpr int F_VOREC = 4;  // epilogue store offsets recomputed from the lane id (EPI_RES16 always)
 constexpr int F_GSTAGE = 8; // QuickGELU over a store's 8 values in stage order (quick_gelu8_8q)
 constexpr int F_GSTAGE16 = 32;   // the same over a 16-row block's 16 values (A/B)
+constexpr int F_ANT = 64;   // A-operand DMAs non-temporal (A/B: keep the weight panel in L2 against the A stream)
+constexpr int F_ONT = 128;  // output stores non-temporal (A/B)
 
 __device__ __forceinline__ f32x2 quick_gelu2_8q(f32x2 v) {
   const f32x2 t = v * (f32x2){-2.45546696f, -2.45546696f};   // -1.702 * log2(e)
@@ -221,7 +223,7 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
         glds16(src, dst + j * 1024);
       } else if (h == H_A0 || h == H_A1) {
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (LDS_AS void*)(dst + j * 1024), 16, h == H_A1 ? voA1[j] : voA0[j],
-                                                 kofs * 2, 0, 0);
+                                                 kofs * 2, 0, (F & F_ANT) ? 2 : 0);
       } else {
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rsW, (LDS_AS void*)(dst + j * 1024), 16, voB[j],
                                                  kofs * 2 + (h == H_B1 ? b1_sofs : 0), 0, 0);
@@ -490,8 +492,8 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
         dp[p] = d;
         if (F & F_FULL) continue;
         if (ABL == 10) asm volatile("" ::"v"(d));   // stamp probe without the stores
-        else if (p == 0) __builtin_amdgcn_raw_buffer_store_b128(d, rsO, vo + mi * blkO, 0, ABL == 13 ? 2 : 0);
-        else __builtin_amdgcn_raw_buffer_store_b128(d, rsO, vo + mi * blkO + 64, 0, ABL == 13 ? 2 : 0);
+        else if (p == 0) __builtin_amdgcn_raw_buffer_store_b128(d, rsO, vo + mi * blkO, 0, (ABL == 13 || (F & F_ONT)) ? 2 : 0);
+        else __builtin_amdgcn_raw_buffer_store_b128(d, rsO, vo + mi * blkO + 64, 0, (ABL == 13 || (F & F_ONT)) ? 2 : 0);
       }
       if (F & F_FULL) {
         const bool top = fr < 8;
@@ -761,14 +763,21 @@ hipError_t gemm_8q(const GemmArgs& a0, int epi, hipStream_t s, int cus, int mode
       hipLaunchKernelGGL((gemm_8q_kernel<EPI_LN_GELU_BF16, 0, 0, true>), dim3(grid), dim3(512), 0, s, a);
       return hipGetLastError();
     }
-    if (ff == 4 || ff == 8 || ff == 12 || ff == 44) {
+    // + 64: A DMAs non-temporal (F_ANT), + 128: output stores non-temporal (F_ONT)
+    if (ff == 4 || ff == 8 || ff == 12 || ff == 44 || ff == 64 || ff == 192 || ff == 76 || ff == 204 || ff == 108 ||
+        ff == 140) {
 #define LNF(E, FL) hipLaunchKernelGGL((gemm_8q_kernel<E, 0, FL, true>), dim3(grid), dim3(512), 0, s, a)
       if (epi == EPI_LN_BF16) {
-        if (ff == 4) LNF(EPI_LN_BF16, F_VOREC);
+        if (ff == 64 || ff == 76) LNF(EPI_LN_BF16, F_ANT);
+        else if (ff == 192 || ff == 204) LNF(EPI_LN_BF16, F_ANT | F_ONT);
         else LNF(EPI_LN_BF16, F_VOREC);   // (no GELU: F_GSTAGE has nothing to reorder)
       } else if (ff == 4) LNF(EPI_LN_GELU_BF16, F_VOREC);
       else if (ff == 8) LNF(EPI_LN_GELU_BF16, F_GSTAGE);
       else if (ff == 44) LNF(EPI_LN_GELU_BF16, F_GSTAGE16 | F_GSTAGE | F_VOREC);
+      else if (ff == 76 || ff == 64) LNF(EPI_LN_GELU_BF16, F_ANT | F_GSTAGE | F_VOREC);
+      else if (ff == 204 || ff == 192) LNF(EPI_LN_GELU_BF16, F_ONT | F_ANT | F_GSTAGE | F_VOREC);
+      else if (ff == 140) LNF(EPI_LN_GELU_BF16, F_ONT | F_GSTAGE | F_VOREC);
+      else if (ff == 108) LNF(EPI_LN_GELU_BF16, F_ANT | F_GSTAGE16 | F_GSTAGE | F_VOREC);
       else LNF(EPI_LN_GELU_BF16, F_GSTAGE | F_VOREC);
 #undef LNF
       return hipGetLastError();

@@ -99,6 +99,7 @@ struct JpegXform {
   int n, mode, out_bf16;
   void* out;
 };
+bool jpeg_xform_fits(int H, int W, int n, int mode);
 hipError_t jpeg_decode(const uint8_t* data, int64_t data_bytes, const int64_t* seg_off, const int64_t* seg_end,
                        const void* huff, const int32_t* huff_idx, int nsets, const uint16_t* qtab, const int32_t* geom,
                        int nframes, uint8_t* out_rgb, void* ws, size_t ws_bytes, hipStream_t s,

@@ -1546,6 +1546,14 @@ hipError_t jpeg_xform_plan(int H, int W, int n, int mode, XformK& xk, size_t& ld
   return hipErrorInvalidValue;   // a source too wide / tall for one band in LDS: decode + preprocess instead
 }
 
+// Whether the fused transform has a launch plan for H x W -> n (mi_jpeg_decode_transform checks
+// this before any decode work is queued)
+bool jpeg_xform_fits(int H, int W, int n, int mode) {
+  XformK xk{};
+  size_t lds = 0;
+  return jpeg_xform_plan(H, W, n, mode, xk, lds) == hipSuccess;
+}
+
 // Host launch: see include/miclip.h mi_jpeg_decode for the argument contract.
 hipError_t jpeg_decode(const uint8_t* data, int64_t data_bytes, const int64_t* seg_off, const int64_t* seg_end,
                        const void* huff, const int32_t* huff_idx, int nsets, const uint16_t* qtab, const int32_t* geom,

@@ -58,8 +58,10 @@ def mfma_pass(root):
         c = per[k]
         cyc = c.get("GRBM_GUI_ACTIVE", 0.0) / 8
         busy = c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / (cyc * 1024) if cyc else None
+        hit, miss = c.get("TCC_HIT_sum"), c.get("TCC_MISS_sum")
         out.append({"mfma_busy": busy, "clock_ghz": cyc / dur[k] / 1e9 if k in dur and dur[k] > 0 else None,
-                    "us": dur[k] * 1e6 if k in dur else None})
+                    "us": dur[k] * 1e6 if k in dur else None,
+                    "l2_hit": hit / (hit + miss) if hit is not None and miss is not None and hit + miss > 0 else None})
     return out
 
 
@@ -90,10 +92,14 @@ def main():
                 res[name]["mfma_busy"] = round(sum(x["mfma_busy"] for x in m) / len(m), 4)
                 ck = [x["clock_ghz"] for x in m if x["clock_ghz"]]
                 res[name]["clock_ghz_mfma_pass"] = round(sum(ck) / len(ck), 3) if ck else None
+                hr = [x["l2_hit"] for x in m if x.get("l2_hit") is not None]
+                if hr:
+                    res[name]["l2_hit_rate"] = round(sum(hr) / len(hr), 4)
     json.dump(res, open(out, "w"), indent=1)
     for k, v in res.items():
         print(k, v["traffic_bytes"] / 1e6, "MB vs", v["algorithmic_bytes"] / 1e6, "MB alg",
-              v["traffic_over_algorithmic"], "mfma busy", v.get("mfma_busy"))
+              v["traffic_over_algorithmic"], "fetch/operands", round(v["fetch_bytes"] / (2 * (SHAPES[k][0] * SHAPES[k][2]
+              + SHAPES[k][1] * SHAPES[k][2])), 2), "mfma busy", v.get("mfma_busy"), "L2 hit", v.get("l2_hit_rate"))
 
 
 if __name__ == "__main__":
