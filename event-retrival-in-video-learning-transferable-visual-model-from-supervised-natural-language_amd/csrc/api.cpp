@@ -68,6 +68,10 @@ struct Layer {
   const float *f_qkv = nullptr, *f_out = nullptr, *f_fc = nullptr, *f_proj = nullptr;
   // ... and split into three bf16 terms, [N][6K] (split6_rows role 1): the split-bf16 GEMMs
   const uint16_t *s6_qkv = nullptr, *s6_out = nullptr, *s6_fc = nullptr, *s6_proj = nullptr;
+  // ... or split into two fp16 terms, [N][3K] (split2h_rows role 1) + their column scales: the
+  // split-f16 GEMMs (the default since round 5)
+  const uint16_t *h3_qkv = nullptr, *h3_out = nullptr, *h3_fc = nullptr, *h3_proj = nullptr;
+  const float *c3_qkv = nullptr, *c3_out = nullptr, *c3_fc = nullptr, *c3_proj = nullptr;
   // MX-fp8 copies (weight_dtype MI_FP8, vision tower): e4m3 codes + stage-major e8m0 scales
   const uint8_t *q_qkv = nullptr, *s_qkv = nullptr, *q_out = nullptr, *s_out = nullptr;
   const uint8_t *q_fc = nullptr, *s_fc = nullptr, *q_proj = nullptr, *s_proj = nullptr;
@@ -249,7 +253,11 @@ struct mi_clip {
   int Kp32 = 0;           // f32 mode: conv1 K padded to the f32 GEMM's 32-k stage
   const float *conv_f = nullptr, *vproj_f = nullptr, *tproj_f = nullptr;
   char* wq = nullptr;     // MX-fp8 weight copies
-  char* w6 = nullptr;     // f32 mode: split-bf16 weight copies (Layer::s6_*)
+  char* w6 = nullptr;     // f32 mode, A/B: split-bf16 weight copies (Layer::s6_*)
+  char* w3 = nullptr;     // f32 mode: split-f16 weight copies + column scales (Layer::h3_* / c3_*, conv_h3)
+  const uint16_t* conv_h3 = nullptr;
+  const float* conv_c3 = nullptr;
+  float* rsc = nullptr;   // f32 mode: row scales of the split-f16 activations (workspace)
   uint16_t* a6 = nullptr; // f32 mode: split-bf16 activations of one GEMM, [M][6K] (workspace)
   // vision
   const uint16_t* conv_w = nullptr;
@@ -293,6 +301,8 @@ static hipError_t ws_release(mi_clip* c, hipStream_t s) {
   c->ws_used = true;
   return hipEventRecord(c->ws_evt, s);
 }
+
+static int f32_gemm_mode();
 
 extern "C" {
 
@@ -443,20 +453,56 @@ int mi_clip_create(const mi_clip_arch* arch, const float* weights, int64_t numel
   conv_layers(vlo, c->vl);
   conv_layers(tlo, c->tl);
   if (full) {
-    // split-bf16 copies of every tower GEMM weight (run_tower_f32): [N][6K] bf16, 144 W^2 bytes
-    // per layer; they need N % 128 == 0 and 6K % 64 == 0 (gemm_bf16), true for W % 128 == 0
+    // the GEMM operands of the fp32 tower (run_tower_f32): split-f16 copies of every tower GEMM
+    // weight and of conv1 ([N][3K] fp16 + column scales, 72 W^2 bytes per layer; the default), or
+    // split-bf16 copies ([N][6K] bf16, 144 W^2; A/B, MICLIP_F32_SPLIT=6).  They need N % 128 == 0
+    // and K' % 32 == 0 (gemm_bf16), true for W % 128 == 0.  When the copies cannot be built the
+    // exact-f32 GEMM runs instead (it needs none of them).
     const int64_t Wv = a.vision_width, Wt = a.text_width;
-    if (Wv % 128 == 0 && Wt % 128 == 0) {
+    const int mode = f32_gemm_mode();
+    hipError_t e3 = hipSuccess;
+    if (mode == 3) {
+      const int64_t Kc = c->Kp32;
+      size_t bytes = (size_t)(Wv * 3 * Kc * 2 + Wv * 4 + 512);
+      for (int t = 0; t < 2; ++t) {
+        const int64_t W = t ? Wt : Wv;
+        bytes += (size_t)(t ? c->tl.size() : c->vl.size()) * (size_t)(72 * W * W + 36 * W + 8 * 256);
+      }
+      e3 = hipMalloc(&c->w3, bytes);
+      char* p3 = c->w3;
+      auto split = [&](const float* w, int64_t N, int64_t K, const uint16_t** o, const float** cs) {
+        uint16_t* ow = (uint16_t*)p3;
+        p3 += ((size_t)N * 3 * K * 2 + 255) & ~(size_t)255;
+        float* oc = (float*)p3;
+        p3 += ((size_t)N * 4 + 255) & ~(size_t)255;
+        if (e3 == hipSuccess) e3 = split2h_rows(w, K, N, (int)K, 1, 0, ow, oc, nullptr);
+        *o = ow;
+        *cs = oc;
+      };
+      if (e3 == hipSuccess) {
+        split(c->conv_f, Wv, Kc, &c->conv_h3, &c->conv_c3);
+        for (int t = 0; t < 2; ++t) {
+          const int64_t W = t ? Wt : Wv;
+          for (Layer& L : t ? c->tl : c->vl) {
+            split(L.f_qkv, 3 * W, W, &L.h3_qkv, &L.c3_qkv);
+            split(L.f_out, W, W, &L.h3_out, &L.c3_out);
+            split(L.f_fc, 4 * W, W, &L.h3_fc, &L.c3_fc);
+            split(L.f_proj, W, 4 * W, &L.h3_proj, &L.c3_proj);
+          }
+        }
+      }
+      if (e3 == hipSuccess) e3 = hipDeviceSynchronize();
+    } else if (mode == 6) {
       const size_t bytes = (size_t)(144 * Wv * Wv * (int64_t)c->vl.size() + 144 * Wt * Wt * (int64_t)c->tl.size());
-      hipError_t e6 = hipMalloc(&c->w6, bytes);
+      e3 = hipMalloc(&c->w6, bytes);
       char* p6 = c->w6;
       auto split = [&](const float* w, int64_t N, int64_t K) -> const uint16_t* {
         uint16_t* o = (uint16_t*)p6;
         p6 += (size_t)N * 6 * K * 2;
-        if (e6 == hipSuccess) e6 = split6_rows(w, K, N, (int)K, 1, 0, o, nullptr);
+        if (e3 == hipSuccess) e3 = split6_rows(w, K, N, (int)K, 1, 0, o, nullptr);
         return o;
       };
-      for (int t = 0; t < 2 && e6 == hipSuccess; ++t) {
+      for (int t = 0; t < 2 && e3 == hipSuccess; ++t) {
         const int64_t W = t ? Wt : Wv;
         for (Layer& L : t ? c->tl : c->vl) {
           L.s6_qkv = split(L.f_qkv, 3 * W, W);
@@ -465,18 +511,24 @@ int mi_clip_create(const mi_clip_arch* arch, const float* weights, int64_t numel
           L.s6_proj = split(L.f_proj, W, 4 * W);
         }
       }
-      if (e6 == hipSuccess) e6 = hipDeviceSynchronize();
-      if (e6 != hipSuccess) {
-        // no room (or no split): the exact-f32 GEMMs need none of these copies (run_tower_f32
-        // takes them when layers[0].s6_qkv is null), so the context is still usable
-        (void)hipGetLastError();
-        if (c->w6) (void)hipFree(c->w6);
-        c->w6 = nullptr;
-        for (int t = 0; t < 2; ++t)
-          for (Layer& L : t ? c->tl : c->vl) L.s6_qkv = L.s6_out = L.s6_fc = L.s6_proj = nullptr;
-        fprintf(stderr, "miclip: split-bf16 weights unavailable (%s); fp32 tower on the exact-f32 GEMM\n",
-                hipGetErrorString(e6));
-      }
+      if (e3 == hipSuccess) e3 = hipDeviceSynchronize();
+    }
+    if (e3 != hipSuccess) {
+      // no room (or no split): the exact-f32 GEMMs need none of these copies, so the context is
+      // still usable
+      (void)hipGetLastError();
+      if (c->w6) (void)hipFree(c->w6);
+      if (c->w3) (void)hipFree(c->w3);
+      c->w6 = c->w3 = nullptr;
+      c->conv_h3 = nullptr;
+      c->conv_c3 = nullptr;
+      for (int t = 0; t < 2; ++t)
+        for (Layer& L : t ? c->tl : c->vl) {
+          L.s6_qkv = L.s6_out = L.s6_fc = L.s6_proj = nullptr;
+          L.h3_qkv = L.h3_out = L.h3_fc = L.h3_proj = nullptr;
+        }
+      fprintf(stderr, "miclip: split GEMM weights unavailable (%s); fp32 tower on the exact-f32 GEMM\n",
+              hipGetErrorString(e3));
     }
   }
   if (weight_dtype == MI_FP8) {
@@ -526,6 +578,7 @@ int mi_clip_destroy(mi_clip* c) {
     if (c->wdev) (void)hipFree(c->wdev);
     if (c->wq) (void)hipFree(c->wq);
     if (c->w6) (void)hipFree(c->w6);
+    if (c->w3) (void)hipFree(c->w3);
     if (c->ws_evt) (void)hipEventDestroy(c->ws_evt);
   }
   delete c;
@@ -555,8 +608,12 @@ static int reserve_locked(mi_clip* c, int64_t ic, int64_t tc) {
   const size_t o_cls = carve((size_t)rows_max * mx(Wv, Wt) * es);
   const size_t o_y = carve((size_t)rows_max * a.embed_dim * 4);
   const size_t o_rs = carve((size_t)(Mv + 256) * 8);
-  // f32 mode, split-bf16 GEMMs: the widest A operand, c_proj's [M][6 * 4W]
-  const size_t o_a6 = c->w6 ? carve((size_t)mx(Mv * Wv, Mt * Wt) * 24 * 2) : carve(0);
+  // f32 mode, split GEMM operands: the widest A operand, c_proj's [M][6 * 4W] bf16 (split-bf16)
+  // or [M][3 * 4W] fp16 (split-f16), and conv1's patches [ic G^2][3 Kp32] fp16; + row scales
+  const bool split_ops = c->w6 || c->w3;
+  const size_t o_a6 = split_ops ? carve((size_t)mx(mx(Mv * Wv, Mt * Wt) * 24 * 2, ic * c->G * c->G * 3 * c->Kp32 * 2))
+                                : carve(0);
+  const size_t o_rsc = c->w3 ? carve((size_t)mx(mx(Mv, Mt), ic * c->G * c->G) * 4) : carve(0);
   size_t o_hq = 0, o_hqs = 0, o_attq = 0, o_attqs = 0, o_mlpq = 0, o_mlpqs = 0;
   if (c->fp8) {
     const size_t mp = (size_t)((Mv + 1) & ~1);
@@ -585,7 +642,8 @@ static int reserve_locked(mi_clip* c, int64_t ic, int64_t tc) {
   c->cls_ln = (uint16_t*)(ws + o_cls);
   c->y = (float*)(ws + o_y);
   c->rs = (float*)(ws + o_rs);
-  c->a6 = c->w6 ? (uint16_t*)(ws + o_a6) : nullptr;
+  c->a6 = split_ops ? (uint16_t*)(ws + o_a6) : nullptr;
+  c->rsc = c->w3 ? (float*)(ws + o_rsc) : nullptr;
   if (c->fp8) {
     c->hq = (uint8_t*)(ws + o_hq);
     c->hqs = (uint8_t*)(ws + o_hqs);
@@ -833,11 +891,15 @@ static int run_tower_mx(mi_clip* c, const std::vector<Layer>& layers, int B, int
 
 static size_t dtype_size(int dt) { return dt == MI_F32 ? 4 : 2; }
 
-// fp32 tower GEMMs as split-bf16 GEMMs (the default); MICLIP_F32_SPLIT=0 (A/B build) runs
-// precise.hip's exact-f32 MFMA GEMM instead
-static bool split6_on() {
+// The fp32 tower's GEMMs (run_tower_f32): 3 = split-f16 operands on the f16 MFMA (the
+// default since round 5, K' = 3K), 6 = split-bf16 operands (round 4, K' = 6K), 0 = the exact-f32
+// MFMA GEMM (precise.hip gemm_f32).  MICLIP_F32_SPLIT selects one in the A/B build (read when a
+// context is created: the weight copies are built for the mode).
+static int f32_gemm_mode() {
   const char* e = ab_getenv("MICLIP_F32_SPLIT");
-  return e ? atoi(e) != 0 : true;
+  if (!e) return 3;
+  const int v = atoi(e);
+  return v == 0 || v == 6 ? v : 3;
 }
 
 // The fp32 tower (weight_dtype MI_F32; kernels in precise.hip).  openai/CLIP
@@ -852,7 +914,35 @@ static int run_tower_f32(mi_clip* c, const std::vector<Layer>& layers, int B, in
   float* qkv = (float*)c->qkv;
   float* att = (float*)c->att;
   float* mlp = (float*)c->mlp;
-  if (c->a6 && layers.size() && layers[0].s6_qkv && split6_on()) {
+  if (c->a6 && c->rsc && layers.size() && layers[0].h3_qkv) {
+    // split-f16 GEMMs (split2h_rows): one f16 GEMM over K' = 3K per linear layer, a1 w1 + a1 w2 +
+    // a2 w1 in f32 with the row / column scales in the epilogue -- f32-grade results; ln_1 / ln_2
+    // write the split operand directly (layernorm_split2h), attention's and c_fc's outputs are
+    // split by one pass each (c_proj's with QuickGELU applied first)
+    uint16_t* a3 = c->a6;
+    float* rsc = c->rsc;
+    auto gemm3 = [&](int K, const uint16_t* w3, const float* c3, const float* b, float* out, int N, int epi) -> int {
+      GemmArgs g = gargs(a3, 3 * K, w3, 3 * K, b, out, N, M, N, 3 * K);
+      g.a_f16 = 1;
+      g.rsc = rsc;
+      g.csc = c3;
+      HIP_TRY(gemm_bf16(g, epi, s));
+      return MI_OK;
+    };
+    for (const Layer& L : layers) {
+      HIP_TRY(layernorm_split2h(c->x, W, L.ln1_g, L.ln1_b, M, W, a3, rsc, s));
+      MI_TRY(gemm3(W, L.h3_qkv, L.c3_qkv, L.b_qkv, qkv, 3 * W, EPI_F32));
+      HIP_TRY(attention_f32(qkv, att, B, S, W, causal, s));
+      HIP_TRY(split2h_rows(att, W, M, W, 0, 0, a3, rsc, s));
+      MI_TRY(gemm3(W, L.h3_out, L.c3_out, L.b_out, c->x, W, EPI_RESID_F32));
+      HIP_TRY(layernorm_split2h(c->x, W, L.ln2_g, L.ln2_b, M, W, a3, rsc, s));
+      MI_TRY(gemm3(W, L.h3_fc, L.c3_fc, L.b_fc, mlp, 4 * W, EPI_F32));   // pre-activation
+      HIP_TRY(split2h_rows(mlp, 4 * W, M, 4 * W, 0, 1, a3, rsc, s));       // QuickGELU, then split
+      MI_TRY(gemm3(4 * W, L.h3_proj, L.c3_proj, L.b_proj, c->x, W, EPI_RESID_F32));
+    }
+    return MI_OK;
+  }
+  if (c->a6 && layers.size() && layers[0].s6_qkv) {
     // split-bf16 GEMMs (split6_rows): one bf16 GEMM over K' = 6K per linear layer, every product
     // term to 2^-16 relative, f32 accumulation -- f32-grade results at bf16 MFMA rates
     uint16_t* a6 = c->a6;
@@ -892,8 +982,21 @@ static int encode_image_f32(mi_clip* c, const char* px, int nb, int in_dtype, ch
   const int G2 = c->G * c->G;
   float* patches = (float*)c->patches;
   HIP_TRY(im2col_f32(px, in_dtype == MI_BF16, patches, nb, R, P, c->Kp32, s));
-  HIP_TRY(gemm_f32(patches, c->Kp32, c->conv_f, c->Kp32, nullptr, c->x, W, nb * G2, W, c->Kp32, EPI_F32, s, G2, S,
-                   1));
+  if (c->conv_h3 && c->a6 && c->rsc) {   // conv1 as a split-f16 GEMM (rows remapped past CLS)
+    const int K = c->Kp32;
+    HIP_TRY(split2h_rows(patches, K, (int64_t)nb * G2, K, 0, 0, c->a6, c->rsc, s));
+    GemmArgs g = gargs(c->a6, 3 * K, c->conv_h3, 3 * K, nullptr, c->x, W, nb * G2, W, 3 * K);
+    g.a_f16 = 1;
+    g.rsc = c->rsc;
+    g.csc = c->conv_c3;
+    g.group = G2;
+    g.gstride = S;
+    g.goffset = 1;
+    HIP_TRY(gemm_bf16(g, EPI_F32, s));
+  } else {
+    HIP_TRY(gemm_f32(patches, c->Kp32, c->conv_f, c->Kp32, nullptr, c->x, W, nb * G2, W, c->Kp32, EPI_F32, s, G2, S,
+                     1));
+  }
   HIP_TRY(vision_embed_ln(c->x, c->cls, c->vpos, c->ln_pre_g, c->ln_pre_b, nb, S, W, s));
   int r = run_tower_f32(c, c->vl, nb, S, W, 0, s);
   if (r) return r;
@@ -1194,6 +1297,36 @@ int mi_op_split6(const float* x, int64_t ldx, int64_t rows, int32_t K, int32_t r
   if (!x || !out || rows < 0 || (role & ~1) || (gelu & ~1)) return fail(MI_ERR_ARG, "mi_op_split6: bad arguments");
   if (K < 4 || K % 4 || ldx < K || ldx % 4) return fail(MI_ERR_UNSUPPORTED, "mi_op_split6: K %% 4 == 0, ldx >= K, ldx %% 4 == 0");
   HIP_TRY(split6_rows(x, ldx, rows, K, role, gelu, (uint16_t*)out, (hipStream_t)stream));
+  return MI_OK;
+}
+
+int mi_op_split2h(const float* x, int64_t ldx, int64_t rows, int32_t K, int32_t role, int32_t gelu, void* out,
+                  float* scale, void* stream) {
+  if (!x || !out || !scale || rows < 0 || (role & ~1) || (gelu & ~1)) return fail(MI_ERR_ARG, "mi_op_split2h: bad arguments");
+  if (K < 4 || K > 4096 || K % 4 || ldx < K || ldx % 4)
+    return fail(MI_ERR_UNSUPPORTED, "mi_op_split2h: 4 <= K <= 4096, K %% 4 == 0, ldx >= K, ldx %% 4 == 0");
+  HIP_TRY(split2h_rows(x, ldx, rows, K, role, gelu, (uint16_t*)out, scale, (hipStream_t)stream));
+  return MI_OK;
+}
+
+int mi_op_gemm_split2h(const void* A3, const void* W3, const float* a_scale, const float* w_scale, const float* bias,
+                       float* out, int32_t M, int32_t N, int32_t K3, int32_t epi, void* stream) {
+  if (!A3 || !W3 || !a_scale || !w_scale || !out || M < 0 || N < 1 || K3 < 1 || (epi != EPI_F32 && epi != EPI_RESID_F32))
+    return fail(MI_ERR_ARG, "mi_op_gemm_split2h: bad arguments");
+  if (N % 128 || K3 % 32) return fail(MI_ERR_UNSUPPORTED, "mi_op_gemm_split2h: N %% 128 == 0, K3 %% 32 == 0");
+  GemmArgs g = gargs((const uint16_t*)A3, K3, (const uint16_t*)W3, K3, bias, out, N, M, N, K3);
+  g.variant = 0;
+  g.a_f16 = 1;
+  g.rsc = a_scale;
+  g.csc = w_scale;
+  HIP_TRY(gemm_bf16(g, epi, (hipStream_t)stream));
+  return MI_OK;
+}
+
+int mi_op_attention_f32(const float* qkv, float* out, int32_t B, int32_t S, int32_t W, int32_t causal, void* stream) {
+  if (!qkv || !out || B < 0 || S < 1 || W < 64 || (causal & ~1)) return fail(MI_ERR_ARG, "mi_op_attention_f32: bad arguments");
+  if (W % 64) return fail(MI_ERR_UNSUPPORTED, "mi_op_attention_f32: W %% 64 == 0");
+  HIP_TRY(attention_f32(qkv, out, B, S, W, causal, (hipStream_t)stream));
   return MI_OK;
 }
 

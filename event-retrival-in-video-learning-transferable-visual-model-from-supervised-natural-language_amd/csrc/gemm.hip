@@ -87,6 +87,17 @@ __device__ __forceinline__ void tile_coords(int t, int tiles_m, int tiles_n, int
   nb = g * ng + r % ngg;
 }
 
+template <bool V>
+struct BoolT {};
+typedef _Float16 f16x8_g __attribute__((ext_vector_type(8)));
+// one 16x16x32 MFMA on bf16 or (split-f16 operands) fp16 fragments of the same bytes
+__device__ __forceinline__ f32x4 mfma16(BoolT<false>, bf16x8 b, bf16x8 a, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(b, a, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mfma16(BoolT<true>, bf16x8 b, bf16x8 a, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_g, b), __builtin_bit_cast(f16x8_g, a), c, 0, 0, 0);
+}
+
 template <int N>
 __device__ __forceinline__ void wait_vm_barrier() {
   // retire all but the N youngest vector-memory ops of this wave, then a raw
@@ -94,7 +105,8 @@ __device__ __forceinline__ void wait_vm_barrier() {
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"i"(N) : "memory");
 }
 
-template <int EPI, int BM, int BN, int WAVES_M, int WAVES_N>
+// F16: fp16 operands on the f16 MFMA (split-f16 operands of the fp32 tower, GemmArgs rsc / csc)
+template <int EPI, int BM, int BN, int WAVES_M, int WAVES_N, bool F16 = false>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_kernel(GemmArgs a) {
   constexpr int NT = 64 * WAVES_M * WAVES_N;
   constexpr int NWAVES = WAVES_M * WAVES_N;
@@ -191,7 +203,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_kernel(GemmArgs a
       for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
         for (int ni = 0; ni < NI; ++ni)
-          acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[ni], af[mi], acc[mi][ni], 0, 0, 0);
+          acc[mi][ni] = mfma16(BoolT<F16>{}, bfr[ni], af[mi], acc[mi][ni]);
     }
 
     // ---------------------------------------------------------- epilogue
@@ -201,15 +213,24 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_kernel(GemmArgs a
     float4 bias[NI];
 #pragma unroll
     for (int ni = 0; ni < NI; ++ni) bias[ni] = lds_read_f4(sbias + n0 + wc * WTN + ni * 16 + 4 * (lane >> 4));
+    float4 csc[NI];
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni)
+      csc[ni] = F16 ? *(const float4*)(a.csc + n0 + wc * WTN + ni * 16 + 4 * (lane >> 4)) : make_float4(1.f, 1.f, 1.f, 1.f);
 #pragma unroll
     for (int mi = 0; mi < MI; ++mi) {
       const int m = m0 + wr * WTM + mi * 16 + (lane & 15);
       if (tail && m >= a.M) continue;
       int64_t orow = m;
       if (a.group) orow = (int64_t)(m / a.group) * a.gstride + a.goffset + m % a.group;
+      const float rs = F16 ? a.rsc[m] : 1.f;
 #pragma unroll
       for (int ni = 0; ni < NI; ++ni) {
         const int n = n0 + wc * WTN + ni * 16 + 4 * (lane >> 4);
+        if (F16) {   // split-f16 operands: 1 / (s_row s_col), exact (powers of two)
+          acc[mi][ni][0] *= rs * csc[ni].x; acc[mi][ni][1] *= rs * csc[ni].y;
+          acc[mi][ni][2] *= rs * csc[ni].z; acc[mi][ni][3] *= rs * csc[ni].w;
+        }
         float v0 = acc[mi][ni][0] + bias[ni].x, v1 = acc[mi][ni][1] + bias[ni].y;
         float v2 = acc[mi][ni][2] + bias[ni].z, v3 = acc[mi][ni][3] + bias[ni].w;
         if (EPI == EPI_BF16 || EPI == EPI_GELU_BF16) {
@@ -260,7 +281,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_kernel(GemmArgs a
 // row (channel st / 32, patch row st % 32), so the DMA source of row m at
 // stage st is pix(m) + (st >> 5) * R^2 + (st & 31) * R: the im2col gather
 // rides on the LDS-DMA address and no patch matrix is written or read.
-template <int EPI, int CL, bool PRIO, bool DIRECT = false, bool NTS = false, bool PATCH = false>
+template <int EPI, int CL, bool PRIO, bool DIRECT = false, bool NTS = false, bool PATCH = false, bool F16 = false>
 __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs a) {
   constexpr int BM = 256, BN = 256, NT = 512;
   constexpr int WTM = 128, WTN = 64;
@@ -344,7 +365,7 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs a) {
     for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
       for (int ni = 0; ni < 4; ++ni)
-        acc[mbase + mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[ni], af[(mbase % (8 / CL)) + mi], acc[mbase + mi][ni], 0, 0, 0);
+        acc[mbase + mi][ni] = mfma16(BoolT<F16>{}, bfr[ni], af[(mbase % (8 / CL)) + mi], acc[mbase + mi][ni]);
     if (PRIO) __builtin_amdgcn_s_setprio(0);
     (void)count;
   };
@@ -475,19 +496,27 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs a) {
     }
   } else {
     constexpr int RS = BN * 4 + 16;
+    float4 csc[4];   // split-f16 operands: 1 / (s_row s_col) on the accumulator (exact)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni)
+      csc[ni] = F16 ? *(const float4*)(a.csc + n0 + wc * WTN + ni * 16 + 4 * (lane >> 4)) : make_float4(1.f, 1.f, 1.f, 1.f);
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
       if (wr == p) {
 #pragma unroll
-        for (int mi = 0; mi < 8; ++mi)
+        for (int mi = 0; mi < 8; ++mi) {
+          const int mr = min(m0 + wr * WTM + mi * 16 + (lane & 15), a.M - 1);
+          const float rs = F16 ? a.rsc[mr] : 1.f;
 #pragma unroll
           for (int ni = 0; ni < 4; ++ni) {
             const int r = mi * 16 + (lane & 15);
             const int c = wc * WTN + ni * 16 + 4 * (lane >> 4);
+            f32x4 v = acc[mi][ni];
+            if (F16) v = v * (f32x4){rs * csc[ni].x, rs * csc[ni].y, rs * csc[ni].z, rs * csc[ni].w};
             *(float4*)(smem + r * RS + c * 4) =
-                make_float4(acc[mi][ni][0] + bias[ni].x, acc[mi][ni][1] + bias[ni].y, acc[mi][ni][2] + bias[ni].z,
-                            acc[mi][ni][3] + bias[ni].w);
+                make_float4(v[0] + bias[ni].x, v[1] + bias[ni].y, v[2] + bias[ni].z, v[3] + bias[ni].w);
           }
+        }
       }
       __syncthreads();
       constexpr int C4 = BN / 4;
@@ -1048,6 +1077,23 @@ hipError_t launch(const GemmArgs& a, hipStream_t s) {
     if (!big || a.K != 3 * 32 * 32 || (a.patch_R & 31)) return hipErrorInvalidValue;
     const int nt = ((a.M + 255) / 256) * (a.N / 256);
     hipLaunchKernelGGL((gemm_pp_kernel<EPI, 1, false, false, false, true>), dim3(nt), dim3(512), 0, s, a);
+    return hipGetLastError();
+  }
+  if (a.a_f16) {   // split-f16 operands (fp32 tower): f32 epilogues with the rsc / csc factors
+    if ((EPI != EPI_F32 && EPI != EPI_RESID_F32) || !a.rsc || !a.csc || a.variant) return hipErrorInvalidValue;
+    if constexpr (EPI == EPI_F32 || EPI == EPI_RESID_F32) {
+      const int ntf = ((a.M + 255) / 256) * (a.N / 256);
+      if (big && a.K / BK >= LEAD) {
+        hipLaunchKernelGGL((gemm_pp_kernel<EPI, 1, false, false, false, false, true>), dim3(ntf), dim3(512), 0, s, a);
+      } else if (big) {
+        const int g = ntf < cu_count() ? ntf : cu_count();
+        hipLaunchKernelGGL((gemm_kernel<EPI, 256, 256, 2, 4, true>), dim3(g), dim3(512), 0, s, a);
+      } else {
+        const int nt2 = ((a.M + 127) / 128) * (a.N / 128);
+        const int g = nt2 < 2 * cu_count() ? nt2 : 2 * cu_count();
+        hipLaunchKernelGGL((gemm_kernel<EPI, 128, 128, 2, 2, true>), dim3(g), dim3(256), 0, s, a);
+      }
+    }
     return hipGetLastError();
   }
 #if MICLIP_AB

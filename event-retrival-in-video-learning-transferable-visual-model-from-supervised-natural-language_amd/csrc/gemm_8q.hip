@@ -783,10 +783,14 @@ hipError_t gemm_8q(const GemmArgs& a0, int epi, hipStream_t s, int cus, int mode
       return hipGetLastError();
     }
 #endif
-    // c_fc: QuickGELU in stage order + store offsets from the lane id (bit-identical; lnfc500
-    // 2281 vs 2318 us, profiles/r04_ag_lnflags.log); in_proj: no difference, kept as it was
+    // c_fc: QuickGELU in stage order over each 16-row block's 16 values + store offsets from the
+    // lane id (bit-identical; lnfc500 2281 vs 2318 us for the 8-value order against none,
+    // profiles/r04_ag_lnflags.log; the 16-value order 2296 vs 2354 us, profiles/r05_a_lnfc.log);
+    // in_proj: no difference, kept as it was
     if (epi == EPI_LN_BF16) hipLaunchKernelGGL((gemm_8q_kernel<EPI_LN_BF16, 0, 0, true>), dim3(grid), dim3(512), 0, s, a);
-    else hipLaunchKernelGGL((gemm_8q_kernel<EPI_LN_GELU_BF16, 0, F_GSTAGE | F_VOREC, true>), dim3(grid), dim3(512), 0, s, a);
+    else
+      hipLaunchKernelGGL((gemm_8q_kernel<EPI_LN_GELU_BF16, 0, F_GSTAGE16 | F_GSTAGE | F_VOREC, true>), dim3(grid),
+                         dim3(512), 0, s, a);
     return hipGetLastError();
   }
   if (a.a_f16) return hipErrorInvalidValue;

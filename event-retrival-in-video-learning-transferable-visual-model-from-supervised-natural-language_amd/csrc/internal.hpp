@@ -78,6 +78,10 @@ struct GemmArgs {
   const float* rs = nullptr;     // [M + 256][2] (rstd, rstd * mean) per row
   const float* colv = nullptr;   // [N] s_n
   float* ps = nullptr;           // EPI_RES16_BF16: [M][N / 64][2] row partial statistics
+  // split-f16 operands (split2h_rows; a_f16 with EPI_F32 / EPI_RESID_F32): the accumulator is
+  // multiplied by rsc[m] * csc[n] (powers of two) before the bias
+  const float* rsc = nullptr;
+  const float* csc = nullptr;
 };
 
 // Requirements: K % 64 == 0, N % 128 == 0, A/W 16-byte aligned rows.
@@ -187,6 +191,16 @@ hipError_t im2col_f32(const void* pixels, int in_bf16, float* out, int B, int R,
 // gelu: QuickGELU (the fp32 epilogue's expf form) applied to x first (c_proj's input).
 hipError_t split6_rows(const float* x, int64_t ldx, int64_t rows, int K, int role, int gelu, uint16_t* out,
                        hipStream_t s);
+// Split-f16 operands (precise.hip; the fp32 tower's default since round 5): row r of x scaled by
+// a power of two s_r (max |x s_r| in [2^13, 2^14)) becomes 3K fp16 as [x1 x1 x2] (role 0,
+// activations) or [x1 x2 x1] (role 1, weights), x1 = f16(x s), x2 = f16(x s - x1), and
+// sc[r] = 1 / s_r; ONE f16 GEMM over K' = 3K with epilogue factor rsc[m] * csc[n] (GemmArgs)
+// then gives a1 w1 + a1 w2 + a2 w1 in f32: every term to 2^-22 relative.  K % 4 == 0, K <= 4096.
+hipError_t split2h_rows(const float* x, int64_t ldx, int64_t rows, int K, int role, int gelu, uint16_t* out,
+                        float* sc, hipStream_t s);
+// LayerNorm (f32 statistics) written directly as the split-f16 operand (role 0) + its row scales
+hipError_t layernorm_split2h(const float* x, int64_t in_stride, const float* g, const float* b, int rows, int W,
+                             uint16_t* out, float* sc, hipStream_t s);
 
 }  // namespace miclip
 

@@ -14,6 +14,8 @@
 //   ln_f32     LayerNorm rows in f32 -> f32 (optionally the EOT row of each token row)
 //   attn_f32   softmax(q k^T / 8 [+ causal]) v per (sequence, head), f32
 //   im2col_f32 conv1 patches in f32
+#include <cstdlib>
+
 #include "common.hpp"
 #include "internal.hpp"
 
@@ -166,6 +168,133 @@ __global__ __launch_bounds__(256) void split6_kernel(const float* __restrict__ x
   }
 }
 
+// ------------------------------------------------------------- split-f16 operands
+// (internal.hpp split2h_rows; round 5, the default GEMM operands of the fp32 tower).  A row x
+// of K values is scaled by a power of two s, max |x s| in [2^13, 2^14), and split as
+//   x s = x1 + x2 + r,  x1 = f16(x s),  x2 = f16(x s - x1),  |r| <= 2^-11 |x s - x1| <= 2^-22 |x s|
+// (x s - x1 is exact in f32; f16's subnormal floor adds at most 2^-25, i.e. 2^-39 of the row's
+// largest value).  Activations are stored [x1 | x1 | x2] and weights [w1 | w2 | w1], so ONE f16
+// GEMM over K' = 3K sums a1 w1 + a1 w2 + a2 w1 with f32 accumulation -- the dropped a2 w2 is
+// <= 2^-22 |a w| -- and the epilogue multiplies by 1 / (s_row s_col) (powers of two: exact).
+// Against the split-bf16 form (split6_rows, K' = 6K) that halves the MFMA work and the operand
+// bytes at the same accuracy (numpy simulation at K = 768 / 3072: 7.1e-7 / 4.7e-7 of max |ref|
+// for f16 x 3 against 3.2e-7 / 5.8e-7 for bf16 x 6).
+__device__ __forceinline__ int split_exp(float mx) {   // s = 2^e: mx * s in [2^13, 2^14)
+  if (!(mx > 0.f) || !__builtin_isfinite(mx)) return 0;   // zero / non-finite row: unscaled
+  int ex;
+  (void)frexpf(mx, &ex);                                 // mx = f 2^ex, f in [0.5, 1)
+  const int e = 14 - ex;
+  return e > 126 ? 126 : (e < -126 ? -126 : e);          // 1 / s stays a normal float
+}
+
+__device__ __forceinline__ void split2h(float xs, _Float16& x1, _Float16& x2) {
+  x1 = (_Float16)xs;
+  const float f1 = (float)x1;
+  // inf / NaN (only in rows left unscaled): carried by x1 alone
+  x2 = __builtin_isfinite(f1) ? (_Float16)(xs - f1) : (_Float16)0.f;
+}
+
+__device__ __forceinline__ float quick_gelu_f32(float v) { return v * (1.0f / (1.0f + expf(-1.702f * v))); }
+
+__device__ __forceinline__ float absmax4(float m, float4 v) {
+  return fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+}
+
+typedef _Float16 f16x4_p __attribute__((ext_vector_type(4)));
+
+// the lane's 4 values (columns c..c+3) of a row scaled by 2^e into the three K-blocks of out
+// (row stride 3K): role 0 [x1 | x1 | x2], role 1 [x1 | x2 | x1]
+__device__ __forceinline__ void store_split4(float4 v, int e, int role, _Float16* o, int K, int c) {
+  _Float16 a0, a1, a2, a3, b0, b1, b2, b3;
+  split2h(ldexpf(v.x, e), a0, b0);
+  split2h(ldexpf(v.y, e), a1, b1);
+  split2h(ldexpf(v.z, e), a2, b2);
+  split2h(ldexpf(v.w, e), a3, b3);
+  const f16x4_p h1 = {a0, a1, a2, a3}, h2 = {b0, b1, b2, b3};
+  *(f16x4_p*)(o + c) = h1;
+  *(f16x4_p*)(o + K + c) = role ? h2 : h1;
+  *(f16x4_p*)(o + 2 * K + c) = role ? h1 : h2;
+}
+
+// One wave per row, a lane's float4 at columns 4 lane + 256 i (K % 4 == 0, K <= 256 NV).
+// sc[row] = 1 / s (the GEMM epilogue's factor for this row / column).
+template <int NV>
+__global__ __launch_bounds__(256) void split2h_kernel(const float* __restrict__ x, int64_t ldx, int64_t rows, int K,
+                                                      int role, int gelu, _Float16* __restrict__ out,
+                                                      float* __restrict__ sc) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const float* xr = x + row * ldx;
+  float4 v[NV];
+  float mx = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = 4 * lane + 256 * i;
+    v[i] = c < K ? *(const float4*)(xr + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    if (gelu) v[i] = make_float4(quick_gelu_f32(v[i].x), quick_gelu_f32(v[i].y), quick_gelu_f32(v[i].z),
+                                 quick_gelu_f32(v[i].w));
+    mx = absmax4(mx, v[i]);
+  }
+  const int e = split_exp(wave_max(mx));
+  if (lane == 0) sc[row] = ldexpf(1.f, -e);
+  _Float16* o = out + row * 3 * (int64_t)K;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = 4 * lane + 256 * i;
+    if (c < K) store_split4(v[i], e, role, o, K, c);
+  }
+}
+
+// LayerNorm (ln_f32_kernel's statistics: two-pass mean / variance in f32) straight into the
+// split operand of the following GEMM: no f32 LN output is written or re-read.  W <= 1024.
+__global__ __launch_bounds__(256) void ln_split2h_kernel(const float* __restrict__ x, int64_t in_stride,
+                                                         const float* __restrict__ g, const float* __restrict__ b,
+                                                         int rows, int W, _Float16* __restrict__ out,
+                                                         float* __restrict__ sc) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const float* xr = x + (int64_t)row * in_stride;
+  float4 v[4];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = 4 * lane + 256 * i;
+    v[i] = c < W ? *(const float4*)(xr + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+  }
+  const float mean = wave_sum(s) / (float)W;
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = 4 * lane + 256 * i;
+    if (c < W) {
+      const float a0 = v[i].x - mean, a1 = v[i].y - mean, a2 = v[i].z - mean, a3 = v[i].w - mean;
+      ss += (a0 * a0 + a1 * a1) + (a2 * a2 + a3 * a3);
+    }
+  }
+  const float rstd = 1.0f / sqrtf(wave_sum(ss) / (float)W + LN_EPS);
+  float mx = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = 4 * lane + 256 * i;
+    if (c < W) {
+      const float4 gg = *(const float4*)(g + c), bb = *(const float4*)(b + c);
+      v[i] = make_float4((v[i].x - mean) * rstd * gg.x + bb.x, (v[i].y - mean) * rstd * gg.y + bb.y,
+                         (v[i].z - mean) * rstd * gg.z + bb.z, (v[i].w - mean) * rstd * gg.w + bb.w);
+      mx = absmax4(mx, v[i]);
+    }
+  }
+  const int e = split_exp(wave_max(mx));
+  if (lane == 0) sc[row] = ldexpf(1.f, -e);
+  _Float16* o = out + (int64_t)row * 3 * W;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = 4 * lane + 256 * i;
+    if (c < W) store_split4(v[i], e, 0, o, W, c);
+  }
+}
+
 // ------------------------------------------------------------- LayerNorm
 // One wave per row, W <= 1024, two-pass mean / variance in f32 (torch's
 // LayerNorm on fp32).  tokens != nullptr: row q of the output is the row
@@ -284,6 +413,107 @@ __global__ __launch_bounds__(NT) void attn_f32_kernel(const float* __restrict__ 
   }
 }
 
+// ------------------------------------------------------------- attention (MFMA)
+// S <= 32 NKT (<= 128: B/32's 50 tokens, the text tower's 77): one wave per (sequence, head),
+// every operand in registers, on the exact-f32 MFMA (v_mfma_f32_32x32x2_f32: exact products,
+// f32 accumulation, as fmaf chains).  The 32x32 C layout puts column (lane & 31) in the lane
+// and rows rho(r, h) = (r & 3) + 8 (r >> 2) + 4 h, h = lane >> 5, in its registers r = 0..15.
+//   S^T = K Q^T per key tile kt and 32-query block: A = K (lane (key i, h) gives K[i][32 h + s]
+//     at step s), B = Q (lane (query j, h) gives q[j][32 h + s] / 8): lane (query j, h) then
+//     holds its query's scores against keys rho(r, h) -- the softmax over keys is in-lane over
+//     16 NKT values plus the partner lane j + 32.
+//   O = P V per 32-dim tile dt: A = P, and the k pair of step s is keys {rho(s, 0), rho(s, 1)},
+//     so lane (query i, h) gives its own register s (no data movement); B = V (lane (dim j, h)
+//     gives V[rho(s, h)][32 dt + j]).  C: lane (dim j, h) holds queries rho(r, h), so each
+//     register's 32 lanes store one 128-byte row segment.
+// Replaces attn_f32_kernel (a thread per query row, scalar fmaf over LDS; 10.4 ms per B/32 layer
+// at 10k frames, profiles/r05_a_fp32_bench_kernel_stats.csv).
+template <int NKT>
+__global__ __launch_bounds__(256) void attn_f32_mfma_kernel(const float* __restrict__ qkv, float* __restrict__ out,
+                                                            int nseq, int S, int W, int causal) {
+  const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
+  const int H = W / 64;
+  const int item = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (item >= nseq * H) return;
+  const int bseq = item / H, head = item % H;
+  const int64_t ld = 3 * (int64_t)W;
+  const float* base = qkv + (int64_t)bseq * S * ld + head * 64;
+  float* obase = out + (int64_t)bseq * S * W + head * 64;
+  auto rho = [&](int r) { return (r & 3) + 8 * (r >> 2) + 4 * h; };
+  for (int q0 = 0; q0 < S; q0 += 32) {
+    const int qi = q0 + j;   // this lane's query in the S^T layout
+    float qv[32];
+    {
+      const float* qp = base + (int64_t)min(qi, S - 1) * ld + 32 * h;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const float4 t = qi < S ? *(const float4*)(qp + 4 * c) : make_float4(0.f, 0.f, 0.f, 0.f);
+        qv[4 * c] = t.x * 0.125f; qv[4 * c + 1] = t.y * 0.125f; qv[4 * c + 2] = t.z * 0.125f; qv[4 * c + 3] = t.w * 0.125f;
+      }
+    }
+    f32x16 sc[NKT];
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+      sc[kt] = f32x16{};
+      if (kt * 32 >= S) continue;
+      const int ki = kt * 32 + j;   // this lane's key as an A-operand row
+      const float* kp = base + W + (int64_t)min(ki, S - 1) * ld + 32 * h;
+      float kv[32];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const float4 t = ki < S ? *(const float4*)(kp + 4 * c) : make_float4(0.f, 0.f, 0.f, 0.f);
+        kv[4 * c] = t.x; kv[4 * c + 1] = t.y; kv[4 * c + 2] = t.z; kv[4 * c + 3] = t.w;
+      }
+#pragma unroll
+      for (int st = 0; st < 32; ++st) sc[kt] = __builtin_amdgcn_mfma_f32_32x32x2f32(kv[st], qv[st], sc[kt], 0, 0, 0);
+    }
+    // masks and the softmax statistics of query qi (keys rho(r, h) of every tile, with lane ^ 32)
+    float m = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kt * 32 + rho(r);
+        if (key >= S || (causal && key > qi)) sc[kt][r] = -INFINITY;
+        m = fmaxf(m, sc[kt][r]);
+      }
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    float l = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = expf(sc[kt][r] - m);   // masked keys: exp(-inf) = 0
+        sc[kt][r] = p;
+        l += p;
+      }
+    l += __shfl_xor(l, 32, 64);
+    const float inv = 1.0f / l;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+      f32x16 o = f32x16{};
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt) {
+        if (kt * 32 >= S) continue;
+        float vv[16];
+#pragma unroll
+        for (int st = 0; st < 16; ++st) {
+          const int key = kt * 32 + (st & 3) + 8 * (st >> 2) + 4 * h;
+          vv[st] = key < S ? base[2 * W + (int64_t)key * ld + 32 * dt + j] : 0.f;
+        }
+#pragma unroll
+        for (int st = 0; st < 16; ++st) o = __builtin_amdgcn_mfma_f32_32x32x2f32(sc[kt][st], vv[st], o, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int qr = q0 + rho(r);
+        const float iv = __shfl(inv, rho(r), 64);   // 1 / l of query rho(r) (held by lane rho(r))
+        if (qr < S) obase[(int64_t)qr * W + 32 * dt + j] = o[r] * iv;
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------ im2col
 // patches [B*G*G, Kp] f32, k = c*P*P + kh*P + kw (conv1 weight order), zero pad.
 __global__ __launch_bounds__(256) void im2col_f32_kernel(const void* __restrict__ pixels, int in_bf16,
@@ -339,6 +569,27 @@ hipError_t split6_rows(const float* x, int64_t ldx, int64_t rows, int K, int rol
   return hipGetLastError();
 }
 
+hipError_t split2h_rows(const float* x, int64_t ldx, int64_t rows, int K, int role, int gelu, uint16_t* out,
+                        float* sc, hipStream_t s) {
+  if (rows <= 0) return hipSuccess;
+  if (K % 4 || ldx % 4 || K < 4 || K > 4096 || !sc) return hipErrorInvalidValue;
+  const dim3 grid((unsigned)((rows + 3) / 4));
+  _Float16* o = (_Float16*)out;
+  if (K <= 1024) hipLaunchKernelGGL(split2h_kernel<4>, grid, dim3(256), 0, s, x, ldx, rows, K, role, gelu, o, sc);
+  else if (K <= 3072) hipLaunchKernelGGL(split2h_kernel<12>, grid, dim3(256), 0, s, x, ldx, rows, K, role, gelu, o, sc);
+  else hipLaunchKernelGGL(split2h_kernel<16>, grid, dim3(256), 0, s, x, ldx, rows, K, role, gelu, o, sc);
+  return hipGetLastError();
+}
+
+hipError_t layernorm_split2h(const float* x, int64_t in_stride, const float* g, const float* b, int rows, int W,
+                             uint16_t* out, float* sc, hipStream_t s) {
+  if (rows <= 0) return hipSuccess;
+  if (W > 1024 || W < 4 || W % 4 || in_stride % 4) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(ln_split2h_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, x, in_stride, g, b, rows, W,
+                     (_Float16*)out, sc);
+  return hipGetLastError();
+}
+
 hipError_t layernorm_f32(const float* x, int64_t in_stride, const float* g, const float* b, float* out,
                          int64_t out_stride, int rows, int W, hipStream_t s, const int32_t* tokens, int S) {
   if (rows <= 0) return hipSuccess;
@@ -348,11 +599,28 @@ hipError_t layernorm_f32(const float* x, int64_t in_stride, const float* g, cons
   return hipGetLastError();
 }
 
+// the MFMA attention (S <= 128) is the default; MICLIP_ATTN_F32_MFMA=0 (A/B build) keeps the
+// scalar kernel for comparison
+static bool attn_f32_mfma_on() {
+#if MICLIP_AB
+  const char* e = std::getenv("MICLIP_ATTN_F32_MFMA");
+  if (e) return std::atoi(e) != 0;
+#endif
+  return true;
+}
+
 hipError_t attention_f32(const float* qkv, float* out, int B, int S, int W, int causal, hipStream_t s) {
   if (B <= 0) return hipSuccess;
   if (W % 64 || S < 1) return hipErrorInvalidValue;
   const dim3 grid((unsigned)B * (W / 64));
-  if (S <= 64)
+  const dim3 grid4((unsigned)(((int64_t)B * (W / 64) + 3) / 4));
+  if (attn_f32_mfma_on() && S <= 64)
+    hipLaunchKernelGGL(attn_f32_mfma_kernel<2>, grid4, dim3(256), 0, s, qkv, out, B, S, W, causal);
+  else if (attn_f32_mfma_on() && S <= 96)
+    hipLaunchKernelGGL(attn_f32_mfma_kernel<3>, grid4, dim3(256), 0, s, qkv, out, B, S, W, causal);
+  else if (attn_f32_mfma_on() && S <= 128)
+    hipLaunchKernelGGL(attn_f32_mfma_kernel<4>, grid4, dim3(256), 0, s, qkv, out, B, S, W, causal);
+  else if (S <= 64)
     hipLaunchKernelGGL(attn_f32_kernel<64>, grid, dim3(64), 0, s, qkv, out, S, W, causal);
   else
     hipLaunchKernelGGL(attn_f32_kernel<256>, grid, dim3(256), 0, s, qkv, out, S, W, causal);

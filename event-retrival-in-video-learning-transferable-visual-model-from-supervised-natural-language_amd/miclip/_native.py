@@ -38,7 +38,7 @@ EXPORTS = (
     "mi_jpeg_workspace_bytes", "mi_jpeg_decode", "mi_host_gather",
     "mi_op_quantize_mx", "mi_op_gemm_mx",
     "mi_mirror_build", "mi_rank_mirror_workspace_bytes", "mi_rank_mirror", "mi_normalize_rows_f16",
-    "mi_jpeg_decode_transform",
+    "mi_jpeg_decode_transform", "mi_op_split2h", "mi_op_gemm_split2h", "mi_op_attention_f32",
 )
 
 
@@ -128,6 +128,9 @@ def _bind(path):
         "mi_op_gemm_ln": (ctypes.c_int, [P, I64, P, P, P, P, P, I32, I32, I32, I32, P]),
         "mi_op_gemm_residual": (ctypes.c_int, [P, I64, P, I64, P, P, P, P, I32, I32, I32, P]),
         "mi_op_split6": (ctypes.c_int, [P, I64, I64, I32, I32, I32, P, P]),
+        "mi_op_split2h": (ctypes.c_int, [P, I64, I64, I32, I32, I32, P, P, P]),
+        "mi_op_gemm_split2h": (ctypes.c_int, [P, P, P, P, P, P, I32, I32, I32, I32, P]),
+        "mi_op_attention_f32": (ctypes.c_int, [P, P, I32, I32, I32, I32, P]),
         "mi_op_quantize_mx": (ctypes.c_int, [P, P, P, I32, I32, P]),
         "mi_op_gemm_mx": (ctypes.c_int, [P, P, P, P, P, P, I32, I32, I32, I32, P]),
         "mi_resample_coeffs": (ctypes.c_int, [I32, ctypes.c_double, ctypes.c_double, I32, ctypes.c_int, P, I64, P]),
@@ -143,7 +146,7 @@ def _bind(path):
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
-    if L.mi_abi_version() != 3:
+    if L.mi_abi_version() != 4:
         raise MiClipError("libmiclip ABI version mismatch")
     return L
 

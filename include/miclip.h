@@ -35,8 +35,9 @@
 extern "C" {
 #endif
 
-#define MICLIP_ABI_VERSION 3   /* 2: mi_jpeg_workspace_bytes / mi_jpeg_decode take the data size;
-                                  3: mi_normalize_rows_f16, mi_jpeg_decode_transform */
+#define MICLIP_ABI_VERSION 4   /* 2: mi_jpeg_workspace_bytes / mi_jpeg_decode take the data size;
+                                  3: mi_normalize_rows_f16, mi_jpeg_decode_transform;
+                                  4: mi_op_split2h, mi_op_gemm_split2h, mi_op_attention_f32 */
 
 enum mi_dtype { MI_F32 = 0, MI_BF16 = 1, MI_F16 = 2, MI_FP8 = 3 /* weights only: MX-fp8 vision GEMMs */ };
 enum mi_status { MI_OK = 0, MI_ERR_ARG = -1, MI_ERR_HIP = -2, MI_ERR_UNSUPPORTED = -3, MI_ERR_STATE = -4 };
@@ -330,6 +331,26 @@ int mi_op_residual_stats(void* x, const void* delta, float* rs, int32_t rows, in
  *   a1w3 in f32.  gelu 1 applies QuickGELU (x * 1 / (1 + exp(-1.702 x))) first. */
 int mi_op_split6(const float* x, int64_t ldx, int64_t rows, int32_t K, int32_t role, int32_t gelu, void* out,
                  void* stream);
+/* mi_op_split2h: the split-f16 operands of the fp32 tower's GEMMs (weight_dtype MI_F32, the
+ *   default since ABI 4).  Row r of x [rows][K] (stride ldx floats) is scaled
+ *   by a power of two s_r with max_k |x[r][k] s_r| in [2^13, 2^14) (s_r = 1 for an all-zero or
+ *   non-finite row; the exponent clamped to [-126, 126]) and split as x s = x1 + x2 + O(2^-22
+ *   |x s|), x1 = f16(x s), x2 = f16(x s - x1) (round to nearest even; x2 = 0 where x1 is not
+ *   finite); out[r] = 3K fp16 in three K-blocks, role 0 (activations) [x1 x1 x2], role 1
+ *   (weights [N][K]) [x1 x2 x1]; scale[r] = 1 / s_r.  gelu 1 applies QuickGELU first (as
+ *   mi_op_split6).  K % 4 == 0, 4 <= K <= 4096, ldx % 4 == 0.
+ * mi_op_gemm_split2h: out f32 [M,N] (epi 3) or out += (epi 2) of
+ *   (A3 . W3^T) * a_scale[m] * w_scale[n] + bias[n], with A3 [M][K3] / W3 [N][K3] the fp16
+ *   operands above (K3 = 3K) on the f16 MFMA with f32 accumulation: a1 w1 + a1 w2 + a2 w1, an
+ *   f32-grade product.  N % 128 == 0, K3 % 32 == 0.
+ * mi_op_attention_f32: f32 MHA core of the fp32 tower: qkv f32 [B*S, 3W] (q | k | v, head dim
+ *   64) -> out f32 [B*S, W], softmax(q k^T / 8 (+ causal mask)) v per (sequence, head); S <= 128
+ *   on the exact-f32 MFMA, longer sequences on a per-row f32 kernel. */
+int mi_op_split2h(const float* x, int64_t ldx, int64_t rows, int32_t K, int32_t role, int32_t gelu, void* out,
+                  float* scale, void* stream);
+int mi_op_gemm_split2h(const void* A3, const void* W3, const float* a_scale, const float* w_scale, const float* bias,
+                       float* out, int32_t M, int32_t N, int32_t K3, int32_t epi, void* stream);
+int mi_op_attention_f32(const float* qkv, float* out, int32_t B, int32_t S, int32_t W, int32_t causal, void* stream);
 int mi_op_gemm_ln(const void* x16, int64_t lda, const float* rs, const void* Wf, const float* colsum,
                   const float* colc, void* out, int32_t M, int32_t N, int32_t K, int32_t gelu, void* stream);
 /* mi_op_gemm_residual: attn.out_proj / mlp.c_proj with the residual add fused (replaces

@@ -584,3 +584,135 @@ def test_split6_gemm_f32_grade(gpu, M, N, K, epi):
         ref = ref + base.double()
     err = (out.double() - ref).abs().max().item()
     assert err < 1e-5 * max(1.0, ref.abs().max().item()), err
+
+
+# ---------------------------------------------------------------- split-f16 operands (round 5)
+def _split2h_ref(x, role, gelu):
+    """numpy restatement of split2h_rows (precise.hip): per-row power-of-two scale with the row's
+    max |x s| in [2^13, 2^14), x1 = f16(x s), x2 = f16(x s - x1) (0 where x1 is not finite),
+    activations [x1 x1 x2] / weights [x1 x2 x1], scale = 1 / s."""
+    x = np.asarray(x, np.float32)
+    if gelu:
+        x = (x * (np.float32(1) / (np.float32(1) + np.exp(np.float32(-1.702) * x)))).astype(np.float32)
+    with np.errstate(invalid="ignore", over="ignore"):
+        mx = np.nanmax(np.where(np.isnan(x), 0, np.abs(x)), axis=1)
+        ok = (mx > 0) & np.isfinite(mx)
+        _, ex = np.frexp(np.where(ok, mx, 1).astype(np.float32))
+        e = np.clip(np.where(ok, 14 - ex, 0), -126, 126).astype(np.int32)
+        xs = np.ldexp(x, e[:, None]).astype(np.float32)
+        x1 = xs.astype(np.float16)
+        r = (xs - x1.astype(np.float32)).astype(np.float32)
+        x2 = np.where(np.isfinite(x1), r.astype(np.float16), np.float16(0))
+    t = (x1.view(np.uint16), x2.view(np.uint16))
+    order = (0, 1, 0) if role else (0, 0, 1)
+    return np.concatenate([t[o] for o in order], axis=1), np.ldexp(np.float32(1), -e).astype(np.float32)
+
+
+@pytest.mark.parametrize("role,gelu,K", [(0, 0, 768), (1, 0, 768), (0, 0, 3072), (0, 1, 3072), (1, 0, 128)])
+def test_split2h_bit_exact(gpu, role, gelu, K):
+    """mi_op_split2h (the fp32 tower's split-f16 operands) against its numpy restatement, bit for
+    bit, rows of magnitudes 1e-30 .. 1e30 with inf / NaN / zero / subnormal entries and an
+    all-zero row; and (x1 + x2) / s = x to 2^-22 of the row's largest value."""
+    import torch
+    N_ = _lib()
+    rng = np.random.default_rng(11 + role + 2 * gelu + K)
+    rows = 300
+    x = (rng.standard_normal((rows, K)) * np.exp(rng.uniform(-5, 5, (rows, K)))
+         * np.exp(rng.uniform(-60, 60, (rows, 1)))).astype(np.float32)
+    if gelu:
+        x = (rng.standard_normal((rows, K)) * 3).astype(np.float32)
+    else:
+        x[0, :8] = [np.inf, -np.inf, np.nan, 0.0, -0.0, 1e-40, -3e-39, 3.4e38]
+        x[1, :4] = [1e-40, -2e-39, 0.0, 5e-45]
+        x[2] = 0.0
+        x[3, :3] = [np.nan, 1.0, -2.0]
+    xd = torch.from_numpy(x).to(gpu)
+    out = torch.zeros(rows, 3 * K, dtype=torch.int16, device=gpu)
+    sc = torch.zeros(rows, device=gpu)
+    N_.check(N_.lib().mi_op_split2h(xd.data_ptr(), K, rows, K, role, gelu, out.data_ptr(), sc.data_ptr(), _stream()),
+             "split2h")
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(np.uint16)
+    gsc = sc.cpu().numpy()
+    if gelu:   # the device's QuickGELU values (expf vs numpy's exp may differ in the last bit), then split
+        xg = (xd * (1.0 / (1.0 + torch.exp(-1.702 * xd)))).cpu().numpy()
+        ref, rsc = _split2h_ref(xg, role, 0)
+        assert (got == ref).mean() > 0.999 and (gsc == rsc).mean() > 0.99
+        return
+    ref, rsc = _split2h_ref(x, role, 0)
+    assert np.array_equal(gsc, rsc)
+    assert np.array_equal(got, ref), np.argwhere(got != ref)[:5]
+    h = lambda u: u.view(np.float16).astype(np.float64)
+    x1, x2 = h(got[:, :K]), h(got[:, 2 * K:] if role == 0 else got[:, K:2 * K])
+    fin = np.isfinite(x).all(axis=1)
+    back = (x1 + x2) * gsc[:, None].astype(np.float64)
+    bound = 2.0 ** -22 * np.abs(x.astype(np.float64)).max(axis=1, keepdims=True) + 2.0 ** -149
+    assert (np.abs(back - x.astype(np.float64))[fin] <= bound[fin]).all()
+
+
+@pytest.mark.parametrize("M,N,K,epi", [(513, 384, 768, 3), (3000, 768, 3072, 2), (20000, 2304, 768, 3),
+                                       (1000, 256, 608, 3)])
+def test_split2h_gemm_f32_grade(gpu, M, N, K, epi):
+    """The fp32 tower's GEMM since round 5: split-f16 operands (mi_op_split2h) and one f16 GEMM
+    over K' = 3K with the row / column scales in its f32 epilogue (mi_op_gemm_split2h 3 = store,
+    2 = +=), against float64 within f32-GEMM error (1e-5 of max(1, |ref|), as test_gemm_f32);
+    rows and weight rows of magnitudes spread over 1e-8 .. 1e8 (the scales keep every row's
+    precision) -- checked row-relative."""
+    import torch
+    N_ = _lib()
+    g = torch.Generator(device="cpu").manual_seed(M + N + K + epi)
+    A = (torch.randn(M, K, generator=g) * 0.5 * torch.exp(torch.empty(M, 1).uniform_(-18, 18, generator=g))).to(gpu)
+    W = (torch.randn(N, K, generator=g) * K ** -0.5 * torch.exp(torch.empty(N, 1).uniform_(-2, 2, generator=g))).to(gpu)
+    bias = torch.randn(N, generator=g).to(gpu) * 0
+    base = torch.randn(M, N, generator=g).to(gpu)
+    A3 = torch.empty(M, 3 * K, dtype=torch.int16, device=gpu)
+    W3 = torch.empty(N, 3 * K, dtype=torch.int16, device=gpu)
+    sa, sw = torch.empty(M, device=gpu), torch.empty(N, device=gpu)
+    L = N_.lib()
+    N_.check(L.mi_op_split2h(A.data_ptr(), K, M, K, 0, 0, A3.data_ptr(), sa.data_ptr(), _stream()), "split2h A")
+    N_.check(L.mi_op_split2h(W.data_ptr(), K, N, K, 1, 0, W3.data_ptr(), sw.data_ptr(), _stream()), "split2h W")
+    out = base.clone() if epi == 2 else torch.full((M, N), float("nan"), device=gpu)
+    N_.check(L.mi_op_gemm_split2h(A3.data_ptr(), W3.data_ptr(), sa.data_ptr(), sw.data_ptr(), bias.data_ptr(),
+                                  out.data_ptr(), M, N, 3 * K, epi, _stream()), "gemm_split2h")
+    torch.cuda.synchronize()
+    prod = A.double() @ W.double().t()
+    ref = prod + bias.double() + (base.double() if epi == 2 else 0)
+    got = out.double() - (base.double() if epi == 2 else 0)
+    # row-relative: the row's |A| |W| scale (the f32 GEMM's own error bound is relative to it)
+    rowscale = (A.double().abs() @ W.double().abs().t()).max(dim=1, keepdim=True).values
+    err = ((got - (ref - (base.double() if epi == 2 else 0))).abs() / rowscale.clamp_min(1e-300)).max().item()
+    assert err < 1e-6, err
+    if epi == 2:   # the += path against float64 in absolute terms too
+        assert (out.double() - ref).abs().max().item() < 1e-5 * max(1.0, ref.abs().max().item())
+
+
+def _attn_ref(qkv, B, S, W, causal):
+    H = W // 64
+    x = qkv.reshape(B, S, 3, H, 64).astype(np.float64)
+    q, k, v = x[:, :, 0], x[:, :, 1], x[:, :, 2]
+    s = np.einsum("bqhd,bkhd->bhqk", q, k) / 8.0
+    if causal:
+        s = s + np.triu(np.full((S, S), -np.inf), 1)
+    s = np.exp(s - s.max(-1, keepdims=True))
+    p = s / s.sum(-1, keepdims=True)
+    return np.einsum("bhqk,bkhd->bqhd", p, v).reshape(B * S, W)
+
+
+@pytest.mark.parametrize("B,S,W,causal", [(37, 50, 768, 0), (5, 77, 512, 1), (3, 1, 128, 0), (4, 33, 128, 1),
+                                          (6, 96, 256, 0), (2, 128, 128, 1), (2, 257, 128, 0)])
+def test_attention_f32_vs_float64(gpu, B, S, W, causal):
+    """mi_op_attention_f32 (the fp32 tower's MHA core: the exact-f32 MFMA kernel for S <= 128,
+    the per-row kernel above) against float64 within f32 rounding."""
+    import torch
+    N_ = _lib()
+    rng = np.random.default_rng(B * 1000 + S + W + causal)
+    qkv = (rng.standard_normal((B * S, 3 * W)) * 2).astype(np.float32)
+    d = torch.from_numpy(qkv).to(gpu)
+    out = torch.full((B * S, W), float("nan"), device=gpu)
+    N_.check(N_.lib().mi_op_attention_f32(d.data_ptr(), out.data_ptr(), B, S, W, causal, _stream()), "attn f32")
+    torch.cuda.synchronize()
+    ref = _attn_ref(qkv, B, S, W, causal)
+    got = out.cpu().numpy().astype(np.float64)
+    assert np.isfinite(got).all()
+    err = np.abs(got - ref).max()
+    assert err < 2e-6 * max(1.0, np.abs(ref).max()), err
