@@ -75,6 +75,7 @@ constexpr int F_GSTAGE = 8; // QuickGELU over a store's 8 values in stage order 
 constexpr int F_GSTAGE16 = 32;   // the same over a 16-row block's 16 values (A/B)
 constexpr int F_ANT = 64;   // A-operand DMAs non-temporal (A/B: keep the weight panel in L2 against the A stream)
 constexpr int F_ONT = 128;  // output stores non-temporal (A/B)
+constexpr int F_GPK = 256;  // QuickGELU's "+ 1" as packed adds (v_pk_add_f32: 5.1 cycles per pair vs 4.7 per value)
 
 __device__ __forceinline__ f32x2 quick_gelu2_8q(f32x2 v) {
   const f32x2 t = v * (f32x2){-2.45546696f, -2.45546696f};   // -1.702 * log2(e)
@@ -85,7 +86,9 @@ __device__ __forceinline__ f32x2 quick_gelu2_8q(f32x2 v) {
 
 // QuickGELU of 8 values in stage order (all multiplies, all exponentials, all adds, all
 // reciprocals, all products), so consecutive transcendental ops are independent (F_GSTAGE)
-template <int NP>
+// (PK: the adds as packed pairs -- the same additions, bit-identical; one wave alone issues a
+// v_pk_add_f32 in 5.1 cycles against 4.7 for a v_add_f32, scripts/probes/valu_rate.hip)
+template <int NP, bool PK = false>
 __device__ __forceinline__ void quick_gelu_stage_8q(f32x2 (&v)[NP]) {
   float e[2 * NP];
 #pragma unroll
@@ -96,8 +99,17 @@ __device__ __forceinline__ void quick_gelu_stage_8q(f32x2 (&v)[NP]) {
   }
 #pragma unroll
   for (int k = 0; k < 2 * NP; ++k) e[k] = __builtin_amdgcn_exp2f(e[k]);
+  if (PK) {
 #pragma unroll
-  for (int k = 0; k < 2 * NP; ++k) e[k] = e[k] + 1.0f;
+    for (int k = 0; k < NP; ++k) {
+      const f32x2 p = (f32x2){e[2 * k], e[2 * k + 1]} + (f32x2){1.0f, 1.0f};
+      e[2 * k] = p.x;
+      e[2 * k + 1] = p.y;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 2 * NP; ++k) e[k] = e[k] + 1.0f;
+  }
 #pragma unroll
   for (int k = 0; k < 2 * NP; ++k) e[k] = __builtin_amdgcn_rcpf(e[k]);
 #pragma unroll
@@ -431,7 +443,7 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
           gw[2 * ni] = lo;
           gw[2 * ni + 1] = hi;
         }
-        quick_gelu_stage_8q<8>(gw);
+        quick_gelu_stage_8q<8, (F & F_GPK) != 0>(gw);
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni) pkb[ni >> 1][ni & 1] = make_uint2(pack_bf16x2(gw[2 * ni]), pack_bf16x2(gw[2 * ni + 1]));
       }
@@ -506,8 +518,8 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
           s1[e] = top ? dp[0][e] : r1;
           s2[e] = top ? r0 : dp[1][e];
         }
-        __builtin_amdgcn_raw_buffer_store_b128(s1, rsO, voF + mi * blkO, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b128(s2, rsO, voF + mi * blkO + rows8, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(s1, rsO, voF + mi * blkO, 0, (F & F_ONT) ? 2 : 0);
+        __builtin_amdgcn_raw_buffer_store_b128(s2, rsO, voF + mi * blkO + rows8, 0, (F & F_ONT) ? 2 : 0);
       }
       if (EK::RES && ABL == 11) {   // timing probe: no statistics, no partial stores
         __builtin_amdgcn_sched_barrier(0);
@@ -764,11 +776,14 @@ hipError_t gemm_8q(const GemmArgs& a0, int epi, hipStream_t s, int cus, int mode
       return hipGetLastError();
     }
     // + 64: A DMAs non-temporal (F_ANT), + 128: output stores non-temporal (F_ONT)
+    // + 2: whole-line (128-B) row stores (F_FULL), alone (46 / 2) or non-temporal (174 / 130)
     if (ff == 4 || ff == 8 || ff == 12 || ff == 44 || ff == 64 || ff == 192 || ff == 76 || ff == 204 || ff == 108 ||
-        ff == 140) {
+        ff == 140 || ff == 46 || ff == 174 || ff == 2 || ff == 130 || ff == 300 || ff == 430) {
 #define LNF(E, FL) hipLaunchKernelGGL((gemm_8q_kernel<E, 0, FL, true>), dim3(grid), dim3(512), 0, s, a)
       if (epi == EPI_LN_BF16) {
-        if (ff == 64 || ff == 76) LNF(EPI_LN_BF16, F_ANT);
+        if (ff == 2 || ff == 46) LNF(EPI_LN_BF16, F_FULL);
+        else if (ff == 130 || ff == 174) LNF(EPI_LN_BF16, F_FULL | F_ONT);
+        else if (ff == 64 || ff == 76) LNF(EPI_LN_BF16, F_ANT);
         else if (ff == 192 || ff == 204) LNF(EPI_LN_BF16, F_ANT | F_ONT);
         else LNF(EPI_LN_BF16, F_VOREC);   // (no GELU: F_GSTAGE has nothing to reorder)
       } else if (ff == 4) LNF(EPI_LN_GELU_BF16, F_VOREC);
@@ -778,19 +793,28 @@ hipError_t gemm_8q(const GemmArgs& a0, int epi, hipStream_t s, int cus, int mode
       else if (ff == 204 || ff == 192) LNF(EPI_LN_GELU_BF16, F_ONT | F_ANT | F_GSTAGE | F_VOREC);
       else if (ff == 140) LNF(EPI_LN_GELU_BF16, F_ONT | F_GSTAGE | F_VOREC);
       else if (ff == 108) LNF(EPI_LN_GELU_BF16, F_ANT | F_GSTAGE16 | F_GSTAGE | F_VOREC);
+      else if (ff == 46 || ff == 2) LNF(EPI_LN_GELU_BF16, F_FULL | F_GSTAGE16 | F_GSTAGE | F_VOREC);
+      else if (ff == 174 || ff == 130) LNF(EPI_LN_GELU_BF16, F_ONT | F_FULL | F_GSTAGE16 | F_GSTAGE | F_VOREC);
+      else if (ff == 300) LNF(EPI_LN_GELU_BF16, F_GPK | F_GSTAGE16 | F_GSTAGE | F_VOREC);
+      else if (ff == 430) LNF(EPI_LN_GELU_BF16, F_GPK | F_ONT | F_FULL | F_GSTAGE16 | F_GSTAGE | F_VOREC);
       else LNF(EPI_LN_GELU_BF16, F_GSTAGE | F_VOREC);
 #undef LNF
       return hipGetLastError();
     }
 #endif
-    // c_fc: QuickGELU in stage order over each 16-row block's 16 values + store offsets from the
-    // lane id (bit-identical; lnfc500 2281 vs 2318 us for the 8-value order against none,
-    // profiles/r04_ag_lnflags.log; the 16-value order 2296 vs 2354 us, profiles/r05_a_lnfc.log);
-    // in_proj: no difference, kept as it was
-    if (epi == EPI_LN_BF16) hipLaunchKernelGGL((gemm_8q_kernel<EPI_LN_BF16, 0, 0, true>), dim3(grid), dim3(512), 0, s, a);
+    // c_fc: QuickGELU in stage order over each 16-row block's 16 values, its "+ 1" as packed adds,
+    // store offsets from the lane id, and whole-line (128-B) non-temporal row stores -- all
+    // bit-identical (lnfc500 2281 vs 2318 us for the 8-value order against none,
+    // profiles/r04_ag_lnflags.log; the 16-value order 2296 vs 2354 us, profiles/r05_a_lnfc.log;
+    // + packed adds + whole-line non-temporal stores 2239-2259 vs 2304-2311 us,
+    // profiles/r05_d_lnfc.log).  in_proj: whole-line non-temporal stores, 1646 vs 1690 us
+    // (r05_d_lnqkv.log; FETCH 5.4 -> 3.7x the operand bytes: the output no longer displaces the
+    // weight panel from L2, profiles/r05_b_fullnt_gemm_traffic_ab.json)
+    if (epi == EPI_LN_BF16)
+      hipLaunchKernelGGL((gemm_8q_kernel<EPI_LN_BF16, 0, F_FULL | F_ONT, true>), dim3(grid), dim3(512), 0, s, a);
     else
-      hipLaunchKernelGGL((gemm_8q_kernel<EPI_LN_GELU_BF16, 0, F_GSTAGE16 | F_GSTAGE | F_VOREC, true>), dim3(grid),
-                         dim3(512), 0, s, a);
+      hipLaunchKernelGGL((gemm_8q_kernel<EPI_LN_GELU_BF16, 0, F_GPK | F_ONT | F_FULL | F_GSTAGE16 | F_GSTAGE | F_VOREC, true>),
+                         dim3(grid), dim3(512), 0, s, a);
     return hipGetLastError();
   }
   if (a.a_f16) return hipErrorInvalidValue;
