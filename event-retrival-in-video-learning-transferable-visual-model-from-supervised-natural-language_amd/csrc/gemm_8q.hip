@@ -76,6 +76,11 @@ constexpr int F_GSTAGE16 = 32;   // the same over a 16-row block's 16 values (A/
 constexpr int F_ANT = 64;   // A-operand DMAs non-temporal (A/B: keep the weight panel in L2 against the A stream)
 constexpr int F_ONT = 128;  // output stores non-temporal (A/B)
 constexpr int F_GPK = 256;  // QuickGELU's "+ 1" as packed adds (v_pk_add_f32: 5.1 cycles per pair vs 4.7 per value)
+// F_BEARLY: the lagging M-group (wr = 1) runs its epilogue right after its last MFMA section of
+// the tile (the same barrier interval as the leading group's epilogue) instead of one interval
+// later, so the two waves of each SIMD issue their epilogue VALU concurrently (two waves: 2x the
+// plain-VALU and 1.37x the transcendental issue rate of one, scripts/probes/valu_rate.hip)
+constexpr int F_BEARLY = 512;
 
 __device__ __forceinline__ f32x2 quick_gelu2_8q(f32x2 v) {
   const f32x2 t = v * (f32x2){-2.45546696f, -2.45546696f};   // -1.702 * log2(e)
@@ -566,7 +571,7 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
       // previous tile's stores: the last pair did not re-read it in phase 8
       if (FIRST) issue(H_B0, 1);
       __builtin_amdgcn_sched_barrier(0);
-      if (FIRST && has_prev) {
+      if (FIRST && has_prev && !((F & F_BEARLY) && wr == 1)) {
         // the previous tile's whole epilogue, ahead of this phase's fragment
         // reads (its bias reads wait lgkmcnt(0)), behind the phase's DMAs
         epilogue();
@@ -621,7 +626,9 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
       // (EPI_RES16: 16 stores, 8 partial stores and the x16 loads of blocks 4-7 are younger;
       // the epilogue's wait for block 7 already retired the odd buffer)
       if (FIRST && has_prev && EK::RES) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(ABL == 11 ? 20 : 28) : "memory");
-      else if (FIRST && has_prev && ABL != 10) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+      else if (FIRST && has_prev && ABL != 10 && !((F & F_BEARLY) && wr == 1)) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+      // (F_BEARLY, lagging group: its stores are OLDER than phase 1's DMAs, so vmcnt(4) below also
+      // retires them -- issued three barrier intervals earlier)
       else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
       if (FIRST) stamp(3);   // S3: first pair's phase-4 wait passed
     }
@@ -662,6 +669,16 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
                   fb[ni][ks], fa[mi][ks], (FIRST && P <= 4 && ks == 0) ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[mh * 4 + mi][nh * 2 + ni],
                   0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
+    if constexpr ((F & F_BEARLY) && !EK::RES && P == 8 && LAST) {
+      if (wr == 1) {   // this tile's epilogue now, beside the leading group's (see F_BEARLY)
+        pm0 = cur_m0;
+        pn0 = cur_n0;
+        ppar = cpar;
+        __builtin_amdgcn_sched_barrier(0);
+        epilogue();
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
     barrier();
   };
   auto pair = [&](auto firstc, auto lastc) {
@@ -721,7 +738,7 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
   // the last tile's epilogue
   if (wr == 0) barrier();   // the M-groups' barrier counts meet
   res_prefetch(2, 8, pm0, pn0);
-  epilogue();
+  if (!((F & F_BEARLY) && wr == 1)) epilogue();   // (F_BEARLY: the lagging group's is done)
   if ((ABL == 9 || ABL == 10) && lane == 0 && (wave & 3) == 0 && blockIdx.x < 1024) {
 #pragma unroll
     for (int i = 0; i < 9; ++i) g_probe8q[(blockIdx.x * 2 + wr) * 9 + i] = st[i];
@@ -778,11 +795,13 @@ hipError_t gemm_8q(const GemmArgs& a0, int epi, hipStream_t s, int cus, int mode
     // + 64: A DMAs non-temporal (F_ANT), + 128: output stores non-temporal (F_ONT)
     // + 2: whole-line (128-B) row stores (F_FULL), alone (46 / 2) or non-temporal (174 / 130)
     if (ff == 4 || ff == 8 || ff == 12 || ff == 44 || ff == 64 || ff == 192 || ff == 76 || ff == 204 || ff == 108 ||
-        ff == 140 || ff == 46 || ff == 174 || ff == 2 || ff == 130 || ff == 300 || ff == 430) {
+        ff == 140 || ff == 46 || ff == 174 || ff == 2 || ff == 130 || ff == 300 || ff == 430 || ff == 942 ||
+        ff == 642) {
 #define LNF(E, FL) hipLaunchKernelGGL((gemm_8q_kernel<E, 0, FL, true>), dim3(grid), dim3(512), 0, s, a)
       if (epi == EPI_LN_BF16) {
         if (ff == 2 || ff == 46) LNF(EPI_LN_BF16, F_FULL);
         else if (ff == 130 || ff == 174) LNF(EPI_LN_BF16, F_FULL | F_ONT);
+        else if (ff == 642 || ff == 942) LNF(EPI_LN_BF16, F_BEARLY | F_FULL | F_ONT);
         else if (ff == 64 || ff == 76) LNF(EPI_LN_BF16, F_ANT);
         else if (ff == 192 || ff == 204) LNF(EPI_LN_BF16, F_ANT | F_ONT);
         else LNF(EPI_LN_BF16, F_VOREC);   // (no GELU: F_GSTAGE has nothing to reorder)
@@ -797,6 +816,8 @@ hipError_t gemm_8q(const GemmArgs& a0, int epi, hipStream_t s, int cus, int mode
       else if (ff == 174 || ff == 130) LNF(EPI_LN_GELU_BF16, F_ONT | F_FULL | F_GSTAGE16 | F_GSTAGE | F_VOREC);
       else if (ff == 300) LNF(EPI_LN_GELU_BF16, F_GPK | F_GSTAGE16 | F_GSTAGE | F_VOREC);
       else if (ff == 430) LNF(EPI_LN_GELU_BF16, F_GPK | F_ONT | F_FULL | F_GSTAGE16 | F_GSTAGE | F_VOREC);
+      else if (ff == 942 || ff == 642)
+        LNF(EPI_LN_GELU_BF16, F_BEARLY | F_GPK | F_ONT | F_FULL | F_GSTAGE16 | F_GSTAGE | F_VOREC);
       else LNF(EPI_LN_GELU_BF16, F_GSTAGE | F_VOREC);
 #undef LNF
       return hipGetLastError();
@@ -809,12 +830,15 @@ hipError_t gemm_8q(const GemmArgs& a0, int epi, hipStream_t s, int cus, int mode
     // + packed adds + whole-line non-temporal stores 2239-2259 vs 2304-2311 us,
     // profiles/r05_d_lnfc.log).  in_proj: whole-line non-temporal stores, 1646 vs 1690 us
     // (r05_d_lnqkv.log; FETCH 5.4 -> 3.7x the operand bytes: the output no longer displaces the
-    // weight panel from L2, profiles/r05_b_fullnt_gemm_traffic_ab.json)
+    // weight panel from L2, profiles/r05_b_fullnt_gemm_traffic_ab.json).  Both: the lagging
+    // M-group's epilogue beside the leading one's (F_BEARLY): c_fc 2143-2149 vs 2230 us, qkv 1606
+    // vs 1615 us, bit-identical (profiles/r05_f_lnfc.log, r05_f_lnqkv.log)
     if (epi == EPI_LN_BF16)
-      hipLaunchKernelGGL((gemm_8q_kernel<EPI_LN_BF16, 0, F_FULL | F_ONT, true>), dim3(grid), dim3(512), 0, s, a);
+      hipLaunchKernelGGL((gemm_8q_kernel<EPI_LN_BF16, 0, F_BEARLY | F_FULL | F_ONT, true>), dim3(grid), dim3(512), 0, s, a);
     else
-      hipLaunchKernelGGL((gemm_8q_kernel<EPI_LN_GELU_BF16, 0, F_GPK | F_ONT | F_FULL | F_GSTAGE16 | F_GSTAGE | F_VOREC, true>),
-                         dim3(grid), dim3(512), 0, s, a);
+      hipLaunchKernelGGL(
+          (gemm_8q_kernel<EPI_LN_GELU_BF16, 0, F_BEARLY | F_GPK | F_ONT | F_FULL | F_GSTAGE16 | F_GSTAGE | F_VOREC, true>),
+          dim3(grid), dim3(512), 0, s, a);
     return hipGetLastError();
   }
   if (a.a_f16) return hipErrorInvalidValue;

@@ -273,7 +273,7 @@ constexpr size_t rank_reg_lds_bytes(int NB) { return (size_t)4 * NB * (32 * 128)
 
 // STAMP (A/B build, MICLIP_RANK_STAMP=1): s_memrealtime (100 MHz) per workgroup at entry, after the query
 // load, after the stream, after fold_publish and at exit (mi_debug_rank_stamp)
-__device__ unsigned long long g_rank_stamp[256 * 16];
+__device__ unsigned long long g_rank_stamp[256 * 10];
 
 template <int D, int NB = 8, int PF = 6, bool NOMFMA = false, bool ILV = false, bool PIPE = false, int DT = 0,
           bool STAMP = false>
@@ -316,7 +316,7 @@ __global__ __launch_bounds__(256) void rank_reg(const void* __restrict__ corpus,
   const int64_t q0 = (int64_t)QB * RQ;
   const bool qvalid = q0 + r < Q;
   if (gate && __all(!qvalid || gate[q0 + r] != 0)) return;
-  unsigned long long* stamp = g_rank_stamp + 16 * ((int)RB & 255);
+  unsigned long long* stamp = g_rank_stamp + 10 * ((int)RB & 255);
   if (STAMP && tid == 0) stamp[0] = __builtin_amdgcn_s_memrealtime();
 
   // queries -> registers (zeros past Q)
@@ -1193,7 +1193,7 @@ hipError_t rank_of_targets(const float* S, int64_t Q, int64_t N, const int64_t* 
 
 }  // namespace miclip
 
-// Diagnostics (A/B build): the rank_reg stamps of the last MICLIP_RANK_STAMP launch, 256 x 16
+// Diagnostics (A/B build): the rank_reg stamps of the last MICLIP_RANK_STAMP launch, 256 x 10
 extern "C" int mi_debug_rank_stamp(unsigned long long* host, int n) {
 #if MICLIP_AB
   if (!host || n < 0) return -1;

@@ -325,9 +325,7 @@ __device__ __forceinline__ void fold_reduce(char* smem, const FoldWs& f, int64_t
 
   // merge `count` slab lines (slab w of query q at base[(w Qpad + q) 16]) into the query's top-k:
   // into gdst's line (sorted packed keys, zeros after) or, final, into out_s / out_i
-  // stamps (MICLIP_RANK_STAMP, A/B): [sb] reduce entry, [sb + 1] slab lines merged, [sb + 2] entries appended
-  auto reduce = [&](const uint64_t* base, int count, uint64_t* gdst, int sb) {
-    if (stamp && tid == 0) stamp[sb] = __builtin_amdgcn_s_memrealtime();
+  auto reduce = [&](const uint64_t* base, int count, uint64_t* gdst) {
     if (tid < FQ) hdr[tid] = 0u;
     __syncthreads();
     uint64_t L[16];
@@ -343,31 +341,29 @@ __device__ __forceinline__ void fold_reduce(char* smem, const FoldWs& f, int64_t
       // after the acquire a plain (atomic) load sees every workgroup's raise; the fetch_max(0) it
       // replaces was a device-scope RMW per lane, tpq lanes to one address
       const uint64_t tauP = (uint64_t)__hip_atomic_load(&f.gtau[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) << 32;
-      // whole slab lines, one at a time: the line is parked in this thread's 128-byte LDS slot and
-      // merged by ONE rolled insertion loop while the next line's loads are in flight.  (The
-      // unrolled form -- 4 lines in registers, 64 inlined insertions -- was ~18 KB of code that
-      // runs once per launch from a cold instruction cache: the group merge took ~35 us and the
-      // final one ~20 us at 1M rows, scripts/rank_stamp.py.)
-      uint64_t* park = buf + (int64_t)tid * 16;
-      uint4 nx[8];
-      auto load_line = [&](int w) {
-        const uint4* p = (const uint4*)(base + ((int64_t)w * f.Qpad + q) * 16);
+      // whole slab lines, unconditionally, a batch at a time (all pieces in flight together)
+      constexpr int BATCH = 4;
+      for (int w0 = sub; w0 < count; w0 += BATCH * tpq) {
+        uint4 hv[BATCH][8];
 #pragma unroll
-        for (int c = 0; c < 8; ++c) nx[c] = p[c];
-      };
-      int w = sub;
-      if (w < count) load_line(w);
-      while (w < count) {
+        for (int b = 0; b < BATCH; ++b) {
+          const int w = w0 + b * tpq;
+          const uint4* p = (const uint4*)(base + ((int64_t)(w < count ? w : 0) * f.Qpad + q) * 16);
 #pragma unroll
-        for (int c = 0; c < 8; ++c) ((uint4*)park)[c] = nx[c];
-        w += tpq;
-        if (w < count) load_line(w);
-#pragma nounroll
-        for (int e = 0; e < 2 * nld; ++e) take(park[e], tauP);
+          for (int c = 0; c < 8; ++c) hv[b][c] = p[c];
+        }
+#pragma unroll
+        for (int b = 0; b < BATCH; ++b) {
+          if (w0 + b * tpq >= count) continue;
+#pragma unroll
+          for (int c = 0; c < 8; ++c) {
+            if (c >= nld) break;
+            take(((uint64_t)hv[b][c].y << 32) | hv[b][c].x, tauP);
+            take(((uint64_t)hv[b][c].w << 32) | hv[b][c].z, tauP);
+          }
+        }
       }
     }
-    __syncthreads();   // every park slot read before the appends below reuse the area
-    if (stamp && tid == 0) stamp[sb + 1] = __builtin_amdgcn_s_memrealtime();
     // cut: the largest k-th key among the query's tpq threads (one of them holds k entries at or
     // above it, so the query's k-th is too); entries below it cannot rank, so fewer are appended
     // and counted.  Ties on the key stay in (the cut compares keys only).
@@ -395,7 +391,6 @@ __device__ __forceinline__ void fold_reduce(char* smem, const FoldWs& f, int64_t
         if (p < m) qb[at + p] = L[p];
     }
     __syncthreads();
-    if (stamp && tid == 0) stamp[sb + 2] = __builtin_amdgcn_s_memrealtime();
     if (act) {
       const int n = (int)hdr[qi];
       int rk[16];
@@ -431,15 +426,15 @@ __device__ __forceinline__ void fold_reduce(char* smem, const FoldWs& f, int64_t
   if (stamp && tid == 0) stamp[5] = __builtin_amdgcn_s_memrealtime();
   if (f.ngrp == 1) {                                   // one group: its last arrival writes the result
     if (stamp && tid == 0) stamp[6] = __builtin_amdgcn_s_memrealtime();
-    reduce(f.slab, nwg, nullptr, 9);
+    reduce(f.slab, nwg, nullptr);
     if (stamp && tid == 0) stamp[8] = __builtin_amdgcn_s_memrealtime();
     return;
   }
-  reduce(f.slab + (int64_t)g0 * f.Qpad * 16, gsz, f.gslab + (int64_t)grp * f.Qpad * 16, 9);
+  reduce(f.slab + (int64_t)g0 * f.Qpad * 16, gsz, f.gslab + (int64_t)grp * f.Qpad * 16);
   if (stamp && tid == 0) stamp[6] = __builtin_amdgcn_s_memrealtime();
   if (!last_arrival(f.cnt + QB, (uint32_t)f.ngrp)) return;
   if (stamp && tid == 0) stamp[7] = __builtin_amdgcn_s_memrealtime();
-  reduce(f.gslab, f.ngrp, nullptr, 12);
+  reduce(f.gslab, f.ngrp, nullptr);
   if (stamp && tid == 0) stamp[8] = __builtin_amdgcn_s_memrealtime();
 }
 

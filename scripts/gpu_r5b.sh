@@ -14,4 +14,18 @@ tail -1 gpurun_out/r5b/bench.log | cut -c1-600
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r5b/prof_fp32 -o bench -- \
   python3 bench.py --weights fp32 --steps 2 --warmup 1 --no-cpu-baseline --no-rank-roofline --no-kernel-timing \
   > gpurun_out/r5b/prof_fp32.log 2>&1 || exit $?
+export LN_FLAGS=1
+timeout -k 10 300 python -u scripts/gemm_micro.py 10 lnfc500 44,46,174 > gpurun_out/r5b/lnfc_full.log 2>&1 || exit $?
+timeout -k 10 300 python -u scripts/gemm_micro.py 10 lnqkv500 0,2,130 > gpurun_out/r5b/lnqkv_full.log 2>&1 || exit $?
+grep -v amdgpu.ids gpurun_out/r5b/lnfc_full.log gpurun_out/r5b/lnqkv_full.log
+for SV in lnfc500:174 lnqkv500:130 lnfc500:46; do
+  S=${SV%%:*}; V=${SV##*:}; D=gpurun_out/r5b/pmc_${S}_$V
+  for c in FETCH_SIZE WRITE_SIZE; do
+    timeout -s KILL 90 rocprofv3 --pmc $c --output-format csv -d $D/$c -o run -- \
+      python3 scripts/gemm_micro.py 1 $S $V > $D.$c.log 2>&1 || exit $?
+  done
+  timeout -s KILL 90 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES TCC_HIT_sum TCC_MISS_sum \
+    --output-format csv -d $D/MFMA -o run -- python3 scripts/gemm_micro.py 1 $S $V > $D.MFMA.log 2>&1 || exit $?
+  python3 scripts/pmc_traffic.py $D $S $D/traffic.json || exit $?
+done
 echo done

@@ -28,9 +28,9 @@ def main():
         for _ in range(3):
             retrieval.rank_topk(corpus, q, 10)
         torch.cuda.synchronize()
-        buf = np.zeros(256 * 16, dtype=np.uint64)
+        buf = np.zeros(256 * 10, dtype=np.uint64)
         assert L.mi_debug_rank_stamp(buf.ctypes.data, buf.size) == 0
-        st = buf.reshape(256, 16).astype(np.int64)
+        st = buf.reshape(256, 10).astype(np.int64)
         st = st[st[:, 0] > 0]
         t0 = st[:, 0].min()
         rel = (st - t0) / 100.0   # s_memtime ticks at 100 MHz -> us
@@ -41,10 +41,8 @@ def main():
         last = st[st[:, 6] > st[:, 5]]   # this launch's reducer (older launches' stamps 6-9 linger)
         for row in last:
             r = (row - t0) / 100.0
-            print(f"  group reducer: ticket {r[5]:.1f} reduce entry {r[9]:.1f} lines merged {r[10]:.1f} appended "
-                  f"{r[11]:.1f} group merged {r[6]:.1f}"
-                  + (f" | final ticket {r[7]:.1f} entry {r[12]:.1f} lines {r[13]:.1f} appended {r[14]:.1f} final merged "
-                     f"{r[8]:.1f}" if row[8] > row[6] else "") + f" exit {r[4]:.1f}")
+            print(f"  group reducer: ticket {r[5]:.1f} slabs taken {r[9]:.1f} group merged {r[6]:.1f}"
+                  + (f" final ticket {r[7]:.1f} final merged {r[8]:.1f}" if row[8] > row[6] else "") + f" exit {r[4]:.1f}")
         del corpus
 
 
