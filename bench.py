@@ -654,6 +654,13 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
+    # the roofline kernel (mlp.c_fc of the LayerNorm-folded bf16 tower) timed live: HIP events on
+    # the launch stream around each of its launches inside the timed steps (mi_clip_kernel_events)
+    from miclip import _native as _N
+    n_fc = args.steps * cfg.vision_layers * (-(-Nf // chunk))
+    fc_live = lnfold_active(model, cfg) and not args.no_kernel_timing
+    if fc_live:
+        _N.check(_N.lib().mi_clip_kernel_events(model._ctx, 1, n_fc), "mi_clip_kernel_events")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -665,6 +672,14 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
+    fc_us = None
+    if fc_live:
+        import ctypes
+        buf = (ctypes.c_float * n_fc)()
+        got = _N.lib().mi_clip_kernel_times(model._ctx, buf, n_fc)
+        _N.check(0 if got >= 0 else got, "mi_clip_kernel_times")
+        _N.check(_N.lib().mi_clip_kernel_events(model._ctx, 0, 0), "mi_clip_kernel_events off")
+        fc_us = [buf[i] for i in range(got)]
     seen = 1
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
@@ -706,6 +721,10 @@ def main():
         step_peak = {"fp8": FP8_PEAK_TFLOPS, "fp32": F32_MFMA_PEAK_TFLOPS}.get(args.weights, BF16_PEAK_TFLOPS)
         mfma_frac = step_flops / (ms / 1e3) / (step_peak * 1e12) / world
         dom = kern.get("gemm_fc")
+        if dom and fc_us:   # the launches of the timed steps (events), not the micro loop
+            dom = {"us": round(sum(fc_us) / len(fc_us), 2), "launches": len(fc_us),
+                   "min_us": round(min(fc_us), 2), "max_us": round(max(fc_us), 2),
+                   "micro_us": kern["gemm_fc"]["us"]}
         M = chunk * cfg.vision_tokens
         roof = None
         if dom:
@@ -734,7 +753,11 @@ def main():
                                              + (4 if f32 else 2) * M * 4 * cfg.vision_width
                                              + (8 * M + 8 * 4 * cfg.vision_width if lnf else 0)),
                     "flops_per_launch": fl, "launch_shape": [M, 4 * cfg.vision_width, cfg.vision_width],
-                    "avg_launch_us": dom["us"]}
+                    "avg_launch_us": dom["us"],
+                    "timing": ("HIP events around each c_fc launch of the timed steps (mi_clip_kernel_events): "
+                               f"{dom['launches']} launches, {dom['min_us']}-{dom['max_us']} us; the random-operand "
+                               f"micro loop (kernels.gemm_fc) {dom['micro_us']} us") if "launches" in dom
+                              else "HIP events around the kernel_timing micro loop (random operands)"}
         parity = None
         _progress("parity mode / cpu baseline")
         if not args.no_parity_mode and world == 1 and args.weights == "bf16":

@@ -283,6 +283,9 @@ struct mi_clip {
   // mutex only covers their launch, so a call on another stream first waits for the event
   // recorded after the previous call's last kernel
   hipEvent_t ws_evt = nullptr;
+  // kernel timing (mi_clip_kernel_events): start / stop events around the launches of one tower GEMM
+  int ev_kind = 0, ev_cap = 0, ev_n = 0;
+  std::vector<hipEvent_t> ev;
   hipStream_t ws_stream = nullptr;
   bool ws_used = false;
 };
@@ -580,6 +583,7 @@ int mi_clip_destroy(mi_clip* c) {
     if (c->w6) (void)hipFree(c->w6);
     if (c->w3) (void)hipFree(c->w3);
     if (c->ws_evt) (void)hipEventDestroy(c->ws_evt);
+    for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
   }
   delete c;
   return MI_OK;
@@ -844,7 +848,10 @@ static int run_tower_fold(mi_clip* c, const std::vector<Layer>& layers, int B, i
       HIP_TRY(gemm_bf16(with_variant(gargs(c->att, W, L.w_out, W, L.b_out, c->delta, W, M, W, W), GV_OUT), EPI_BF16, s));
       HIP_TRY(residual_stats(c->x, c->delta, c->rs, M, W, s));
     }
+    const bool tm = c->ev_kind == MI_KERNEL_C_FC && c->ev_n < c->ev_cap;
+    if (tm) HIP_TRY(hipEventRecord(c->ev[2 * c->ev_n], s));
     HIP_TRY(gemm_bf16(ln_args(c, L.lw_fc, L.ls_fc, L.lc_fc, c->mlp, 4 * W, M, W), EPI_LN_GELU_BF16, s));
+    if (tm) HIP_TRY(hipEventRecord(c->ev[2 * c->ev_n++ + 1], s));
     if (fuse && !last) {
       MI_TRY(gemm_residual(c, c->mlp, 4 * W, L.w_proj, L.b_proj, M, W, 4 * W, s));
     } else {
@@ -1298,6 +1305,35 @@ int mi_op_split6(const float* x, int64_t ldx, int64_t rows, int32_t K, int32_t r
   if (K < 4 || K % 4 || ldx < K || ldx % 4) return fail(MI_ERR_UNSUPPORTED, "mi_op_split6: K %% 4 == 0, ldx >= K, ldx %% 4 == 0");
   HIP_TRY(split6_rows(x, ldx, rows, K, role, gelu, (uint16_t*)out, (hipStream_t)stream));
   return MI_OK;
+}
+
+int mi_clip_kernel_events(mi_clip* c, int32_t kind, int32_t capacity) {
+  if (!c || kind < 0 || kind > MI_KERNEL_C_FC || capacity < 0 || capacity > (1 << 16))
+    return fail(MI_ERR_ARG, "mi_clip_kernel_events: bad arguments");
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  while ((int)c->ev.size() < 2 * capacity) {
+    hipEvent_t e;
+    HIP_TRY(hipEventCreate(&e));
+    c->ev.push_back(e);
+  }
+  c->ev_kind = capacity ? kind : 0;
+  c->ev_cap = capacity;
+  c->ev_n = 0;
+  return MI_OK;
+}
+
+int mi_clip_kernel_times(mi_clip* c, float* us, int32_t n) {
+  if (!c || (!us && n > 0) || n < 0) return fail(MI_ERR_ARG, "mi_clip_kernel_times: bad arguments");
+  std::lock_guard<std::mutex> g(c->mu);
+  const int m = c->ev_n < n ? c->ev_n : n;
+  for (int i = 0; i < m; ++i) {
+    HIP_TRY(hipEventSynchronize(c->ev[2 * i + 1]));
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, c->ev[2 * i], c->ev[2 * i + 1]));
+    us[i] = ms * 1e3f;
+  }
+  return m;
 }
 
 int mi_op_split2h(const float* x, int64_t ldx, int64_t rows, int32_t K, int32_t role, int32_t gelu, void* out,

@@ -39,6 +39,7 @@ EXPORTS = (
     "mi_op_quantize_mx", "mi_op_gemm_mx",
     "mi_mirror_build", "mi_rank_mirror_workspace_bytes", "mi_rank_mirror", "mi_normalize_rows_f16",
     "mi_jpeg_decode_transform", "mi_op_split2h", "mi_op_gemm_split2h", "mi_op_attention_f32",
+    "mi_clip_kernel_events", "mi_clip_kernel_times",
 )
 
 
@@ -131,6 +132,8 @@ def _bind(path):
         "mi_op_split2h": (ctypes.c_int, [P, I64, I64, I32, I32, I32, P, P, P]),
         "mi_op_gemm_split2h": (ctypes.c_int, [P, P, P, P, P, P, I32, I32, I32, I32, P]),
         "mi_op_attention_f32": (ctypes.c_int, [P, P, I32, I32, I32, I32, P]),
+        "mi_clip_kernel_events": (ctypes.c_int, [P, I32, I32]),
+        "mi_clip_kernel_times": (ctypes.c_int, [P, P, I32]),
         "mi_op_quantize_mx": (ctypes.c_int, [P, P, P, I32, I32, P]),
         "mi_op_gemm_mx": (ctypes.c_int, [P, P, P, P, P, P, I32, I32, I32, I32, P]),
         "mi_resample_coeffs": (ctypes.c_int, [I32, ctypes.c_double, ctypes.c_double, I32, ctypes.c_int, P, I64, P]),
@@ -146,7 +149,7 @@ def _bind(path):
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
-    if L.mi_abi_version() != 4:
+    if L.mi_abi_version() != 5:
         raise MiClipError("libmiclip ABI version mismatch")
     return L
 

@@ -35,9 +35,10 @@
 extern "C" {
 #endif
 
-#define MICLIP_ABI_VERSION 4   /* 2: mi_jpeg_workspace_bytes / mi_jpeg_decode take the data size;
+#define MICLIP_ABI_VERSION 5   /* 2: mi_jpeg_workspace_bytes / mi_jpeg_decode take the data size;
                                   3: mi_normalize_rows_f16, mi_jpeg_decode_transform;
-                                  4: mi_op_split2h, mi_op_gemm_split2h, mi_op_attention_f32 */
+                                  4: mi_op_split2h, mi_op_gemm_split2h, mi_op_attention_f32;
+                                  5: mi_clip_kernel_events, mi_clip_kernel_times */
 
 enum mi_dtype { MI_F32 = 0, MI_BF16 = 1, MI_F16 = 2, MI_FP8 = 3 /* weights only: MX-fp8 vision GEMMs */ };
 enum mi_status { MI_OK = 0, MI_ERR_ARG = -1, MI_ERR_HIP = -2, MI_ERR_UNSUPPORTED = -3, MI_ERR_STATE = -4 };
@@ -348,6 +349,15 @@ int mi_op_split6(const float* x, int64_t ldx, int64_t rows, int32_t K, int32_t r
  *   on the exact-f32 MFMA, longer sequences on a per-row f32 kernel. */
 int mi_op_split2h(const float* x, int64_t ldx, int64_t rows, int32_t K, int32_t role, int32_t gelu, void* out,
                   float* scale, void* stream);
+/* Kernel timing of the product path (measurement only; bench.py's roofline): after
+ * mi_clip_kernel_events(ctx, MI_KERNEL_C_FC, capacity) the next `capacity` launches of the
+ * vision tower's mlp.c_fc GEMM (the LayerNorm-folded bf16 tower) are bracketed by HIP events on
+ * the caller's stream; mi_clip_kernel_times(ctx, us, n) waits for them and writes the first
+ * min(n, recorded) durations in microseconds, returning that count.  capacity 0 (or kind
+ * MI_KERNEL_NONE) switches the recording off. */
+enum mi_kernel_kind { MI_KERNEL_NONE = 0, MI_KERNEL_C_FC = 1 };
+int mi_clip_kernel_events(mi_clip* ctx, int32_t kind, int32_t capacity);
+int mi_clip_kernel_times(mi_clip* ctx, float* us, int32_t n);
 int mi_op_gemm_split2h(const void* A3, const void* W3, const float* a_scale, const float* w_scale, const float* bias,
                        float* out, int32_t M, int32_t N, int32_t K3, int32_t epi, void* stream);
 int mi_op_attention_f32(const float* qkv, float* out, int32_t B, int32_t S, int32_t W, int32_t causal, void* stream);

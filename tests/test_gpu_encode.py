@@ -246,3 +246,30 @@ def test_lnfold_tower_matches_oracle(gpu, monkeypatch, name, n):
     assert np.array_equal(prod, got if cfg.vision_width <= 1024 else got0)
     if n * cfg.vision_tokens < 256:
         assert np.array_equal(got, got0)     # the same (unfolded) path in both libraries
+
+
+def test_kernel_events_time_the_c_fc_launches(gpu):
+    """mi_clip_kernel_events / mi_clip_kernel_times (bench.py's live roofline timing): the c_fc
+    launches of the folded bf16 tower are bracketed by events -- one per layer and chunk, up to
+    the capacity -- with positive durations, and the outputs do not change."""
+    import ctypes
+    import torch
+    from miclip import _native as N, config, weights
+    cfg = config.get_config("ViT-B/32")
+    m = _model("ViT-B/32", gpu, image_chunk=8)
+    px = torch.from_numpy(weights.synthetic_pixels(16, cfg.image_resolution, seed=5)).to(gpu).bfloat16()
+    ref = m.encode_image(px).cpu().numpy()
+    L = N.lib()
+    cap = 2 * cfg.vision_layers + 5
+    N.check(L.mi_clip_kernel_events(m._ctx, 1, cap), "events")
+    got = m.encode_image(px).cpu().numpy()
+    buf = (ctypes.c_float * cap)()
+    n = L.mi_clip_kernel_times(m._ctx, buf, cap)
+    assert n == 2 * cfg.vision_layers                       # 16 frames = two 8-frame chunks
+    assert all(0 < buf[i] < 1e5 for i in range(n))
+    N.check(L.mi_clip_kernel_events(m._ctx, 0, 0), "off")
+    m.encode_image(px)
+    assert L.mi_clip_kernel_times(m._ctx, buf, cap) == 0
+    assert np.array_equal(got, ref)
+    with pytest.raises(N.MiClipError):
+        N.check(L.mi_clip_kernel_events(m._ctx, 7, 1), "bad kind")
