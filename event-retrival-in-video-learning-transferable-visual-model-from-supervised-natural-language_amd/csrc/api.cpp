@@ -72,6 +72,8 @@ struct Layer {
   // split-f16 GEMMs (the default since round 5)
   const uint16_t *h3_qkv = nullptr, *h3_out = nullptr, *h3_fc = nullptr, *h3_proj = nullptr;
   const float *c3_qkv = nullptr, *c3_out = nullptr, *c3_fc = nullptr, *c3_proj = nullptr;
+  // c_fc's output bound for the fused split (EPI_SPLIT_GELU): max_n sum_k |W_fc| and max |b_fc|
+  float fc_bw = 0.f, fc_bb = 0.f;
   // MX-fp8 copies (weight_dtype MI_FP8, vision tower): e4m3 codes + stage-major e8m0 scales
   const uint8_t *q_qkv = nullptr, *s_qkv = nullptr, *q_out = nullptr, *s_out = nullptr;
   const uint8_t *q_fc = nullptr, *s_fc = nullptr, *q_proj = nullptr, *s_proj = nullptr;
@@ -257,7 +259,8 @@ struct mi_clip {
   char* w3 = nullptr;     // f32 mode: split-f16 weight copies + column scales (Layer::h3_* / c3_*, conv_h3)
   const uint16_t* conv_h3 = nullptr;
   const float* conv_c3 = nullptr;
-  float* rsc = nullptr;   // f32 mode: row scales of the split-f16 activations (workspace)
+  float* rsc = nullptr;   // f32 mode: row scales of the split-f16 activations (workspace, 3 x rsc_rows)
+  int64_t rsc_rows = 0;
   uint16_t* a6 = nullptr; // f32 mode: split-bf16 activations of one GEMM, [M][6K] (workspace)
   // vision
   const uint16_t* conv_w = nullptr;
@@ -439,6 +442,20 @@ int mi_clip_create(const mi_clip_arch* arch, const float* weights, int64_t numel
         L[i].f_out = F(o.w_out);
         L[i].f_fc = F(o.w_fc);
         L[i].f_proj = F(o.w_proj);
+        {   // EPI_SPLIT_GELU's bound constants, from the host blob (rounded up to stay bounds)
+          const int64_t Wd = (int64_t)(&lo == &vlo ? a.vision_width : a.text_width);
+          const float* wfc = b.src + o.p_w_fc;
+          const float* bfc = b.src + o.p_b_fc;
+          double bw = 0, bb = 0;
+          for (int64_t n = 0; n < 4 * Wd; ++n) {
+            double r = 0;
+            for (int64_t k = 0; k < Wd; ++k) r += std::fabs((double)wfc[n * Wd + k]);
+            bw = r > bw ? r : bw;
+            bb = std::fabs((double)bfc[n]) > bb ? std::fabs((double)bfc[n]) : bb;
+          }
+          L[i].fc_bw = (float)(bw * (1.0 + 1e-6));
+          L[i].fc_bb = (float)(bb * (1.0 + 1e-6));
+        }
       } else {
         L[i] = Layer{F(o.ln1_g), F(o.ln1_b), F(o.b_qkv), F(o.b_out), F(o.ln2_g), F(o.ln2_b), F(o.b_fc), F(o.b_proj),
                      H(o.w_qkv), H(o.w_out), H(o.w_fc), H(o.w_proj)};
@@ -617,7 +634,8 @@ static int reserve_locked(mi_clip* c, int64_t ic, int64_t tc) {
   const bool split_ops = c->w6 || c->w3;
   const size_t o_a6 = split_ops ? carve((size_t)mx(mx(Mv * Wv, Mt * Wt) * 24 * 2, ic * c->G * c->G * 3 * c->Kp32 * 2))
                                 : carve(0);
-  const size_t o_rsc = c->w3 ? carve((size_t)mx(mx(Mv, Mt), ic * c->G * c->G) * 4) : carve(0);
+  // row scales: the split operand's (rsc), the fused c_fc split's (rsc + rows) and the LN rows' max |h|
+  const size_t o_rsc = c->w3 ? carve((size_t)mx(mx(Mv, Mt), ic * c->G * c->G) * 4 * 3) : carve(0);
   size_t o_hq = 0, o_hqs = 0, o_attq = 0, o_attqs = 0, o_mlpq = 0, o_mlpqs = 0;
   if (c->fp8) {
     const size_t mp = (size_t)((Mv + 1) & ~1);
@@ -648,6 +666,7 @@ static int reserve_locked(mi_clip* c, int64_t ic, int64_t tc) {
   c->rs = (float*)(ws + o_rs);
   c->a6 = split_ops ? (uint16_t*)(ws + o_a6) : nullptr;
   c->rsc = c->w3 ? (float*)(ws + o_rsc) : nullptr;
+  c->rsc_rows = mx(mx(Mv, Mt), ic * c->G * c->G);
   if (c->fp8) {
     c->hq = (uint8_t*)(ws + o_hq);
     c->hqs = (uint8_t*)(ws + o_hqs);
@@ -928,6 +947,13 @@ static int run_tower_f32(mi_clip* c, const std::vector<Layer>& layers, int B, in
     // split by one pass each (c_proj's with QuickGELU applied first)
     uint16_t* a3 = c->a6;
     float* rsc = c->rsc;
+    // the fused c_fc split (the default; MICLIP_F32_FUSED_SPLIT=0 in the A/B build keeps the f32
+    // pre-activation + split pass): c_proj's operand [M][12W] after c_fc's [M][3W] in the workspace
+    const char* fe = ab_getenv("MICLIP_F32_FUSED_SPLIT");
+    const bool fuse_split = !fe || atoi(fe) != 0;
+    uint16_t* a3o = a3 + (int64_t)M * 3 * W;
+    float* rsc_o = rsc + c->rsc_rows;
+    float* rmax = rsc + 2 * c->rsc_rows;
     auto gemm3 = [&](int K, const uint16_t* w3, const float* c3, const float* b, float* out, int N, int epi) -> int {
       GemmArgs g = gargs(a3, 3 * K, w3, 3 * K, b, out, N, M, N, 3 * K);
       g.a_f16 = 1;
@@ -942,6 +968,24 @@ static int run_tower_f32(mi_clip* c, const std::vector<Layer>& layers, int B, in
       HIP_TRY(attention_f32(qkv, att, B, S, W, causal, s));
       HIP_TRY(split2h_rows(att, W, M, W, 0, 0, a3, rsc, s));
       MI_TRY(gemm3(W, L.h3_out, L.c3_out, L.b_out, c->x, W, EPI_RESID_F32));
+      if (fuse_split) {   // c_fc's epilogue writes c_proj's split operand (EPI_SPLIT_GELU)
+        HIP_TRY(layernorm_split2h(c->x, W, L.ln2_g, L.ln2_b, M, W, a3, rsc, s, rmax));
+        GemmArgs g = gargs(a3, 3 * W, L.h3_fc, 3 * W, L.b_fc, a3o, 3 * 4 * W, M, 4 * W, 3 * W);
+        g.a_f16 = 1;
+        g.rsc = rsc;
+        g.csc = L.c3_fc;
+        g.rmax = rmax;
+        g.bnd_w = L.fc_bw;
+        g.bnd_b = L.fc_bb;
+        g.rsc_out = rsc_o;
+        HIP_TRY(gemm_bf16(g, EPI_SPLIT_GELU, s));
+        GemmArgs p = gargs(a3o, 3 * 4 * W, L.h3_proj, 3 * 4 * W, L.b_proj, c->x, W, M, W, 3 * 4 * W);
+        p.a_f16 = 1;
+        p.rsc = rsc_o;
+        p.csc = L.c3_proj;
+        HIP_TRY(gemm_bf16(p, EPI_RESID_F32, s));
+        continue;
+      }
       HIP_TRY(layernorm_split2h(c->x, W, L.ln2_g, L.ln2_b, M, W, a3, rsc, s));
       MI_TRY(gemm3(W, L.h3_fc, L.c3_fc, L.b_fc, mlp, 4 * W, EPI_F32));   // pre-activation
       HIP_TRY(split2h_rows(mlp, 4 * W, M, 4 * W, 0, 1, a3, rsc, s));       // QuickGELU, then split

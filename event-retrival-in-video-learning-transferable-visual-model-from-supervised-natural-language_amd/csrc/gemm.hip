@@ -89,6 +89,42 @@ __device__ __forceinline__ void tile_coords(int t, int tiles_m, int tiles_n, int
 
 template <bool V>
 struct BoolT {};
+
+// EPI_SPLIT_GELU (split-f16 GEMM, fp32 tower c_fc): QuickGELU of the f32 pre-activations v
+// (columns n .. n + 3 of row m; the f32 epilogue's expf form) scaled by the row's power of two
+// and split into the next GEMM's operand [y1 | y1 | y2] (precise.hip split2h_rows, role 0).  The
+// scale comes from a bound instead of the row's max, which this tile cannot see:
+// |y| <= |v| <= max|a_m| * max_n sum_k |W_nk| + max|b| (with 2^-8 of slack for the f32 rounding
+// of v), so |y s| < 2^14 (1 + 2^-8); a loose bound only lowers the subnormal floor's share.
+__device__ __forceinline__ int split_exp_g(float mx) {
+  if (!(mx > 0.f) || !__builtin_isfinite(mx)) return 0;
+  int ex;
+  (void)frexpf(mx, &ex);
+  const int e = 14 - ex;
+  return e > 126 ? 126 : (e < -126 ? -126 : e);
+}
+__device__ __forceinline__ void split_gelu_store(const GemmArgs& a, int m, int n, float4 v) {
+  const float bound = (a.rmax[m] * a.bnd_w + a.bnd_b) * (1.0f + 0.00390625f);
+  const int e = split_exp_g(bound);
+  const float y[4] = {v.x * (1.0f / (1.0f + expf(-1.702f * v.x))), v.y * (1.0f / (1.0f + expf(-1.702f * v.y))),
+                      v.z * (1.0f / (1.0f + expf(-1.702f * v.z))), v.w * (1.0f / (1.0f + expf(-1.702f * v.w)))};
+  typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+  _Float16 p1[4], p2[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float ys = ldexpf(y[i], e);
+    p1[i] = (_Float16)ys;
+    const float f1 = (float)p1[i];
+    p2[i] = __builtin_isfinite(f1) ? (_Float16)(ys - f1) : (_Float16)0.f;
+  }
+  const h4 h1 = {p1[0], p1[1], p1[2], p1[3]}, h2 = {p2[0], p2[1], p2[2], p2[3]};
+  _Float16* o = (_Float16*)a.out + (int64_t)m * a.ldo + n;
+  const int N = a.N;
+  *(h4*)o = h1;
+  *(h4*)(o + N) = h1;
+  *(h4*)(o + 2 * N) = h2;
+  if (n == 0) a.rsc_out[m] = ldexpf(1.f, -e);
+}
 typedef _Float16 f16x8_g __attribute__((ext_vector_type(8)));
 // one 16x16x32 MFMA on bf16 or (split-f16 operands) fp16 fragments of the same bytes
 __device__ __forceinline__ f32x4 mfma16(BoolT<false>, bf16x8 b, bf16x8 a, f32x4 c) {
@@ -240,6 +276,8 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_kernel(GemmArgs a
           *(uint2*)((uint16_t*)a.out + orow * a.ldo + n) = make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
         } else if (EPI == EPI_F32) {
           *(float4*)((float*)a.out + orow * a.ldo + n) = make_float4(v0, v1, v2, v3);
+        } else if constexpr (EPI == EPI_SPLIT_GELU) {
+          split_gelu_store(a, m, n, make_float4(v0, v1, v2, v3));
         } else {  // EPI_RESID_F32 (operator API only): read-modify-write, not overlapped
           float4* dst = (float4*)((float*)a.out + orow * a.ldo + n);
           const float4 o = *dst;
@@ -249,7 +287,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_kernel(GemmArgs a
     }
     // a tail tile issues fewer than S stores (and the residual form issues
     // loads): drain so the counted waits stay exact
-    if (tail || EPI == EPI_RESID_F32) {
+    if (tail || EPI == EPI_RESID_F32 || EPI == EPI_SPLIT_GELU) {   // (the split form: 3 stores + a load each)
       vm_wait_all();
       pend = false;
     } else {
@@ -526,6 +564,10 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs a) {
         const int m = m0 + p * WTM + r;
         if (m < a.M) {
           const float4 v = *(const float4*)(smem + r * RS + c4 * 16);
+          if constexpr (EPI == EPI_SPLIT_GELU) {
+            split_gelu_store(a, m, n0 + c4 * 4, v);
+            continue;
+          }
           float4* dst = (float4*)((float*)a.out + out_row(m) * a.ldo + n0 + c4 * 4);
           if (EPI == EPI_RESID_F32) {
             const float4 o = *dst;
@@ -1080,8 +1122,11 @@ hipError_t launch(const GemmArgs& a, hipStream_t s) {
     return hipGetLastError();
   }
   if (a.a_f16) {   // split-f16 operands (fp32 tower): f32 epilogues with the rsc / csc factors
-    if ((EPI != EPI_F32 && EPI != EPI_RESID_F32) || !a.rsc || !a.csc || a.variant) return hipErrorInvalidValue;
-    if constexpr (EPI == EPI_F32 || EPI == EPI_RESID_F32) {
+    if ((EPI != EPI_F32 && EPI != EPI_RESID_F32 && EPI != EPI_SPLIT_GELU) || !a.rsc || !a.csc || a.variant)
+      return hipErrorInvalidValue;
+    if (EPI == EPI_SPLIT_GELU && (!a.rmax || !a.rsc_out || a.group || a.ldo != 3 * (int64_t)a.N))
+      return hipErrorInvalidValue;
+    if constexpr (EPI == EPI_F32 || EPI == EPI_RESID_F32 || EPI == EPI_SPLIT_GELU) {
       const int ntf = ((a.M + 255) / 256) * (a.N / 256);
       if (big && a.K / BK >= LEAD) {
         hipLaunchKernelGGL((gemm_pp_kernel<EPI, 1, false, false, false, false, true>), dim3(ntf), dim3(512), 0, s, a);
@@ -1144,6 +1189,7 @@ hipError_t gemm_bf16(const GemmArgs& a, int epi, hipStream_t s) {
     case EPI_GELU_BF16: return launch<EPI_GELU_BF16>(a, s);
     case EPI_RESID_F32: return launch<EPI_RESID_F32>(a, s);
     case EPI_F32: return launch<EPI_F32>(a, s);
+    case EPI_SPLIT_GELU: return launch<EPI_SPLIT_GELU>(a, s);
     case EPI_LN_BF16:
     case EPI_LN_GELU_BF16:   // LayerNorm-folded vision tower: the 8-phase kernel only
     case EPI_RES16_BF16:

@@ -56,6 +56,7 @@
 // Result (scripts/gemm_micro.py, M = 500k, interleaved with v98 in one process):
 // fc -4..-7 %, qkv -3..-4 %, proj -6 %, out +-3 %; bit-identical to gemm_8p.
 #include <cstdlib>
+#include <cstring>
 
 #include "common.hpp"
 #include "internal.hpp"
@@ -847,6 +848,13 @@ hipError_t gemm_8q(const GemmArgs& a0, int epi, hipStream_t s, int cus, int mode
 #if MICLIP_AB   // timing probes (scripts/gemm_micro.py resout500 / resproj500): 11 no statistics, 12 no x16 loads
     const char* ab = std::getenv("MICLIP_RES_ABL");
     const int abl = ab ? std::atoi(ab) : 0;
+    // start stagger (A/B, MICLIP_RES_STAGGER=phases:ticks): workgroups start (blockIdx / 8) % phases
+    // x ticks (100 MHz) late, so the CUs' epilogue x16 read bursts do not coincide chip-wide
+    if (const char* st = std::getenv("MICLIP_RES_STAGGER")) {
+      a.stagger_phases = std::atoi(st);
+      const char* c = std::strchr(st, ':');
+      a.stagger_ticks = c ? std::atoi(c + 1) : 0;
+    }
     if (abl == 11) hipLaunchKernelGGL((gemm_8q_kernel<EPI_RES16_BF16, 11, 0>), dim3(grid), dim3(512), 0, s, a);
     else if (abl == 12) hipLaunchKernelGGL((gemm_8q_kernel<EPI_RES16_BF16, 12, 0>), dim3(grid), dim3(512), 0, s, a);
     else if (abl == 13) hipLaunchKernelGGL((gemm_8q_kernel<EPI_RES16_BF16, 13, 0>), dim3(grid), dim3(512), 0, s, a);

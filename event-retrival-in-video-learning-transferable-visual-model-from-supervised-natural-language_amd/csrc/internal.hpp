@@ -25,7 +25,12 @@ enum GemmEpi {
   // stride ldo), x16 = f16(x16 + bf16(acc + bias)) — residual_stats' arithmetic — and ps[r][n / 64]
   // = (sum, sum of squared deviations from that sum's mean) of the 64 stored values of row r,
   // columns n .. n + 63; residual_finalize turns a row's N / 64 partials into rs
-  EPI_RES16_BF16 = 8
+  EPI_RES16_BF16 = 8,
+  // split-f16 GEMM only (a_f16; the fp32 tower's c_fc): y = QuickGELU(acc * rsc[m] * csc[n] + b[n])
+  // (the f32 expf form) written as the NEXT GEMM's split-f16 operand (role 0, fp16 [M][3N] at out,
+  // ldo = 3N) with a per-row power-of-two scale from the bound |y| <= rmax[m] * bnd_w + bnd_b, and
+  // rsc_out[m] = 1 / that scale (the n-tile-0 workgroups write it)
+  EPI_SPLIT_GELU = 10
 };
 
 // MX block quantisation shared by the fp8 producers (gemm_mx.hip, encoder.hip):
@@ -82,6 +87,11 @@ struct GemmArgs {
   // multiplied by rsc[m] * csc[n] (powers of two) before the bias
   const float* rsc = nullptr;
   const float* csc = nullptr;
+  // EPI_SPLIT_GELU: the input rows' max |a| (layernorm_split2h), the weights' max row 1-norm and
+  // max |bias|, and the output row scales
+  const float* rmax = nullptr;
+  float bnd_w = 0.f, bnd_b = 0.f;
+  float* rsc_out = nullptr;
 };
 
 // Requirements: K % 64 == 0, N % 128 == 0, A/W 16-byte aligned rows.
@@ -199,8 +209,9 @@ hipError_t split6_rows(const float* x, int64_t ldx, int64_t rows, int K, int rol
 hipError_t split2h_rows(const float* x, int64_t ldx, int64_t rows, int K, int role, int gelu, uint16_t* out,
                         float* sc, hipStream_t s);
 // LayerNorm (f32 statistics) written directly as the split-f16 operand (role 0) + its row scales
+// rmax (nullable): the row's max |LN(x)| (EPI_SPLIT_GELU's bound)
 hipError_t layernorm_split2h(const float* x, int64_t in_stride, const float* g, const float* b, int rows, int W,
-                             uint16_t* out, float* sc, hipStream_t s);
+                             uint16_t* out, float* sc, hipStream_t s, float* rmax = nullptr);
 
 }  // namespace miclip
 

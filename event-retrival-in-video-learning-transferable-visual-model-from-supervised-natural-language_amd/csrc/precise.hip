@@ -251,7 +251,7 @@ __global__ __launch_bounds__(256) void split2h_kernel(const float* __restrict__ 
 __global__ __launch_bounds__(256) void ln_split2h_kernel(const float* __restrict__ x, int64_t in_stride,
                                                          const float* __restrict__ g, const float* __restrict__ b,
                                                          int rows, int W, _Float16* __restrict__ out,
-                                                         float* __restrict__ sc) {
+                                                         float* __restrict__ sc, float* __restrict__ rmax) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= rows) return;
   const float* xr = x + (int64_t)row * in_stride;
@@ -285,8 +285,12 @@ __global__ __launch_bounds__(256) void ln_split2h_kernel(const float* __restrict
       mx = absmax4(mx, v[i]);
     }
   }
-  const int e = split_exp(wave_max(mx));
-  if (lane == 0) sc[row] = ldexpf(1.f, -e);
+  const float rm = wave_max(mx);
+  const int e = split_exp(rm);
+  if (lane == 0) {
+    sc[row] = ldexpf(1.f, -e);
+    if (rmax) rmax[row] = rm;
+  }
   _Float16* o = out + (int64_t)row * 3 * W;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -582,11 +586,11 @@ hipError_t split2h_rows(const float* x, int64_t ldx, int64_t rows, int K, int ro
 }
 
 hipError_t layernorm_split2h(const float* x, int64_t in_stride, const float* g, const float* b, int rows, int W,
-                             uint16_t* out, float* sc, hipStream_t s) {
+                             uint16_t* out, float* sc, hipStream_t s, float* rmax) {
   if (rows <= 0) return hipSuccess;
   if (W > 1024 || W < 4 || W % 4 || in_stride % 4) return hipErrorInvalidValue;
   hipLaunchKernelGGL(ln_split2h_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, x, in_stride, g, b, rows, W,
-                     (_Float16*)out, sc);
+                     (_Float16*)out, sc, rmax);
   return hipGetLastError();
 }
 

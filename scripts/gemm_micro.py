@@ -79,7 +79,8 @@ def main():
         A, W = A.to(dt), W.to(dt)
         bias = torch.rand(Nn, device=dev, generator=g)
         res = epi == 8
-        variants = (all_variants if os.environ.get("LN_FLAGS") else [0]) if ln else ([0, 1, 2, 3, 5] if res else all_variants)
+        variants = (all_variants if os.environ.get("LN_FLAGS") else [0]) if ln else (
+            (all_variants if os.environ.get("RES_VARIANTS") else [0, 1, 2, 3, 5]) if res else all_variants)
         if os.environ.get("GEMM_MICRO_V0"):   # PMC passes (scripts/pmc_traffic.py): the product kernel only
             variants = [0]
         if res:
@@ -96,6 +97,8 @@ def main():
             if res:   # (x16 grows by the GEMM output each call: timing only, outputs not compared)
                 # v2 / v3: timing probes of the fused kernel without statistics / without x16 loads
                 os.environ["MICLIP_RES_ABL"] = {2: "11", 3: "12", 5: "13"}.get(v, "0")   # v5: non-temporal x16 loads / stores
+                # v6-v8: start stagger of half / a quarter of the workgroups (phases:ticks at 100 MHz)
+                os.environ["MICLIP_RES_STAGGER"] = {6: "2:1500", 7: "2:750", 8: "4:750"}.get(v, "")
                 if v != 1:
                     N.check(L.mi_op_gemm_residual(x16.data_ptr(), 2 * Nn, A.data_ptr(), K, W.data_ptr(),
                                                   bias.data_ptr(), ps.data_ptr(), rs2.data_ptr(), M, Nn, K, sp),
