@@ -581,7 +581,7 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
       if (FIRST) stamp(1);   // S1: epilogue issued
     }
     if (P == 1 && EK::RES && FIRST) {
-      if (has_prev) {
+      if (has_prev && !((F & F_BEARLY) && wr == 1)) {
         // the previous tile's x16 blocks 0-3 ahead of the phase's DMAs (one conditional block
         // from the loads to the epilogue: split across two, the loads' registers spilled)
         res_prefetch(2, 8, pm0, pn0);
@@ -626,7 +626,8 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
     if (P == 4) {
       // (EPI_RES16: 16 stores, 8 partial stores and the x16 loads of blocks 4-7 are younger;
       // the epilogue's wait for block 7 already retired the odd buffer)
-      if (FIRST && has_prev && EK::RES) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(ABL == 11 ? 20 : 28) : "memory");
+      if (FIRST && has_prev && EK::RES && !((F & F_BEARLY) && wr == 1))
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(ABL == 11 ? 20 : 28) : "memory");
       else if (FIRST && has_prev && ABL != 10 && !((F & F_BEARLY) && wr == 1)) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
       // (F_BEARLY, lagging group: its stores are OLDER than phase 1's DMAs, so vmcnt(4) below also
       // retires them -- issued three barrier intervals earlier)
@@ -670,11 +671,16 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
                   fb[ni][ks], fa[mi][ks], (FIRST && P <= 4 && ks == 0) ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[mh * 4 + mi][nh * 2 + ni],
                   0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
-    if constexpr ((F & F_BEARLY) && !EK::RES && P == 8 && LAST) {
+    if constexpr ((F & F_BEARLY) && P == 8 && LAST) {
       if (wr == 1) {   // this tile's epilogue now, beside the leading group's (see F_BEARLY)
         pm0 = cur_m0;
         pn0 = cur_n0;
         ppar = cpar;
+        __builtin_amdgcn_sched_barrier(0);
+        // EPI_RES16: x16 blocks 2-7 here, after the MFMA section (blocks 0-1 went out in phase 6;
+        // the fragment registers are dead, so all eight blocks fit); their latency runs beside the
+        // leading group's epilogue in the same barrier interval
+        res_prefetch(2, 8, pm0, pn0);
         __builtin_amdgcn_sched_barrier(0);
         epilogue();
         __builtin_amdgcn_sched_barrier(0);
@@ -738,8 +744,10 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
   }
   // the last tile's epilogue
   if (wr == 0) barrier();   // the M-groups' barrier counts meet
-  res_prefetch(2, 8, pm0, pn0);
-  if (!((F & F_BEARLY) && wr == 1)) epilogue();   // (F_BEARLY: the lagging group's is done)
+  if (!((F & F_BEARLY) && wr == 1)) {   // (F_BEARLY: the lagging group's is done)
+    res_prefetch(2, 8, pm0, pn0);
+    epilogue();
+  }
   if ((ABL == 9 || ABL == 10) && lane == 0 && (wave & 3) == 0 && blockIdx.x < 1024) {
 #pragma unroll
     for (int i = 0; i < 9; ++i) g_probe8q[(blockIdx.x * 2 + wr) * 9 + i] = st[i];
@@ -858,6 +866,7 @@ hipError_t gemm_8q(const GemmArgs& a0, int epi, hipStream_t s, int cus, int mode
     if (abl == 11) hipLaunchKernelGGL((gemm_8q_kernel<EPI_RES16_BF16, 11, 0>), dim3(grid), dim3(512), 0, s, a);
     else if (abl == 12) hipLaunchKernelGGL((gemm_8q_kernel<EPI_RES16_BF16, 12, 0>), dim3(grid), dim3(512), 0, s, a);
     else if (abl == 13) hipLaunchKernelGGL((gemm_8q_kernel<EPI_RES16_BF16, 13, 0>), dim3(grid), dim3(512), 0, s, a);
+    else if (abl == 14) hipLaunchKernelGGL((gemm_8q_kernel<EPI_RES16_BF16, 0, F_BEARLY>), dim3(grid), dim3(512), 0, s, a);
     else
 #endif
     hipLaunchKernelGGL((gemm_8q_kernel<EPI_RES16_BF16, 0, 0>), dim3(grid), dim3(512), 0, s, a);

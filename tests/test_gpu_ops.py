@@ -714,3 +714,31 @@ def test_attention_f32_vs_float64(gpu, B, S, W, causal):
     assert np.isfinite(got).all()
     err = np.abs(got - ref).max()
     assert err < 2e-6 * max(1.0, np.abs(ref).max()), err
+
+
+@pytest.mark.parametrize("M,W,K", [(3000, 768, 768), (2049, 768, 3072), (70001, 768, 768)])
+def test_gemm_residual_lagging_group_early_epilogue_bit_identical(gpu, monkeypatch, M, W, K):
+    """The fused residual GEMM with the lagging M-group's epilogue beside the leading one's
+    (gemm_8q F_BEARLY; A/B build, MICLIP_RES_ABL=14) against the product kernel: the stored fp16
+    stream, the row statistics and the partials bit for bit (the same arithmetic, another place
+    in the schedule); partial last tiles and multi-tile persistent walks."""
+    import torch
+    from miclip import _native
+    g = torch.Generator(device="cpu").manual_seed(M + W + K)
+    x16 = _half_slots((torch.randn(M, W, generator=g) * 3 + 1).half()).to(gpu)
+    A = (torch.randn(M, K, generator=g) * 0.5).bfloat16().to(gpu)
+    Wt = (torch.randn(W, K, generator=g) * K ** -0.5).bfloat16().to(gpu)
+    bias = torch.randn(W, generator=g).float().to(gpu)
+    outs = []
+    for lib, env in ((_native.lib(), None), (_native.lib_ab(), "14")):
+        if env:
+            monkeypatch.setenv("MICLIP_RES_ABL", env)
+        x = x16.clone()
+        ps = torch.full((M, W // 64, 2), float("nan"), device=gpu)
+        rs = torch.full((M, 2), float("nan"), device=gpu)
+        _native.check(lib.mi_op_gemm_residual(x.data_ptr(), 2 * W, A.data_ptr(), K, Wt.data_ptr(), bias.data_ptr(),
+                                              ps.data_ptr(), rs.data_ptr(), M, W, K, _stream()), "gemm_residual")
+        torch.cuda.synchronize()
+        outs.append((x.cpu(), ps.cpu(), rs.cpu()))
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)
