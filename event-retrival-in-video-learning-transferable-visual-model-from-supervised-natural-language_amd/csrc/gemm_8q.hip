@@ -797,6 +797,8 @@ hipError_t gemm_8q(const GemmArgs& a0, int epi, hipStream_t s, int cus, int mode
 #if MICLIP_AB   // A/B (MICLIP_8Q_F): epilogue flags F_VOREC (4) / F_GSTAGE (8) / both (12); 1 = none
     const char* fe = std::getenv("MICLIP_8Q_F");
     const int ff = fe ? std::atoi(fe) : 0;
+    // 1000: the deferred-epilogue one-wave kernel (gemm_1d.hip), 1004 its no-epilogue probe
+    if ((ff == 1000 || ff == 1004) && epi == EPI_LN_GELU_BF16) return gemm_1d(a0, ff - 1000, s, cus);
     if (ff == 1 && epi == EPI_LN_GELU_BF16) {
       hipLaunchKernelGGL((gemm_8q_kernel<EPI_LN_GELU_BF16, 0, 0, true>), dim3(grid), dim3(512), 0, s, a);
       return hipGetLastError();

@@ -103,6 +103,10 @@ hipError_t gemm_w4(const GemmArgs& a, int epi, hipStream_t s, int cus);
 int gemm_8p_ok(const GemmArgs& a);
 hipError_t gemm_8p(const GemmArgs& a, int epi, hipStream_t s, int cus, int abl = 0);
 // 8-phase, second schedule: descriptor DMAs, template-form waits, quadrant-split epilogue (gemm_8q.hip)
+// LN-folded c_fc with the epilogue deferred into the next tile's MFMAs, one wave per SIMD
+// (gemm_1d.hip, A/B build only); abl 4 = no-epilogue probe
+int gemm_1d_ok(const GemmArgs& a);
+hipError_t gemm_1d(const GemmArgs& a, int abl, hipStream_t s, int cus);
 int gemm_8q_ok(const GemmArgs& a);
 hipError_t gemm_8q(const GemmArgs& a, int epi, hipStream_t s, int cus, int mode = 0);
 hipError_t gemm8q_probe_read(unsigned long long* host, int n);   // ABL 9 stamps (gemm_8q.hip)

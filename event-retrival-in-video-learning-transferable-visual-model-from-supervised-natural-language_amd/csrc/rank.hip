@@ -276,7 +276,7 @@ constexpr size_t rank_reg_lds_bytes(int NB) { return (size_t)4 * NB * (32 * 128)
 __device__ unsigned long long g_rank_stamp[256 * 10];
 
 template <int D, int NB = 8, int PF = 6, bool NOMFMA = false, bool ILV = false, bool PIPE = false, int DT = 0,
-          bool STAMP = false>
+          bool STAMP = false, bool SPLITM = true>
 __global__ __launch_bounds__(256) void rank_reg(const void* __restrict__ corpus, int64_t N,
                                                 const float* __restrict__ queries, int64_t Q, int k,
                                                 int64_t rows_per_wg, int norm_mode, int nan_first, int64_t index_base,
@@ -512,6 +512,10 @@ __global__ __launch_bounds__(256) void rank_reg(const void* __restrict__ corpus,
   }
   // trailing (zero-range) DMAs and the pipelined read past the last chunk complete before the ring is reused
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  if (SPLITM) {   // split merge: the lists raw, then fold_merge_kernel (rank_keys.hpp)
+    lines_publish<NW>(L, smem, wave, lane, q0, Q, k, r_begin, f);
+    return;
+  }
   __syncthreads();   // ring free -> lists
   if (STAMP && tid == 0) stamp[2] = __builtin_amdgcn_s_memrealtime();
   uint32_t* Lk = (uint32_t*)smem;
@@ -683,6 +687,93 @@ __global__ __launch_bounds__(NT) void rank_merge_kernel(const float* __restrict_
         out_i[q * k + o] = bi;
       }
     }
+  }
+}
+
+// The split merge's second launch (rank_keys.hpp lines_publish): one workgroup per query
+// reduces the pass's nlines slab lines (one per pass workgroup: its top-k, sorted desc), thread
+// w loading line w whole.  A cut first: the k-th largest key among a wave's 64 line heads (k
+// distinct rows score at least that much, so the query's k-th does too), the largest such over
+// the waves and gtau (the largest workgroup k-th); sorting the heads' keys across the lanes is a
+// 21-step bitonic network of 32-bit shuffles.  Each line's prefix at or above the cut (ties on the
+// key kept) is appended to LDS, and thread j ranks appended entry j by counting the entries that
+// beat it (packed keys are unique: index asc breaks ties) -- the in-launch reducer's rule, so
+// results are bit-identical.  gtau alone kept ~800 of 2450 entries at 125k rows (a 117-us count).
+// gate (nullable): a query block whose queries are all certified holds its results (the
+// gated exact pass skipped it), so its queries are skipped here too.
+template <int NT>
+__global__ __launch_bounds__(NT) void fold_merge_kernel(const uint64_t* __restrict__ lines, const uint32_t* __restrict__ gtau,
+                                                        int64_t Qpad, int nlines, int64_t Q, int k, int nan_first,
+                                                        int64_t index_base, float* __restrict__ out_s,
+                                                        int64_t* __restrict__ out_i, const int32_t* __restrict__ gate) {
+  __shared__ uint64_t buf[NT * 16];
+  __shared__ uint32_t cnt, cutk;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int64_t q = blockIdx.x;
+  if (gate) {   // the same 32 reads in every wave: a uniform exit
+    const int64_t qq = q / FQ * FQ + (lane & 31);
+    if (__all(qq >= Q || gate[qq] != 0)) return;
+  }
+  if (tid == 0) {
+    cnt = 0u;
+    cutk = gtau[q];
+  }
+  const int nld = (k + 1) >> 1;   // 16-byte pieces of a line holding k entries
+  typedef unsigned int u32x4m __attribute__((ext_vector_type(4)));
+  uint64_t e[16];
+  {
+    const int w = tid < nlines ? tid : 0;   // (nlines <= NT: one line per thread)
+    const u32x4m* lp = (const u32x4m*)(lines + ((int64_t)w * Qpad + q) * 16);
+    u32x4m pc[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) pc[c] = (c < nld && tid < nlines) ? lp[c] : (u32x4m){0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      e[2 * c] = ((uint64_t)pc[c][1] << 32) | pc[c][0];
+      e[2 * c + 1] = ((uint64_t)pc[c][3] << 32) | pc[c][2];
+    }
+  }
+  // the wave's line heads' keys sorted descending across the lanes (an empty head sorts as key 0;
+  // a real key 0 is a NaN-last row, which then only makes the cut 0: no cut)
+  uint32_t hk = e[0] ? (uint32_t)(e[0] >> 32) : 0u;
+#pragma unroll
+  for (int size = 2; size <= 64; size <<= 1)
+#pragma unroll
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      const uint32_t o = (uint32_t)__shfl_xor((int)hk, stride, 64);
+      const bool lower = (lane & stride) == 0;        // this lane holds the pair's first position
+      const bool desc = (lane & size) == 0 || size == 64;
+      const uint32_t mx = hk > o ? hk : o, mn = hk > o ? o : hk;
+      hk = (lower == desc) ? mx : mn;
+    }
+  const uint32_t kth_head = (uint32_t)__shfl((int)hk, k - 1, 64);
+  __syncthreads();   // cnt / cutk initialised
+  if (lane == 0 && kth_head) atomicMax(&cutk, kth_head);
+  __syncthreads();
+  const uint64_t cut = (uint64_t)cutk << 32;
+  int m = 0;   // the line's prefix at or above the cut (sorted desc, zeros after)
+#pragma unroll
+  for (int p = 0; p < 16; ++p) m += (p < k && e[p] != 0ull && e[p] >= cut) ? 1 : 0;
+  if (m) {
+    const uint32_t at = atomicAdd(&cnt, (uint32_t)m);
+#pragma unroll
+    for (int p = 0; p < 16; ++p)
+      if (p < m) buf[at + p] = e[p];
+  }
+  __syncthreads();
+  const int n = (int)cnt;
+  for (int j = tid; j < n; j += NT) {
+    const uint64_t x = buf[j];
+    int rk = 0;
+    for (int i = 0; i < n; ++i) rk += buf[i] > x ? 1 : 0;
+    if (rk < k) {
+      out_s[q * k + rk] = decode_key((uint32_t)(x >> 32), nan_first);
+      out_i[q * k + rk] = index_base + (int64_t)(uint32_t)~(uint32_t)x;
+    }
+  }
+  for (int r = n + tid; r < k; r += NT) {   // fewer than k rows in all
+    out_s[q * k + r] = -INFINITY;
+    out_i[q * k + r] = -1;
   }
 }
 
@@ -1030,6 +1121,18 @@ hipError_t rank_merge(const float* cs, const int64_t* ci, int64_t Q, int64_t C, 
   return hipGetLastError();
 }
 
+namespace rankk {
+hipError_t fold_merge(const FoldWs& f, int64_t nwg, int64_t Q, int k, int nan_first, int64_t index_base, float* out_s,
+                      int64_t* out_i, const int32_t* gate, hipStream_t s) {
+  if (Q <= 0) return hipSuccess;
+  constexpr int NT = 256;
+  if (nwg > NT) return hipErrorInvalidValue;   // one slab line per thread (every pass has <= 256 workgroups)
+  hipLaunchKernelGGL((fold_merge_kernel<NT>), dim3((unsigned)Q), dim3(NT), 0, s, f.slab, f.gtau, f.Qpad, (int)nwg, Q, k,
+                     nan_first, index_base, out_s, out_i, gate);
+  return hipGetLastError();
+}
+}  // namespace rankk
+
 // rank_reg's workgroups: one per CU (LDS ring 128 KB), rows per workgroup a multiple of 128
 // (one 32-row tile per wave); never more workgroups than rank_chunks (workspace)
 static int64_t reg_rows_per_wg(int64_t N) {
@@ -1070,7 +1173,11 @@ static hipError_t launch_reg(int64_t N, const void* corpus, const float* q, int6
   const char* pipe = getenv("MICLIP_RANK_PIPE");
   const bool pp = pipe && pipe[0] == '1';
   const char* stp = getenv("MICLIP_RANK_STAMP");
-  auto fn = (stp && stp[0] == '1') ? rank_reg<D, 8, 6, false, false, false, DT, true>
+  // in-launch merge (the round-4 tail) instead of the split merge: A/B (MICLIP_RANK_FOLD=1)
+  const char* fold = getenv("MICLIP_RANK_FOLD");
+  const bool inl = fold && fold[0] == '1';
+  auto fn = (stp && stp[0] == '1') ? rank_reg<D, 8, 6, false, false, false, DT, true, false>
+            : inl ? rank_reg<D, 8, 6, false, false, false, DT, false, false>
             : nb9 ? rank_reg<D, 9, 7, false, false, false, DT>
             : (probe && probe[0] == '1') ? (il ? rank_reg<D, 8, 6, true, true, false, DT> : rank_reg<D, 8, 6, true, false, false, DT>)
             : il ? (pp ? rank_reg<D, 8, 6, false, true, true, DT> : rank_reg<D, 8, 6, false, true, false, DT>)
@@ -1078,13 +1185,18 @@ static hipError_t launch_reg(int64_t N, const void* corpus, const float* q, int6
 #else   // product: the measured default (8 slots, 6 chunks in flight, contiguous row ranges)
   const size_t lds = rank_reg_lds_bytes(8);
   auto fn = rank_reg<D, 8, 6, false, false, false, DT>;
+  constexpr bool inl = false;
 #endif
   hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
   if (!prezeroed && (e = fold_zero(f, s)) != hipSuccess) return e;
   const dim3 grid((unsigned)((Q + RQ - 1) / RQ), (unsigned)nwg);   // (query blocks, row blocks): RB / QB
   hipLaunchKernelGGL(fn, grid, dim3(256), lds, s, corpus, N, q, Q, k, rpw, nm, nf, base, f, out_s, out_i, gate);
-  return hipGetLastError();
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+#if MICLIP_AB
+  if (inl || (stp && stp[0] == '1')) return hipSuccess;
+#endif
+  return inl ? hipSuccess : fold_merge(f, nwg, Q, k, nf, base, out_s, out_i, gate, s);
 }
 
 template <int DT, int NW>

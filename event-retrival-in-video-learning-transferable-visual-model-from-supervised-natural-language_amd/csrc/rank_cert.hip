@@ -91,7 +91,7 @@ __device__ unsigned long long g_cert_probe[256 * 4 * 5];
 // ABL (A/B timing probes, wrong results): 1 = no Gram MFMAs (unit norms), 2 = no MFMAs at
 // all, 3 = no list update, 7 = no bucket writes; 5 = the epilogue stamp probe, 6 = the bucket
 // writes at the tile end instead of spread over the next tile (correct results)
-template <int DT, int ABL = 0>
+template <int DT, int ABL = 0, bool SPLITM = true>
 __global__ __launch_bounds__(256) void rank_cert_kernel(const void* __restrict__ corpus, int64_t N,
                                                         const float* __restrict__ queries, int64_t Q, int kc,
                                                         int64_t rows_per_wg, int norm_mode, int nan_first, FoldWs f,
@@ -440,6 +440,10 @@ __global__ __launch_bounds__(256) void rank_cert_kernel(const void* __restrict__
   }
   if (__any(bad) && lane == 0) __hip_atomic_store(unsafe, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  if (SPLITM) {   // split merge: the lists raw, then fold_merge_kernel (rank_keys.hpp)
+    lines_publish<NW>(L, smem, wave, lane, q0, Q, kc, r_begin, f);
+    return;
+  }
   __syncthreads();   // ring free -> lists
   uint32_t* Lk = (uint32_t*)smem;
   int32_t* Li = (int32_t*)(smem + NT * KC * 4);
@@ -516,7 +520,11 @@ hipError_t rank_cert_topk(const void* corpus, int64_t N, int dt, const float* q,
   const int abl = ab ? atoi(ab) : 0;
 #endif
   auto fn = dt == 0 ? rank_cert_kernel<0> : rank_cert_kernel<1>;
+  bool inl = false;   // the in-launch merge (A/B: MICLIP_RANK_FOLD=1)
 #if MICLIP_AB
+  const char* fold = getenv("MICLIP_RANK_FOLD");
+  inl = fold && fold[0] == '1';
+  if (inl) fn = dt == 0 ? rank_cert_kernel<0, 0, false> : rank_cert_kernel<1, 0, false>;
   if (abl == 1) fn = dt == 0 ? rank_cert_kernel<0, 1> : rank_cert_kernel<1, 1>;
   else if (abl == 2) fn = dt == 0 ? rank_cert_kernel<0, 2> : rank_cert_kernel<1, 2>;
   else if (abl == 3) fn = dt == 0 ? rank_cert_kernel<0, 3> : rank_cert_kernel<1, 3>;
@@ -528,6 +536,7 @@ hipError_t rank_cert_topk(const void* corpus, int64_t N, int dt, const float* q,
     return e;
   hipLaunchKernelGGL(fn, grid, dim3(256), lds, s, corpus, N, q, Q, CKC, rpw, norm_mode, nan_first, fu, unsafe, m_s, m_i);
   if ((e = hipGetLastError()) != hipSuccess) return e;
+  if (!inl && (e = fold_merge(fu, nwg_used, Q, CKC, nan_first, 0, m_s, m_i, nullptr, s)) != hipSuccess) return e;
   float d_rel, d_abs;
   rank_cert_delta(dt, d_rel, d_abs);
   return rank_rescore(corpus, N, CD, dt, q, Q, k, CKC, m_s, m_i, base, d_rel, d_abs, norm_mode, nan_first, unsafe,

@@ -439,6 +439,70 @@ __device__ __forceinline__ void fold_reduce(char* smem, const FoldWs& f, int64_t
 }
 
 
+// ---- split merge (round 5): the pass publishes its workgroup's top-k, a second launch merges.
+// The in-launch merge above chains global round trips after the stream (a ticket, the group
+// reducer's slab lines, a second ticket, the final reducer: ~60-90 us at 125k-1M rows,
+// scripts/rank_stamp.py), and its fold_publish merged the 8 lists of a query with one thread
+// per query (~10-20 us).  Here each query's 8 lists (4 waves x 2 lane halves) merge as a tree:
+// the two halves by shuffles (merge16_desc), then wave 0 folds the other waves' lists from LDS;
+// the workgroup's top-k goes to its slab line (rows global) and raises gtau[q] to its k-th key.
+// fold_merge_kernel (rank.hip) then reduces each query's nwg lines in one workgroup.
+// smem: >= 4 waves x 32 queries x 16 entries x 8 B = 16 KB, free (the caller's ring, after the
+// stream's last wait); every thread of the workgroup calls this.
+__device__ __forceinline__ void merge16_xor(uint64_t (&L)[16], int off) {
+  uint64_t c[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)L[j], off, 64);
+    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(L[j] >> 32), off, 64);
+    c[j] = ((uint64_t)hi << 32) | lo;
+  }
+  merge16_desc(L, c);
+}
+
+template <int NW>
+__device__ __forceinline__ void lines_publish(uint64_t (&L)[16], char* smem, int wave, int lane, int64_t q0, int64_t Q,
+                                              int k, int64_t r_begin, const FoldWs& f) {
+  const int r = lane & 31;
+#pragma unroll
+  for (int p = 0; p < 16; ++p) {   // rows relative to the workgroup's range -> global (same order)
+    const uint64_t e = L[p];
+    L[p] = e ? ((e & 0xffffffff00000000ull) | (uint32_t)~(uint32_t)(r_begin + (int64_t)~(uint32_t)e)) : 0ull;
+  }
+  merge16_xor(L, 32);              // the wave's two half-lists of query r (both halves get it)
+  uint64_t* wl = (uint64_t*)smem;  // [NW][32][16]
+  __syncthreads();                 // every wave is done with its ring slots
+  if (wave > 0 && lane < 32) {
+#pragma unroll
+    for (int p = 0; p < 16; ++p) wl[((wave * 32) + r) * 16 + p] = L[p];
+  }
+  __syncthreads();
+  if (wave == 0 && lane < 32) {
+#pragma unroll
+    for (int w = 1; w < NW; ++w) {
+      uint64_t c[16];
+#pragma unroll
+      for (int p = 0; p < 16; ++p) c[p] = wl[((w * 32) + r) * 16 + p];
+      merge16_desc(L, c);
+    }
+    if (q0 + r < Q) {
+      typedef unsigned int u32x4lp __attribute__((ext_vector_type(4)));
+      u32x4lp* dst = (u32x4lp*)(f.slab + ((int64_t)RB * f.Qpad + q0 + r) * 16);
+      const int nld = (k + 1) >> 1;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        if (c >= nld) break;
+        dst[c] = (u32x4lp){(uint32_t)L[2 * c], (uint32_t)(L[2 * c] >> 32), (uint32_t)L[2 * c + 1],
+                           (uint32_t)(L[2 * c + 1] >> 32)};
+      }
+      uint64_t kth = L[0];
+#pragma unroll
+      for (int p = 1; p < 16; ++p) kth = p == k - 1 ? L[p] : kth;
+      if (kth) __hip_atomic_fetch_max(&f.gtau[q0 + r], (uint32_t)(kth >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 static inline int64_t qpad(int64_t Q) { return (Q + FQ - 1) / FQ * FQ; }
 static inline size_t al128(size_t b) { return (b + 127) / 128 * 128; }
 
@@ -467,6 +531,10 @@ static inline FoldWs fold_ws(void* ws, int64_t nwg, int64_t Q) {
   f.ngrp = (int)ng;
   return f;
 }
+
+// the split merge's second launch (rank.hip): grid Q, results into out_s / out_i [Q][k]
+hipError_t fold_merge(const FoldWs& f, int64_t nwg, int64_t Q, int k, int nan_first, int64_t index_base, float* out_s,
+                      int64_t* out_i, const int32_t* gate, hipStream_t s);
 
 static inline int64_t fold_zero_words(const FoldWs& f) { return (int64_t)((f.aux + 32) - f.cnt); }
 static inline uint32_t* fold_zero_base(const FoldWs& f) { return f.cnt; }

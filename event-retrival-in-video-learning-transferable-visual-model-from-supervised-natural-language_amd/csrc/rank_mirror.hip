@@ -89,7 +89,7 @@ __global__ __launch_bounds__(256) void mirror_build_kernel(const void* __restric
 // ILV: interleaved tile order (rank.hip rank_reg); otherwise each workgroup
 // streams rows_per_wg contiguous rows
 // PIPE: fragments read one chunk ahead (rank.hip rank_reg)
-template <int D, bool SPLIT, bool ILV = false, bool PIPE = true, int NB = 8, int PF = 6>
+template <int D, bool SPLIT, bool ILV = false, bool PIPE = true, int NB = 8, int PF = 6, bool SPLITM = true>
 __global__ __launch_bounds__(256) void rank_mirror_kernel(const uint16_t* __restrict__ mirror, int64_t N,
                                                           const float* __restrict__ queries, int64_t Q, int k,
                                                           int64_t rows_per_wg, int nan_first, FoldWs f,
@@ -253,6 +253,10 @@ __global__ __launch_bounds__(256) void rank_mirror_kernel(const uint16_t* __rest
     }
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  if (SPLITM) {   // split merge: the lists raw, then fold_merge_kernel (rank_keys.hpp)
+    lines_publish<NW>(L, smem, wave, lane, q0, Q, k, r_begin, f);
+    return;
+  }
   __syncthreads();   // ring free -> lists
   uint32_t* Lk = (uint32_t*)smem;
   int32_t* Li = (int32_t*)(smem + NT * KC * 4);
@@ -416,11 +420,16 @@ static hipError_t launch_mirror(const uint16_t* mirror, int64_t N, const float* 
 #if MICLIP_AB
   const char* var = getenv("MICLIP_MIRROR_VAR");
   const int v = var ? atoi(var) : 0;
-  auto fn = v == 1 ? rank_mirror_kernel<D, SPLIT, false, false>
+  // MICLIP_RANK_FOLD=1 (A/B): the in-launch merge instead of the split merge
+  const char* fold = getenv("MICLIP_RANK_FOLD");
+  const bool inl = fold && fold[0] == '1';
+  auto fn = inl ? rank_mirror_kernel<D, SPLIT, false, true, 8, 6, false>
+            : v == 1 ? rank_mirror_kernel<D, SPLIT, false, false>
             : v == 2 ? rank_mirror_kernel<D, SPLIT, false, true, 8, 7>
             : v == 3 ? rank_mirror_kernel<D, SPLIT, true> : rank_mirror_kernel<D, SPLIT>;
 #else
   auto fn = rank_mirror_kernel<D, SPLIT>;
+  constexpr bool inl = false;
 #endif
   hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
@@ -428,7 +437,8 @@ static hipError_t launch_mirror(const uint16_t* mirror, int64_t N, const float* 
   const FoldWs f = fold_ws(fws, nwg, Q);
   if ((e = fold_zero(f, s)) != hipSuccess) return e;
   hipLaunchKernelGGL(fn, grid, dim3(256), lds, s, mirror, N, q, Q, kc, rpw, nf, f, out_s, out_i);
-  return hipGetLastError();
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  return inl ? hipSuccess : fold_merge(f, nwg, Q, kc, nf, 0, out_s, out_i, nullptr, s);
 }
 
 hipError_t rank_mirror(const uint16_t* mirror, const void* master, int64_t N, int64_t D, int dt, const float* q,

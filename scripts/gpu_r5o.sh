@@ -1,0 +1,12 @@
+# r05 o: split rank merge: workgroup top-k by a shuffle/LDS tree in the pass, fold_merge_kernel over nwg lines
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out/r5o
+timeout -k 10 500 python -u -m pytest tests/test_gpu_rank.py tests/test_gpu_rank_scale.py tests/test_gpu_distributed.py \
+  tests/test_gpu_service.py -x -q --timeout 200 --timeout-method thread \
+  > gpurun_out/r5o/pytest_rank.log 2>&1 || { tail -30 gpurun_out/r5o/pytest_rank.log; exit 1; }
+tail -2 gpurun_out/r5o/pytest_rank.log
+export RANK_MICRO_VARIANTS=default,inl,exact,exact_inl
+timeout -k 10 240 python -u scripts/rank_micro.py 5 > gpurun_out/r5o/rank_micro.log 2>&1 || exit $?
+grep -v amdgpu.ids gpurun_out/r5o/rank_micro.log | head -4 | cut -c1-300
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r5o/prof -o rk -- python -u scripts/rank_micro.py 1 > gpurun_out/r5o/prof.log 2>&1 || exit $?
+echo done

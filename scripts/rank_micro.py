@@ -24,16 +24,21 @@ VARIANTS = {"default": {}, "exact": {"MICLIP_RANK_CERT": "0"},
             # certified-pass timing probes (wrong results): no Gram MFMAs, no MFMAs, no list update
             "c_nogram": {"MICLIP_RANK_CERT_ABL": "1"}, "c_nomfma": {"MICLIP_RANK_CERT_ABL": "2"},
             "c_nolist": {"MICLIP_RANK_CERT_ABL": "3"}, "c_endput": {"MICLIP_RANK_CERT_ABL": "6"},
-            "c_noput": {"MICLIP_RANK_CERT_ABL": "7"}}
+            "c_noput": {"MICLIP_RANK_CERT_ABL": "7"},
+            # round-4 in-launch merge instead of the split merge (r05)
+            "inl": {"MICLIP_RANK_FOLD": "1"}, "exact_inl": {"MICLIP_RANK_CERT": "0", "MICLIP_RANK_FOLD": "1"}}
 SHAPES = [(125_000, 512, 32, torch.float32), (1_000_000, 512, 32, torch.float32),
           (1_000_000, 512, 32, torch.bfloat16), (1_000_000, 768, 32, torch.float32)]
+if os.environ.get("RANK_MICRO_VARIANTS"):   # a comma list of the variants to time
+    VARIANTS = {v: VARIANTS[v] for v in os.environ["RANK_MICRO_VARIANTS"].split(",")}
 if os.environ.get("RANK_MICRO_SHAPES") == "cert":   # the certified pass's shapes only
     SHAPES = SHAPES[1:3]
 
 
 def setenv(v):
     for k in ("MICLIP_RANK_STAGE1", "MICLIP_RANK_NW", "MICLIP_RANK_REG", "MICLIP_RANK_PROBE", "MICLIP_RANK_ILV",
-              "MICLIP_RANK_PIPE", "MICLIP_RANK_SEED", "MICLIP_RANK_CERT", "MICLIP_RANK_CERT_ABL"):
+              "MICLIP_RANK_PIPE", "MICLIP_RANK_SEED", "MICLIP_RANK_CERT", "MICLIP_RANK_CERT_ABL",
+              "MICLIP_RANK_FOLD"):
         os.environ.pop(k, None)
     os.environ.update(VARIANTS[v])
 

@@ -464,3 +464,42 @@ def test_certified_pass_product_default_large_corpus(gpu, monkeypatch):
         monkeypatch.undo()
         torch.cuda.synchronize()
         assert torch.equal(i1, i0) and torch.equal(s1.view(torch.int32), s0.view(torch.int32))
+
+
+@pytest.mark.parametrize("N,Q,k,dt", [(1, 1, 1, "f32"), (9, 3, 10, "f32"), (4099, 33, 16, "bf16"),
+                                      (125_000, 32, 10, "f32"), (300_001, 40, 10, "f32"),
+                                      (300_001, 33, 12, "bf16"), (1_000_003, 32, 10, "f32")])
+def test_split_merge_bit_identical_to_in_launch_merge(gpu, monkeypatch, N, Q, k, dt):
+    """The split merge (the pass writes every lane's sorted list, fold_merge_kernel reduces
+    each query's lines; the product default of rank_reg, the certified pass and the mirror)
+    gives the round-4 in-launch merge's results bit for bit (A/B build, MICLIP_RANK_FOLD=1):
+    one and two query blocks, 1 .. 256 workgroups, the exact and the certified routes, with
+    a block of duplicated rows (ties across workgroups) and a zero row (NaN)."""
+    import torch
+    from miclip import _native, retrieval, weights
+    c32 = weights.normal(51, f"sm{N}", (N, 512))
+    if N > 1000:
+        c32[N // 3: N // 3 + 40] = c32[N // 2]      # 41 equal rows in different workgroups
+        c32[N // 4] = 0.0
+    c = _t(c32, gpu) if dt == "f32" else torch.from_numpy(c32).to(torch.bfloat16).to(gpu)
+    q = _t(weights.synthetic_corpus(Q, 512, seed=52), gpu)
+    q[0] = torch.from_numpy(c32[N // 2]).to(gpu)       # a query whose best rows tie
+    for pol in ("first", "last"):
+        s1, i1 = retrieval.rank_topk(c, q, k, nan_policy=pol)
+        monkeypatch.setattr(_native, "lib", _native.lib_ab)
+        monkeypatch.setenv("MICLIP_RANK_FOLD", "1")
+        s0, i0 = retrieval.rank_topk(c, q, k, nan_policy=pol)
+        monkeypatch.undo()
+        torch.cuda.synchronize()
+        assert torch.equal(i1, i0), pol
+        assert torch.equal(s1.view(torch.int32), s0.view(torch.int32)), pol
+    if N >= 262_144 and dt == "f32":   # the mirror's pass merges the same way
+        mc = retrieval.MirroredCorpus(c)
+        s1, i1 = mc.topk(q, k)
+        monkeypatch.setattr(_native, "lib", _native.lib_ab)
+        monkeypatch.setenv("MICLIP_RANK_FOLD", "1")
+        mc0 = retrieval.MirroredCorpus(c)
+        s0, i0 = mc0.topk(q, k)
+        monkeypatch.undo()
+        torch.cuda.synchronize()
+        assert torch.equal(i1, i0) and torch.equal(s1.view(torch.int32), s0.view(torch.int32))
