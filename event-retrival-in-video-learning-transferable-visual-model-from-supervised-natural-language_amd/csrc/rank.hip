@@ -99,7 +99,7 @@ __device__ __forceinline__ void score_tile(const void* corpus, int64_t N, int64_
 // LDS: queries [32][D+4] f32, row norms [NW][32], tau [32]; the lists
 // [64*NW lanes][16] (key u32, idx i32) reuse the query area after a barrier.
 
-template <int DT, int NW>
+template <int DT, int NW, bool SPLITM = true>
 __global__ __launch_bounds__(64 * NW) void rank_stream(const void* __restrict__ corpus, int64_t N, int64_t D,
                                                        const float* __restrict__ queries, int64_t Q, int k,
                                                        int64_t rows_per_wg, int norm_mode, int nan_first,
@@ -220,6 +220,10 @@ __global__ __launch_bounds__(64 * NW) void rank_stream(const void* __restrict__ 
       next_load(b1);
       consume(b2);
     }
+  }
+  if (SPLITM) {   // split merge: the workgroup's top-k published, then fold_merge_kernel
+    lines_publish<NW>(L, smem, wave, lane, q0, Q, k, r_begin, f);   // (its first barrier: the query area is free)
+    return;
   }
   __syncthreads();  // query area free -> lists
   uint32_t* Lk = (uint32_t*)smem;
@@ -706,8 +710,10 @@ __global__ __launch_bounds__(NT) void fold_merge_kernel(const uint64_t* __restri
                                                         int64_t Qpad, int nlines, int64_t Q, int k, int nan_first,
                                                         int64_t index_base, float* __restrict__ out_s,
                                                         int64_t* __restrict__ out_i, const int32_t* __restrict__ gate) {
-  __shared__ uint64_t buf[NT * 16];
-  __shared__ uint32_t cnt, cutk;
+  extern __shared__ __attribute__((aligned(16))) char fm_lds[];   // cnt, cut, then nlines x k entries
+  uint32_t& cnt = *(uint32_t*)fm_lds;
+  uint32_t& cutk = *((uint32_t*)fm_lds + 1);
+  uint64_t* buf = (uint64_t*)(fm_lds + 16);
   const int tid = threadIdx.x, lane = tid & 63;
   const int64_t q = blockIdx.x;
   if (gate) {   // the same 32 reads in every wave: a uniform exit
@@ -1125,10 +1131,24 @@ namespace rankk {
 hipError_t fold_merge(const FoldWs& f, int64_t nwg, int64_t Q, int k, int nan_first, int64_t index_base, float* out_s,
                       int64_t* out_i, const int32_t* gate, hipStream_t s) {
   if (Q <= 0) return hipSuccess;
-  constexpr int NT = 256;
-  if (nwg > NT) return hipErrorInvalidValue;   // one slab line per thread (every pass has <= 256 workgroups)
-  hipLaunchKernelGGL((fold_merge_kernel<NT>), dim3((unsigned)Q), dim3(NT), 0, s, f.slab, f.gtau, f.Qpad, (int)nwg, Q, k,
-                     nan_first, index_base, out_s, out_i, gate);
+  // one slab line per thread: 256 threads (rank_reg / rank_cert / the mirror: <= 256 workgroups)
+  // or 512 (rank_stream: up to 512)
+  if (nwg > 512) return hipErrorInvalidValue;
+  const size_t lds = 16 + (size_t)nwg * k * 8;
+  if (nwg <= 256) {
+    hipLaunchKernelGGL((fold_merge_kernel<256>), dim3((unsigned)Q), dim3(256), lds, s, f.slab, f.gtau, f.Qpad, (int)nwg,
+                       Q, k, nan_first, index_base, out_s, out_i, gate);
+  } else {
+    static bool attr = false;   // > 64 KB of LDS at nwg = 512, k = 16
+    if (!attr) {
+      const hipError_t e = hipFuncSetAttribute((const void*)fold_merge_kernel<512>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, 16 + 512 * 16 * 8);
+      if (e != hipSuccess) return e;
+      attr = true;
+    }
+    hipLaunchKernelGGL((fold_merge_kernel<512>), dim3((unsigned)Q), dim3(512), lds, s, f.slab, f.gtau, f.Qpad, (int)nwg,
+                       Q, k, nan_first, index_base, out_s, out_i, gate);
+  }
   return hipGetLastError();
 }
 }  // namespace rankk
@@ -1203,14 +1223,20 @@ template <int DT, int NW>
 static hipError_t launch_stream(dim3 grid, size_t lds, hipStream_t s, const void* corpus, int64_t N, int64_t D,
                                 const float* q, int64_t Q, int k, int64_t rpw, int nm, int nf, int64_t base,
                                 void* ws, float* out_s, int64_t* out_i) {
-  auto fn = rank_stream<DT, NW>;
+  bool inl = false;   // the in-launch merge (A/B: MICLIP_RANK_FOLD=1)
+#if MICLIP_AB
+  const char* fold = getenv("MICLIP_RANK_FOLD");
+  inl = fold && fold[0] == '1';
+#endif
+  auto fn = inl ? rank_stream<DT, NW, false> : rank_stream<DT, NW, true>;
   const size_t l = lds > fold_lds(64 * NW) ? lds : fold_lds(64 * NW);
   hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)l);
   if (e != hipSuccess) return e;
   const FoldWs f = fold_ws(ws, grid.y, Q);
   if ((e = fold_zero(f, s)) != hipSuccess) return e;
   hipLaunchKernelGGL(fn, grid, dim3(64 * NW), l, s, corpus, N, D, q, Q, k, rpw, nm, nf, base, f, out_s, out_i);
-  return hipGetLastError();
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  return inl ? hipSuccess : fold_merge(f, grid.y, Q, k, nf, base, out_s, out_i, nullptr, s);
 }
 
 hipError_t rank_topk(const void* corpus, int64_t N, int64_t D, int dt, const float* q, int64_t Q, int k,
