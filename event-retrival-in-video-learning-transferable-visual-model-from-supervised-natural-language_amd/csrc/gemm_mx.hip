@@ -414,14 +414,27 @@ __global__ __launch_bounds__(512) void gemm_mxpp_kernel(GemmArgs a) {
       amax = fmaxf(__uint_as_float(sx[0]), __uint_as_float(sx[1]));
       const int X = mx_block_exp(amax);
       const float inv = ldexpf(1.0f, -X);
+      // dword i of block ni holds bytes ni*32 + 8i + 4h .. +3 of the row; a half swap gives lanes
+      // 0-31 bytes ni*32 + 0..15 and lanes 32-63 bytes ni*32 + 16..31, so each lane stores 16
+      // contiguous bytes (2 store instructions per row block instead of 8 dword stores: the
+      // per-CU store issue, not the bytes, set the epilogue's time)
+      uint4 q16[2];
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) {
+        uint32_t d[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) d[i] = mx_pack4(v[ni][4 * i], v[ni][4 * i + 1], v[ni][4 * i + 2], v[ni][4 * i + 3], inv);
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_nop 4");   // wait states between the packs and the swaps (gemm_mx8q.hip permlane_gap)
+        __builtin_amdgcn_sched_barrier(0);
+        const auto s02 = __builtin_amdgcn_permlane32_swap(d[0], d[2], false, false);
+        const auto s13 = __builtin_amdgcn_permlane32_swap(d[1], d[3], false, false);
+        q16[ni] = make_uint4(s02[0], s02[1], s13[0], s13[1]);
+      }
       if (m < a.M) {
-        uint8_t* o = (uint8_t*)a.out + (int64_t)m * a.ldo + n0 + wc * WTN + 4 * h;
+        uint8_t* o = (uint8_t*)a.out + (int64_t)m * a.ldo + n0 + wc * WTN + 16 * h;
 #pragma unroll
-        for (int ni = 0; ni < 2; ++ni)
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            *(uint32_t*)(o + ni * 32 + 8 * i) =
-                mx_pack4(v[ni][4 * i], v[ni][4 * i + 1], v[ni][4 * i + 2], v[ni][4 * i + 3], inv);
+        for (int ni = 0; ni < 2; ++ni) *(uint4*)(o + ni * 32) = q16[ni];
         if (h == 0) a.o_scale[mx_scale_index(m, blk, m_pad)] = (uint8_t)(X + 127);
       }
     }
@@ -506,6 +519,7 @@ hipError_t gemm_mx(const GemmArgs& a, int epi, hipStream_t s) {
   if (a.M <= 0) return hipSuccess;
   if (a.K % MX_BK || a.N % 256 || a.K <= 0 || !a.a_scale || !a.w_scale) return hipErrorInvalidValue;
   if ((a.lda % 16) || (a.ldw % 16) || (a.ldo % 8) || ((uintptr_t)a.out & 15)) return hipErrorInvalidValue;
+  if (epi == EPI_GELU_MX && (a.ldo % 16)) return hipErrorInvalidValue;   // 16-byte fp8 row stores
   const int nt = ((a.M + 255) / 256) * (a.N / 256);
   // default: the ping-pong 32x32x64 kernel (needs K / 64 >= 3 stages).  A/B variants:
   // 1 the double-buffered 16x16x128 kernel; 8 the 8-phase persistent kernel (gemm_mx8q.hip:

@@ -153,3 +153,33 @@ def test_gemm_mx8q_matches_16x16x128_kernel(gpu, M, N, K, epi):
         # e4m3 keeps 3 mantissa bits (half an ulp = 2^-4 of the value); block values scaled into
         # [448, 512) saturate at 448 (up to 1/8); plus the block's subnormal floor
         assert np.all(np.abs(got - ref) <= 0.125 * np.abs(ref) + 0.01 * np.abs(ref).max())
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 512), (1001, 1024, 1024), (40000, 4096, 1024)])
+def test_gemm_mx_default_fp8_output_rows(gpu, M, N, K):
+    """The product MX kernel's (ping-pong 32x32x64) QuickGELU -> MX-fp8 epilogue, whose 16-byte
+    row stores take each lane's four e4m3 dwords through a half swap: every e4m3 byte and scale
+    lands where the consumer reads it -- decoded, the output matches the oracle's GELU within e4m3
+    rounding (row tails past M, odd M, 40000 rows)."""
+    import torch
+    N_ = _lib()
+    g = torch.Generator(device="cpu").manual_seed(M + K + 7)
+    a = (torch.randn(M, K, generator=g) * 2).bfloat16()
+    w = (torch.randn(N, K, generator=g) * K ** -0.5).bfloat16()
+    bias = torch.randn(N, generator=g).to(gpu)
+    qa, sa = _quant_gpu(a.to(gpu))
+    qw, sw = _quant_gpu(w.to(gpu))
+    mp = M + (M & 1)
+    out = torch.zeros((M * N + 255) // 256 * 256 + (N // 128) * mp * 2, dtype=torch.uint8, device=gpu)
+    N_.check(N_.lib().mi_op_gemm_mx(qa.data_ptr(), sa.data_ptr(), qw.data_ptr(), sw.data_ptr(), bias.data_ptr(),
+                                    out.data_ptr(), M, N, K, 4, _stream()), "gemm_mx")
+    torch.cuda.synchronize()
+    rows = np.arange(M) if M <= 2000 else np.r_[0:300, M // 2:M // 2 + 300, M - 300:M]
+    q = out[:M * N].cpu().numpy().reshape(M, N)[rows]
+    s = out[(M * N + 255) // 256 * 256:].cpu().numpy()
+    got = mx_ref.E4M3[q] * 2.0 ** (mx_ref.from_stage_major(s, M, N)[rows].repeat(64, 1).astype(np.float64) - 127)
+    sa_ = mx_ref.from_stage_major(sa.cpu().numpy(), M, K)[rows]
+    sw_ = mx_ref.from_stage_major(sw.cpu().numpy(), N, K)
+    ref = mx_ref.gemm(qa.cpu().numpy()[rows], sa_, qw.cpu().numpy(), sw_) + bias.double().cpu().numpy()
+    ref = ref / (1 + np.exp(-1.702 * ref))
+    assert np.all(np.abs(got - ref) <= 0.125 * np.abs(ref) + 0.01 * np.abs(ref).max())
