@@ -461,7 +461,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6))) void a
 // would add a third tile to wave 0 while the other waves idle with two; instead every wave
 // runs it over its share of the 16-key tiles (w, w + NW, ...) and wave 0 merges the partial
 // softmax states (m, l, o) of its valid rows through LDS.
-template <int NW, bool TT2 = true, bool SPLIT = false>
+template <int NW, bool TT2 = true, bool SPLIT = false, bool SFIRST = false, bool QPF = false>
 __global__ __launch_bounds__(NW * 64) void attention_res_kernel(const uint16_t* __restrict__ qkv,
                                                                 uint16_t* __restrict__ out, int S, int W, int H,
                                                                 uint8_t* __restrict__ q8, uint8_t* __restrict__ qs,
@@ -507,6 +507,15 @@ __global__ __launch_bounds__(NW * 64) void attention_res_kernel(const uint16_t* 
     return __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(LDS_AS char*)(uintptr_t)(const LDS_AS char*)p);
   };
 
+  // QPF (A/B): a tile's Q fragments are loaded one tile ahead (the wave's first tile's beside the
+  // K/V load), so their latency is not exposed at the head of every tile
+  bf16x8 qn[2];
+  auto load_q = [&](int t, bf16x8 (&q)[2]) {
+    const int qrow = min(t * 16 + fr, S - 1);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) q[s2] = *(const bf16x8*)(qb + (int64_t)qrow * ld + 32 * s2 + 8 * g);
+  };
+  if (QPF) load_q(wave, qn);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
@@ -519,11 +528,17 @@ __global__ __launch_bounds__(NW * 64) void attention_res_kernel(const uint16_t* 
     constexpr int TT = decltype(tt_c)::value;
     const int tq[2] = {t0, t1};
     bf16x8 qf[TT][2];
+    if (QPF && TT == 1) {
+      qf[0][0] = qn[0];
+      qf[0][1] = qn[1];
+      if (t0 + NW < (SPLIT ? nqt - 1 : nqt)) load_q(t0 + NW, qn);   // the wave's next tile
+    } else {
 #pragma unroll
-    for (int u = 0; u < TT; ++u) {
-      const int qrow = min(tq[u] * 16 + fr, S - 1);
+      for (int u = 0; u < TT; ++u) {
+        const int qrow = min(tq[u] * 16 + fr, S - 1);
 #pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) qf[u][s2] = *(const bf16x8*)(qb + (int64_t)qrow * ld + 32 * s2 + 8 * g);
+        for (int s2 = 0; s2 < 2; ++s2) qf[u][s2] = *(const bf16x8*)(qb + (int64_t)qrow * ld + 32 * s2 + 8 * g);
+      }
     }
     float m[TT], l[TT];
     f32x4 o[TT][4];
@@ -668,15 +683,9 @@ __global__ __launch_bounds__(NW * 64) void attention_res_kernel(const uint16_t* 
       }
     }
   };
-  const int nfull = SPLIT ? nqt - 1 : nqt;   // SPLIT: the last tile is shared out below
-  for (int t = wave; t < nfull; t += 2 * NW) {
-    if (TT2 && t + NW < nfull) tiles(std::integral_constant<int, 2>{}, t, t + NW);
-    else {
-      tiles(std::integral_constant<int, 1>{}, t, t);
-      if (!TT2 && t + NW < nfull) tiles(std::integral_constant<int, 1>{}, t + NW, t + NW);
-    }
-  }
-  if (SPLIT) {
+  // SPLIT: the last tile's rows over this wave's key tiles, partial states to LDS (SFIRST: before the
+  // full tiles, so every wave reaches the merge barrier with the same work behind it)
+  auto split_part = [&]() __attribute__((always_inline)) {
     // the last query tile (rows 16 (nqt - 1) .. S - 1, vr <= 16 of them) over this wave's
     // 16-key tiles; the same arithmetic as chunk() per key tile (log2-domain online softmax)
     const int tl = nqt - 1, vr = S - 16 * tl;
@@ -754,6 +763,20 @@ __global__ __launch_bounds__(NW * 64) void attention_res_kernel(const uint16_t* 
         pw[1] = lt;
       }
     }
+  };
+  if (SPLIT && SFIRST) split_part();
+  const int nfull = SPLIT ? nqt - 1 : nqt;   // SPLIT: the last tile is shared out below
+  for (int t = wave; t < nfull; t += 2 * NW) {
+    if (TT2 && t + NW < nfull) tiles(std::integral_constant<int, 2>{}, t, t + NW);
+    else {
+      tiles(std::integral_constant<int, 1>{}, t, t);
+      if (!TT2 && t + NW < nfull) tiles(std::integral_constant<int, 1>{}, t + NW, t + NW);
+    }
+  }
+  if (SPLIT && !SFIRST) split_part();
+  if (SPLIT) {
+    const int tl = nqt - 1, vr = S - 16 * tl;
+    float* part = (float*)(res_lds + 2 * spad * 128);
     __syncthreads();
     if (wave == 0 && fr < vr) {
       float M = -INFINITY;
@@ -1175,10 +1198,10 @@ hipError_t attention(const uint16_t* qkv, uint16_t* out, int B, int S, int W, in
 #else
     int var = 0;
 #endif
-    if (var < 1 || var > 12) var = S > 320 ? 5 : 1;
+    if (var < 1 || var > 14) var = S > 320 ? 5 : 1;
     const int64_t rp = ((int64_t)B * S + 1) & ~1;
     auto set_lds = [&](const void* fn, int slot) -> hipError_t {
-      static bool attr_set[11] = {false, false, false, false, false, false, false, false, false, false, false};
+      static bool attr_set[13] = {false, false, false, false, false, false, false, false, false, false, false, false, false};
       if (attr_set[slot]) return hipSuccess;
       hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       if (e == hipSuccess) attr_set[slot] = true;
@@ -1203,8 +1226,21 @@ hipError_t attention(const uint16_t* qkv, uint16_t* out, int B, int S, int W, in
                          rp);
       return hipGetLastError();
     }
+    if (var == 13 && vr <= 4 && !q8) {   // A/B: the split tile first, then the full tiles, then the merge
+      const size_t lds_s = lds + (size_t)8 * vr * 68 * 4;
+      if ((e = set_lds((const void*)attention_res_kernel<8, false, true, true>, 11)) != hipSuccess) return e;
+      hipLaunchKernelGGL((attention_res_kernel<8, false, true, true>), grid, dim3(512), lds_s, s, qkv, out, S, W, H, q8,
+                         qs, rp);
+      return hipGetLastError();
+    }
+    if (var == 14) {   // A/B: Q fragments one tile ahead
+      if ((e = set_lds((const void*)attention_res_kernel<8, false, false, false, true>, 12)) != hipSuccess) return e;
+      hipLaunchKernelGGL((attention_res_kernel<8, false, false, false, true>), grid, dim3(512), lds, s, qkv, out, S, W,
+                         H, q8, qs, rp);
+      return hipGetLastError();
+    }
 #endif
-    if (var == 11 || var == 12) var = 1;
+    if (var == 11 || var == 12 || var == 13) var = 1;
     if (var == 1) ATT_LAUNCH(1, (attention_res_kernel<8, false>), 512, qkv, out, S, W, H, q8, qs, rp)
     else if (var == 5) ATT_LAUNCH(5, (attention_r32_kernel<12, false>), 768, qkv, out, S, W, H, q8, qs, rp, 0)
 #if MICLIP_AB

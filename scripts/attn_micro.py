@@ -66,7 +66,7 @@ def main():
             fl = 4.0 * B * S * S * W * (0.5 if causal else 1.0)
             by = B * S * 4 * W * 2
             d = (outs[mode].float() - outs[0].float()).abs().max().item()
-            kind = {0: "default", "v1": "res 8w x1", "v11": "res 8w x1 unsplit", "v12": "res 8w x1 split", "v2": "res 8w x2", "v3": "res 16w x1", "v4": "r32 8w x2", "v5": "r32 12w", "v6": "r32 12w stag1", "v7": "r32 12w stag2", "v8": "r32 12w noload", "v9": "r32 12w noexp", "v10": "r32 12w 2-phase", "short": "res 4w (S<=64)", "short2": "flash 2 heads/wg", "short3": "flash 1h occ-6", "pipe4": "pipe 4/CU", "pipe8": "pipe 8/CU", 0x100: "one-wave", 0x200: "flash(chunked)"}[mode]
+            kind = {0: "default", "v1": "res 8w x1", "v11": "res 8w x1 unsplit", "v12": "res 8w x1 split", "v13": "res 8w split first", "v14": "res 8w Q ahead", "v2": "res 8w x2", "v3": "res 16w x1", "v4": "r32 8w x2", "v5": "r32 12w", "v6": "r32 12w stag1", "v7": "r32 12w stag2", "v8": "r32 12w noload", "v9": "r32 12w noexp", "v10": "r32 12w 2-phase", "short": "res 4w (S<=64)", "short2": "flash 2 heads/wg", "short3": "flash 1h occ-6", "pipe4": "pipe 4/CU", "pipe8": "pipe 8/CU", 0x100: "one-wave", 0x200: "flash(chunked)"}[mode]
             print(f"{name:9s} {kind:16s} B={B} S={S} W={W}: {us:8.1f} us "
                   f"{fl / us / 1e6:6.1f} TFLOP/s {by / us / 1e3:7.1f} GB/s  maxdiff {d:.3g}", flush=True)
 
