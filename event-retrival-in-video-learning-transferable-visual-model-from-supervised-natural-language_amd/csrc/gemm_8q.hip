@@ -773,7 +773,13 @@ int gemm_8q_ok(const GemmArgs& a) {
 // K = 768, ng = 6): FETCH 7.8 -> 3.6 GB per launch, shader clock ~1.6 ->
 // ~1.85 GHz, 2282 -> 2207 us (scripts/gpu_gemm_group.sh).  Narrower groups,
 // and qkv's 9 n-tiles in groups of 3, were slower; ngroup < 0 forces the raster.
+// Wide GEMMs whose n-tiles split evenly over the 8 XCDs take one group per XCD: the ViT-L/14 c_fc
+// ([428459, 4096, 1024], 16 n-tiles) in groups of 2 (a 1-MB panel per XCD's L2) ran 3006-3011 us
+// against 3145-3164 m-major, groups of 4 3065 and of 8 3095 (profiles/r05_y_ngroup.log,
+// r05_x_ngroup.log); B/32's 12 n-tiles keep groups of 6 (2185 us; 2, 3, 4 and m-major 2235-2359)
+// and L/14's in_proj (12 n-tiles) m-major (2292 us; groups of 4 or 8 2304-2377).
 int default_ngroup_8q(int tiles_n, int K) {
+  if (tiles_n >= 16 && tiles_n % 8 == 0 && (int64_t)(tiles_n / 8) * 256 * K * 2 <= 2400000) return tiles_n / 8;
   if (tiles_n < 12) return 0;
   for (int ng = tiles_n / 2; ng >= 6; --ng)
     if (tiles_n % ng == 0 && (int64_t)ng * 256 * K * 2 <= 2400000) return ng;
@@ -782,6 +788,9 @@ int default_ngroup_8q(int tiles_n, int K) {
 
 hipError_t gemm_8q(const GemmArgs& a0, int epi, hipStream_t s, int cus, int mode) {
   GemmArgs a = a0;
+#if MICLIP_AB   // A/B: MICLIP_8Q_NG forces the tile-order group width (-1 = m-major raster)
+  if (const char* ng = std::getenv("MICLIP_8Q_NG")) a.ngroup = std::atoi(ng);
+#endif
   if (a.ngroup == 0) a.ngroup = default_ngroup_8q(a.N / BN, a.K);
   if (mode == 5 || mode == 6 || mode == 7 || mode == 8) {   // start-stagger probes: 2 / 4 / 2 phases of ~1/2, 1/4, 1/4 tile
     const int tile_ticks = (int)(2200LL * a.K / 768);   // ~22 us per 256 x 256 tile at K = 768

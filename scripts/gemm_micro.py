@@ -42,6 +42,7 @@ SHAPES = {
     "lnfc500": (500000, 3072, 768, 7),
     "lnfc1k": (1000, 3072, 768, 7), "lnfc40k": (40003, 3072, 768, 7),   # (few / odd tile counts per CU)
     "lnfcL": (428459, 4096, 1024, 7),   # ViT-L/14 c_fc (1667 frames x 257 tokens)
+    "lnqkvL": (428459, 3072, 1024, 6),   # ViT-L/14 in_proj
     "lnqkv250": (250000, 2304, 768, 6),
     "lnfc250": (250000, 3072, 768, 7),
     # residual add fused into out_proj / c_proj (epi 8, mi_op_gemm_residual: x16 half-slot stream
