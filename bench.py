@@ -778,7 +778,7 @@ def main():
             workload += " (BASELINE configs[1])"
         result = {
             "metric": "frames/sec embedded+ranked, ViT-B/32 224², 1/2/4/8 MI355X; R@1/5/10 parity",
-            "value": round(value, 1), "unit": "frames/s", "n_gpus": world, "world_size_seen": seen,
+            "value": round(value, 1), "unit": "frames/s", "n_gpus": world, "world_size_seen": seen, "build_id": _N.lib().mi_build_id().decode(),
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
             "scaling": "strong" if strong else "weak", "vs_baseline": None,
             "dtype": {"bf16": "bf16", "fp32": "f32"}.get(args.weights, "fp8-e4m3(MX) vision GEMMs, bf16 rest"),

@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "../../include/miclip.h"
+#include "src_hash.h"   // MICLIP_SRC_HASH / MICLIP_SRC_FILES (Makefile)
 #include "internal.hpp"
 
 using namespace miclip;
@@ -313,6 +314,8 @@ static int f32_gemm_mode();
 extern "C" {
 
 int mi_abi_version(void) { return MICLIP_ABI_VERSION; }
+const char* mi_build_id(void) { return MICLIP_SRC_HASH; }
+const char* mi_build_sources(void) { return MICLIP_SRC_FILES; }
 
 const char* mi_last_error(void) { return g_err.c_str(); }
 

@@ -15,6 +15,8 @@ from .config import CLIPConfig
 
 LIB_NAME = "libmiclip.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+# the sources both libraries are built from (their fingerprint is checked at load, _check_sources)
+CSRC_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc")
 # the A/B build (csrc `make ab`): the same C-ABI plus every alternative kernel
 # schedule, ablation and probe; used by scripts/*_micro.py (MICLIP_LIB=ab) and
 # the bit-identity tests of the alternatives, never by the product path
@@ -29,7 +31,7 @@ MI_RESAMPLE_BICUBIC, MI_RESAMPLE_BILINEAR = 0, 1
 
 # every symbol include/miclip.h declares (checked by tests/test_abi.py)
 EXPORTS = (
-    "mi_abi_version", "mi_last_error", "mi_clip_weights_numel", "mi_clip_create", "mi_clip_destroy",
+    "mi_abi_version", "mi_build_id", "mi_build_sources", "mi_last_error", "mi_clip_weights_numel", "mi_clip_create", "mi_clip_destroy",
     "mi_clip_reserve", "mi_clip_encode_image", "mi_clip_encode_text", "mi_rank_workspace_bytes",
     "mi_rank_topk", "mi_rank_merge", "mi_score_matrix", "mi_rank_of_targets",
     "mi_op_gemm", "mi_op_gemm_f32", "mi_op_layernorm", "mi_op_attention", "mi_op_residual_ln",
@@ -101,6 +103,8 @@ def _bind(path):
     P, I32, I64, SZ = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_size_t
     sig = {
         "mi_abi_version": (ctypes.c_int, []),
+        "mi_build_id": (ctypes.c_char_p, []),
+        "mi_build_sources": (ctypes.c_char_p, []),
         "mi_last_error": (ctypes.c_char_p, []),
         "mi_clip_weights_numel": (I64, [ctypes.POINTER(Arch)]),
         "mi_clip_create": (ctypes.c_int, [ctypes.POINTER(Arch), P, I64, ctypes.c_int, ctypes.c_int,
@@ -149,9 +153,38 @@ def _bind(path):
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
-    if L.mi_abi_version() != 5:
+    if L.mi_abi_version() != 6:
         raise MiClipError("libmiclip ABI version mismatch")
+    _check_sources(L, path)
     return L
+
+
+def source_fingerprint(names, csrc=None):
+    """The Makefile's fingerprint of `names` (paths relative to csrc/): the first 16 hex digits of
+    the sha256 of the files concatenated in that order (``cat ... | sha256sum``)."""
+    import hashlib
+    csrc = csrc or CSRC_DIR
+    h = hashlib.sha256()
+    for n in names:
+        with open(os.path.join(csrc, n), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def _check_sources(L, path):
+    """Refuse a library built from other sources than the csrc/ next to it (a stale or foreign
+    binary): its mi_build_id must equal the fingerprint of the files it names.  A library shipped
+    without its sources is not checked."""
+    if not os.path.isdir(CSRC_DIR):
+        return
+    names = L.mi_build_sources().decode().split()
+    missing = [n for n in names if not os.path.isfile(os.path.join(CSRC_DIR, n))]
+    if missing:
+        raise MiClipError(f"{path}: built from sources missing here ({', '.join(missing)}); rebuild with build()")
+    built, here = L.mi_build_id().decode(), source_fingerprint(names)
+    if built != here:
+        raise MiClipError(f"{path} was built from other sources (fingerprint {built}) than {CSRC_DIR} ({here}): "
+                          "rebuild with `python -c 'import __graft_entry__ as g; g.build()'` or `make -C <pkg>/csrc`")
 
 
 def check(rc: int, what: str):

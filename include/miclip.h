@@ -35,10 +35,11 @@
 extern "C" {
 #endif
 
-#define MICLIP_ABI_VERSION 5   /* 2: mi_jpeg_workspace_bytes / mi_jpeg_decode take the data size;
+#define MICLIP_ABI_VERSION 6   /* 2: mi_jpeg_workspace_bytes / mi_jpeg_decode take the data size;
                                   3: mi_normalize_rows_f16, mi_jpeg_decode_transform;
                                   4: mi_op_split2h, mi_op_gemm_split2h, mi_op_attention_f32;
-                                  5: mi_clip_kernel_events, mi_clip_kernel_times */
+                                  5: mi_clip_kernel_events, mi_clip_kernel_times;
+                                  6: mi_build_id, mi_build_sources */
 
 enum mi_dtype { MI_F32 = 0, MI_BF16 = 1, MI_F16 = 2, MI_FP8 = 3 /* weights only: MX-fp8 vision GEMMs */ };
 enum mi_status { MI_OK = 0, MI_ERR_ARG = -1, MI_ERR_HIP = -2, MI_ERR_UNSUPPORTED = -3, MI_ERR_STATE = -4 };
@@ -74,6 +75,11 @@ typedef struct mi_clip_arch {
 typedef struct mi_clip mi_clip;
 
 int mi_abi_version(void);
+/* The library's source fingerprint: the first 16 hex digits of the sha256 of the concatenated
+   sources it was compiled from (mi_build_sources: their names, relative to csrc/, in order).
+   miclip._native recomputes it from the sources next to the library and refuses a mismatch. */
+const char* mi_build_id(void);
+const char* mi_build_sources(void);
 const char* mi_last_error(void);
 
 /* Number of float32 elements of the canonical weight blob for `arch`

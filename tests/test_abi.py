@@ -28,7 +28,31 @@ def test_library_exports_every_symbol():
     out = os.popen(f"nm -D --defined-only {_native.LIB_PATH}").read()
     for name in _declared():
         assert re.search(rf"\bT {name}$", out, re.M), f"{name} not exported"
-    assert L.mi_abi_version() == 5
+    assert L.mi_abi_version() == 6
+
+
+def test_library_fingerprint_matches_its_sources(tmp_path):
+    """Both libraries carry the fingerprint of the sources they were built from
+    (mi_build_id: sha256 of the files mi_build_sources names); the loader recomputes it from
+    csrc/ and refuses a mismatch, so a stale or foreign binary cannot run."""
+    import shutil
+    from miclip import _native
+    for L in (_native.lib(), _native.lib_ab()):
+        names = L.mi_build_sources().decode().split()
+        assert "api.cpp" in names and "../../include/miclip.h" in names
+        assert L.mi_build_id().decode() == _native.source_fingerprint(names)
+    # a one-byte change in any source changes the fingerprint the loader compares
+    names = _native.lib().mi_build_sources().decode().split()
+    csrc = tmp_path / "pkg" / "csrc"   # (the header sits at ../../include/ from csrc/)
+    csrc.mkdir(parents=True)
+    for n in names:
+        dst = csrc / n
+        dst.parent.mkdir(parents=True, exist_ok=True)
+        shutil.copyfile(os.path.join(_native.CSRC_DIR, n), dst)
+    assert _native.source_fingerprint(names, str(csrc)) == _native.lib().mi_build_id().decode()
+    with open(csrc / "rank.hip", "ab") as f:
+        f.write(b" ")
+    assert _native.source_fingerprint(names, str(csrc)) != _native.lib().mi_build_id().decode()
 
 
 def test_weights_numel_matches_packer():
