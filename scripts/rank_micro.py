@@ -26,8 +26,9 @@ VARIANTS = {"default": {}, "exact": {"MICLIP_RANK_CERT": "0"},
             "c_nolist": {"MICLIP_RANK_CERT_ABL": "3"}, "c_endput": {"MICLIP_RANK_CERT_ABL": "6"},
             "c_noput": {"MICLIP_RANK_CERT_ABL": "7"},
             # round-4 in-launch merge instead of the split merge (r05)
+            "cert_any": {"MICLIP_RANK_CERT": "2"},   # the certified route at every size (default: >= 262144 rows)
             "inl": {"MICLIP_RANK_FOLD": "1"}, "exact_inl": {"MICLIP_RANK_CERT": "0", "MICLIP_RANK_FOLD": "1"}}
-SHAPES = [(125_000, 512, 32, torch.float32), (1_000_000, 512, 32, torch.float32),
+SHAPES = [(125_000, 512, 32, torch.float32), (250_000, 512, 32, torch.float32), (125_000, 512, 32, torch.bfloat16), (1_000_000, 512, 32, torch.float32),
           (1_000_000, 512, 32, torch.bfloat16), (1_000_000, 768, 32, torch.float32)]
 if os.environ.get("RANK_MICRO_VARIANTS"):   # a comma list of the variants to time
     VARIANTS = {v: VARIANTS[v] for v in os.environ["RANK_MICRO_VARIANTS"].split(",")}
