@@ -1127,6 +1127,15 @@ hipError_t launch(const GemmArgs& a, hipStream_t s) {
     if (EPI == EPI_SPLIT_GELU && (!a.rmax || !a.rsc_out || a.group || a.ldo != 3 * (int64_t)a.N))
       return hipErrorInvalidValue;
     if constexpr (EPI == EPI_F32 || EPI == EPI_RESID_F32 || EPI == EPI_SPLIT_GELU) {
+      // the 8-phase kernel (gemm_8q.hip) wherever it applies; MICLIP_F32_8Q=0 (A/B build) keeps the
+      // ping-pong kernel below
+#if MICLIP_AB
+      const char* e8 = std::getenv("MICLIP_F32_8Q");
+      const bool use8q = !e8 || std::atoi(e8) != 0;
+#else
+      const bool use8q = true;
+#endif
+      if (use8q && gemm_8q_ok(a)) return gemm_8q(a, EPI, s, cu_count(), 0);
       const int ntf = ((a.M + 255) / 256) * (a.N / 256);
       if (big && a.K / BK >= LEAD) {
         hipLaunchKernelGGL((gemm_pp_kernel<EPI, 1, false, false, false, false, true>), dim3(ntf), dim3(512), 0, s, a);

@@ -123,6 +123,15 @@ __device__ __forceinline__ void quick_gelu_stage_8q(f32x2 (&v)[NP]) {
 }
 __device__ __forceinline__ void quick_gelu8_8q(f32x2 (&v)[4]) { quick_gelu_stage_8q<4>(v); }
 
+// EPI_SPLIT_GELU's row exponent (gemm.hip split_exp_g): 2^e scales the row bound into [2^13, 2^14)
+__device__ __forceinline__ int split_exp_8q(float mx) {
+  if (!(mx > 0.f) || !__builtin_isfinite(mx)) return 0;
+  int ex;
+  (void)frexpf(mx, &ex);
+  const int e = 14 - ex;
+  return e > 126 ? 126 : (e < -126 ? -126 : e);
+}
+
 __device__ __forceinline__ void tile_coords_8q(int t, int tiles_m, int tiles_n, int ng, int& mb, int& nb) {
   if (ng <= 0 || ng >= tiles_n) {
     mb = t / tiles_n;
@@ -157,8 +166,13 @@ struct EpiKind8q {
   static constexpr bool LN = EPI == EPI_LN_BF16 || EPI == EPI_LN_GELU_BF16;   // LayerNorm folded in (fp16 operands)
   static constexpr bool GELU = EPI == EPI_GELU_BF16 || EPI == EPI_LN_GELU_BF16;
   static constexpr bool RES = EPI == EPI_RES16_BF16;   // residual add + row partial statistics fused
-  // LDS: 2 K-tile buffers, bias [2][BN]; LN: + row statistics [2][BM][2] + column sums [2][BN]
-  static constexpr int LDS = 2 * BUF + 2 * BN * 4 + (LN ? 2 * BM * 8 + 2 * BN * 4 : 0);
+  // split-f16 operands of the fp32 tower (split2h_rows; OPF16): f32 epilogues with the row / column
+  // scales rsc[m] * csc[n] (EPI_F32: in_proj; EPI_RESID_F32: out_proj / c_proj into the f32
+  // stream; EPI_SPLIT_GELU: c_fc's QuickGELU split into c_proj's operand), gemm.hip's arithmetic
+  static constexpr bool SPL = EPI == EPI_F32 || EPI == EPI_RESID_F32 || EPI == EPI_SPLIT_GELU;
+  // LDS: 2 K-tile buffers, bias [2][BN]; LN: + row statistics [2][BM][2] + column sums [2][BN];
+  // SPL: + rsc / rmax [2][2][BM] in the row-statistics slot + csc [2][BN] in the column-sum slot
+  static constexpr int LDS = 2 * BUF + 2 * BN * 4 + (LN || SPL ? 2 * BM * 8 + 2 * BN * 4 : 0);
 };
 
 template <int EPI, int ABL = 0, int F = 0, bool OPF16 = false>
@@ -253,8 +267,8 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
   // tile's 256 rows of (rstd, rstd * mean) (waves 2, 3; rs is readable 256 rows past M)
   // (buffer-descriptor DMAs: the base is scalar, the lane offset lane * 16 -- no 64-bit
   // per-lane address kept live across the tile)
-  auto dma_vec = [&](const float* base, float* lds) {
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 1024, 0x00020000);
+  auto dma_vec = [&](const float* base, float* lds, int bytes = 1024) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, bytes, 0x00020000);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (LDS_AS void*)lds, 16, (uint32_t)lane * 16, 0, 0, 0);
   };
   auto stage_vectors = [&](int m0, int n0, int par) {
@@ -263,6 +277,12 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
       if (wave == 1) dma_vec(a.colv + n0, scol + par * BN);
       if (wave == 2) dma_vec(a.rs + (int64_t)m0 * 2, srs + par * BM * 2);
       if (wave == 3) dma_vec(a.rs + (int64_t)(m0 + 128) * 2, srs + par * BM * 2 + 256);
+    }
+    if (EK::SPL) {   // rows past M read zeros (the descriptor's range ends at row M)
+      const int rb = min(a.M - m0, BM) * 4;
+      if (wave == 1) dma_vec(a.csc + n0, scol + par * BN);
+      if (wave == 2) dma_vec(a.rsc + m0, srs + par * BM * 2, rb);
+      if (EPI == EPI_SPLIT_GELU && wave == 3) dma_vec(a.rmax + m0, srs + par * BM * 2 + BM, rb);
     }
   };
 
@@ -373,7 +393,127 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
     const auto b2 = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
     return __uint_as_float(b2[0]) + __uint_as_float(b2[1]);
   };
+  // SPL: the split-f16 GEMM's f32 epilogues with gemm.hip's arithmetic (v = acc * (rsc[m] csc[n]) + b;
+  // then the f32 store, the in-place add o + v, or split_gelu_store's QuickGELU split), so the
+  // results are bit-identical to gemm_pp_kernel's.  A lane holds 4 consecutive columns of one row
+  // per 16 x 16 block: the f32 pieces are 16-byte row stores straight from the accumulators, the
+  // split's fp16 pieces pair blocks ni / ni + 1 by permlane16 swaps (the bf16 epilogue's layout)
+  auto epilogue_spl = [&]() __attribute__((always_inline)) {
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    const int lr = l & 15, lg = l >> 4;
+    float4 bias[4], cs[4];
+    const uint32_t ca = (uint32_t)(uintptr_t)(const LDS_AS float*)(scol + ppar * BN + wc * 64 + 4 * lg);
+    asm volatile("ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:64\n\tds_read_b128 %2, %4 offset:128\n\t"
+                 "ds_read_b128 %3, %4 offset:192\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&v"(cs[0]), "=&v"(cs[1]), "=&v"(cs[2]), "=&v"(cs[3]) : "v"(ca) : "memory");
+    if (a.bias) {
+      const uint32_t ba = (uint32_t)(uintptr_t)(const LDS_AS float*)(sbias + ppar * BN + wc * 64 + 4 * lg);
+      asm volatile("ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:64\n\tds_read_b128 %2, %4 offset:128\n\t"
+                   "ds_read_b128 %3, %4 offset:192\n\ts_waitcnt lgkmcnt(0)"
+                   : "=&v"(bias[0]), "=&v"(bias[1]), "=&v"(bias[2]), "=&v"(bias[3]) : "v"(ba) : "memory");
+    } else {
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) bias[ni] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    // the lane's 8 rows' rsc (and rmax for the split's bound), one row per 16-row block
+    float rsv[8], rmv[8];
+    const uint32_t ra = (uint32_t)(uintptr_t)(const LDS_AS float*)(srs + ppar * BM * 2 + wr * 128 + lr);
+    asm volatile("ds_read_b32 %0, %8\n\tds_read_b32 %1, %8 offset:64\n\tds_read_b32 %2, %8 offset:128\n\t"
+                 "ds_read_b32 %3, %8 offset:192\n\tds_read_b32 %4, %8 offset:256\n\tds_read_b32 %5, %8 offset:320\n\t"
+                 "ds_read_b32 %6, %8 offset:384\n\tds_read_b32 %7, %8 offset:448\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&v"(rsv[0]), "=&v"(rsv[1]), "=&v"(rsv[2]), "=&v"(rsv[3]), "=&v"(rsv[4]), "=&v"(rsv[5]),
+                   "=&v"(rsv[6]), "=&v"(rsv[7])
+                 : "v"(ra) : "memory");
+    if (EPI == EPI_SPLIT_GELU)
+      asm volatile("ds_read_b32 %0, %8 offset:1024\n\tds_read_b32 %1, %8 offset:1088\n\tds_read_b32 %2, %8 offset:1152\n\t"
+                   "ds_read_b32 %3, %8 offset:1216\n\tds_read_b32 %4, %8 offset:1280\n\tds_read_b32 %5, %8 offset:1344\n\t"
+                   "ds_read_b32 %6, %8 offset:1408\n\tds_read_b32 %7, %8 offset:1472\n\ts_waitcnt lgkmcnt(0)"
+                   : "=&v"(rmv[0]), "=&v"(rmv[1]), "=&v"(rmv[2]), "=&v"(rmv[3]), "=&v"(rmv[4]), "=&v"(rmv[5]),
+                     "=&v"(rmv[6]), "=&v"(rmv[7])
+                   : "v"(ra) : "memory");
+    const int rows = min(a.M - pm0, BM);
+    auto scaled = [&](int mi, int ni) {   // acc * (rsc[m] csc[n]) + b
+      f32x4 v = acc[mi][ni] * (f32x4){rsv[mi] * cs[ni].x, rsv[mi] * cs[ni].y, rsv[mi] * cs[ni].z, rsv[mi] * cs[ni].w};
+      return (f32x4){v[0] + bias[ni].x, v[1] + bias[ni].y, v[2] + bias[ni].z, v[3] + bias[ni].w};
+    };
+    if constexpr (EPI == EPI_F32 || EPI == EPI_RESID_F32) {
+      const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)((float*)a.out + (int64_t)pm0 * a.ldo + pn0), (short)0, rows * (int)a.ldo * 4, 0x00020000);
+      const uint32_t vo = (uint32_t)(((wr * 128 + lr) * (int)a.ldo + wc * 64 + 4 * lg) * 4);
+      const uint32_t blk = (uint32_t)(16 * a.ldo * 4);
+      u32x4_8q xo[2][4];   // EPI_RESID_F32: the stream's values, one 16-row block ahead
+      auto load_blk = [&](int mi) {
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni)
+          xo[mi & 1][ni] = __builtin_bit_cast(u32x4_8q, __builtin_amdgcn_raw_buffer_load_b128(ro, vo + mi * blk + ni * 64, 0, 0));
+      };
+      if (EPI == EPI_RESID_F32) load_blk(0);
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi) {
+        if (EPI == EPI_RESID_F32 && mi < 7) load_blk(mi + 1);
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+          f32x4 v = scaled(mi, ni);
+          if (EPI == EPI_RESID_F32) {
+            const u32x4_8q ov = xo[mi & 1][ni];
+            const f32x4 o = {__uint_as_float(ov[0]), __uint_as_float(ov[1]), __uint_as_float(ov[2]), __uint_as_float(ov[3])};
+            v = (f32x4){o[0] + v[0], o[1] + v[1], o[2] + v[2], o[3] + v[3]};
+          }
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_8q, v), ro, vo + mi * blk + ni * 64, 0, 0);
+        }
+      }
+    } else {   // EPI_SPLIT_GELU: [y1 | y1 | y2] at columns n, n + N, n + 2N; rsc_out[m] by the n = 0 tile
+      const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)((uint16_t*)a.out + (int64_t)pm0 * a.ldo + pn0), (short)0, rows * (int)a.ldo * 2, 0x00020000);
+      const uint32_t vo = (uint32_t)(((wr * 128 + lr) * (int)a.ldo + wc * 64 + (lg & 1) * 16 + (lg >> 1) * 8) * 2);
+      const uint32_t blk = (uint32_t)(16 * a.ldo * 2);
+      const int n2 = a.N * 2, n4 = a.N * 4;   // byte offsets of the second and third copies (soffset)
+      const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.rsc_out + pm0), (short)0, rows * 4, 0x00020000);
+      // one writer per row (the n = 0 tile's columns 0-3); other lanes store out of range (dropped)
+      const uint32_t vr = (pn0 == 0 && wc == 0 && lg == 0) ? (uint32_t)((wr * 128 + lr) * 4) : 0x7ff00000u;
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi) {
+        const float bound = (rmv[mi] * a.bnd_w + a.bnd_b) * (1.0f + 0.00390625f);
+        const int e = split_exp_8q(bound);
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          uint2 k1[2], k2[2];
+#pragma unroll
+          for (int qq = 0; qq < 2; ++qq) {
+            const f32x4 v = scaled(mi, 2 * p + qq);
+            uint32_t h1[4], h2[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const float y = v[i] * (1.0f / (1.0f + expf(-1.702f * v[i])));
+              const float ys = ldexpf(y, e);
+              const _Float16 p1 = (_Float16)ys;
+              const float f1 = (float)p1;
+              const _Float16 p2 = __builtin_isfinite(f1) ? (_Float16)(ys - f1) : (_Float16)0.f;
+              h1[i] = __builtin_bit_cast(uint16_t, p1);
+              h2[i] = __builtin_bit_cast(uint16_t, p2);
+            }
+            k1[qq] = make_uint2(h1[0] | (h1[1] << 16), h1[2] | (h1[3] << 16));
+            k2[qq] = make_uint2(h2[0] | (h2[1] << 16), h2[2] | (h2[3] << 16));
+          }
+          const auto ax = __builtin_amdgcn_permlane16_swap(k1[0].x, k1[1].x, false, false);
+          const auto ay = __builtin_amdgcn_permlane16_swap(k1[0].y, k1[1].y, false, false);
+          const auto bx = __builtin_amdgcn_permlane16_swap(k2[0].x, k2[1].x, false, false);
+          const auto by = __builtin_amdgcn_permlane16_swap(k2[0].y, k2[1].y, false, false);
+          const u32x4_8q d1 = {ax[0], ay[0], ax[1], ay[1]}, d2 = {bx[0], by[0], bx[1], by[1]};
+          __builtin_amdgcn_raw_buffer_store_b128(d1, ro, vo + mi * blk + p * 64, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(d1, ro, vo + mi * blk + p * 64, n2, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(d2, ro, vo + mi * blk + p * 64, n4, 0);
+        }
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(ldexpf(1.f, -e)), rr, vr + mi * 64, 0, 0);
+      }
+    }
+  };
   auto epilogue = [&]() __attribute__((always_inline)) {
+    if constexpr (EK::SPL) {
+      if (ABL != 4) epilogue_spl();
+      return;
+    }
     if (ABL == 4) {
 #pragma unroll
       for (int mi = 0; mi < 8; ++mi)
@@ -626,7 +766,12 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
     if (P == 4) {
       // (EPI_RES16: 16 stores, 8 partial stores and the x16 loads of blocks 4-7 are younger;
       // the epilogue's wait for block 7 already retired the odd buffer)
-      if (FIRST && has_prev && EK::RES && !((F & F_BEARLY) && wr == 1))
+      // (SPL: the epilogue's VMEM ops per wave -- F32 32 stores, RESID 32 loads + 32 stores, SPLIT
+      // 48 + 8 stores -- are younger; vmcnt holds at most 63)
+      constexpr int SPL_VM = EPI == EPI_F32 ? 36 : (EPI == EPI_RESID_F32 ? 63 : 60);
+      if (EK::SPL && FIRST && has_prev && !((F & F_BEARLY) && wr == 1))
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SPL_VM) : "memory");
+      else if (FIRST && has_prev && EK::RES && !((F & F_BEARLY) && wr == 1))
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(ABL == 11 ? 20 : 28) : "memory");
       else if (FIRST && has_prev && ABL != 10 && !((F & F_BEARLY) && wr == 1)) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
       // (F_BEARLY, lagging group: its stores are OLDER than phase 1's DMAs, so vmcnt(4) below also
@@ -859,6 +1004,29 @@ hipError_t gemm_8q(const GemmArgs& a0, int epi, hipStream_t s, int cus, int mode
       hipLaunchKernelGGL(
           (gemm_8q_kernel<EPI_LN_GELU_BF16, 0, F_BEARLY | F_GPK | F_ONT | F_FULL | F_GSTAGE16 | F_GSTAGE | F_VOREC, true>),
           dim3(grid), dim3(512), 0, s, a);
+    return hipGetLastError();
+  }
+  // the fp32 tower's split-f16 GEMMs (K' = 3K; gemm.hip launch checks the vectors)
+  if (epi == EPI_F32 || epi == EPI_RESID_F32 || epi == EPI_SPLIT_GELU) {
+    if (!a.a_f16 || !a.rsc || !a.csc || mode || a.group || (a.ldo % 4) || (int64_t)BM * a.ldo * 4 >= (1LL << 31))
+      return hipErrorInvalidValue;
+    if (epi == EPI_SPLIT_GELU && (!a.rmax || !a.rsc_out || a.ldo != 3 * (int64_t)a.N)) return hipErrorInvalidValue;
+#if MICLIP_AB   // A/B (MICLIP_F32_8Q=2): the lagging M-group's epilogue beside the leading one's (F_BEARLY)
+    const char* fv = std::getenv("MICLIP_F32_8Q");
+    if (fv && std::atoi(fv) == 2) {
+      if (epi == EPI_SPLIT_GELU) hipLaunchKernelGGL((gemm_8q_kernel<EPI_SPLIT_GELU, 0, F_BEARLY, true>), dim3(grid), dim3(512), 0, s, a);
+      else if (epi == EPI_RESID_F32) hipLaunchKernelGGL((gemm_8q_kernel<EPI_RESID_F32, 0, F_BEARLY, true>), dim3(grid), dim3(512), 0, s, a);
+      else hipLaunchKernelGGL((gemm_8q_kernel<EPI_F32, 0, F_BEARLY, true>), dim3(grid), dim3(512), 0, s, a);
+      return hipGetLastError();
+    }
+#endif
+    if (epi == EPI_SPLIT_GELU) {
+      hipLaunchKernelGGL((gemm_8q_kernel<EPI_SPLIT_GELU, 0, 0, true>), dim3(grid), dim3(512), 0, s, a);
+    } else if (epi == EPI_RESID_F32) {
+      hipLaunchKernelGGL((gemm_8q_kernel<EPI_RESID_F32, 0, 0, true>), dim3(grid), dim3(512), 0, s, a);
+    } else {
+      hipLaunchKernelGGL((gemm_8q_kernel<EPI_F32, 0, 0, true>), dim3(grid), dim3(512), 0, s, a);
+    }
     return hipGetLastError();
   }
   if (a.a_f16) return hipErrorInvalidValue;

@@ -97,11 +97,12 @@ class CLIP:
         N.check(L.mi_clip_create(ctypes.byref(arch), blob.ctypes.data, blob.size, self.device.index, wdt,
                                  ctypes.byref(ctx)), "mi_clip_create")
         self._ctx = ctx
+        self._destroy = L.mi_clip_destroy   # the library that made the context frees it
         N.check(L.mi_clip_reserve(self._ctx, self._chunks[0], self._chunks[1]), "mi_clip_reserve")
 
     def close(self):
         if self._ctx is not None and self._ctx.value:
-            N.lib().mi_clip_destroy(self._ctx)
+            self._destroy(self._ctx)
         self._ctx = None
 
     def __del__(self):

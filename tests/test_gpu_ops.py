@@ -684,6 +684,44 @@ def test_split2h_gemm_f32_grade(gpu, M, N, K, epi):
     assert err < 1e-6, err
 
 
+@pytest.mark.parametrize("M,N,K,epi", [(3000, 768, 3072, 2), (20000, 2304, 768, 3), (257, 256, 256, 3),
+                                       (777, 512, 1024, 2), (256, 1024, 512, 3)])
+def test_split2h_gemm_8phase_bit_identical(gpu, monkeypatch, M, N, K, epi):
+    """The split-f16 GEMM on the 8-phase kernel (gemm_8q.hip's SPL epilogues, the default where
+    it applies: N % 256 == 0, K' % 128 == 0, M >= 256) gives the ping-pong kernel's results bit
+    for bit (A/B build, MICLIP_F32_8Q=0): store and += forms, with a bias, partial last m-tiles,
+    rows of widely spread magnitudes; and it stays within the f32 grade of float64."""
+    import torch
+    N_ = _lib()
+    g = torch.Generator(device="cpu").manual_seed(7 * M + N + K + epi)
+    A = (torch.randn(M, K, generator=g) * torch.exp(torch.empty(M, 1).uniform_(-9, 9, generator=g))).to(gpu)
+    W = (torch.randn(N, K, generator=g) * K ** -0.5 * torch.exp(torch.empty(N, 1).uniform_(-2, 2, generator=g))).to(gpu)
+    bias = torch.randn(N, generator=g).to(gpu)
+    base = torch.randn(M, N, generator=g).to(gpu)
+    A3 = torch.empty(M, 3 * K, dtype=torch.int16, device=gpu)
+    W3 = torch.empty(N, 3 * K, dtype=torch.int16, device=gpu)
+    sa, sw = torch.empty(M, device=gpu), torch.empty(N, device=gpu)
+    L = N_.lib()
+    N_.check(L.mi_op_split2h(A.data_ptr(), K, M, K, 0, 0, A3.data_ptr(), sa.data_ptr(), _stream()), "split2h A")
+    N_.check(L.mi_op_split2h(W.data_ptr(), K, N, K, 1, 0, W3.data_ptr(), sw.data_ptr(), _stream()), "split2h W")
+    outs = []
+    for lib, flag in ((L, None), (N_.lib_ab(), "0")):
+        if flag is None:
+            monkeypatch.delenv("MICLIP_F32_8Q", raising=False)
+        else:
+            monkeypatch.setenv("MICLIP_F32_8Q", flag)
+        out = base.clone() if epi == 2 else torch.full((M, N), float("nan"), device=gpu)
+        N_.check(lib.mi_op_gemm_split2h(A3.data_ptr(), W3.data_ptr(), sa.data_ptr(), sw.data_ptr(), bias.data_ptr(),
+                                        out.data_ptr(), M, N, 3 * K, epi, _stream()), "gemm_split2h")
+        outs.append(out)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))
+    ref = A.double() @ W.double().t() + bias.double() + (base.double() if epi == 2 else 0)
+    rowscale = (A.double().abs() @ W.double().abs().t()).max(dim=1, keepdim=True).values + bias.double().abs().max()
+    err = (outs[0].double() - ref).abs() - (2.0 ** -24 * ref.abs() if epi == 2 else 0)
+    assert (err / rowscale).max().item() < 1e-6
+
+
 def _attn_ref(qkv, B, S, W, causal):
     H = W // 64
     x = qkv.reshape(B, S, 3, H, 64).astype(np.float64)

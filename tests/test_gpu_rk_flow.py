@@ -111,6 +111,34 @@ def test_fp32_tower_vs_oracle(gpu, name):
     np.testing.assert_allclose(g, img / np.linalg.norm(img, axis=1, keepdims=True), rtol=0, atol=1e-6)
 
 
+@pytest.mark.parametrize("name,n", [("ViT-B/32", 8), ("ViT-B/32", 13), ("test-small", 40)])
+def test_fp32_tower_8phase_bit_identical(gpu, monkeypatch, name, n):
+    """The fp32 tower's split-f16 GEMMs on the 8-phase kernel (in_proj EPI_F32, out_proj / c_proj
+    EPI_RESID_F32, c_fc EPI_SPLIT_GELU writing c_proj's operand; the default for >= 256 rows)
+    against the ping-pong kernel (A/B build, MICLIP_F32_8Q=0): image and text embeddings bit for
+    bit (whole and partial 256-row tiles), and within f32 rounding of the float64 oracle."""
+    import torch
+    from miclip import _native, config, model as M, weights
+    from oracle import clip_ref
+    cfg = config.get_config(name)
+    sd = state_dict(name)
+    px = torch.from_numpy(weights.synthetic_pixels(n, cfg.image_resolution, seed=n))
+    tk = torch.from_numpy(weights.synthetic_tokens(n, cfg.context_length, cfg.vocab_size, seed=n))
+    m = M.CLIP(cfg, sd, device=gpu, weights="fp32", image_chunk=n, text_chunk=n)
+    img, txt = m.encode_image(px).cpu().numpy(), m.encode_text(tk).cpu().numpy()
+    monkeypatch.setattr(_native, "lib", _native.lib_ab)
+    monkeypatch.setenv("MICLIP_F32_8Q", "0")
+    m0 = M.CLIP(cfg, sd, device=gpu, weights="fp32", image_chunk=n, text_chunk=n)
+    img0, txt0 = m0.encode_image(px).cpu().numpy(), m0.encode_text(tk).cpu().numpy()
+    del m0
+    monkeypatch.undo()
+    assert np.array_equal(img.view(np.int32), img0.view(np.int32))
+    assert np.array_equal(txt.view(np.int32), txt0.view(np.int32))
+    ri = clip_ref.encode_image(px.numpy(), sd, cfg, np.float64)
+    assert np.abs(img - ri).max() / np.abs(ri).max() < 2e-5
+    assert clip_ref.cosine(img, ri).min() > 1 - 1e-9
+
+
 @pytest.mark.parametrize("name,fname", [("ViT-L/14", "vit_l14.npz"), ("ViT-L/14@336px", "vit_l14_336px.npz")])
 def test_fp32_tower_l14_golden(gpu, name, fname):
     """L/14 (257 tokens) and L/14@336px (577 tokens: the 256-thread attention
