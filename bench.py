@@ -529,8 +529,9 @@ def parity_mode(args, dev, pixels, tokens, Q, k, base, chunk):
            "note": "fp32 tower (split-f16 GEMMs, f32-grade; exact-f32 MFMA attention): the mode whose R@1/5/10 "
                    "equal the float64 oracle flow (tests/test_gpu_rk_flow.py)",
            "roofline": {"bound": "mfma",
-                        "kernel": "gemm_pp_kernel<EPI_F32, F16> over split-f16 operands, K' = 3K (mlp.c_fc "
-                                  "pre-activation; QuickGELU in c_proj's operand split)",
+                        "kernel": "gemm_8q_kernel<EPI_F32> over split-f16 operands, K' = 3K, at mlp.c_fc's shape "
+                                  "(mi_op_gemm_split2h; the tower's own c_fc launch adds QuickGELU and c_proj's "
+                                  "operand split in the epilogue, EPI_SPLIT_GELU)",
                         "achieved": round(3 * fl / (fc * 1e-6) / 1e12, 1), "peak": BF16_PEAK_TFLOPS,
                         "unit": "TFLOP/s", "frac": round(3 * fl / (fc * 1e-6) / 1e12 / BF16_PEAK_TFLOPS, 4),
                         "f32_equivalent_tflops": round(fl / (fc * 1e-6) / 1e12, 1),
@@ -741,7 +742,7 @@ def main():
             eb = 1 if fp8 else 2   # operand element bytes (fp8 adds 1/64 B of scales per element; fp32: 3 fp16 terms)
             roof = {"bound": "mfma",
                     "kernel": ("gemm_mx_kernel<EPI_GELU_BF16> (mlp.c_fc + QuickGELU, MX-fp8 operands)" if fp8
-                               else "gemm_pp_kernel<EPI_F32, F16> (split-f16 operands, K' = 3K; mlp.c_fc pre-activation)" if f32
+                               else "gemm_8q_kernel<EPI_F32> (split-f16 operands, K' = 3K, at mlp.c_fc's shape)" if f32
                                else "gemm_8q_kernel<EPI_LN_GELU_BF16> (8-phase interleaved persistent, 256x256x64, descriptor DMAs; "
                                "ln_2 folded into the epilogue, fp16 operands on the f16 MFMA; mlp.c_fc + QuickGELU)" if lnf
                                else "gemm_8q_kernel<EPI_GELU_BF16> (8-phase interleaved persistent, 256x256x64, descriptor DMAs; mlp.c_fc + QuickGELU)"),
