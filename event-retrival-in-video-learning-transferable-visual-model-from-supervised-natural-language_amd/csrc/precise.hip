@@ -432,8 +432,12 @@ __global__ __launch_bounds__(NT) void attn_f32_kernel(const float* __restrict__ 
 //     register's 32 lanes store one 128-byte row segment.
 // Replaces attn_f32_kernel (a thread per query row, scalar fmaf over LDS; 10.4 ms per B/32 layer
 // at 10k frames, profiles/r05_a_fp32_bench_kernel_stats.csv).
-template <int NKT>
-__global__ __launch_bounds__(256) void attn_f32_mfma_kernel(const float* __restrict__ qkv, float* __restrict__ out,
+// CL: loads and stores through buffer descriptors whose range ends at the sequence's last row, so
+// the padding rows read zeros and their stores drop with no branch (a conditional load or store
+// compiles to an exec-masked branch around each one: 119 branches per wave and SGPR spills through
+// v_writelane in the NKT = 2 kernel); the same values, bit-identical
+template <int NKT, int MINB = 1, bool CL = true>
+__global__ __launch_bounds__(256, MINB) void attn_f32_mfma_kernel(const float* __restrict__ qkv, float* __restrict__ out,
                                                             int nseq, int S, int W, int causal) {
   const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
   const int H = W / 64;
@@ -444,6 +448,23 @@ __global__ __launch_bounds__(256) void attn_f32_mfma_kernel(const float* __restr
   const float* base = qkv + (int64_t)bseq * S * ld + head * 64;
   float* obase = out + (int64_t)bseq * S * W + head * 64;
   auto rho = [&](int r) { return (r & 3) + 8 * (r >> 2) + 4 * h; };
+  // (CL: p's row r is passed too; offsets from the sequence's first row, rows >= S out of range)
+  const __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(qkv + (int64_t)bseq * S * ld), (short)0, S * (int)ld * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rout = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(out + (int64_t)bseq * S * W), (short)0, S * W * 4, 0x00020000);
+  auto ld4 = [&](const float* p, bool ok, int r, int col) {
+    if (CL) {
+      typedef unsigned int u32x4a __attribute__((ext_vector_type(4)));
+      const u32x4a t = __builtin_bit_cast(u32x4a, __builtin_amdgcn_raw_buffer_load_b128(rin, (uint32_t)((r * (int)ld + col) * 4), 0, 0));
+      return make_float4(__uint_as_float(t[0]), __uint_as_float(t[1]), __uint_as_float(t[2]), __uint_as_float(t[3]));
+    }
+    return ok ? *(const float4*)p : make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  auto ld1 = [&](const float* p, bool ok, int r, int col) {
+    if (CL) return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rin, (uint32_t)((r * (int)ld + col) * 4), 0, 0));
+    return ok ? *p : 0.f;
+  };
   for (int q0 = 0; q0 < S; q0 += 32) {
     const int qi = q0 + j;   // this lane's query in the S^T layout
     float qv[32];
@@ -451,7 +472,7 @@ __global__ __launch_bounds__(256) void attn_f32_mfma_kernel(const float* __restr
       const float* qp = base + (int64_t)min(qi, S - 1) * ld + 32 * h;
 #pragma unroll
       for (int c = 0; c < 8; ++c) {
-        const float4 t = qi < S ? *(const float4*)(qp + 4 * c) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 t = ld4(qp + 4 * c, qi < S, qi, head * 64 + 32 * h + 4 * c);
         qv[4 * c] = t.x * 0.125f; qv[4 * c + 1] = t.y * 0.125f; qv[4 * c + 2] = t.z * 0.125f; qv[4 * c + 3] = t.w * 0.125f;
       }
     }
@@ -465,7 +486,7 @@ __global__ __launch_bounds__(256) void attn_f32_mfma_kernel(const float* __restr
       float kv[32];
 #pragma unroll
       for (int c = 0; c < 8; ++c) {
-        const float4 t = ki < S ? *(const float4*)(kp + 4 * c) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 t = ld4(kp + 4 * c, ki < S, ki, W + head * 64 + 32 * h + 4 * c);
         kv[4 * c] = t.x; kv[4 * c + 1] = t.y; kv[4 * c + 2] = t.z; kv[4 * c + 3] = t.w;
       }
 #pragma unroll
@@ -503,7 +524,7 @@ __global__ __launch_bounds__(256) void attn_f32_mfma_kernel(const float* __restr
 #pragma unroll
         for (int st = 0; st < 16; ++st) {
           const int key = kt * 32 + (st & 3) + 8 * (st >> 2) + 4 * h;
-          vv[st] = key < S ? base[2 * W + (int64_t)key * ld + 32 * dt + j] : 0.f;
+          vv[st] = ld1(base + 2 * W + (int64_t)min(key, S - 1) * ld + 32 * dt + j, key < S, key, 2 * W + head * 64 + 32 * dt + j);
         }
 #pragma unroll
         for (int st = 0; st < 16; ++st) o = __builtin_amdgcn_mfma_f32_32x32x2f32(sc[kt][st], vv[st], o, 0, 0, 0);
@@ -512,7 +533,10 @@ __global__ __launch_bounds__(256) void attn_f32_mfma_kernel(const float* __restr
       for (int r = 0; r < 16; ++r) {
         const int qr = q0 + rho(r);
         const float iv = __shfl(inv, rho(r), 64);   // 1 / l of query rho(r) (held by lane rho(r))
-        if (qr < S) obase[(int64_t)qr * W + 32 * dt + j] = o[r] * iv;
+        if (CL)
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(o[r] * iv), rout, (uint32_t)((qr * W + head * 64 + 32 * dt + j) * 4), 0, 0);
+        else if (qr < S)
+          obase[(int64_t)qr * W + 32 * dt + j] = o[r] * iv;
       }
     }
   }
@@ -612,14 +636,29 @@ static bool attn_f32_mfma_on() {
 #endif
   return true;
 }
+static int attn_f32_variant() {
+#if MICLIP_AB
+  const char* e = std::getenv("MICLIP_ATTN_F32_V");
+  if (e) return std::atoi(e);
+#endif
+  return 0;
+}
 
 hipError_t attention_f32(const float* qkv, float* out, int B, int S, int W, int causal, hipStream_t s) {
   if (B <= 0) return hipSuccess;
   if (W % 64 || S < 1) return hipErrorInvalidValue;
   const dim3 grid((unsigned)B * (W / 64));
   const dim3 grid4((unsigned)(((int64_t)B * (W / 64) + 3) / 4));
-  if (attn_f32_mfma_on() && S <= 64)
-    hipLaunchKernelGGL(attn_f32_mfma_kernel<2>, grid4, dim3(256), 0, s, qkv, out, B, S, W, causal);
+#if MICLIP_AB
+  if (attn_f32_mfma_on() && attn_f32_variant() == 1 && S <= 128) {   // 1: conditional loads / stores (A/B)
+    if (S <= 64) hipLaunchKernelGGL((attn_f32_mfma_kernel<2, 1, false>), grid4, dim3(256), 0, s, qkv, out, B, S, W, causal);
+    else if (S <= 96) hipLaunchKernelGGL((attn_f32_mfma_kernel<3, 1, false>), grid4, dim3(256), 0, s, qkv, out, B, S, W, causal);
+    else hipLaunchKernelGGL((attn_f32_mfma_kernel<4, 1, false>), grid4, dim3(256), 0, s, qkv, out, B, S, W, causal);
+    return hipGetLastError();
+  }
+#endif
+  if (attn_f32_mfma_on() && S <= 64)   // (held to 256 registers: two waves per SIMD, no spills)
+    hipLaunchKernelGGL((attn_f32_mfma_kernel<2, 2>), grid4, dim3(256), 0, s, qkv, out, B, S, W, causal);
   else if (attn_f32_mfma_on() && S <= 96)
     hipLaunchKernelGGL(attn_f32_mfma_kernel<3>, grid4, dim3(256), 0, s, qkv, out, B, S, W, causal);
   else if (attn_f32_mfma_on() && S <= 128)

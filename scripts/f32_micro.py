@@ -28,13 +28,14 @@ def main():
              "bearly": (_native.lib_ab, {"MICLIP_F32_8Q": "2"}),
              "ng1": (_native.lib_ab, {"MICLIP_F32_8Q": "1", "MICLIP_8Q_NG": "1"}),
              "ng3": (_native.lib_ab, {"MICLIP_F32_8Q": "1", "MICLIP_8Q_NG": "3"}),
-             "ab8q": (_native.lib_ab, {"MICLIP_F32_8Q": "1"})}
+             "ab8q": (_native.lib_ab, {"MICLIP_F32_8Q": "1"}),
+             "attv1": (_native.lib_ab, {"MICLIP_F32_8Q": "1", "MICLIP_ATTN_F32_V": "1"})}
     names = os.environ.get("F32_VARIANTS", "8q,pp").split(",")
     libs = {k: table[k][0] for k in names}
 
     def use(k):   # (a model's calls go to whichever library _native.lib names)
         _native.lib = table[k][0]
-        for e in ("MICLIP_F32_8Q", "MICLIP_8Q_NG"):
+        for e in ("MICLIP_F32_8Q", "MICLIP_8Q_NG", "MICLIP_ATTN_F32_V"):
             os.environ.pop(e, None)
         os.environ.update(table[k][1])
 

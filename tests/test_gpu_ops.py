@@ -722,6 +722,30 @@ def test_split2h_gemm_8phase_bit_identical(gpu, monkeypatch, M, N, K, epi):
     assert (err / rowscale).max().item() < 1e-6
 
 
+@pytest.mark.parametrize("B,S,W,causal", [(37, 50, 768, 0), (5, 77, 512, 1), (3, 1, 128, 0), (4, 33, 128, 1),
+                                          (6, 96, 256, 0), (2, 128, 128, 1), (9, 64, 192, 0)])
+def test_attention_f32_descriptor_form_bit_identical(gpu, monkeypatch, B, S, W, causal):
+    """The exact-f32 MFMA attention with its loads and stores through range-limited buffer
+    descriptors (the default: padding rows read zeros, their stores drop, no branches) against
+    the conditional-load form (A/B build, MICLIP_ATTN_F32_V=1), bit for bit."""
+    import torch
+    N_ = _lib()
+    rng = np.random.default_rng(B * 7 + S + W + causal)
+    d = torch.from_numpy((rng.standard_normal((B * S, 3 * W)) * 2).astype(np.float32)).to(gpu)
+    outs = []
+    for lib, v in ((N_.lib(), None), (N_.lib_ab(), "1")):
+        if v is None:
+            monkeypatch.delenv("MICLIP_ATTN_F32_V", raising=False)
+        else:
+            monkeypatch.setenv("MICLIP_ATTN_F32_V", v)
+        out = torch.full((B * S + 64, W), float("nan"), device=gpu)   # rows past B * S stay untouched
+        N_.check(lib.mi_op_attention_f32(d.data_ptr(), out.data_ptr(), B, S, W, causal, _stream()), "attn f32")
+        outs.append(out)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][:B * S].view(torch.int32), outs[1][:B * S].view(torch.int32))
+    assert torch.isnan(outs[0][B * S:]).all()
+
+
 def _attn_ref(qkv, B, S, W, causal):
     H = W // 64
     x = qkv.reshape(B, S, 3, H, 64).astype(np.float64)
