@@ -523,7 +523,9 @@ def parity_mode(args, dev, pixels, tokens, Q, k, base, chunk):
     M = chunk * cfg.vision_tokens
     fl = 2.0 * M * 4 * cfg.vision_width * cfg.vision_width
     fc = kern["gemm_fc"]["us"]
-    step_flops = pixels.shape[0] * cfg.image_flops() + Q * cfg.text_flops() + 2.0 * pixels.shape[0] * Q * cfg.embed_dim
+    # executed flops: the last block's row-wise part runs on the CLS rows alone at >= 256 frames per chunk
+    step_flops = (pixels.shape[0] * cfg.image_flops_executed(chunk >= 256) + Q * cfg.text_flops()
+                  + 2.0 * pixels.shape[0] * Q * cfg.embed_dim)
     out = {"weights": "fp32", "value": round(pixels.shape[0] / (ms / 1e3), 1), "unit": "frames/s",
            "ms_per_step": round(ms, 3), "steps": args.parity_steps,
            "note": "fp32 tower (split-f16 GEMMs, f32-grade; exact-f32 MFMA attention): the mode whose R@1/5/10 "
@@ -714,7 +716,10 @@ def main():
             kern["jpeg_ingest_720p"] = ingest
         _progress("rank roofline")
         rank_roof = None if args.no_rank_roofline else rank_roofline(dev)
-        F_frame, F_text = cfg.image_flops(), cfg.text_flops()
+        # executed flops: the folded bf16 tower and the fp32 tower run the last block's row-wise part on
+        # the CLS rows alone at >= 256 frames per chunk (api.cpp last_block_cls); the MX tower does not
+        cls_last = chunk >= 256 and (args.weights == "fp32" or (args.weights == "bf16" and lnfold_active(model, cfg)))
+        F_frame, F_text = cfg.image_flops_executed(cls_last), cfg.text_flops()
         step_flops = Nf * world * F_frame + Q * world * F_text + 2.0 * Nf * world * Q * cfg.embed_dim
         # against the peak of the arithmetic the step's GEMMs run on (fp8 runs: the MX-fp8 peak)
         # (fp32 runs: f32-equivalent flops against the f32 MFMA peak -- the split-f16 GEMMs execute 3x
@@ -790,6 +795,8 @@ def main():
             "roofline": roof,
             "rank_roofline": rank_roof,
             "mfma_frac_end_to_end": round(mfma_frac, 4),
+            "mfma_frac_flops": ("executed: the last block's out_proj / c_fc / c_proj on the CLS rows only "
+                                "(their other rows are never read)" if cls_last else "the full model"),
             "parity_mode": parity,
             "verify": verify,
             "kernels": kern,

@@ -854,16 +854,60 @@ static int gemm_residual(mi_clip* c, const uint16_t* A, int64_t lda, const uint1
   return MI_OK;
 }
 
+// The last block after its attention on the CLS rows only.  encode_image reads the tower at
+// x[:, 0] alone (ln_post(x[:, 0]) @ proj, openai/CLIP VisionTransformer.forward), and every op of
+// the block after attention is row-wise (out_proj, the residual add, ln_2, c_fc, c_proj), so the
+// other S - 1 rows of each sequence are never read: the CLS rows of att and of the fp16 stream
+// are gathered (B rows) and the rest of the block runs on them with the same kernels -- the
+// values of the full pass's CLS rows bit for bit (each GEMM row's arithmetic does not depend on
+// the rows beside it).  Needs the 8-phase kernel's 256 rows (B >= 256); the compact rows live in
+// the qkv buffer, dead after attention.  MICLIP_CLS_LAST=0 (A/B) runs the full block.
+static int cls_last() {
+  const char* e = ab_getenv("MICLIP_CLS_LAST");
+  return e ? atoi(e) != 0 : 1;
+}
+
+static int last_block_cls(mi_clip* c, const Layer& L, int B, int S, int W, float** xpost, hipStream_t s) {
+  uint16_t* att_c = c->qkv;                                                  // [B][W] bf16
+  float* x_c = (float*)((char*)c->qkv + (((size_t)B * W * 2 + 255) & ~(size_t)255));   // [B] fp16 row slots
+  HIP_TRY(hipMemcpy2DAsync(att_c, (size_t)W * 2, c->att, (size_t)S * W * 2, (size_t)W * 2, B, hipMemcpyDeviceToDevice, s));
+  HIP_TRY(hipMemcpy2DAsync(x_c, (size_t)W * 4, c->x, (size_t)S * W * 4, (size_t)W * 2, B, hipMemcpyDeviceToDevice, s));
+  GemmArgs o = gargs(att_c, W, L.w_out, W, L.b_out, x_c, 2 * W, B, W, W);
+  o.ps = (float*)c->h;
+  HIP_TRY(gemm_bf16(o, EPI_RES16_BF16, s));
+  HIP_TRY(residual_finalize((const float*)c->h, c->rs, B, W, s));
+  GemmArgs f = gargs((const uint16_t*)x_c, 2 * W, L.lw_fc, W, L.lc_fc, c->mlp, 4 * W, B, 4 * W, W);
+  f.variant = 0;
+  f.a_f16 = 1;
+  f.rs = c->rs;
+  f.colv = L.ls_fc;
+  HIP_TRY(gemm_bf16(f, EPI_LN_GELU_BF16, s));
+  HIP_TRY(gemm_bf16(with_variant(gargs(c->mlp, 4 * W, L.w_proj, 4 * W, L.b_proj, c->delta, W, B, W, 4 * W), GV_PROJ),
+                    EPI_BF16, s));
+  *xpost = x_c;
+  return MI_OK;
+}
+
 // x16 / rs hold the embedding output and ln_1's statistics (vision_embed_ln16).  On return x16
-// + delta is the final residual stream (the last c_proj output stays in delta, as run_tower).
-static int run_tower_fold(mi_clip* c, const std::vector<Layer>& layers, int B, int S, int W, hipStream_t s) {
+// + delta is the final residual stream (the last c_proj output stays in delta, as run_tower), at
+// rows r * post_stride of (*xpost, delta): the full stream's CLS rows (stride S), or the last
+// block's compact CLS rows (stride 1, last_block_cls).
+static int run_tower_fold(mi_clip* c, const std::vector<Layer>& layers, int B, int S, int W, hipStream_t s,
+                          float** xpost, int64_t* post_stride) {
   const int M = B * S;
   const bool fuse = resfuse() && !gemm_variant_for(GV_OUT) && !gemm_variant_for(GV_PROJ) && !gemm_variant();
+  *xpost = c->x;
+  *post_stride = S;
   for (size_t l = 0; l < layers.size(); ++l) {
     const Layer& L = layers[l];
     const bool last = l + 1 == layers.size();
     HIP_TRY(gemm_bf16(ln_args(c, L.lw_qkv, L.ls_qkv, L.lc_qkv, c->qkv, 3 * W, M, W), EPI_LN_BF16, s));
     HIP_TRY(attention(c->qkv, c->att, B, S, W, 0, s));
+    if (last && fuse && B >= 256 && S > 1 && cls_last()) {
+      MI_TRY(last_block_cls(c, L, B, S, W, xpost, s));
+      *post_stride = 1;
+      break;
+    }
     if (fuse) {
       MI_TRY(gemm_residual(c, c->att, W, L.w_out, L.b_out, M, W, W, s));
     } else {
@@ -936,9 +980,15 @@ static int f32_gemm_mode() {
 // out_proj / c_proj GEMM epilogues:
 //   h = ln_1(x) ; qkv = h W_qkv^T + b ; att = MHA(qkv) ; x += att W_o^T + b_o
 //   h = ln_2(x) ; m = QuickGELU(h W_fc^T + b_fc) ; x += m W_pr^T + b_pr
+// xpost / post_stride (vision): where ln_post reads the CLS rows (the last block may run on them
+// alone, as run_tower_fold's last_block_cls)
 static int run_tower_f32(mi_clip* c, const std::vector<Layer>& layers, int B, int S, int W, int causal,
-                         hipStream_t s) {
+                         hipStream_t s, float** xpost = nullptr, int64_t* post_stride = nullptr) {
   const int M = B * S;
+  if (xpost) {
+    *xpost = c->x;
+    *post_stride = S;
+  }
   float* h = (float*)c->h;
   float* qkv = (float*)c->qkv;
   float* att = (float*)c->att;
@@ -957,23 +1007,41 @@ static int run_tower_f32(mi_clip* c, const std::vector<Layer>& layers, int B, in
     uint16_t* a3o = a3 + (int64_t)M * 3 * W;
     float* rsc_o = rsc + c->rsc_rows;
     float* rmax = rsc + 2 * c->rsc_rows;
+    int Mr = M;   // the rows the block's row-wise part runs on (B for the last block's CLS rows)
     auto gemm3 = [&](int K, const uint16_t* w3, const float* c3, const float* b, float* out, int N, int epi) -> int {
-      GemmArgs g = gargs(a3, 3 * K, w3, 3 * K, b, out, N, M, N, 3 * K);
+      GemmArgs g = gargs(a3, 3 * K, w3, 3 * K, b, out, N, Mr, N, 3 * K);
       g.a_f16 = 1;
       g.rsc = rsc;
       g.csc = c3;
       HIP_TRY(gemm_bf16(g, epi, s));
       return MI_OK;
     };
-    for (const Layer& L : layers) {
+    for (size_t li = 0; li < layers.size(); ++li) {
+      const Layer& L = layers[li];
+      Mr = M;
       HIP_TRY(layernorm_split2h(c->x, W, L.ln1_g, L.ln1_b, M, W, a3, rsc, s));
       MI_TRY(gemm3(W, L.h3_qkv, L.c3_qkv, L.b_qkv, qkv, 3 * W, EPI_F32));
       HIP_TRY(attention_f32(qkv, att, B, S, W, causal, s));
-      HIP_TRY(split2h_rows(att, W, M, W, 0, 0, a3, rsc, s));
-      MI_TRY(gemm3(W, L.h3_out, L.c3_out, L.b_out, c->x, W, EPI_RESID_F32));
+      float* xr = c->x;
+      const float* ar = att;
+      if (xpost && li + 1 == layers.size() && !causal && B >= 256 && S > 1 && cls_last()) {
+        // the last block after attention on the CLS rows only (see last_block_cls), gathered into
+        // the qkv buffer (dead after attention)
+        float* att_c = qkv;
+        float* x_c = qkv + (((size_t)B * W + 63) & ~(size_t)63);
+        HIP_TRY(hipMemcpy2DAsync(att_c, (size_t)W * 4, att, (size_t)S * W * 4, (size_t)W * 4, B, hipMemcpyDeviceToDevice, s));
+        HIP_TRY(hipMemcpy2DAsync(x_c, (size_t)W * 4, c->x, (size_t)S * W * 4, (size_t)W * 4, B, hipMemcpyDeviceToDevice, s));
+        Mr = B;
+        xr = x_c;
+        ar = att_c;
+        *xpost = x_c;
+        *post_stride = 1;
+      }
+      HIP_TRY(split2h_rows(ar, W, Mr, W, 0, 0, a3, rsc, s));
+      MI_TRY(gemm3(W, L.h3_out, L.c3_out, L.b_out, xr, W, EPI_RESID_F32));
       if (fuse_split) {   // c_fc's epilogue writes c_proj's split operand (EPI_SPLIT_GELU)
-        HIP_TRY(layernorm_split2h(c->x, W, L.ln2_g, L.ln2_b, M, W, a3, rsc, s, rmax));
-        GemmArgs g = gargs(a3, 3 * W, L.h3_fc, 3 * W, L.b_fc, a3o, 3 * 4 * W, M, 4 * W, 3 * W);
+        HIP_TRY(layernorm_split2h(xr, W, L.ln2_g, L.ln2_b, Mr, W, a3, rsc, s, rmax));
+        GemmArgs g = gargs(a3, 3 * W, L.h3_fc, 3 * W, L.b_fc, a3o, 3 * 4 * W, Mr, 4 * W, 3 * W);
         g.a_f16 = 1;
         g.rsc = rsc;
         g.csc = L.c3_fc;
@@ -982,17 +1050,17 @@ static int run_tower_f32(mi_clip* c, const std::vector<Layer>& layers, int B, in
         g.bnd_b = L.fc_bb;
         g.rsc_out = rsc_o;
         HIP_TRY(gemm_bf16(g, EPI_SPLIT_GELU, s));
-        GemmArgs p = gargs(a3o, 3 * 4 * W, L.h3_proj, 3 * 4 * W, L.b_proj, c->x, W, M, W, 3 * 4 * W);
+        GemmArgs p = gargs(a3o, 3 * 4 * W, L.h3_proj, 3 * 4 * W, L.b_proj, xr, W, Mr, W, 3 * 4 * W);
         p.a_f16 = 1;
         p.rsc = rsc_o;
         p.csc = L.c3_proj;
         HIP_TRY(gemm_bf16(p, EPI_RESID_F32, s));
         continue;
       }
-      HIP_TRY(layernorm_split2h(c->x, W, L.ln2_g, L.ln2_b, M, W, a3, rsc, s));
+      HIP_TRY(layernorm_split2h(xr, W, L.ln2_g, L.ln2_b, Mr, W, a3, rsc, s));
       MI_TRY(gemm3(W, L.h3_fc, L.c3_fc, L.b_fc, mlp, 4 * W, EPI_F32));   // pre-activation
-      HIP_TRY(split2h_rows(mlp, 4 * W, M, 4 * W, 0, 1, a3, rsc, s));       // QuickGELU, then split
-      MI_TRY(gemm3(4 * W, L.h3_proj, L.c3_proj, L.b_proj, c->x, W, EPI_RESID_F32));
+      HIP_TRY(split2h_rows(mlp, 4 * W, Mr, 4 * W, 0, 1, a3, rsc, s));      // QuickGELU, then split
+      MI_TRY(gemm3(4 * W, L.h3_proj, L.c3_proj, L.b_proj, xr, W, EPI_RESID_F32));
     }
     return MI_OK;
   }
@@ -1052,10 +1120,12 @@ static int encode_image_f32(mi_clip* c, const char* px, int nb, int in_dtype, ch
                      1));
   }
   HIP_TRY(vision_embed_ln(c->x, c->cls, c->vpos, c->ln_pre_g, c->ln_pre_b, nb, S, W, s));
-  int r = run_tower_f32(c, c->vl, nb, S, W, 0, s);
+  float* xpost = c->x;
+  int64_t post_stride = S;
+  int r = run_tower_f32(c, c->vl, nb, S, W, 0, s, &xpost, &post_stride);
   if (r) return r;
   float* cls = (float*)c->cls_ln;
-  HIP_TRY(layernorm_f32(c->x, (int64_t)S * W, c->ln_post_g, c->ln_post_b, cls, W, nb, W, s));
+  HIP_TRY(layernorm_f32(xpost, post_stride * W, c->ln_post_g, c->ln_post_b, cls, W, nb, W, s));
   HIP_TRY(gemm_f32(cls, W, c->vproj_f, W, nullptr, c->y, E, nb, E, W, EPI_F32, s));
   HIP_TRY(finalize_rows(c->y, out, out_dtype, nb, E, l2_normalize, s));
   return MI_OK;
@@ -1119,9 +1189,11 @@ int mi_clip_encode_image(mi_clip* c, const void* pixels, int64_t B, int in_dtype
     // LayerNorm-folded tower: bf16 weights folded at create (W % 256 == 0), whole 256-row tiles
     const bool fold = !c->fp8 && !c->vl.empty() && c->vl[0].lw_qkv && lnfold(W) && (int64_t)nb * S >= 256;
     int r;
+    float* xpost = c->x;
+    int64_t post_stride = S;
     if (fold) {
       HIP_TRY(vision_embed_ln16(c->x, c->cls, c->vpos, c->ln_pre_g, c->ln_pre_b, nb, S, W, c->rs, s));
-      r = run_tower_fold(c, c->vl, nb, S, W, s);
+      r = run_tower_fold(c, c->vl, nb, S, W, s, &xpost, &post_stride);
     } else {
       const bool fuse_ln1 = !c->fp8 && !c->vl.empty() && embed_ln1();  // the MX tower's first LN writes fp8 itself
       HIP_TRY(vision_embed_ln(c->x, c->cls, c->vpos, c->ln_pre_g, c->ln_pre_b, nb, S, W, s,
@@ -1133,7 +1205,7 @@ int mi_clip_encode_image(mi_clip* c, const void* pixels, int64_t B, int in_dtype
     if (r) return r;
     const int r16 = fold || (resid16() && !c->vl.empty());
     // ln_post(x[:, 0] + last c_proj delta) over the CLS rows only
-    HIP_TRY(residual_ln(c->x, c->delta, (int64_t)S * W, 0, c->ln_post_g, c->ln_post_b, c->cls_ln, nb, W, s, nullptr,
+    HIP_TRY(residual_ln(xpost, c->delta, post_stride * W, 0, c->ln_post_g, c->ln_post_b, c->cls_ln, nb, W, s, nullptr,
                         nullptr, r16 ? 2 : 0));
     HIP_TRY(gemm_bf16(gargs(c->cls_ln, W, c->vproj_t, W, nullptr, c->y, E, nb, E, W), EPI_F32, s));
     HIP_TRY(finalize_rows(c->y, (char*)out + c0 * E * dtype_size(out_dtype), out_dtype, nb, E, l2_normalize, s));

@@ -59,6 +59,13 @@ class CLIPConfig:
         f += 2.0 * W * self.embed_dim                        # CLS projection
         return f
 
+    def image_flops_executed(self, cls_last: bool = True) -> float:
+        """image_flops less the work the last block skips when it runs its row-wise part on the
+        CLS rows only (api.cpp last_block_cls: out_proj, c_fc and c_proj for S - 1 of S rows per
+        frame; their outputs are never read)."""
+        W, S = self.vision_width, self.vision_tokens
+        return self.image_flops() - (2.0 * (S - 1) * W * (W + 4 * W + 4 * W) if cls_last else 0.0)
+
     def text_flops(self) -> float:
         W, S, L = self.text_width, self.context_length, self.text_layers
         per_layer = 2.0 * S * W * 12 * W + 2.0 * 2.0 * S * S * W

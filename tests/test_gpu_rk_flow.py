@@ -139,6 +139,23 @@ def test_fp32_tower_8phase_bit_identical(gpu, monkeypatch, name, n):
     assert clip_ref.cosine(img, ri).min() > 1 - 1e-9
 
 
+def test_fp32_tower_last_block_on_cls_rows_bit_identical(gpu, monkeypatch):
+    """The fp32 tower's last block after attention on the gathered CLS rows only (the default
+    for >= 256 frames per chunk, as the bf16 tower's last_block_cls): image embeddings equal the
+    full block's (A/B build, MICLIP_CLS_LAST=0) bit for bit."""
+    import torch
+    from miclip import _native, config, model as M, weights
+    cfg = config.get_config("ViT-B/32")
+    sd = state_dict("ViT-B/32")
+    px = torch.from_numpy(weights.synthetic_pixels(300, cfg.image_resolution, seed=3))
+    got = M.CLIP(cfg, sd, device=gpu, weights="fp32", image_chunk=300).encode_image(px).cpu().numpy()
+    monkeypatch.setattr(_native, "lib", _native.lib_ab)
+    monkeypatch.setenv("MICLIP_CLS_LAST", "0")
+    full = M.CLIP(cfg, sd, device=gpu, weights="fp32", image_chunk=300).encode_image(px).cpu().numpy()
+    monkeypatch.undo()
+    assert np.array_equal(got.view(np.int32), full.view(np.int32))
+
+
 @pytest.mark.parametrize("name,fname", [("ViT-L/14", "vit_l14.npz"), ("ViT-L/14@336px", "vit_l14_336px.npz")])
 def test_fp32_tower_l14_golden(gpu, name, fname):
     """L/14 (257 tokens) and L/14@336px (577 tokens: the 256-thread attention
