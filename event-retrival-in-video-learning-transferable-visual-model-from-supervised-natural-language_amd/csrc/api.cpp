@@ -901,9 +901,27 @@ static int run_tower_fold(mi_clip* c, const std::vector<Layer>& layers, int B, i
   for (size_t l = 0; l < layers.size(); ++l) {
     const Layer& L = layers[l];
     const bool last = l + 1 == layers.size();
-    HIP_TRY(gemm_bf16(ln_args(c, L.lw_qkv, L.ls_qkv, L.lc_qkv, c->qkv, 3 * W, M, W), EPI_LN_BF16, s));
+    const bool cls = last && fuse && B >= 256 && S > 1 && cls_last();
+    if (cls) {
+      // the last block reads attention at the CLS queries only: K and V for every row, Q for the
+      // CLS rows (strided A and output rows, their LN statistics gathered); the other rows' Q
+      // columns keep stale finite values, which reach only their own queries' outputs (a query's
+      // scores, softmax and P V use its own Q row alone), never read
+      GemmArgs kv = ln_args(c, L.lw_qkv + (size_t)W * W, L.ls_qkv + W, L.lc_qkv + W, c->qkv + W, 2 * W, M, W);
+      kv.ldo = 3 * W;
+      HIP_TRY(gemm_bf16(kv, EPI_LN_BF16, s));
+      float* rs_c = (float*)c->h;
+      HIP_TRY(hipMemcpy2DAsync(rs_c, 8, c->rs, (size_t)S * 8, 8, B, hipMemcpyDeviceToDevice, s));
+      GemmArgs q = ln_args(c, L.lw_qkv, L.ls_qkv, L.lc_qkv, c->qkv, W, B, W);
+      q.lda = (int64_t)S * 2 * W;
+      q.ldo = (int64_t)S * 3 * W;
+      q.rs = rs_c;
+      HIP_TRY(gemm_bf16(q, EPI_LN_BF16, s));
+    } else {
+      HIP_TRY(gemm_bf16(ln_args(c, L.lw_qkv, L.ls_qkv, L.lc_qkv, c->qkv, 3 * W, M, W), EPI_LN_BF16, s));
+    }
     HIP_TRY(attention(c->qkv, c->att, B, S, W, 0, s));
-    if (last && fuse && B >= 256 && S > 1 && cls_last()) {
+    if (cls) {
       MI_TRY(last_block_cls(c, L, B, S, W, xpost, s));
       *post_stride = 1;
       break;
@@ -1019,12 +1037,28 @@ static int run_tower_f32(mi_clip* c, const std::vector<Layer>& layers, int B, in
     for (size_t li = 0; li < layers.size(); ++li) {
       const Layer& L = layers[li];
       Mr = M;
+      const bool cls = xpost && li + 1 == layers.size() && !causal && B >= 256 && S > 1 && cls_last();
       HIP_TRY(layernorm_split2h(c->x, W, L.ln1_g, L.ln1_b, M, W, a3, rsc, s));
-      MI_TRY(gemm3(W, L.h3_qkv, L.c3_qkv, L.b_qkv, qkv, 3 * W, EPI_F32));
+      if (cls) {   // K and V for every row, Q for the CLS rows only (as run_tower_fold's last block)
+        GemmArgs kv = gargs(a3, 3 * W, L.h3_qkv + (size_t)W * 3 * W, 3 * W, L.b_qkv + W, qkv + W, 3 * W, M, 2 * W, 3 * W);
+        kv.a_f16 = 1;
+        kv.rsc = rsc;
+        kv.csc = L.c3_qkv + W;
+        HIP_TRY(gemm_bf16(kv, EPI_F32, s));
+        float* rsc_c = (float*)c->h;
+        HIP_TRY(hipMemcpy2DAsync(rsc_c, 4, rsc, (size_t)S * 4, 4, B, hipMemcpyDeviceToDevice, s));
+        GemmArgs q = gargs(a3, (int64_t)S * 3 * W, L.h3_qkv, 3 * W, L.b_qkv, qkv, (int64_t)S * 3 * W, B, W, 3 * W);
+        q.a_f16 = 1;
+        q.rsc = rsc_c;
+        q.csc = L.c3_qkv;
+        HIP_TRY(gemm_bf16(q, EPI_F32, s));
+      } else {
+        MI_TRY(gemm3(W, L.h3_qkv, L.c3_qkv, L.b_qkv, qkv, 3 * W, EPI_F32));
+      }
       HIP_TRY(attention_f32(qkv, att, B, S, W, causal, s));
       float* xr = c->x;
       const float* ar = att;
-      if (xpost && li + 1 == layers.size() && !causal && B >= 256 && S > 1 && cls_last()) {
+      if (cls) {
         // the last block after attention on the CLS rows only (see last_block_cls), gathered into
         // the qkv buffer (dead after attention)
         float* att_c = qkv;
