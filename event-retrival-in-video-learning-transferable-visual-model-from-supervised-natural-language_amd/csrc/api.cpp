@@ -960,19 +960,45 @@ static GemmArgs margs(const uint8_t* A, const uint8_t* as, const uint8_t* W, con
 // run_tower, every GEMM on the block-scaled MFMA; the producers of GEMM A
 // operands (the LayerNorms, attention, c_fc's QuickGELU epilogue) emit MX-fp8
 // directly, so no separate quantisation pass runs.
-static int run_tower_mx(mi_clip* c, const std::vector<Layer>& layers, int B, int S, int W, hipStream_t s, int r16) {
+// xpost / post_stride: where ln_post reads the CLS rows (the last block after attention runs on
+// them alone at >= 256 frames, as run_tower_fold's last_block_cls: the CLS rows of the MX-fp8
+// attention output -- codes and their stage-major scales -- and of the residual stream gathered)
+static int run_tower_mx(mi_clip* c, const std::vector<Layer>& layers, int B, int S, int W, hipStream_t s, int r16,
+                        float** xpost, int64_t* post_stride) {
   const int M = B * S;
+  *xpost = c->x;
+  *post_stride = S;
   HIP_TRY(layernorm_bf16(c->x, W, layers[0].ln1_g, layers[0].ln1_b, c->h, W, M, W, s, c->hq, c->hqs));
   for (size_t l = 0; l < layers.size(); ++l) {
     const Layer& L = layers[l];
     HIP_TRY(gemm_mx(margs(c->hq, c->hqs, L.q_qkv, L.s_qkv, L.b_qkv, c->qkv, 3 * W, M, 3 * W, W), EPI_BF16, s));
     HIP_TRY(attention(c->qkv, c->att, B, S, W, 0, s, c->attq, c->attqs));
-    HIP_TRY(gemm_mx(margs(c->attq, c->attqs, L.q_out, L.s_out, L.b_out, c->delta, W, M, W, W), EPI_BF16, s));
-    HIP_TRY(residual_ln(c->x, c->delta, W, 1, L.ln2_g, L.ln2_b, c->h, M, W, s, c->hq, c->hqs, xmode_at(r16, l)));
-    GemmArgs fc = margs(c->hq, c->hqs, L.q_fc, L.s_fc, L.b_fc, c->mlpq, 4 * W, M, 4 * W, W);
+    int Mr = M;
+    const uint8_t *aq = c->attq, *aqs = c->attqs;
+    float* xr = c->x;
+    if (l + 1 == layers.size() && B >= 256 && S > 1 && W % 128 == 0 && cls_last()) {
+      uint8_t* aq_c = (uint8_t*)c->qkv;                                    // [B][W] e4m3
+      uint8_t* aqs_c = aq_c + (((size_t)B * W + 255) & ~(size_t)255);       // [W / 128][Bp][2]
+      float* x_c = (float*)(aqs_c + ((((size_t)W / 128) * (B + 2) * 2 + 255) & ~(size_t)255));
+      const size_t mp = (size_t)((M + 1) & ~1), bp = (size_t)((B + 1) & ~1);
+      HIP_TRY(hipMemcpy2DAsync(aq_c, W, c->attq, (size_t)S * W, W, B, hipMemcpyDeviceToDevice, s));
+      for (int st = 0; st < W / 128; ++st)
+        HIP_TRY(hipMemcpy2DAsync(aqs_c + st * bp * 2, 2, c->attqs + st * mp * 2, (size_t)S * 2, 2, B,
+                                 hipMemcpyDeviceToDevice, s));
+      HIP_TRY(hipMemcpy2DAsync(x_c, (size_t)W * 4, c->x, (size_t)S * W * 4, (size_t)W * 4, B, hipMemcpyDeviceToDevice, s));
+      Mr = B;
+      aq = aq_c;
+      aqs = aqs_c;
+      xr = x_c;
+      *xpost = x_c;
+      *post_stride = 1;
+    }
+    HIP_TRY(gemm_mx(margs(aq, aqs, L.q_out, L.s_out, L.b_out, c->delta, W, Mr, W, W), EPI_BF16, s));
+    HIP_TRY(residual_ln(xr, c->delta, W, 1, L.ln2_g, L.ln2_b, c->h, Mr, W, s, c->hq, c->hqs, xmode_at(r16, l)));
+    GemmArgs fc = margs(c->hq, c->hqs, L.q_fc, L.s_fc, L.b_fc, c->mlpq, 4 * W, Mr, 4 * W, W);
     fc.o_scale = c->mlpqs;
     HIP_TRY(gemm_mx(fc, EPI_GELU_MX, s));
-    HIP_TRY(gemm_mx(margs(c->mlpq, c->mlpqs, L.q_proj, L.s_proj, L.b_proj, c->delta, W, M, W, 4 * W), EPI_BF16, s));
+    HIP_TRY(gemm_mx(margs(c->mlpq, c->mlpqs, L.q_proj, L.s_proj, L.b_proj, c->delta, W, Mr, W, 4 * W), EPI_BF16, s));
     if (l + 1 < layers.size())
       HIP_TRY(residual_ln(c->x, c->delta, W, 1, layers[l + 1].ln1_g, layers[l + 1].ln1_b, c->h, M, W, s, c->hq,
                           c->hqs, r16 ? 2 : 0));
@@ -1233,7 +1259,7 @@ int mi_clip_encode_image(mi_clip* c, const void* pixels, int64_t B, int in_dtype
       HIP_TRY(vision_embed_ln(c->x, c->cls, c->vpos, c->ln_pre_g, c->ln_pre_b, nb, S, W, s,
                               fuse_ln1 ? c->vl[0].ln1_g : nullptr, fuse_ln1 ? c->vl[0].ln1_b : nullptr,
                               fuse_ln1 ? c->h : nullptr));
-      r = c->fp8 ? run_tower_mx(c, c->vl, nb, S, W, s, resid16() && !c->vl.empty())
+      r = c->fp8 ? run_tower_mx(c, c->vl, nb, S, W, s, resid16() && !c->vl.empty(), &xpost, &post_stride)
                  : run_tower(c, c->vl, nb, S, W, 0, s, resid16() && !c->vl.empty(), fuse_ln1);
     }
     if (r) return r;

@@ -1155,6 +1155,21 @@ hipError_t launch(const GemmArgs& a, hipStream_t s) {
 #else
   if (a.variant != 0) return hipErrorNotSupported;   // schedule overrides exist in the A/B build only
 #endif
+  // Small grids (fewer than 64 tiles of 256 x 256: the text tower's in_proj / out_proj / c_proj at
+  // 32 queries, small image batches) take 128 x 128 tiles: 4x the workgroups on a chip of 256
+  // CUs, the same k order and epilogue arithmetic (bit-identical for EPI_BF16).  B/32 encode_text
+  // of 32 queries 1272 -> 1134 us (scripts/text_micro.py, profiles/r05_zl_text_micro.log).
+  // MICLIP_SMALLM=t (A/B build) moves the threshold (0: off).
+  int small_t = 64;
+#if MICLIP_AB
+  if (const char* sm = std::getenv("MICLIP_SMALLM")) small_t = std::atoi(sm);
+#endif
+  if (EPI == EPI_BF16 && ((a.M + 255) / 256) * (a.N / 256) < small_t && a.N % 128 == 0 && !a.group) {
+    const int nt2 = ((a.M + 127) / 128) * (a.N / 128);
+    const int g = nt2 < 2 * cu_count() ? nt2 : 2 * cu_count();
+    hipLaunchKernelGGL((gemm_kernel<EPI, 128, 128, 2, 2>), dim3(g), dim3(256), 0, s, a);
+    return hipGetLastError();
+  }
   if (bf16_out && gemm_8q_ok(a)) return gemm_8q(a, EPI, s, cu_count(), 0);
   const int nt = ((a.M + 255) / 256) * (a.N / 256);
   const bool staged = big && a.K / BK >= LEAD;

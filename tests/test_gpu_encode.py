@@ -248,23 +248,24 @@ def test_lnfold_tower_matches_oracle(gpu, monkeypatch, name, n):
         assert np.array_equal(got, got0)     # the same (unfolded) path in both libraries
 
 
-@pytest.mark.parametrize("name,n", [("ViT-B/32", 300), ("ViT-B/32", 257)])
-def test_last_block_on_cls_rows_bit_identical(gpu, monkeypatch, name, n):
-    """The folded tower's last block after attention on the gathered CLS rows only (api.cpp
-    last_block_cls, the default for >= 256 frames per chunk): the embeddings equal the full
-    block's (A/B build, MICLIP_CLS_LAST=0) bit for bit, and a chunk of 8 frames (the full block)
-    gives the same rows as the big chunk."""
+@pytest.mark.parametrize("name,n,wts", [("ViT-B/32", 300, "bf16"), ("ViT-B/32", 257, "bf16"), ("ViT-B/32", 300, "fp8"),
+                                        ("test-small", 301, "fp8")])
+def test_last_block_on_cls_rows_bit_identical(gpu, monkeypatch, name, n, wts):
+    """The last block after attention on the gathered CLS rows only (api.cpp last_block_cls for
+    the folded bf16 tower, run_tower_mx for the MX-fp8 one; the default for >= 256 frames per
+    chunk): the embeddings equal the full block's (A/B build, MICLIP_CLS_LAST=0) bit for bit, and
+    a chunk of 8 frames (the full block) gives the same rows as the big chunk."""
     import torch
     from miclip import _native, config, weights
     cfg = config.get_config(name)
     px = torch.from_numpy(weights.synthetic_pixels(n, cfg.image_resolution, seed=n)).to(gpu).bfloat16()
-    got = _model(name, gpu, image_chunk=n).encode_image(px).cpu().numpy()
+    got = _model(name, gpu, image_chunk=n, weights=wts).encode_image(px).cpu().numpy()
     monkeypatch.setattr(_native, "lib", _native.lib_ab)
     monkeypatch.setenv("MICLIP_CLS_LAST", "0")
-    full = _model(name, gpu, image_chunk=n).encode_image(px).cpu().numpy()
+    full = _model(name, gpu, image_chunk=n, weights=wts).encode_image(px).cpu().numpy()
     monkeypatch.undo()
     assert np.array_equal(got.view(np.int32), full.view(np.int32))
-    small = _model(name, gpu, image_chunk=8).encode_image(px[:16]).cpu().numpy()
+    small = _model(name, gpu, image_chunk=8, weights=wts).encode_image(px[:16]).cpu().numpy()
     assert np.array_equal(got[:16].view(np.int32), small.view(np.int32))
 
 
