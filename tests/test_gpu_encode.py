@@ -269,6 +269,21 @@ def test_last_block_on_cls_rows_bit_identical(gpu, monkeypatch, name, n, wts):
     assert np.array_equal(got[:16].view(np.int32), small.view(np.int32))
 
 
+@pytest.mark.parametrize("wts", ["bf16", "fp8"])
+def test_last_block_cls_rows_across_chunks(gpu, wts):
+    """300 frames in chunks of 256 (the CLS-row last block) and 44 (the full block), of exactly
+    256 (the boundary) and in one 300-frame chunk give the same embeddings bit for bit."""
+    import torch
+    from miclip import config, weights
+    cfg = config.get_config("ViT-B/32")
+    px = torch.from_numpy(weights.synthetic_pixels(300, cfg.image_resolution, seed=31)).to(gpu).bfloat16()
+    one = _model("ViT-B/32", gpu, image_chunk=300, weights=wts).encode_image(px).cpu().numpy()
+    split = _model("ViT-B/32", gpu, image_chunk=256, weights=wts).encode_image(px).cpu().numpy()
+    exact = _model("ViT-B/32", gpu, image_chunk=256, weights=wts).encode_image(px[:256]).cpu().numpy()
+    assert np.array_equal(one.view(np.int32), split.view(np.int32))
+    assert np.array_equal(one[:256].view(np.int32), exact.view(np.int32))
+
+
 def test_kernel_events_time_the_c_fc_launches(gpu):
     """mi_clip_kernel_events / mi_clip_kernel_times (bench.py's live roofline timing): the c_fc
     launches of the folded bf16 tower are bracketed by events -- one per layer and chunk, up to

@@ -685,7 +685,8 @@ def test_split2h_gemm_f32_grade(gpu, M, N, K, epi):
 
 
 @pytest.mark.parametrize("M,N,K,epi", [(3000, 768, 3072, 2), (20000, 2304, 768, 3), (257, 256, 256, 3),
-                                       (777, 512, 1024, 2), (256, 1024, 512, 3)])
+                                       (777, 512, 1024, 2), (256, 1024, 512, 3), (512, 768, 768, 2),
+                                       (1023, 2304, 768, 3)])
 def test_split2h_gemm_8phase_bit_identical(gpu, monkeypatch, M, N, K, epi):
     """The split-f16 GEMM on the 8-phase kernel (gemm_8q.hip's SPL epilogues, the default where
     it applies: N % 256 == 0, K' % 128 == 0, M >= 256) gives the ping-pong kernel's results bit
