@@ -1052,34 +1052,52 @@ static int run_tower_f32(mi_clip* c, const std::vector<Layer>& layers, int B, in
     float* rsc_o = rsc + c->rsc_rows;
     float* rmax = rsc + 2 * c->rsc_rows;
     int Mr = M;   // the rows the block's row-wise part runs on (B for the last block's CLS rows)
-    auto gemm3 = [&](int K, const uint16_t* w3, const float* c3, const float* b, float* out, int N, int epi) -> int {
-      GemmArgs g = gargs(a3, 3 * K, w3, 3 * K, b, out, N, Mr, N, 3 * K);
+    // The activations' split operand stored once, [x1 | x2] (role 2, row stride 2K), where the
+    // consumer GEMM is the 8-phase kernel (its A_DUP read gives the logical [x1 | x1 | x2]): a third
+    // less written by the split passes and by c_fc's split epilogue (o_dup), bit-identical.
+    // MICLIP_F32_DUP=0 (A/B) keeps the full layout everywhere.
+    // (MICLIP_F32_DUP=mask in the A/B build: 1 ln_1's split, 2 attention's, 4 ln_2's, 8 c_fc's output)
+    const char* de = ab_getenv("MICLIP_F32_DUP");
+    const char* e8 = ab_getenv("MICLIP_F32_8Q");
+    const int dmask = de ? atoi(de) : 15;
+    const bool dup_on = dmask != 0 && (!e8 || atoi(e8) != 0);
+    auto sargs = [&](const uint16_t* A, int64_t lda_rows, bool dup, const uint16_t* w3, const float* c3, const float* b,
+                     float* out, int64_t ldo, int rows, int N, int K) {   // lda_rows: row stride in rows of the operand
+      GemmArgs g = gargs(A, lda_rows * (dup ? 2 : 3) * K, w3, 3 * K, b, out, ldo, rows, N, 3 * K);
       g.a_f16 = 1;
       g.rsc = rsc;
       g.csc = c3;
-      HIP_TRY(gemm_bf16(g, epi, s));
+      g.a_dup = dup ? K : 0;
+      return g;
+    };
+    auto dup_ok = [&](int rows, int N, int K, int64_t lda_rows = 1) {   // the consumer takes the 8-phase kernel
+      if (!dup_on) return false;
+      GemmArgs t = sargs(a3, lda_rows, true, nullptr, nullptr, nullptr, nullptr, N, rows, N, K);
+      return gemm_8q_ok(t) != 0;
+    };
+    auto gemm3 = [&](int K, const uint16_t* w3, const float* c3, const float* b, float* out, int N, int epi,
+                     bool dup) -> int {
+      HIP_TRY(gemm_bf16(sargs(a3, 1, dup, w3, c3, b, out, N, Mr, N, K), epi, s));
       return MI_OK;
     };
     for (size_t li = 0; li < layers.size(); ++li) {
       const Layer& L = layers[li];
       Mr = M;
       const bool cls = xpost && li + 1 == layers.size() && !causal && B >= 256 && S > 1 && cls_last();
-      HIP_TRY(layernorm_split2h(c->x, W, L.ln1_g, L.ln1_b, M, W, a3, rsc, s));
+      // ln_1's operand feeds in_proj (every row; in the CLS-row last block K / V for every row and Q
+      // for the CLS rows, read with a row stride of S)
+      const bool d1 = (dmask & 1) && (cls ? dup_ok(M, 2 * W, W) && dup_ok(B, W, W, S) : dup_ok(M, 3 * W, W));
+      HIP_TRY(layernorm_split2h(c->x, W, L.ln1_g, L.ln1_b, M, W, a3, rsc, s, nullptr, d1));
       if (cls) {   // K and V for every row, Q for the CLS rows only (as run_tower_fold's last block)
-        GemmArgs kv = gargs(a3, 3 * W, L.h3_qkv + (size_t)W * 3 * W, 3 * W, L.b_qkv + W, qkv + W, 3 * W, M, 2 * W, 3 * W);
-        kv.a_f16 = 1;
-        kv.rsc = rsc;
-        kv.csc = L.c3_qkv + W;
+        GemmArgs kv = sargs(a3, 1, d1, L.h3_qkv + (size_t)W * 3 * W, L.c3_qkv + W, L.b_qkv + W, qkv + W, 3 * W, M, 2 * W, W);
         HIP_TRY(gemm_bf16(kv, EPI_F32, s));
         float* rsc_c = (float*)c->h;
         HIP_TRY(hipMemcpy2DAsync(rsc_c, 4, rsc, (size_t)S * 4, 4, B, hipMemcpyDeviceToDevice, s));
-        GemmArgs q = gargs(a3, (int64_t)S * 3 * W, L.h3_qkv, 3 * W, L.b_qkv, qkv, (int64_t)S * 3 * W, B, W, 3 * W);
-        q.a_f16 = 1;
+        GemmArgs q = sargs(a3, S, d1, L.h3_qkv, L.c3_qkv, L.b_qkv, qkv, (int64_t)S * 3 * W, B, W, W);
         q.rsc = rsc_c;
-        q.csc = L.c3_qkv;
         HIP_TRY(gemm_bf16(q, EPI_F32, s));
       } else {
-        MI_TRY(gemm3(W, L.h3_qkv, L.c3_qkv, L.b_qkv, qkv, 3 * W, EPI_F32));
+        MI_TRY(gemm3(W, L.h3_qkv, L.c3_qkv, L.b_qkv, qkv, 3 * W, EPI_F32, d1));
       }
       HIP_TRY(attention_f32(qkv, att, B, S, W, causal, s));
       float* xr = c->x;
@@ -1097,30 +1115,31 @@ static int run_tower_f32(mi_clip* c, const std::vector<Layer>& layers, int B, in
         *xpost = x_c;
         *post_stride = 1;
       }
-      HIP_TRY(split2h_rows(ar, W, Mr, W, 0, 0, a3, rsc, s));
-      MI_TRY(gemm3(W, L.h3_out, L.c3_out, L.b_out, xr, W, EPI_RESID_F32));
+      const bool da = (dmask & 2) && dup_ok(Mr, W, W);          // attention's split -> out_proj
+      const bool df = (dmask & 4) && dup_ok(Mr, 4 * W, W);      // ln_2's split -> c_fc
+      const bool dp = (dmask & 8) && dup_ok(Mr, W, 4 * W);      // c_fc's output split -> c_proj
+      HIP_TRY(split2h_rows(ar, W, Mr, W, da ? 2 : 0, 0, a3, rsc, s));
+      MI_TRY(gemm3(W, L.h3_out, L.c3_out, L.b_out, xr, W, EPI_RESID_F32, da));
       if (fuse_split) {   // c_fc's epilogue writes c_proj's split operand (EPI_SPLIT_GELU)
-        HIP_TRY(layernorm_split2h(xr, W, L.ln2_g, L.ln2_b, Mr, W, a3, rsc, s, rmax));
-        GemmArgs g = gargs(a3, 3 * W, L.h3_fc, 3 * W, L.b_fc, a3o, 3 * 4 * W, Mr, 4 * W, 3 * W);
-        g.a_f16 = 1;
-        g.rsc = rsc;
-        g.csc = L.c3_fc;
+        HIP_TRY(layernorm_split2h(xr, W, L.ln2_g, L.ln2_b, Mr, W, a3, rsc, s, rmax, df));
+        GemmArgs g = sargs(a3, 1, df, L.h3_fc, L.c3_fc, L.b_fc, nullptr, 0, Mr, 4 * W, W);
+        g.out = a3o;
+        g.ldo = (dp ? 2 : 3) * 4 * W;
+        g.o_dup = dp ? 1 : 0;
         g.rmax = rmax;
         g.bnd_w = L.fc_bw;
         g.bnd_b = L.fc_bb;
         g.rsc_out = rsc_o;
         HIP_TRY(gemm_bf16(g, EPI_SPLIT_GELU, s));
-        GemmArgs p = gargs(a3o, 3 * 4 * W, L.h3_proj, 3 * 4 * W, L.b_proj, xr, W, Mr, W, 3 * 4 * W);
-        p.a_f16 = 1;
+        GemmArgs p = sargs(a3o, 1, dp, L.h3_proj, L.c3_proj, L.b_proj, xr, W, Mr, W, 4 * W);
         p.rsc = rsc_o;
-        p.csc = L.c3_proj;
         HIP_TRY(gemm_bf16(p, EPI_RESID_F32, s));
         continue;
       }
-      HIP_TRY(layernorm_split2h(xr, W, L.ln2_g, L.ln2_b, Mr, W, a3, rsc, s));
-      MI_TRY(gemm3(W, L.h3_fc, L.c3_fc, L.b_fc, mlp, 4 * W, EPI_F32));   // pre-activation
-      HIP_TRY(split2h_rows(mlp, 4 * W, Mr, 4 * W, 0, 1, a3, rsc, s));      // QuickGELU, then split
-      MI_TRY(gemm3(4 * W, L.h3_proj, L.c3_proj, L.b_proj, xr, W, EPI_RESID_F32));
+      HIP_TRY(layernorm_split2h(xr, W, L.ln2_g, L.ln2_b, Mr, W, a3, rsc, s, nullptr, df));
+      MI_TRY(gemm3(W, L.h3_fc, L.c3_fc, L.b_fc, mlp, 4 * W, EPI_F32, df));   // pre-activation
+      HIP_TRY(split2h_rows(mlp, 4 * W, Mr, 4 * W, dp ? 2 : 0, 1, a3, rsc, s));   // QuickGELU, then split
+      MI_TRY(gemm3(4 * W, L.h3_proj, L.c3_proj, L.b_proj, xr, W, EPI_RESID_F32, dp));
     }
     return MI_OK;
   }
@@ -1517,7 +1536,8 @@ int mi_clip_kernel_times(mi_clip* c, float* us, int32_t n) {
 
 int mi_op_split2h(const float* x, int64_t ldx, int64_t rows, int32_t K, int32_t role, int32_t gelu, void* out,
                   float* scale, void* stream) {
-  if (!x || !out || !scale || rows < 0 || (role & ~1) || (gelu & ~1)) return fail(MI_ERR_ARG, "mi_op_split2h: bad arguments");
+  if (!x || !out || !scale || rows < 0 || role < 0 || role > 2 || (gelu & ~1))
+    return fail(MI_ERR_ARG, "mi_op_split2h: bad arguments");
   if (K < 4 || K > 4096 || K % 4 || ldx < K || ldx % 4)
     return fail(MI_ERR_UNSUPPORTED, "mi_op_split2h: 4 <= K <= 4096, K %% 4 == 0, ldx >= K, ldx %% 4 == 0");
   HIP_TRY(split2h_rows(x, ldx, rows, K, role, gelu, (uint16_t*)out, scale, (hipStream_t)stream));
@@ -1526,14 +1546,19 @@ int mi_op_split2h(const float* x, int64_t ldx, int64_t rows, int32_t K, int32_t 
 
 int mi_op_gemm_split2h(const void* A3, const void* W3, const float* a_scale, const float* w_scale, const float* bias,
                        float* out, int32_t M, int32_t N, int32_t K3, int32_t epi, void* stream) {
+  const int dup = (epi >> 8) & 1;
+  epi &= ~0x100;
   if (!A3 || !W3 || !a_scale || !w_scale || !out || M < 0 || N < 1 || K3 < 1 || (epi != EPI_F32 && epi != EPI_RESID_F32))
     return fail(MI_ERR_ARG, "mi_op_gemm_split2h: bad arguments");
   if (N % 128 || K3 % 32) return fail(MI_ERR_UNSUPPORTED, "mi_op_gemm_split2h: N %% 128 == 0, K3 %% 32 == 0");
-  GemmArgs g = gargs((const uint16_t*)A3, K3, (const uint16_t*)W3, K3, bias, out, N, M, N, K3);
+  GemmArgs g = gargs((const uint16_t*)A3, dup ? 2 * (K3 / 3) : K3, (const uint16_t*)W3, K3, bias, out, N, M, N, K3);
   g.variant = 0;
   g.a_f16 = 1;
   g.rsc = a_scale;
   g.csc = w_scale;
+  g.a_dup = dup ? K3 / 3 : 0;
+  if (dup && (K3 % 3 || !gemm_8q_ok(g)))
+    return fail(MI_ERR_UNSUPPORTED, "mi_op_gemm_split2h: the [x1 x2] layout needs M >= 256, N %% 256 == 0, K %% 64 == 0");
   HIP_TRY(gemm_bf16(g, epi, (hipStream_t)stream));
   return MI_OK;
 }

@@ -1124,18 +1124,22 @@ hipError_t launch(const GemmArgs& a, hipStream_t s) {
   if (a.a_f16) {   // split-f16 operands (fp32 tower): f32 epilogues with the rsc / csc factors
     if ((EPI != EPI_F32 && EPI != EPI_RESID_F32 && EPI != EPI_SPLIT_GELU) || !a.rsc || !a.csc || a.variant)
       return hipErrorInvalidValue;
-    if (EPI == EPI_SPLIT_GELU && (!a.rmax || !a.rsc_out || a.group || a.ldo != 3 * (int64_t)a.N))
+    if (EPI == EPI_SPLIT_GELU && (!a.rmax || !a.rsc_out || a.group || a.ldo != (a.o_dup ? 2 : 3) * (int64_t)a.N))
       return hipErrorInvalidValue;
     if constexpr (EPI == EPI_F32 || EPI == EPI_RESID_F32 || EPI == EPI_SPLIT_GELU) {
       // the 8-phase kernel (gemm_8q.hip) wherever it applies; MICLIP_F32_8Q=0 (A/B build) keeps the
       // ping-pong kernel below
 #if MICLIP_AB
+      // (MICLIP_F32_8Q=1 + MICLIP_F32_8Q_MASK: 1 EPI_F32, 2 EPI_RESID_F32, 4 EPI_SPLIT_GELU on the 8-phase kernel)
       const char* e8 = std::getenv("MICLIP_F32_8Q");
-      const bool use8q = !e8 || std::atoi(e8) != 0;
+      const char* em = std::getenv("MICLIP_F32_8Q_MASK");
+      const int bit = EPI == EPI_F32 ? 1 : (EPI == EPI_RESID_F32 ? 2 : 4);
+      const bool use8q = (!e8 || std::atoi(e8) != 0) && (!em || (std::atoi(em) & bit));
 #else
       const bool use8q = true;
 #endif
       if (use8q && gemm_8q_ok(a)) return gemm_8q(a, EPI, s, cu_count(), 0);
+      if (a.a_dup || a.o_dup) return hipErrorInvalidValue;   // the [x1 | x2] layouts: the 8-phase kernel only
       const int ntf = ((a.M + 255) / 256) * (a.N / 256);
       if (big && a.K / BK >= LEAD) {
         hipLaunchKernelGGL((gemm_pp_kernel<EPI, 1, false, false, false, false, true>), dim3(ntf), dim3(512), 0, s, a);

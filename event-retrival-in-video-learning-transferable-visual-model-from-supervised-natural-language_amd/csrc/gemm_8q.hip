@@ -82,6 +82,10 @@ constexpr int F_GPK = 256;  // QuickGELU's "+ 1" as packed adds (v_pk_add_f32: 5
 // later, so the two waves of each SIMD issue their epilogue VALU concurrently (two waves: 2x the
 // plain-VALU and 1.37x the transcendental issue rate of one, scripts/probes/valu_rate.hip)
 constexpr int F_BEARLY = 512;
+// F_ODUP (EPI_SPLIT_GELU): the output split stored once, [y1 | y2] (GemmArgs o_dup).  A compile-time
+// flag: the same choice as a runtime branch around the second y1 store made the in-loop epilogues of
+// large grids produce non-finite rows at random (measured, scripts/gpu_r5zq.sh)
+constexpr int F_ODUP = 1024;
 
 __device__ __forceinline__ f32x2 quick_gelu2_8q(f32x2 v) {
   const f32x2 t = v * (f32x2){-2.45546696f, -2.45546696f};   // -1.702 * log2(e)
@@ -254,8 +258,10 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
         }
         glds16(src, dst + j * 1024);
       } else if (h == H_A0 || h == H_A1) {
+        // (a_dup: the split operand's [x1 | x2] read as [x1 | x1 | x2]: K-tiles past a_dup from k - a_dup)
+        const int ka = (a.a_dup && kofs >= a.a_dup) ? kofs - a.a_dup : kofs;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (LDS_AS void*)(dst + j * 1024), 16, h == H_A1 ? voA1[j] : voA0[j],
-                                                 kofs * 2, 0, (F & F_ANT) ? 2 : 0);
+                                                 ka * 2, 0, (F & F_ANT) ? 2 : 0);
       } else {
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rsW, (LDS_AS void*)(dst + j * 1024), 16, voB[j],
                                                  kofs * 2 + (h == H_B1 ? b1_sofs : 0), 0, 0);
@@ -468,7 +474,8 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
           (void*)((uint16_t*)a.out + (int64_t)pm0 * a.ldo + pn0), (short)0, rows * (int)a.ldo * 2, 0x00020000);
       const uint32_t vo = (uint32_t)(((wr * 128 + lr) * (int)a.ldo + wc * 64 + (lg & 1) * 16 + (lg >> 1) * 8) * 2);
       const uint32_t blk = (uint32_t)(16 * a.ldo * 2);
-      const int n2 = a.N * 2, n4 = a.N * 4;   // byte offsets of the second and third copies (soffset)
+      // byte offsets of the second and third column blocks (soffset); F_ODUP: [y1 | y2] only
+      const int n2 = a.N * 2, n4 = (F & F_ODUP) ? a.N * 2 : a.N * 4;
       const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.rsc_out + pm0), (short)0, rows * 4, 0x00020000);
       // one writer per row (the n = 0 tile's columns 0-3); other lanes store out of range (dropped)
       const uint32_t vr = (pn0 == 0 && wc == 0 && lg == 0) ? (uint32_t)((wr * 128 + lr) * 4) : 0x7ff00000u;
@@ -502,7 +509,7 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
           const auto by = __builtin_amdgcn_permlane16_swap(k2[0].y, k2[1].y, false, false);
           const u32x4_8q d1 = {ax[0], ay[0], ax[1], ay[1]}, d2 = {bx[0], by[0], bx[1], by[1]};
           __builtin_amdgcn_raw_buffer_store_b128(d1, ro, vo + mi * blk + p * 64, 0, 0);
-          __builtin_amdgcn_raw_buffer_store_b128(d1, ro, vo + mi * blk + p * 64, n2, 0);
+          if constexpr (!(F & F_ODUP)) __builtin_amdgcn_raw_buffer_store_b128(d1, ro, vo + mi * blk + p * 64, n2, 0);
           __builtin_amdgcn_raw_buffer_store_b128(d2, ro, vo + mi * blk + p * 64, n4, 0);
         }
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(ldexpf(1.f, -e)), rr, vr + mi * 64, 0, 0);
@@ -767,8 +774,8 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
       // (EPI_RES16: 16 stores, 8 partial stores and the x16 loads of blocks 4-7 are younger;
       // the epilogue's wait for block 7 already retired the odd buffer)
       // (SPL: the epilogue's VMEM ops per wave -- F32 32 stores, RESID 32 loads + 32 stores, SPLIT
-      // 48 + 8 stores -- are younger; vmcnt holds at most 63)
-      constexpr int SPL_VM = EPI == EPI_F32 ? 36 : (EPI == EPI_RESID_F32 ? 63 : 60);
+      // 48 + 8 stores, 32 + 8 with o_dup -- are younger; vmcnt holds at most 63)
+      constexpr int SPL_VM = EPI == EPI_F32 ? 36 : (EPI == EPI_RESID_F32 ? 63 : ((F & F_ODUP) ? 44 : 60));
       if (EK::SPL && FIRST && has_prev && !((F & F_BEARLY) && wr == 1))
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SPL_VM) : "memory");
       else if (FIRST && has_prev && EK::RES && !((F & F_BEARLY) && wr == 1))
@@ -905,6 +912,7 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
 int gemm_8q_ok(const GemmArgs& a) {
   // descriptors: a tile's rows x row bytes must fit num_records (int)
   return a.N % BN == 0 && a.K % (2 * BK8) == 0 && a.K >= 4 * BK8 && a.M >= BM && !a.group && !a.patch_R &&
+         (!a.a_dup || (a.a_f16 && a.a_dup % BK8 == 0 && a.K == 3 * a.a_dup && a.lda >= 2 * (int64_t)a.a_dup)) &&
          (int64_t)BM * a.lda * 2 < (1LL << 31) && (int64_t)BN * a.ldw * 2 < (1LL << 31) &&
          (int64_t)(BM + 64) * a.lda * 2 < (1LL << 32);
 }
@@ -1010,17 +1018,20 @@ hipError_t gemm_8q(const GemmArgs& a0, int epi, hipStream_t s, int cus, int mode
   if (epi == EPI_F32 || epi == EPI_RESID_F32 || epi == EPI_SPLIT_GELU) {
     if (!a.a_f16 || !a.rsc || !a.csc || mode || a.group || (a.ldo % 4) || (int64_t)BM * a.ldo * 4 >= (1LL << 31))
       return hipErrorInvalidValue;
-    if (epi == EPI_SPLIT_GELU && (!a.rmax || !a.rsc_out || a.ldo != 3 * (int64_t)a.N)) return hipErrorInvalidValue;
+    if (epi == EPI_SPLIT_GELU && (!a.rmax || !a.rsc_out || a.ldo != (a.o_dup ? 2 : 3) * (int64_t)a.N))
+      return hipErrorInvalidValue;
 #if MICLIP_AB   // A/B (MICLIP_F32_8Q=2): the lagging M-group's epilogue beside the leading one's (F_BEARLY)
     const char* fv = std::getenv("MICLIP_F32_8Q");
-    if (fv && std::atoi(fv) == 2) {
+    if (fv && std::atoi(fv) == 2 && !a.o_dup) {
       if (epi == EPI_SPLIT_GELU) hipLaunchKernelGGL((gemm_8q_kernel<EPI_SPLIT_GELU, 0, F_BEARLY, true>), dim3(grid), dim3(512), 0, s, a);
       else if (epi == EPI_RESID_F32) hipLaunchKernelGGL((gemm_8q_kernel<EPI_RESID_F32, 0, F_BEARLY, true>), dim3(grid), dim3(512), 0, s, a);
       else hipLaunchKernelGGL((gemm_8q_kernel<EPI_F32, 0, F_BEARLY, true>), dim3(grid), dim3(512), 0, s, a);
       return hipGetLastError();
     }
 #endif
-    if (epi == EPI_SPLIT_GELU) {
+    if (epi == EPI_SPLIT_GELU && a.o_dup) {
+      hipLaunchKernelGGL((gemm_8q_kernel<EPI_SPLIT_GELU, 0, F_ODUP, true>), dim3(grid), dim3(512), 0, s, a);
+    } else if (epi == EPI_SPLIT_GELU) {
       hipLaunchKernelGGL((gemm_8q_kernel<EPI_SPLIT_GELU, 0, 0, true>), dim3(grid), dim3(512), 0, s, a);
     } else if (epi == EPI_RESID_F32) {
       hipLaunchKernelGGL((gemm_8q_kernel<EPI_RESID_F32, 0, 0, true>), dim3(grid), dim3(512), 0, s, a);

@@ -92,6 +92,11 @@ struct GemmArgs {
   const float* rmax = nullptr;
   float bnd_w = 0.f, bnd_b = 0.f;
   float* rsc_out = nullptr;
+  // split-f16 A operand stored once as [x1 | x2] (2 a_dup wide) for the logical [x1 | x1 | x2]
+  // (K = 3 a_dup): K-tiles at k >= a_dup read from k - a_dup (gemm_8q only); 0 = the full layout
+  int a_dup = 0;
+  // EPI_SPLIT_GELU output in that layout ([y1 | y2], ldo = 2N; gemm_8q only)
+  int o_dup = 0;
 };
 
 // Requirements: K % 64 == 0, N % 128 == 0, A/W 16-byte aligned rows.
@@ -210,12 +215,15 @@ hipError_t split6_rows(const float* x, int64_t ldx, int64_t rows, int K, int rol
 // activations) or [x1 x2 x1] (role 1, weights), x1 = f16(x s), x2 = f16(x s - x1), and
 // sc[r] = 1 / s_r; ONE f16 GEMM over K' = 3K with epilogue factor rsc[m] * csc[n] (GemmArgs)
 // then gives a1 w1 + a1 w2 + a2 w1 in f32: every term to 2^-22 relative.  K % 4 == 0, K <= 4096.
+// role 2: activations stored once, [x1 x2] (row stride 2K), for the 8-phase GEMM's A_DUP read of
+// the logical [x1 x1 x2] (GemmArgs a_dup).
 hipError_t split2h_rows(const float* x, int64_t ldx, int64_t rows, int K, int role, int gelu, uint16_t* out,
                         float* sc, hipStream_t s);
 // LayerNorm (f32 statistics) written directly as the split-f16 operand (role 0) + its row scales
 // rmax (nullable): the row's max |LN(x)| (EPI_SPLIT_GELU's bound)
+// (dup: the [x1 x2] layout of role 2)
 hipError_t layernorm_split2h(const float* x, int64_t in_stride, const float* g, const float* b, int rows, int W,
-                             uint16_t* out, float* sc, hipStream_t s, float* rmax = nullptr);
+                             uint16_t* out, float* sc, hipStream_t s, float* rmax = nullptr, int dup = 0);
 
 }  // namespace miclip
 

@@ -202,8 +202,9 @@ __device__ __forceinline__ float absmax4(float m, float4 v) {
 
 typedef _Float16 f16x4_p __attribute__((ext_vector_type(4)));
 
-// the lane's 4 values (columns c..c+3) of a row scaled by 2^e into the three K-blocks of out
-// (row stride 3K): role 0 [x1 | x1 | x2], role 1 [x1 | x2 | x1]
+// the lane's 4 values (columns c..c+3) of a row scaled by 2^e into the K-blocks of out: role 0
+// [x1 | x1 | x2], role 1 [x1 | x2 | x1] (row stride 3K), role 2 [x1 | x2] (row stride 2K: the
+// activations once, read as [x1 | x1 | x2] by the 8-phase GEMM, GemmArgs a_dup)
 __device__ __forceinline__ void store_split4(float4 v, int e, int role, _Float16* o, int K, int c) {
   _Float16 a0, a1, a2, a3, b0, b1, b2, b3;
   split2h(ldexpf(v.x, e), a0, b0);
@@ -212,6 +213,10 @@ __device__ __forceinline__ void store_split4(float4 v, int e, int role, _Float16
   split2h(ldexpf(v.w, e), a3, b3);
   const f16x4_p h1 = {a0, a1, a2, a3}, h2 = {b0, b1, b2, b3};
   *(f16x4_p*)(o + c) = h1;
+  if (role == 2) {
+    *(f16x4_p*)(o + K + c) = h2;
+    return;
+  }
   *(f16x4_p*)(o + K + c) = role ? h2 : h1;
   *(f16x4_p*)(o + 2 * K + c) = role ? h1 : h2;
 }
@@ -238,7 +243,7 @@ __global__ __launch_bounds__(256) void split2h_kernel(const float* __restrict__ 
   }
   const int e = split_exp(wave_max(mx));
   if (lane == 0) sc[row] = ldexpf(1.f, -e);
-  _Float16* o = out + row * 3 * (int64_t)K;
+  _Float16* o = out + row * (role == 2 ? 2 : 3) * (int64_t)K;
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int c = 4 * lane + 256 * i;
@@ -251,7 +256,7 @@ __global__ __launch_bounds__(256) void split2h_kernel(const float* __restrict__ 
 __global__ __launch_bounds__(256) void ln_split2h_kernel(const float* __restrict__ x, int64_t in_stride,
                                                          const float* __restrict__ g, const float* __restrict__ b,
                                                          int rows, int W, _Float16* __restrict__ out,
-                                                         float* __restrict__ sc, float* __restrict__ rmax) {
+                                                         float* __restrict__ sc, float* __restrict__ rmax, int dup) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= rows) return;
   const float* xr = x + (int64_t)row * in_stride;
@@ -291,11 +296,11 @@ __global__ __launch_bounds__(256) void ln_split2h_kernel(const float* __restrict
     sc[row] = ldexpf(1.f, -e);
     if (rmax) rmax[row] = rm;
   }
-  _Float16* o = out + (int64_t)row * 3 * W;
+  _Float16* o = out + (int64_t)row * (dup ? 2 : 3) * W;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int c = 4 * lane + 256 * i;
-    if (c < W) store_split4(v[i], e, 0, o, W, c);
+    if (c < W) store_split4(v[i], e, dup ? 2 : 0, o, W, c);
   }
 }
 
@@ -610,11 +615,11 @@ hipError_t split2h_rows(const float* x, int64_t ldx, int64_t rows, int K, int ro
 }
 
 hipError_t layernorm_split2h(const float* x, int64_t in_stride, const float* g, const float* b, int rows, int W,
-                             uint16_t* out, float* sc, hipStream_t s, float* rmax) {
+                             uint16_t* out, float* sc, hipStream_t s, float* rmax, int dup) {
   if (rows <= 0) return hipSuccess;
   if (W > 1024 || W < 4 || W % 4 || in_stride % 4) return hipErrorInvalidValue;
   hipLaunchKernelGGL(ln_split2h_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, x, in_stride, g, b, rows, W,
-                     (_Float16*)out, sc, rmax);
+                     (_Float16*)out, sc, rmax, dup ? 1 : 0);
   return hipGetLastError();
 }
 

@@ -344,12 +344,15 @@ int mi_op_split6(const float* x, int64_t ldx, int64_t rows, int32_t K, int32_t r
  *   non-finite row; the exponent clamped to [-126, 126]) and split as x s = x1 + x2 + O(2^-22
  *   |x s|), x1 = f16(x s), x2 = f16(x s - x1) (round to nearest even; x2 = 0 where x1 is not
  *   finite); out[r] = 3K fp16 in three K-blocks, role 0 (activations) [x1 x1 x2], role 1
- *   (weights [N][K]) [x1 x2 x1]; scale[r] = 1 / s_r.  gelu 1 applies QuickGELU first (as
- *   mi_op_split6).  K % 4 == 0, 4 <= K <= 4096, ldx % 4 == 0.
+ *   (weights [N][K]) [x1 x2 x1]; role 2 (activations stored once, 2K fp16 per row) [x1 x2];
+ *   scale[r] = 1 / s_r.  gelu 1 applies QuickGELU first (as mi_op_split6).  K % 4 == 0,
+ *   4 <= K <= 4096, ldx % 4 == 0.
  * mi_op_gemm_split2h: out f32 [M,N] (epi 3) or out += (epi 2) of
  *   (A3 . W3^T) * a_scale[m] * w_scale[n] + bias[n], with A3 [M][K3] / W3 [N][K3] the fp16
  *   operands above (K3 = 3K) on the f16 MFMA with f32 accumulation: a1 w1 + a1 w2 + a2 w1, an
- *   f32-grade product.  N % 128 == 0, K3 % 32 == 0.
+ *   f32-grade product.  N % 128 == 0, K3 % 32 == 0.  epi | 0x100: A3 is the role-2 layout
+ *   [M][2K] (the 8-phase kernel reads it as [x1 x1 x2]; needs M >= 256, N % 256 == 0,
+ *   K % 64 == 0).
  * mi_op_attention_f32: f32 MHA core of the fp32 tower: qkv f32 [B*S, 3W] (q | k | v, head dim
  *   64) -> out f32 [B*S, W], softmax(q k^T / 8 (+ causal mask)) v per (sequence, head); S <= 128
  *   on the exact-f32 MFMA, longer sequences on a per-row f32 kernel. */

@@ -747,6 +747,39 @@ def test_attention_f32_descriptor_form_bit_identical(gpu, monkeypatch, B, S, W, 
     assert torch.isnan(outs[0][B * S:]).all()
 
 
+@pytest.mark.parametrize("M,N,K,epi", [(3000, 768, 3072, 2), (1023, 2304, 768, 3), (256, 256, 512, 3),
+                                       (30000, 768, 768, 2), (30000, 3072, 768, 3)])
+def test_split2h_dedup_layout_bit_identical(gpu, M, N, K, epi):
+    """The activations' split stored once (mi_op_split2h role 2, [x1 x2]) and read by the
+    8-phase GEMM as [x1 x1 x2] (mi_op_gemm_split2h epi | 0x100) give the full layout's results
+    bit for bit; the role-2 rows are the role-0 rows without the repeated x1 block."""
+    import torch
+    N_ = _lib()
+    g = torch.Generator(device="cpu").manual_seed(M + 3 * N + K)
+    A = (torch.randn(M, K, generator=g) * torch.exp(torch.empty(M, 1).uniform_(-9, 9, generator=g))).to(gpu)
+    W = (torch.randn(N, K, generator=g) * K ** -0.5).to(gpu)
+    bias = torch.randn(N, generator=g).to(gpu)
+    base = torch.randn(M, N, generator=g).to(gpu)
+    L = N_.lib()
+    A3 = torch.empty(M, 3 * K, dtype=torch.int16, device=gpu)
+    A2 = torch.empty(M, 2 * K, dtype=torch.int16, device=gpu)
+    W3 = torch.empty(N, 3 * K, dtype=torch.int16, device=gpu)
+    sa, sa2, sw = torch.empty(M, device=gpu), torch.empty(M, device=gpu), torch.empty(N, device=gpu)
+    N_.check(L.mi_op_split2h(A.data_ptr(), K, M, K, 0, 0, A3.data_ptr(), sa.data_ptr(), _stream()), "split2h A")
+    N_.check(L.mi_op_split2h(A.data_ptr(), K, M, K, 2, 0, A2.data_ptr(), sa2.data_ptr(), _stream()), "split2h A dedup")
+    N_.check(L.mi_op_split2h(W.data_ptr(), K, N, K, 1, 0, W3.data_ptr(), sw.data_ptr(), _stream()), "split2h W")
+    torch.cuda.synchronize()
+    assert torch.equal(A2[:, :K], A3[:, :K]) and torch.equal(A2[:, K:], A3[:, 2 * K:]) and torch.equal(sa, sa2)
+    outs = []
+    for a, flag in ((A3, 0), (A2, 0x100)):
+        out = base.clone() if epi == 2 else torch.full((M, N), float("nan"), device=gpu)
+        N_.check(L.mi_op_gemm_split2h(a.data_ptr(), W3.data_ptr(), sa.data_ptr(), sw.data_ptr(), bias.data_ptr(),
+                                      out.data_ptr(), M, N, 3 * K, epi | flag, _stream()), "gemm_split2h")
+        outs.append(out)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))
+
+
 def _attn_ref(qkv, B, S, W, causal):
     H = W // 64
     x = qkv.reshape(B, S, 3, H, 64).astype(np.float64)

@@ -111,12 +111,14 @@ def test_fp32_tower_vs_oracle(gpu, name):
     np.testing.assert_allclose(g, img / np.linalg.norm(img, axis=1, keepdims=True), rtol=0, atol=1e-6)
 
 
-@pytest.mark.parametrize("name,n", [("ViT-B/32", 8), ("ViT-B/32", 13), ("test-small", 40)])
+@pytest.mark.parametrize("name,n", [("ViT-B/32", 8), ("ViT-B/32", 13), ("test-small", 40), ("ViT-B/32", 300)])
 def test_fp32_tower_8phase_bit_identical(gpu, monkeypatch, name, n):
     """The fp32 tower's split-f16 GEMMs on the 8-phase kernel (in_proj EPI_F32, out_proj / c_proj
-    EPI_RESID_F32, c_fc EPI_SPLIT_GELU writing c_proj's operand; the default for >= 256 rows)
-    against the ping-pong kernel (A/B build, MICLIP_F32_8Q=0): image and text embeddings bit for
-    bit (whole and partial 256-row tiles), and within f32 rounding of the float64 oracle."""
+    EPI_RESID_F32, c_fc EPI_SPLIT_GELU writing c_proj's operand; the default for >= 256 rows),
+    with the activations' split stored once and (>= 256 frames) the CLS-row last block, against
+    the ping-pong kernel over the full layout and the full last block (A/B build, MICLIP_F32_8Q=0,
+    MICLIP_CLS_LAST=0): image and text embeddings finite and bit for bit (whole and partial
+    256-row tiles), and within f32 rounding of the float64 oracle."""
     import torch
     from miclip import _native, config, model as M, weights
     from oracle import clip_ref
@@ -126,8 +128,12 @@ def test_fp32_tower_8phase_bit_identical(gpu, monkeypatch, name, n):
     tk = torch.from_numpy(weights.synthetic_tokens(n, cfg.context_length, cfg.vocab_size, seed=n))
     m = M.CLIP(cfg, sd, device=gpu, weights="fp32", image_chunk=n, text_chunk=n)
     img, txt = m.encode_image(px).cpu().numpy(), m.encode_text(tk).cpu().numpy()
+    # (300 frames: 15000 rows, several tiles per workgroup, so the epilogues run inside the tile loop;
+    # also the CLS-row last block and the stored-once split operands against the full pass)
+    assert np.isfinite(img).all() and np.isfinite(txt).all()
     monkeypatch.setattr(_native, "lib", _native.lib_ab)
     monkeypatch.setenv("MICLIP_F32_8Q", "0")
+    monkeypatch.setenv("MICLIP_CLS_LAST", "0")
     m0 = M.CLIP(cfg, sd, device=gpu, weights="fp32", image_chunk=n, text_chunk=n)
     img0, txt0 = m0.encode_image(px).cpu().numpy(), m0.encode_text(tk).cpu().numpy()
     del m0
