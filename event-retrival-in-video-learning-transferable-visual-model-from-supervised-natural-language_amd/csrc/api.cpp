@@ -1557,7 +1557,7 @@ int mi_op_gemm_split2h(const void* A3, const void* W3, const float* a_scale, con
   g.rsc = a_scale;
   g.csc = w_scale;
   g.a_dup = dup ? K3 / 3 : 0;
-  if (dup && (K3 % 3 || !gemm_8q_ok(g)))
+  if (dup && (K3 % 3 || !bias || !gemm_8q_ok(g)))
     return fail(MI_ERR_UNSUPPORTED, "mi_op_gemm_split2h: the [x1 x2] layout needs M >= 256, N %% 256 == 0, K %% 64 == 0");
   HIP_TRY(gemm_bf16(g, epi, (hipStream_t)stream));
   return MI_OK;

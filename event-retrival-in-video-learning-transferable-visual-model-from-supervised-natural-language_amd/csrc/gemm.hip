@@ -1138,7 +1138,8 @@ hipError_t launch(const GemmArgs& a, hipStream_t s) {
 #else
       const bool use8q = true;
 #endif
-      if (use8q && gemm_8q_ok(a)) return gemm_8q(a, EPI, s, cu_count(), 0);
+      // (the 8-phase kernel's f32 epilogues assume a bias: bias-less calls take the ping-pong kernel)
+      if (use8q && a.bias && gemm_8q_ok(a)) return gemm_8q(a, EPI, s, cu_count(), 0);
       if (a.a_dup || a.o_dup) return hipErrorInvalidValue;   // the [x1 | x2] layouts: the 8-phase kernel only
       const int ntf = ((a.M + 255) / 256) * (a.N / 256);
       if (big && a.K / BK >= LEAD) {

@@ -413,14 +413,11 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
     asm volatile("ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:64\n\tds_read_b128 %2, %4 offset:128\n\t"
                  "ds_read_b128 %3, %4 offset:192\n\ts_waitcnt lgkmcnt(0)"
                  : "=&v"(cs[0]), "=&v"(cs[1]), "=&v"(cs[2]), "=&v"(cs[3]) : "v"(ca) : "memory");
-    if (a.bias) {
+    {   // (SPL launches carry a bias, gemm_8q host: no runtime branch inside the epilogue, see F_ODUP)
       const uint32_t ba = (uint32_t)(uintptr_t)(const LDS_AS float*)(sbias + ppar * BN + wc * 64 + 4 * lg);
       asm volatile("ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:64\n\tds_read_b128 %2, %4 offset:128\n\t"
                    "ds_read_b128 %3, %4 offset:192\n\ts_waitcnt lgkmcnt(0)"
                    : "=&v"(bias[0]), "=&v"(bias[1]), "=&v"(bias[2]), "=&v"(bias[3]) : "v"(ba) : "memory");
-    } else {
-#pragma unroll
-      for (int ni = 0; ni < 4; ++ni) bias[ni] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
     // the lane's 8 rows' rsc (and rmax for the split's bound), one row per 16-row block
     float rsv[8], rmv[8];
@@ -1016,7 +1013,7 @@ hipError_t gemm_8q(const GemmArgs& a0, int epi, hipStream_t s, int cus, int mode
   }
   // the fp32 tower's split-f16 GEMMs (K' = 3K; gemm.hip launch checks the vectors)
   if (epi == EPI_F32 || epi == EPI_RESID_F32 || epi == EPI_SPLIT_GELU) {
-    if (!a.a_f16 || !a.rsc || !a.csc || mode || a.group || (a.ldo % 4) || (int64_t)BM * a.ldo * 4 >= (1LL << 31))
+    if (!a.a_f16 || !a.rsc || !a.csc || !a.bias || mode || a.group || (a.ldo % 4) || (int64_t)BM * a.ldo * 4 >= (1LL << 31))
       return hipErrorInvalidValue;
     if (epi == EPI_SPLIT_GELU && (!a.rmax || !a.rsc_out || a.ldo != (a.o_dup ? 2 : 3) * (int64_t)a.N))
       return hipErrorInvalidValue;

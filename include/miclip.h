@@ -351,8 +351,8 @@ int mi_op_split6(const float* x, int64_t ldx, int64_t rows, int32_t K, int32_t r
  *   (A3 . W3^T) * a_scale[m] * w_scale[n] + bias[n], with A3 [M][K3] / W3 [N][K3] the fp16
  *   operands above (K3 = 3K) on the f16 MFMA with f32 accumulation: a1 w1 + a1 w2 + a2 w1, an
  *   f32-grade product.  N % 128 == 0, K3 % 32 == 0.  epi | 0x100: A3 is the role-2 layout
- *   [M][2K] (the 8-phase kernel reads it as [x1 x1 x2]; needs M >= 256, N % 256 == 0,
- *   K % 64 == 0).
+ *   [M][2K] (the 8-phase kernel reads it as [x1 x1 x2]; needs a bias, M >= 256,
+ *   N % 256 == 0, K % 64 == 0).
  * mi_op_attention_f32: f32 MHA core of the fp32 tower: qkv f32 [B*S, 3W] (q | k | v, head dim
  *   64) -> out f32 [B*S, W], softmax(q k^T / 8 (+ causal mask)) v per (sequence, head); S <= 128
  *   on the exact-f32 MFMA, longer sequences on a per-row f32 kernel. */
