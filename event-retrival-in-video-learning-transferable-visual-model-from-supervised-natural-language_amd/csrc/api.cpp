@@ -920,7 +920,7 @@ static int run_tower_fold(mi_clip* c, const std::vector<Layer>& layers, int B, i
     } else {
       HIP_TRY(gemm_bf16(ln_args(c, L.lw_qkv, L.ls_qkv, L.lc_qkv, c->qkv, 3 * W, M, W), EPI_LN_BF16, s));
     }
-    HIP_TRY(attention(c->qkv, c->att, B, S, W, 0, s));
+    HIP_TRY(attention(c->qkv, c->att, B, S, W, cls ? 0x800 : 0, s));   // (cls: the CLS queries' tile only)
     if (cls) {
       MI_TRY(last_block_cls(c, L, B, S, W, xpost, s));
       *post_stride = 1;
@@ -1099,7 +1099,7 @@ static int run_tower_f32(mi_clip* c, const std::vector<Layer>& layers, int B, in
       } else {
         MI_TRY(gemm3(W, L.h3_qkv, L.c3_qkv, L.b_qkv, qkv, 3 * W, EPI_F32, d1));
       }
-      HIP_TRY(attention_f32(qkv, att, B, S, W, causal, s));
+      HIP_TRY(attention_f32(qkv, att, B, S, W, causal | (cls ? 0x800 : 0), s));   // (cls: the CLS queries' block)
       float* xr = c->x;
       const float* ar = att;
       if (cls) {

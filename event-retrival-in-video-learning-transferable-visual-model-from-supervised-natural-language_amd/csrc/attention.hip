@@ -169,6 +169,10 @@ __device__ __forceinline__ void attention_flash_body(const uint16_t* __restrict_
                                                      int S, int W, int H, int causal, uint8_t* __restrict__ q8,
                                                      uint8_t* __restrict__ qs, int64_t rows_pad, int items = 0) {
   static_assert(!PIPE || (NT == 1 && SLOTS == 1 && HP == 1), "PIPE: the single-chunk instance only");
+  // causal bit 11: the first 16-query tile only (the last vision block, whose outputs are read at the
+  // CLS rows alone, api.cpp last_block_cls); the other tiles' waves still stage K / V
+  const bool q0only = (causal >> 11) & 1;
+  causal &= 1;
   constexpr int KS = 72, VS = 68;  // LDS row strides (bf16)
   const int NW = PP == 1 ? 8 : (int)(blockDim.x >> 6) / HP;  // PP = 1 is launched with 8 waves
   __shared__ __attribute__((aligned(16))) uint16_t Ksh[HP][SLOTS][64 * KS];
@@ -187,7 +191,7 @@ __device__ __forceinline__ void attention_flash_body(const uint16_t* __restrict_
   const uint16_t* qb = qkv + (int64_t)bseq * S * ld + h * 64;
   const uint16_t* kb = qb + W;
   const uint16_t* vb = qb + 2 * W;
-  const int nch = (S + 63) / 64, nqt = (S + 15) / 16;
+  const int nch = (S + 63) / 64, nqt = q0only ? 1 : (S + 15) / 16;
   const int fr = lane & 15, g = lane >> 4, fk = 8 * g;
   const float sl2 = 0.125f * 1.4426950408889634f;  // head_dim^-0.5 * log2(e)
   constexpr float RESCALE = 8.0f;                  // lazy-rescale threshold (log2 units)
@@ -1149,6 +1153,7 @@ hipError_t attention(const uint16_t* qkv, uint16_t* out, int B, int S, int W, in
   constexpr bool one_wave = false;
 #endif
   const bool old_flash = (causal >> 9) & 1;   // A/B: the chunk-streaming flash kernel for S > 64
+  const int q0only = (causal >> 11) & 1;      // the first query tile only (S <= 64 kernel; others compute all)
   causal &= 1;
   const dim3 grid(items);
 #if MICLIP_AB
@@ -1276,7 +1281,8 @@ hipError_t attention(const uint16_t* qkv, uint16_t* out, int B, int S, int W, in
 #define FLASH(T) \
   hipLaunchKernelGGL((attention_flash_kernel<T, 1>), grid, dim3(512), 0, s, qkv, out, S, W, H, causal, q8, qs, rp)
   if (nqt <= 4)
-    hipLaunchKernelGGL((attention_flash_kernel<1, 2, 1>), grid, dim3(256), 0, s, qkv, out, S, W, H, causal, q8, qs, rp);
+    hipLaunchKernelGGL((attention_flash_kernel<1, 2, 1>), grid, dim3(256), 0, s, qkv, out, S, W, H, causal | (q0only << 11),
+                       q8, qs, rp);
   else if (nqt <= 8) FLASH(1);
   else if (nqt <= 16) FLASH(2);
   else if (nqt <= 24) FLASH(3);

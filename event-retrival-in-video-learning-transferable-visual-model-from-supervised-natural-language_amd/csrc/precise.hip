@@ -448,6 +448,9 @@ __global__ __launch_bounds__(256, MINB) void attn_f32_mfma_kernel(const float* _
   const int H = W / 64;
   const int item = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (item >= nseq * H) return;
+  // causal bit 11: the first 32-query block only (the last vision block: outputs read at the CLS rows)
+  const int qend = ((causal >> 11) & 1) ? min(S, 32) : S;
+  causal &= 1;
   const int bseq = item / H, head = item % H;
   const int64_t ld = 3 * (int64_t)W;
   const float* base = qkv + (int64_t)bseq * S * ld + head * 64;
@@ -470,7 +473,7 @@ __global__ __launch_bounds__(256, MINB) void attn_f32_mfma_kernel(const float* _
     if (CL) return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rin, (uint32_t)((r * (int)ld + col) * 4), 0, 0));
     return ok ? *p : 0.f;
   };
-  for (int q0 = 0; q0 < S; q0 += 32) {
+  for (int q0 = 0; q0 < qend; q0 += 32) {
     const int qi = q0 + j;   // this lane's query in the S^T layout
     float qv[32];
     {
@@ -652,6 +655,8 @@ static int attn_f32_variant() {
 hipError_t attention_f32(const float* qkv, float* out, int B, int S, int W, int causal, hipStream_t s) {
   if (B <= 0) return hipSuccess;
   if (W % 64 || S < 1) return hipErrorInvalidValue;
+  const int cq = causal;   // (bit 11: the first query block only, MFMA kernels; the scalar kernels compute all)
+  causal &= 1;
   const dim3 grid((unsigned)B * (W / 64));
   const dim3 grid4((unsigned)(((int64_t)B * (W / 64) + 3) / 4));
 #if MICLIP_AB
@@ -663,11 +668,11 @@ hipError_t attention_f32(const float* qkv, float* out, int B, int S, int W, int 
   }
 #endif
   if (attn_f32_mfma_on() && S <= 64)   // (held to 256 registers: two waves per SIMD, no spills)
-    hipLaunchKernelGGL((attn_f32_mfma_kernel<2, 2>), grid4, dim3(256), 0, s, qkv, out, B, S, W, causal);
+    hipLaunchKernelGGL((attn_f32_mfma_kernel<2, 2>), grid4, dim3(256), 0, s, qkv, out, B, S, W, cq);
   else if (attn_f32_mfma_on() && S <= 96)
-    hipLaunchKernelGGL(attn_f32_mfma_kernel<3>, grid4, dim3(256), 0, s, qkv, out, B, S, W, causal);
+    hipLaunchKernelGGL(attn_f32_mfma_kernel<3>, grid4, dim3(256), 0, s, qkv, out, B, S, W, cq);
   else if (attn_f32_mfma_on() && S <= 128)
-    hipLaunchKernelGGL(attn_f32_mfma_kernel<4>, grid4, dim3(256), 0, s, qkv, out, B, S, W, causal);
+    hipLaunchKernelGGL(attn_f32_mfma_kernel<4>, grid4, dim3(256), 0, s, qkv, out, B, S, W, cq);
   else if (S <= 64)
     hipLaunchKernelGGL(attn_f32_kernel<64>, grid, dim3(64), 0, s, qkv, out, S, W, causal);
   else
