@@ -1182,10 +1182,18 @@ static int encode_image_f32(mi_clip* c, const char* px, int nb, int in_dtype, ch
   const int W = a.vision_width, E = a.embed_dim, S = c->S_v, R = a.image_resolution, P = a.vision_patch_size;
   const int G2 = c->G * c->G;
   float* patches = (float*)c->patches;
-  HIP_TRY(im2col_f32(px, in_dtype == MI_BF16, patches, nb, R, P, c->Kp32, s));
-  if (c->conv_h3 && c->a6 && c->rsc) {   // conv1 as a split-f16 GEMM (rows remapped past CLS)
+  // conv1 as a split-f16 GEMM (rows remapped past CLS); its operand straight from the pixels where
+  // the patch rows are float4-aligned (P % 4 == 0: B/32, B/16; MICLIP_IM2COL_SPLIT=0 in the A/B
+  // build keeps im2col_f32 + split2h_rows)
+  const char* fe = ab_getenv("MICLIP_IM2COL_SPLIT");
+  const bool fused = (!fe || atoi(fe) != 0) && P % 4 == 0 && R % 4 == 0 && c->Kp32 == 3 * P * P && c->Kp32 <= 4096 &&
+                     ((uintptr_t)px & 15) == 0;
+  const bool split3 = c->conv_h3 && c->a6 && c->rsc;
+  if (!(split3 && fused)) HIP_TRY(im2col_f32(px, in_dtype == MI_BF16, patches, nb, R, P, c->Kp32, s));
+  if (split3) {
     const int K = c->Kp32;
-    HIP_TRY(split2h_rows(patches, K, (int64_t)nb * G2, K, 0, 0, c->a6, c->rsc, s));
+    if (fused) HIP_TRY(im2col_split2h(px, in_dtype == MI_BF16, nb, R, P, K, c->a6, c->rsc, s));
+    else HIP_TRY(split2h_rows(patches, K, (int64_t)nb * G2, K, 0, 0, c->a6, c->rsc, s));
     GemmArgs g = gargs(c->a6, 3 * K, c->conv_h3, 3 * K, nullptr, c->x, W, nb * G2, W, 3 * K);
     g.a_f16 = 1;
     g.rsc = c->rsc;

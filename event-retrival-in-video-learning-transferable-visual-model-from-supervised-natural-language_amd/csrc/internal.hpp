@@ -202,6 +202,10 @@ hipError_t layernorm_f32(const float* x, int64_t in_stride, const float* g, cons
 hipError_t attention_f32(const float* qkv, float* out, int B, int S, int W, int causal, hipStream_t s);
 // pixels [B,3,R,R] (f32 / bf16) -> patches f32 [B*G*G, Kp]
 hipError_t im2col_f32(const void* pixels, int in_bf16, float* out, int B, int R, int P, int Kp, hipStream_t s);
+// im2col_f32 + split2h_rows (role 0) in one pass: conv1's split operand [B G^2][3 Kp] fp16 and its
+// row scales straight from the pixels (bit-identical); P % 4 == 0, R % 4 == 0, Kp == 3 P^2 <= 4096
+hipError_t im2col_split2h(const void* pixels, int in_bf16, int B, int R, int P, int Kp, uint16_t* out, float* sc,
+                          hipStream_t s);
 // Split-bf16 operands of the fp32 tower's GEMMs (precise.hip): each f32 value x = x1 + x2 + x3
 // + O(2^-24 |x|) with x1 = bf16(x), x2 = bf16(x - x1), x3 = bf16(x - x1 - x2); a row of K values
 // becomes 6K bf16 in six K-blocks, activations (role 0) as [x1 x2 x3 x1 x2 x1] and weights

@@ -550,6 +550,51 @@ __global__ __launch_bounds__(256, MINB) void attn_f32_mfma_kernel(const float* _
   }
 }
 
+// ------------------------------------------------------------------ im2col + split
+// conv1's split-f16 operand straight from the pixels (P % 4 == 0, Kp = 3 P^2; B/32, B/16): one
+// wave per patch row, its 3 P^2 values gathered as float4s (kw .. kw + 3 of one image row), then
+// split2h_kernel's arithmetic (role 0, the same max / exponent / split) -- the values im2col_f32
+// + split2h_rows produce, bit for bit, without writing and re-reading the f32 patches (6 GB at
+// 10k B/32 frames: 5.7 + 2.8 ms -> one pass).
+template <int NV>
+__global__ __launch_bounds__(256) void im2col_split2h_kernel(const void* __restrict__ pixels, int in_bf16, int64_t rows,
+                                                             int R, int P, int G, int K, _Float16* __restrict__ out,
+                                                             float* __restrict__ sc) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const int64_t bimg = row / (G * G);
+  const int p = (int)(row % (G * G));
+  const int gy = p / G, gx = p % G, PP = P * P;
+  float4 v[NV];
+  float mx = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = 4 * lane + 256 * i;
+    v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (c < K) {
+      const int ch = c / PP, rem = c % PP, kh = rem / P, kw = rem % P;
+      const int64_t off = ((bimg * 3 + ch) * R + (gy * P + kh)) * (int64_t)R + gx * P + kw;
+      if (in_bf16) {
+        const uint2 u = *(const uint2*)((const uint16_t*)pixels + off);
+        v[i] = make_float4(bf2f((uint16_t)(u.x & 0xffff)), bf2f((uint16_t)(u.x >> 16)), bf2f((uint16_t)(u.y & 0xffff)),
+                           bf2f((uint16_t)(u.y >> 16)));
+      } else {
+        v[i] = *(const float4*)((const float*)pixels + off);
+      }
+    }
+    mx = absmax4(mx, v[i]);
+  }
+  const int e = split_exp(wave_max(mx));
+  if (lane == 0) sc[row] = ldexpf(1.f, -e);
+  _Float16* o = out + row * 3 * (int64_t)K;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = 4 * lane + 256 * i;
+    if (c < K) store_split4(v[i], e, 0, o, K, c);
+  }
+}
+
 // ------------------------------------------------------------------ im2col
 // patches [B*G*G, Kp] f32, k = c*P*P + kh*P + kw (conv1 weight order), zero pad.
 __global__ __launch_bounds__(256) void im2col_f32_kernel(const void* __restrict__ pixels, int in_bf16,
@@ -677,6 +722,21 @@ hipError_t attention_f32(const float* qkv, float* out, int B, int S, int W, int 
     hipLaunchKernelGGL(attn_f32_kernel<64>, grid, dim3(64), 0, s, qkv, out, S, W, causal);
   else
     hipLaunchKernelGGL(attn_f32_kernel<256>, grid, dim3(256), 0, s, qkv, out, S, W, causal);
+  return hipGetLastError();
+}
+
+hipError_t im2col_split2h(const void* pixels, int in_bf16, int B, int R, int P, int Kp, uint16_t* out, float* sc,
+                          hipStream_t s) {
+  const int G = R / P;
+  const int64_t rows = (int64_t)B * G * G;
+  if (rows <= 0) return hipSuccess;
+  // float4 / 4 x bf16 loads of one image row: P % 4 == 0 (and R % 4 == 0 for their alignment), Kp = 3 P^2 <= 4096
+  if (P % 4 || R % 4 || Kp != 3 * P * P || Kp > 4096 || !sc) return hipErrorInvalidValue;
+  const dim3 grid((unsigned)((rows + 3) / 4));
+  _Float16* o = (_Float16*)out;
+  if (Kp <= 1024) hipLaunchKernelGGL(im2col_split2h_kernel<4>, grid, dim3(256), 0, s, pixels, in_bf16, rows, R, P, G, Kp, o, sc);
+  else if (Kp <= 3072) hipLaunchKernelGGL(im2col_split2h_kernel<12>, grid, dim3(256), 0, s, pixels, in_bf16, rows, R, P, G, Kp, o, sc);
+  else hipLaunchKernelGGL(im2col_split2h_kernel<16>, grid, dim3(256), 0, s, pixels, in_bf16, rows, R, P, G, Kp, o, sc);
   return hipGetLastError();
 }
 

@@ -44,14 +44,15 @@ def main():
              "m1": (_native.lib_ab, {"MICLIP_F32_8Q": "1", "MICLIP_F32_DUP": "0", "MICLIP_CLS_LAST": "0", "MICLIP_F32_8Q_MASK": "1"}),
              "m2": (_native.lib_ab, {"MICLIP_F32_8Q": "1", "MICLIP_F32_DUP": "0", "MICLIP_CLS_LAST": "0", "MICLIP_F32_8Q_MASK": "2"}),
              "m4": (_native.lib_ab, {"MICLIP_F32_8Q": "1", "MICLIP_F32_DUP": "0", "MICLIP_CLS_LAST": "0", "MICLIP_F32_8Q_MASK": "4"}),
-             "d8": (_native.lib_ab, {"MICLIP_F32_8Q": "1", "MICLIP_F32_DUP": "8", "MICLIP_CLS_LAST": "0"})}
+             "d8": (_native.lib_ab, {"MICLIP_F32_8Q": "1", "MICLIP_F32_DUP": "8", "MICLIP_CLS_LAST": "0"}),
+             "noim2s": (_native.lib_ab, {"MICLIP_F32_8Q": "1", "MICLIP_IM2COL_SPLIT": "0"})}
     names = os.environ.get("F32_VARIANTS", "8q,pp").split(",")
     libs = {k: table[k][0] for k in names}
 
     def use(k):   # (a model's calls go to whichever library _native.lib names)
         _native.lib = table[k][0]
         for e in ("MICLIP_F32_8Q", "MICLIP_8Q_NG", "MICLIP_ATTN_F32_V", "MICLIP_F32_DUP", "MICLIP_CLS_LAST",
-                  "MICLIP_F32_8Q_MASK"):
+                  "MICLIP_F32_8Q_MASK", "MICLIP_IM2COL_SPLIT"):
             os.environ.pop(e, None)
         os.environ.update(table[k][1])
 

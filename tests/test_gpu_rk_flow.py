@@ -145,6 +145,27 @@ def test_fp32_tower_8phase_bit_identical(gpu, monkeypatch, name, n):
     assert clip_ref.cosine(img, ri).min() > 1 - 1e-9
 
 
+@pytest.mark.parametrize("pix", ["f32", "bf16"])
+def test_fp32_conv1_split_from_pixels_bit_identical(gpu, monkeypatch, pix):
+    """conv1's split operand built straight from the pixels (precise.hip im2col_split2h, the
+    default for P % 4 == 0) against im2col_f32 + split2h_rows (A/B build, MICLIP_IM2COL_SPLIT=0):
+    image embeddings bit for bit, f32 and bf16 pixel inputs."""
+    import torch
+    from miclip import _native, config, model as M, weights
+    cfg = config.get_config("ViT-B/32")
+    sd = state_dict("ViT-B/32")
+    px = torch.from_numpy(weights.synthetic_pixels(12, cfg.image_resolution, seed=9)).to(gpu)
+    if pix == "bf16":
+        px = px.bfloat16()
+    got = M.CLIP(cfg, sd, device=gpu, weights="fp32", image_chunk=12).encode_image(px).cpu().numpy()
+    monkeypatch.setattr(_native, "lib", _native.lib_ab)
+    monkeypatch.setenv("MICLIP_IM2COL_SPLIT", "0")
+    ref = M.CLIP(cfg, sd, device=gpu, weights="fp32", image_chunk=12).encode_image(px).cpu().numpy()
+    monkeypatch.undo()
+    assert np.isfinite(got).all()
+    assert np.array_equal(got.view(np.int32), ref.view(np.int32))
+
+
 def test_fp32_tower_last_block_on_cls_rows_bit_identical(gpu, monkeypatch):
     """The fp32 tower's last block after attention on the gathered CLS rows only (the default
     for >= 256 frames per chunk, as the bf16 tower's last_block_cls): image embeddings equal the
