@@ -25,6 +25,17 @@ def test_flops_match_survey():
     assert abs(config.get_config("ViT-L/14@336px").image_flops() / 1e9 - 381.92) < 0.1
 
 
+def test_executed_flops_of_the_cls_row_last_block():
+    """image_flops_executed: the last block's out_proj / c_fc / c_proj skipped for S - 1 of S rows
+    (api.cpp last_block_cls) -- what bench.py's end-to-end MFMA fraction counts."""
+    from miclip import config
+    b32 = config.get_config("ViT-B/32")
+    W, S = b32.vision_width, b32.vision_tokens
+    assert b32.image_flops_executed(False) == b32.image_flops()
+    assert b32.image_flops() - b32.image_flops_executed() == 2.0 * (S - 1) * W * 9 * W
+    assert 0.93 < b32.image_flops_executed() / b32.image_flops() < 0.95
+
+
 def test_pack_order_covers_state_dict():
     from miclip import _native, config
     cfg = config.get_config("test-small")
