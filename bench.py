@@ -82,6 +82,43 @@ def lnfold_active(model, cfg):
     return getattr(model, "weights", "bf16") == "bf16" and cfg.vision_width % 256 == 0 and cfg.vision_width <= 1024
 
 
+def step_work(cfg, weights, chunk, lnfold):
+    """The MFMA work one step executes, per frame and per query, split by the engine it runs on
+    (api.cpp: at >= 256 frames per chunk the last block's out_proj / c_fc / c_proj run on the CLS
+    rows only -- in the LN-folded bf16, the MX-fp8 and the fp32 towers; the bf16 and fp32 towers
+    also compute the last in_proj's Q for the CLS rows only and the last attention for the CLS
+    query's tile: 16 rows in the S <= 64 flash kernel, 32 in the f32 MFMA kernel (S <= 128))."""
+    S = cfg.vision_tokens
+    cls_last = chunk >= 256 and ((weights == "bf16" and lnfold) or weights == "fp32"
+                                 or (weights == "fp8" and cfg.vision_width % 128 == 0))
+    q_cls = cls_last and weights in ("bf16", "fp32")
+    rows = None
+    if cls_last and weights == "bf16" and S <= 64:
+        rows = 16
+    elif cls_last and weights == "fp32" and S <= 128:
+        rows = 32
+    return {"cls_last": cls_last, "image": cfg.image_flops_executed(cls_last, q_cls, rows),
+            "image_attn": cfg.image_attention_flops(rows), "text": cfg.text_flops(),
+            "text_attn": cfg.text_attention_flops()}
+
+
+def mfma_time_at_peak(w, weights, frames, queries, dim):
+    """Seconds the step's executed MFMA work needs at each engine's dense peak: bf16 towers on the
+    bf16/f16 MFMA (2.5 PF); MX-fp8 runs' vision GEMMs on the fp8 MFMA (5 PF), their attention and
+    text tower bf16; fp32 runs' GEMMs as split-f16 (3x the products on the f16 MFMA) and their
+    attention on the exact-f32 MFMA; the rank pass's 2 N Q D on the exact-f32 MFMA.  Divided by the
+    step time this is the end-to-end MFMA fraction (<= 1 by construction)."""
+    img_gemm, img_attn = frames * (w["image"] - w["image_attn"]), frames * w["image_attn"]
+    txt_gemm, txt_attn = queries * (w["text"] - w["text_attn"]), queries * w["text_attn"]
+    rank = 2.0 * frames * queries * dim
+    bf, f8, f32 = BF16_PEAK_TFLOPS * 1e12, FP8_PEAK_TFLOPS * 1e12, F32_MFMA_PEAK_TFLOPS * 1e12
+    if weights == "fp32":
+        return 3 * (img_gemm + txt_gemm) / bf + (img_attn + txt_attn + rank) / f32
+    if weights == "fp8":
+        return img_gemm / f8 + (img_attn + txt_gemm + txt_attn) / bf + rank / f32
+    return (img_gemm + img_attn + txt_gemm + txt_attn) / bf + rank / f32
+
+
 def kernel_timing(model, cfg, chunk, reps=20):
     """Average duration of each encoder kernel at the bench's chunk shape, timed
     with HIP events on the stream the kernels are launched on."""
@@ -523,9 +560,8 @@ def parity_mode(args, dev, pixels, tokens, Q, k, base, chunk):
     M = chunk * cfg.vision_tokens
     fl = 2.0 * M * 4 * cfg.vision_width * cfg.vision_width
     fc = kern["gemm_fc"]["us"]
-    # executed flops: the last block's row-wise part runs on the CLS rows alone at >= 256 frames per chunk
-    step_flops = (pixels.shape[0] * cfg.image_flops_executed(chunk >= 256) + Q * cfg.text_flops()
-                  + 2.0 * pixels.shape[0] * Q * cfg.embed_dim)
+    w = step_work(cfg, "fp32", chunk, False)
+    t_peak = mfma_time_at_peak(w, "fp32", pixels.shape[0], Q, cfg.embed_dim)
     out = {"weights": "fp32", "value": round(pixels.shape[0] / (ms / 1e3), 1), "unit": "frames/s",
            "ms_per_step": round(ms, 3), "steps": args.parity_steps,
            "note": "fp32 tower (split-f16 GEMMs, f32-grade; exact-f32 MFMA attention): the mode whose R@1/5/10 "
@@ -540,7 +576,9 @@ def parity_mode(args, dev, pixels, tokens, Q, k, base, chunk):
                         "f32_mfma_peak": F32_MFMA_PEAK_TFLOPS,
                         "traffic": None, "launch_shape": [M, 4 * cfg.vision_width, 3 * cfg.vision_width],
                         "avg_launch_us": fc},
-           "mfma_frac_end_to_end_f32": round(step_flops / (ms / 1e3) / (F32_MFMA_PEAK_TFLOPS * 1e12), 4),
+           # the executed work at its engines' peaks (split-f16 GEMMs: 3x the products on the f16 MFMA;
+           # attention and rank on the exact-f32 MFMA) over the step time
+           "mfma_frac_end_to_end": round(t_peak / (ms / 1e3), 4),
            "kernels": kern}
     del model
     torch.cuda.empty_cache()
@@ -657,13 +695,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
-    # the roofline kernel (mlp.c_fc of the LayerNorm-folded bf16 tower) timed live: HIP events on
-    # the launch stream around each of its launches inside the timed steps (mi_clip_kernel_events)
     from miclip import _native as _N
-    n_fc = args.steps * cfg.vision_layers * (-(-Nf // chunk))
-    fc_live = lnfold_active(model, cfg) and not args.no_kernel_timing
-    if fc_live:
-        _N.check(_N.lib().mi_clip_kernel_events(model._ctx, 1, n_fc), "mi_clip_kernel_events")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -675,9 +707,18 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
+    # the roofline kernel (mlp.c_fc of the LayerNorm-folded bf16 tower) timed live: HIP events on the
+    # launch stream around each of its launches (mi_clip_kernel_events) in `ev_steps` further steps of
+    # the same workload run AFTER the timed loop, so the timed steps carry no event records
+    ev_steps = min(args.steps, 5)
+    n_fc = min(ev_steps * cfg.vision_layers * (-(-Nf // chunk)), 1 << 16)   # the library's event capacity
     fc_us = None
-    if fc_live:
+    if lnfold_active(model, cfg) and not args.no_kernel_timing:
         import ctypes
+        _N.check(_N.lib().mi_clip_kernel_events(model._ctx, 1, n_fc), "mi_clip_kernel_events")
+        for _ in range(ev_steps):
+            step()
+        torch.cuda.synchronize(dev)
         buf = (ctypes.c_float * n_fc)()
         got = _N.lib().mi_clip_kernel_times(model._ctx, buf, n_fc)
         _N.check(0 if got >= 0 else got, "mi_clip_kernel_times")
@@ -716,16 +757,11 @@ def main():
             kern["jpeg_ingest_720p"] = ingest
         _progress("rank roofline")
         rank_roof = None if args.no_rank_roofline else rank_roofline(dev)
-        # executed flops: the folded bf16 tower and the fp32 tower run the last block's row-wise part on
-        # the CLS rows alone at >= 256 frames per chunk (api.cpp last_block_cls); the MX tower does not
-        cls_last = chunk >= 256 and (args.weights == "fp32" or (args.weights == "bf16" and lnfold_active(model, cfg)))
-        F_frame, F_text = cfg.image_flops_executed(cls_last), cfg.text_flops()
-        step_flops = Nf * world * F_frame + Q * world * F_text + 2.0 * Nf * world * Q * cfg.embed_dim
-        # against the peak of the arithmetic the step's GEMMs run on (fp8 runs: the MX-fp8 peak)
-        # (fp32 runs: f32-equivalent flops against the f32 MFMA peak -- the split-f16 GEMMs execute 3x
-        # that work on the f16 MFMA, so this fraction can pass 1)
-        step_peak = {"fp8": FP8_PEAK_TFLOPS, "fp32": F32_MFMA_PEAK_TFLOPS}.get(args.weights, BF16_PEAK_TFLOPS)
-        mfma_frac = step_flops / (ms / 1e3) / (step_peak * 1e12) / world
+        # executed work (step_work: the CLS-row last block of the bf16, MX-fp8 and fp32 towers at >= 256
+        # frames per chunk) at its engines' dense peaks over the step time, per rank
+        work = step_work(cfg, args.weights, chunk, lnfold_active(model, cfg))
+        cls_last = work["cls_last"]
+        mfma_frac = mfma_time_at_peak(work, args.weights, Nf, Q, cfg.embed_dim) / (ms / 1e3)
         dom = kern.get("gemm_fc")
         if dom and fc_us:   # the launches of the timed steps (events), not the micro loop
             dom = {"us": round(sum(fc_us) / len(fc_us), 2), "launches": len(fc_us),
@@ -760,7 +796,8 @@ def main():
                                              + (8 * M + 8 * 4 * cfg.vision_width if lnf else 0)),
                     "flops_per_launch": fl, "launch_shape": [M, 4 * cfg.vision_width, cfg.vision_width],
                     "avg_launch_us": dom["us"],
-                    "timing": ("HIP events around each c_fc launch of the timed steps (mi_clip_kernel_events): "
+                    "timing": (f"HIP events around each c_fc launch of {ev_steps} steps run after the timed loop "
+                               f"(mi_clip_kernel_events; the timed steps are not instrumented): "
                                f"{dom['launches']} launches, {dom['min_us']}-{dom['max_us']} us; the random-operand "
                                f"micro loop (kernels.gemm_fc) {dom['micro_us']} us") if "launches" in dom
                               else "HIP events around the kernel_timing micro loop (random operands)"}
@@ -795,8 +832,10 @@ def main():
             "roofline": roof,
             "rank_roofline": rank_roof,
             "mfma_frac_end_to_end": round(mfma_frac, 4),
-            "mfma_frac_flops": ("executed: the last block's out_proj / c_fc / c_proj on the CLS rows only "
-                                "(their other rows are never read)" if cls_last else "the full model"),
+            "mfma_frac_flops": ("executed work at each engine's dense peak over the step time: the last block's "
+                                "out_proj / c_fc / c_proj on the CLS rows only (their other rows are never read)"
+                                + ("; its Q projection and attention for the CLS queries only" if cls_last and args.weights != "fp8" else "")
+                                if cls_last else "the full model at each engine's dense peak over the step time"),
             "parity_mode": parity,
             "verify": verify,
             "kernels": kern,

@@ -10,6 +10,11 @@
 #ifndef MICLIP_AB
 #define MICLIP_AB 0
 #endif
+// MICLIP_VMCHECK = 1: the counting build of the kernels with counted waits (vm_count_check below;
+// `make` compiles it for the device only, next to the product objects, and fails on a mismatch)
+#ifndef MICLIP_VMCHECK
+#define MICLIP_VMCHECK 0
+#endif
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -66,6 +71,38 @@ __device__ __forceinline__ void glds16(const void* gsrc, void* lds_base) {
 }
 
 __device__ __forceinline__ void vm_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// Counted waits.  vmcnt retires a wave's VMEM ops in issue order and its field holds 0..63, so the
+// wait for one DMA names how many VMEM ops the wave issued AFTER it.  Kernels that count waits derive
+// each immediate from constexpr op counts (VM_MAX bounds them) and wait through vm_wait<N>.
+constexpr int VM_MAX = 63;
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  static_assert(N >= 0 && N <= VM_MAX, "vmcnt immediate outside the 6-bit field");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// A ring of stages of OPS ops each: wait until at most `younger` (0..Y, runtime) stages younger than
+// the awaited one -- plus EXTRA younger ops of another kind (an epilogue's stores) -- are in flight:
+// vmcnt(younger * OPS + EXTRA) through a chain of compile-time immediates
+template <int OPS, int Y, int EXTRA = 0>
+__device__ __forceinline__ void vm_wait_stages(int younger) {
+  if constexpr (Y == 0) {
+    vm_wait<EXTRA>();
+  } else {
+    if (younger >= Y) vm_wait<Y * OPS + EXTRA>();
+    else vm_wait_stages<OPS, Y - 1, EXTRA>(younger);
+  }
+}
+// Compile-time check of an issued-op count: `n` is a local counter bumped at every VMEM op a code
+// section issues, which the optimiser folds to a constant (fully unrolled, template-selected code).
+// When it differs from the constexpr N that a counted wait was derived from, the call to this
+// never-defined function survives and the device link fails -- the count and the code cannot drift
+// apart silently.
+extern "C" __device__ void miclip_vmcnt_count_mismatch();
+template <int N>
+__device__ __forceinline__ void vm_count_check(int n) {
+  if (n != N) miclip_vmcnt_count_mismatch();
+}
 
 // Bijective XCD-aware block remap (cdna_hip_programming.md §5 "XCD swizzle
 // must be bijective"): blocks that share an XCD (b % 8) get a contiguous run of

@@ -48,6 +48,10 @@ namespace {
 constexpr int BK = 32;       // k per stage
 constexpr int RING = 4;      // LDS stages
 constexpr int LEAD = 3;      // stages in flight ahead of the one being read
+// counted waits (common.hpp vm_wait_stages): VMEM ops per wave and stage -- issue_half(st, 0) and
+// issue_half(st, 1) (gemm_ppp_kernel's issue: j = 0, 1), each one A and one W 16-row DMA
+constexpr int STAGE_OPS = 2 * 2;
+static_assert((LEAD - 1) * STAGE_OPS + 16 <= VM_MAX, "counted waits exceed vmcnt's 6-bit field");
 constexpr int MAX_N = 4096;  // bias staged in LDS
 constexpr int EPI_NONE = 9;  // timing probe (variant 8): main loop only
 
@@ -365,11 +369,9 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs a) {
     glds16(asrc[j] + a_off(st), base + (wave * 2 + j) * 1024);
     glds16(wsrc[j] + st * BK, base + A_BYTES + (wave * 2 + j) * 1024);
   };
-  auto wait_stage = [&](int g1) {  // retire this wave's DMA for stage g1
+  auto wait_stage = [&](int g1) {  // retire this wave's DMA for stage g1 (STAGE_OPS per younger stage)
     const int younger = min(LEAD - 1, nk - 1 - g1);
-    if (younger >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (younger == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    vm_wait_stages<STAGE_OPS, LEAD - 1>(younger);
   };
   auto barrier = [&]() {
     __builtin_amdgcn_sched_barrier(0);
@@ -631,11 +633,9 @@ __global__ __launch_bounds__(512) void gemm_abl_kernel(GemmArgs a) {
     glds16(asrc[j] + (int64_t)st * BK, base + (wave * 2 + j) * 1024);
     glds16(wsrc[j] + st * BK, base + A_BYTES + (wave * 2 + j) * 1024);
   };
-  auto wait_stage = [&](int g1) {
+  auto wait_stage = [&](int g1) {  // retire this wave's DMA for stage g1 (STAGE_OPS per younger stage)
     const int younger = min(LEAD - 1, nk - 1 - g1);
-    if (younger >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (younger == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    vm_wait_stages<STAGE_OPS, LEAD - 1>(younger);
   };
   auto barrier = [&]() {
     __builtin_amdgcn_sched_barrier(0);
@@ -726,17 +726,6 @@ __global__ __launch_bounds__(512) void gemm_abl_kernel(GemmArgs a) {
 //   them, it has landed once the tile's first stage wait + barrier return, and
 //   the epilogue reads it with an LDS read hipcc does not see.  A plain global
 //   load of the bias there made hipcc drain the prefetch with vmcnt(0).
-__device__ __forceinline__ void vm_wait_n(int n) {  // n wave-uniform; unlisted values wait for everything
-  switch (n) {
-    case 24: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
-    case 20: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
-    case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
-    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-  }
-}
-
 // Timing probe (variant 19, scripts/gemm_micro.py): s_memrealtime stamps
 // (100 MHz) of each workgroup's third tile - main loop start, main loop end,
 // epilogue stores issued, next tile's main loop start - kept in SGPRs and
@@ -750,7 +739,7 @@ __global__ __launch_bounds__(512) void gemm_ppp_kernel(GemmArgs a) {
   constexpr int BM = 256, BN = 256;
   constexpr int WTM = 128, WTN = 64;
   constexpr int A_BYTES = BM * BK * 2, STAGE_BYTES = (BM + BN) * BK * 2;
-  constexpr int NSTORE = 16;  // epilogue store instructions per wave of a full tile
+  constexpr int NSTORE = 8 * 2;  // epilogue store instructions per wave of a full tile: (mi, p)
   __shared__ __attribute__((aligned(16))) char smem[RING * STAGE_BYTES + 2 * BN * 4];
   float* sbias = (float*)(smem + RING * STAGE_BYTES);
 
@@ -790,16 +779,17 @@ __global__ __launch_bounds__(512) void gemm_ppp_kernel(GemmArgs a) {
       glds16(wsrc[j] + st * BK, base + A_BYTES + (wave * 2 + j) * 1024);
     }
   };
-  int pend = 0;  // the previous tile's stores are in flight, younger than stages 0..LEAD-1
+  bool pend = false;  // the previous tile's NSTORE stores are in flight, younger than stages 0..LEAD-1
   // The stages of a workgroup's tiles form ONE stream through the ring: the
   // next tile's first LEAD stages are issued in this tile's last LEAD main-loop
   // iterations (where a single tile's pipeline would run dry), so they have
   // landed before the epilogue ends.  rb = ring slot of this tile's stage 0.
   int rb = 0, nm0 = 0, nn0 = 0;
   bool has_next = false;
-  auto wait_stage = [&](int g1) {
+  auto wait_stage = [&](int g1) {   // STAGE_OPS per younger stage (+ the previous tile's NSTORE stores)
     const int younger = has_next ? LEAD - 1 : min(LEAD - 1, nk - 1 - g1);
-    vm_wait_n(4 * younger + (g1 < LEAD ? pend : 0));
+    if (g1 < LEAD && pend) vm_wait_stages<STAGE_OPS, LEAD - 1, NSTORE>(younger);
+    else vm_wait_stages<STAGE_OPS, LEAD - 1>(younger);
   };
   auto barrier = [&]() {
     __builtin_amdgcn_sched_barrier(0);
@@ -876,6 +866,7 @@ __global__ __launch_bounds__(512) void gemm_ppp_kernel(GemmArgs a) {
     // the next tile's first stages are already in flight (issued in the main loop)
     const int cm0 = m0, cn0 = n0;
     // ---- epilogue of tile (cm0, cn0): direct permlane-swapped row stores (gemm_pp_kernel DIRECT)
+    int vm_st = 0;   // store instructions of a full tile (MICLIP_VMCHECK: checked against NSTORE)
     float4 bias[4];
 #pragma unroll
     for (int ni = 0; ni < 4; ++ni)
@@ -899,6 +890,7 @@ __global__ __launch_bounds__(512) void gemm_ppp_kernel(GemmArgs a) {
         const auto sx = __builtin_amdgcn_permlane16_swap(pk[0].x, pk[1].x, false, false);
         const auto sy = __builtin_amdgcn_permlane16_swap(pk[0].y, pk[1].y, false, false);
         const int col = cn0 + wc * WTN + (2 * p + (g & 1)) * 16 + (g >> 1) * 8;
+        if (MICLIP_VMCHECK) ++vm_st;
         if (m < a.M) {
           typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
           u32x4* dst = (u32x4*)((uint16_t*)a.out + (int64_t)m * a.ldo + col);
@@ -908,6 +900,7 @@ __global__ __launch_bounds__(512) void gemm_ppp_kernel(GemmArgs a) {
         }
       }
     }
+    if (MICLIP_VMCHECK) vm_count_check<NSTORE>(vm_st);
     if (EARLY && grp == 0) barrier();
     if (PROBE && ti == 2) ts2 = __builtin_amdgcn_s_memrealtime();
     ++ti;
@@ -918,9 +911,9 @@ __global__ __launch_bounds__(512) void gemm_ppp_kernel(GemmArgs a) {
     rb = (rb + nk) % RING;
     tpar ^= 1;
     if (cm0 + BM <= a.M) {
-      pend = NSTORE;
+      pend = true;
     } else {  // partial tile: an unknown number of stores issued
-      pend = 0;
+      pend = false;
       vm_wait_all();
     }
   }

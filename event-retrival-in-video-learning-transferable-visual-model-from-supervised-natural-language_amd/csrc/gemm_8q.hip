@@ -24,7 +24,7 @@
 //    overlaps the barrier instead of lengthening the memory section.  That
 //    needs every half-tile restaged two phases after its last read (WAR),
 //    so the issue table shifts by one phase and each K-tile is waited for
-//    with vmcnt(4) (two phases of DMAs younger than it):
+//    with vmcnt(4) (two phases of DMAs younger than it; Vm8q::YOUNGER):
 //      phase  reads (buffer)      restages
 //      1      even A_m0 + B_n0    odd  A_m1   (current pair)
 //      2      even B_n1           odd  B_n0   (current pair)
@@ -44,7 +44,7 @@
 //    (A_m1 and B_n0): the last pair does not re-read B_n0 in phase 8 (it keeps
 //    phase 5's fragments), so B_n0's last read is three phases back.  The 16
 //    stores are then younger than every DMA the first pair's phase-4 wait
-//    needs (vmcnt(20)) and have until phase 8 to complete.  Stores go through
+//    needs (vmcnt(20) = Vm8q::FIRST_P4) and have until phase 8 to complete.  Stores go through
 //    a descriptor whose range is the tile's valid rows (no per-store branch or
 //    64-bit address math), the four bias reads share one wait, and a tile's
 //    first MFMA into each accumulator takes C = 0 (no zeroing pass).
@@ -179,9 +179,42 @@ struct EpiKind8q {
   static constexpr int LDS = 2 * BUF + 2 * BN * 4 + (LN || SPL ? 2 * BM * 8 + 2 * BN * 4 : 0);
 };
 
+// The kernel's counted waits (common.hpp vm_wait), every immediate derived from the VMEM ops the code
+// issues.  VERDICT r5: a hand-kept immediate (60, the [y1 | y1 | y2] store count) outlived a change
+// that issued 16 fewer epilogue stores per wave (o_dup), so the first pair's phase-4 wait released
+// while up to 16 of the awaited K-tile's DMAs were in flight and stale LDS reached the MFMAs in the
+// in-loop epilogues of large grids.  Now the epilogue counts the ops it issues and vm_count_check
+// ties the count to EPI_VMEM at compile time (a mismatch fails the device link).
+template <int EPI, int ABL, int F>
+struct Vm8q {
+  using EK = EpiKind8q<EPI>;
+  static constexpr int DMA_PER_HALF = 2;   // issue(): two 1-KB DMAs per thread and half-tile
+  // a phase-4 / phase-8 wait (and the prologue's) retires the K-tile whose last half-tile was
+  // restaged before the two preceding phases; those two phases' half-tiles (3-4 / 7-8) are younger
+  static constexpr int YOUNGER = 2 * DMA_PER_HALF;
+  static constexpr int BLOCKS = 8;         // the epilogue's 16-row blocks (a wave's 128 rows)
+  // the epilogue's VMEM ops per block, all issued after phase 1's DMAs (EPI_RES16's x16 loads go out
+  // ahead of them, in phase 6 / ahead of phase 1's DMAs: older than the awaited K-tile, not counted)
+  static constexpr int PER_BLOCK =
+      ABL == 4 ? 0                                                 // probe: no epilogue work
+      : EPI == EPI_F32 ? 4                                         // four f32 16-byte row pieces
+      : EPI == EPI_RESID_F32 ? 4 + 4                               // the stream's four pieces (loaded a block ahead) + four stores
+      : EPI == EPI_SPLIT_GELU ? 2 * ((F & F_ODUP) ? 2 : 3) + 1      // per column half p: y1 (, y1), y2; + rsc_out
+      : EK::RES ? 2 + (ABL == 11 ? 0 : 1)                          // two row stores + the 64-column partial
+      : (ABL == 10 && !(F & F_FULL)) ? 0                           // stamp probe without stores
+      : 2;                                                         // two row stores (F_FULL: rows 0-7, 8-15)
+  static constexpr int EPI_VMEM = BLOCKS * PER_BLOCK;
+  // the first pair's phase-4 wait when the previous tile's epilogue ran in phase 1 (after that
+  // phase's DMAs): the epilogue's ops are younger too.  Saturated at VM_MAX it over-waits (the oldest
+  // epilogue ops retire with the K-tile): correct, only slower (EPI_RESID_F32: 64 + 4)
+  static constexpr int FIRST_P4 = YOUNGER + EPI_VMEM < VM_MAX ? YOUNGER + EPI_VMEM : VM_MAX;
+  static_assert(YOUNGER > 0 && YOUNGER <= VM_MAX && FIRST_P4 >= YOUNGER, "counted waits out of range");
+};
+
 template <int EPI, int ABL = 0, int F = 0, bool OPF16 = false>
 __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
   using EK = EpiKind8q<EPI>;
+  using VM = Vm8q<EPI, ABL, F>;
   __shared__ __attribute__((aligned(16))) char smem[EK::LDS];
   float* sbias = (float*)(smem + 2 * BUF);
   float* srs = (float*)(smem + 2 * BUF + 2 * BN * 4);              // LN: [2][BM][2]
@@ -244,7 +277,7 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
     const int kofs = (2 * rpp + b) * BK8;
     char* dst = smem + b * BUF + h * HALF + (2 * wave) * 1024;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < VM::DMA_PER_HALF; ++j) {
       if (F & F_GLDS) {
         const int ir = (2 * wave + j) * 8 + drow;
         const int c = j ? c1 : c0;
@@ -404,6 +437,14 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
   // results are bit-identical to gemm_pp_kernel's.  A lane holds 4 consecutive columns of one row
   // per 16 x 16 block: the f32 pieces are 16-byte row stores straight from the accumulators, the
   // split's fp16 pieces pair blocks ni / ni + 1 by permlane16 swaps (the bf16 epilogue's layout)
+  // VMEM ops issued by the running epilogue, checked against VM::EPI_VMEM in the counting build
+  // (MICLIP_VMCHECK: `make` compiles it beside the product objects; the counters fold away)
+  int vm_epi = 0;
+#if MICLIP_VMCHECK
+#define MI_VM_ISSUED(n) (vm_epi += (n))
+#else
+#define MI_VM_ISSUED(n) ((void)0)
+#endif
   auto epilogue_spl = [&]() __attribute__((always_inline)) {
     int l;
     asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
@@ -448,8 +489,10 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
       u32x4_8q xo[2][4];   // EPI_RESID_F32: the stream's values, one 16-row block ahead
       auto load_blk = [&](int mi) {
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni)
+        for (int ni = 0; ni < 4; ++ni) {
           xo[mi & 1][ni] = __builtin_bit_cast(u32x4_8q, __builtin_amdgcn_raw_buffer_load_b128(ro, vo + mi * blk + ni * 64, 0, 0));
+          MI_VM_ISSUED(1);
+        }
       };
       if (EPI == EPI_RESID_F32) load_blk(0);
 #pragma unroll
@@ -464,6 +507,7 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
             v = (f32x4){o[0] + v[0], o[1] + v[1], o[2] + v[2], o[3] + v[3]};
           }
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_8q, v), ro, vo + mi * blk + ni * 64, 0, 0);
+          MI_VM_ISSUED(1);
         }
       }
     } else {   // EPI_SPLIT_GELU: [y1 | y1 | y2] at columns n, n + N, n + 2N; rsc_out[m] by the n = 0 tile
@@ -506,14 +550,20 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
           const auto by = __builtin_amdgcn_permlane16_swap(k2[0].y, k2[1].y, false, false);
           const u32x4_8q d1 = {ax[0], ay[0], ax[1], ay[1]}, d2 = {bx[0], by[0], bx[1], by[1]};
           __builtin_amdgcn_raw_buffer_store_b128(d1, ro, vo + mi * blk + p * 64, 0, 0);
-          if constexpr (!(F & F_ODUP)) __builtin_amdgcn_raw_buffer_store_b128(d1, ro, vo + mi * blk + p * 64, n2, 0);
+          MI_VM_ISSUED(1);
+          if constexpr (!(F & F_ODUP)) {
+            __builtin_amdgcn_raw_buffer_store_b128(d1, ro, vo + mi * blk + p * 64, n2, 0);
+            MI_VM_ISSUED(1);
+          }
           __builtin_amdgcn_raw_buffer_store_b128(d2, ro, vo + mi * blk + p * 64, n4, 0);
+          MI_VM_ISSUED(1);
         }
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(ldexpf(1.f, -e)), rr, vr + mi * 64, 0, 0);
+        MI_VM_ISSUED(1);
       }
     }
   };
-  auto epilogue = [&]() __attribute__((always_inline)) {
+  auto epilogue_body = [&]() __attribute__((always_inline)) {
     if constexpr (EK::SPL) {
       if (ABL != 4) epilogue_spl();
       return;
@@ -654,8 +704,11 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
         dp[p] = d;
         if (F & F_FULL) continue;
         if (ABL == 10) asm volatile("" ::"v"(d));   // stamp probe without the stores
-        else if (p == 0) __builtin_amdgcn_raw_buffer_store_b128(d, rsO, vo + mi * blkO, 0, (ABL == 13 || (F & F_ONT)) ? 2 : 0);
-        else __builtin_amdgcn_raw_buffer_store_b128(d, rsO, vo + mi * blkO + 64, 0, (ABL == 13 || (F & F_ONT)) ? 2 : 0);
+        else {
+          if (p == 0) __builtin_amdgcn_raw_buffer_store_b128(d, rsO, vo + mi * blkO, 0, (ABL == 13 || (F & F_ONT)) ? 2 : 0);
+          else __builtin_amdgcn_raw_buffer_store_b128(d, rsO, vo + mi * blkO + 64, 0, (ABL == 13 || (F & F_ONT)) ? 2 : 0);
+          MI_VM_ISSUED(1);
+        }
       }
       if (F & F_FULL) {
         const bool top = fr < 8;
@@ -670,6 +723,7 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
         }
         __builtin_amdgcn_raw_buffer_store_b128(s1, rsO, voF + mi * blkO, 0, (F & F_ONT) ? 2 : 0);
         __builtin_amdgcn_raw_buffer_store_b128(s2, rsO, voF + mi * blkO + rows8, 0, (F & F_ONT) ? 2 : 0);
+        MI_VM_ISSUED(2);
       }
       if (EK::RES && ABL == 11) {   // timing probe: no statistics, no partial stores
         __builtin_amdgcn_sched_barrier(0);
@@ -693,11 +747,24 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
         typedef unsigned int u32x2_8q __attribute__((ext_vector_type(2)));
         __builtin_amdgcn_raw_buffer_store_b64((u32x2_8q){__float_as_uint(s), __float_as_uint(m2)}, rsP,
                                               voP + (uint32_t)(mi * 16 * pstr), 0, 0);
+        MI_VM_ISSUED(1);
         __builtin_amdgcn_sched_barrier(0);
       }
       rab_c = rab_n;
     }
   };
+  // every epilogue instance issues exactly the VMEM ops its waits were derived from
+#if MICLIP_VMCHECK
+  auto epilogue = [&]() __attribute__((always_inline)) {
+    vm_epi = 0;
+    epilogue_body();
+    vm_count_check<VM::EPI_VMEM>(vm_epi);
+  };
+#else
+  auto& epilogue = epilogue_body;
+  (void)vm_epi;
+#endif
+#undef MI_VM_ISSUED
 
   // FIRST / LAST: the tile's first / last K-tile pair (compile-time: separate code paths)
   auto phase = [&](auto pc, auto firstc, auto lastc) {
@@ -768,23 +835,16 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
     // first pair the previous tile's 16 epilogue stores are younger as well
     // (they then have until phase 8 to complete)
     if (P == 4) {
-      // (EPI_RES16: 16 stores, 8 partial stores and the x16 loads of blocks 4-7 are younger;
-      // the epilogue's wait for block 7 already retired the odd buffer)
-      // (SPL: the epilogue's VMEM ops per wave -- F32 32 stores, RESID 32 loads + 32 stores, SPLIT
-      // 48 + 8 stores, 32 + 8 with o_dup -- are younger; vmcnt holds at most 63)
-      constexpr int SPL_VM = EPI == EPI_F32 ? 36 : (EPI == EPI_RESID_F32 ? 63 : ((F & F_ODUP) ? 44 : 60));
-      if (EK::SPL && FIRST && has_prev && !((F & F_BEARLY) && wr == 1))
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SPL_VM) : "memory");
-      else if (FIRST && has_prev && EK::RES && !((F & F_BEARLY) && wr == 1))
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(ABL == 11 ? 20 : 28) : "memory");
-      else if (FIRST && has_prev && ABL != 10 && !((F & F_BEARLY) && wr == 1)) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
-      // (F_BEARLY, lagging group: its stores are OLDER than phase 1's DMAs, so vmcnt(4) below also
-      // retires them -- issued three barrier intervals earlier)
-      else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      // on a tile's first pair the previous tile's epilogue (phase 1, after its DMAs) is younger than
+      // the awaited K-tile as well: VM::FIRST_P4.  (F_BEARLY, lagging group: its epilogue ran at the
+      // previous tile's phase 8, OLDER than phase 1's DMAs, so VM::YOUNGER also retires it --
+      // issued three barrier intervals earlier)
+      if (FIRST && has_prev && !((F & F_BEARLY) && wr == 1)) vm_wait<VM::FIRST_P4>();
+      else vm_wait<VM::YOUNGER>();
       if (FIRST) stamp(3);   // S3: first pair's phase-4 wait passed
     }
     if (P == 8 && FIRST) stamp(4);   // S4: before the first pair's phase-8 wait (the stores must be done)
-    if (P == 8) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    if (P == 8) vm_wait<VM::YOUNGER>();
     if (P == 8 && FIRST) stamp(5);   // S5: after it
     if (P == 8 && LAST && has_next)   // next tile's bias (+ LN vectors), older than phase 1's DMAs
       stage_vectors(nxt_m0, nxt_n0, cpar ^ 1);
@@ -867,7 +927,7 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
   issue(H_B0, 0);
   issue(H_A0, 1);
   issue(H_B1, 1);
-  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  vm_wait<VM::YOUNGER>();   // the even K-tile (and the vectors) landed
   barrier();
   if (wr == 1) barrier();   // stagger the two M-groups by one barrier
 
@@ -901,7 +961,7 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
 #pragma unroll
     for (int i = 0; i < 9; ++i) g_probe8q[(blockIdx.x * 2 + wr) * 9 + i] = st[i];
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // trailing (dummy) DMAs land before the workgroup's LDS is released
+  vm_wait<0>();   // trailing (dummy) DMAs land before the workgroup's LDS is released
 }
 
 }  // namespace

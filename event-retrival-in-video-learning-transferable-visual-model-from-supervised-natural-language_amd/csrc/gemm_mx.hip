@@ -298,25 +298,26 @@ __global__ __launch_bounds__(512) void gemm_mxpp_kernel(GemmArgs a) {
   const uint8_t* ssrc = (wave & 2) ? a.w_scale + (int64_t)(n0 + 2 * spair) * 2
                                    : a.a_scale + (int64_t)min(m0 + 2 * spair, m_pad - 2) * 2;
   const int64_t sstage = (wave & 2) ? (int64_t)a.N * 2 : (int64_t)m_pad * 2;
+  // counted waits (common.hpp vm_wait): a stage is OPS_AW row DMAs per wave (DMA_ROWS instructions
+  // of 16 rows for A and for W) plus, in group 0, one scale dword; vmcnt retires in issue order
+  constexpr int DMA_ROWS = 2;
+  constexpr int OPS_AW = 2 * DMA_ROWS, OPS_SC = 1;
+  constexpr int OPS0 = OPS_AW + OPS_SC, OPS1 = OPS_AW;
+  static_assert((LEAD - 1) * OPS0 <= VM_MAX, "the stages in flight exceed vmcnt's 6-bit field");
   auto issue = [&](int st) {
     char* base = smem + (st % RING) * STAGE;
+    int n = 0;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) glds16(asrc[j] + st * SB, base + (wave * 2 + j) * 1024);
+    for (int j = 0; j < DMA_ROWS; ++j, ++n) glds16(asrc[j] + st * SB, base + (wave * 2 + j) * 1024);
 #pragma unroll
-    for (int j = 0; j < 2; ++j) glds16(wsrc[j] + st * SB, base + A_BYTES + (wave * 2 + j) * 1024);
-    if (grp == 0) glds4(ssrc + (st >> 1) * sstage, smem + RING * STAGE + (st % RING) * SC + (wave & 3) * 256);
+    for (int j = 0; j < DMA_ROWS; ++j, ++n) glds16(wsrc[j] + st * SB, base + A_BYTES + (wave * 2 + j) * 1024);
+    if (MICLIP_VMCHECK) vm_count_check<OPS_AW>(n);
+    if (grp == 0) glds4(ssrc + (st >> 1) * sstage, smem + RING * STAGE + (st % RING) * SC + (wave & 3) * 256);   // OPS_SC
   };
-  auto wait_stage = [&](int g1) {  // retire this wave's DMA for stage g1 (5 ops per stage in group 0, 4 in group 1)
+  auto wait_stage = [&](int g1) {  // retire this wave's DMAs for stage g1: up to LEAD - 1 younger stages
     const int younger = min(LEAD - 1, nk - 1 - g1);
-    if (grp == 0) {
-      if (younger >= 2) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-      else if (younger == 1) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else {
-      if (younger >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else if (younger == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    if (grp == 0) vm_wait_stages<OPS0, LEAD - 1>(younger);
+    else vm_wait_stages<OPS1, LEAD - 1>(younger);
   };
   auto barrier = [&]() {
     __builtin_amdgcn_sched_barrier(0);

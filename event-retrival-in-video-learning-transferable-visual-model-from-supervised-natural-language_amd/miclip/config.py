@@ -59,12 +59,30 @@ class CLIPConfig:
         f += 2.0 * W * self.embed_dim                        # CLS projection
         return f
 
-    def image_flops_executed(self, cls_last: bool = True) -> float:
+    def image_attention_flops(self, last_query_rows: int | None = None) -> float:
+        """QK^T and PV of all layers per frame; ``last_query_rows``: the query rows the last
+        layer's attention computes (the CLS-row last block computes the CLS query's tile only)."""
+        W, S, L = self.vision_width, self.vision_tokens, self.vision_layers
+        r = S if last_query_rows is None else min(S, last_query_rows)
+        return 4.0 * S * S * W * (L - 1) + 4.0 * r * S * W
+
+    def image_flops_executed(self, cls_last: bool = True, q_cls: bool = False,
+                             last_query_rows: int | None = None) -> float:
         """image_flops less the work the last block skips when it runs its row-wise part on the
-        CLS rows only (api.cpp last_block_cls: out_proj, c_fc and c_proj for S - 1 of S rows per
-        frame; their outputs are never read)."""
+        CLS rows only (api.cpp last_block_cls / run_tower_mx: out_proj, c_fc and c_proj for S - 1
+        of S rows per frame; their outputs are never read); ``q_cls``: its in_proj also computes Q
+        for the CLS rows only (the LN-folded bf16 and the fp32 towers; 2 (S - 1) W^2 less);
+        ``last_query_rows``: its attention computes that many query rows (the CLS query's tile)."""
         W, S = self.vision_width, self.vision_tokens
-        return self.image_flops() - (2.0 * (S - 1) * W * (W + 4 * W + 4 * W) if cls_last else 0.0)
+        f = self.image_flops()
+        if cls_last:
+            f -= 2.0 * (S - 1) * W * (W + 4 * W + 4 * W)
+        if q_cls:
+            f -= 2.0 * (S - 1) * W * W
+        return f - (self.image_attention_flops() - self.image_attention_flops(last_query_rows))
+
+    def text_attention_flops(self) -> float:
+        return 4.0 * self.context_length * self.context_length * self.text_width * self.text_layers
 
     def text_flops(self) -> float:
         W, S, L = self.text_width, self.context_length, self.text_layers

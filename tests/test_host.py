@@ -34,6 +34,31 @@ def test_executed_flops_of_the_cls_row_last_block():
     assert b32.image_flops_executed(False) == b32.image_flops()
     assert b32.image_flops() - b32.image_flops_executed() == 2.0 * (S - 1) * W * 9 * W
     assert 0.93 < b32.image_flops_executed() / b32.image_flops() < 0.95
+    # the last in_proj's Q for the CLS rows only, and its attention for the CLS query's 16-row tile
+    assert b32.image_flops_executed() - b32.image_flops_executed(True, True) == 2.0 * (S - 1) * W * W
+    assert (b32.image_flops_executed(True, True) - b32.image_flops_executed(True, True, 16)
+            == 4.0 * (S - 16) * S * W)
+    assert b32.image_attention_flops() == 4.0 * S * S * W * b32.vision_layers
+
+
+def test_bench_step_work_and_mfma_fraction():
+    """bench.py's end-to-end MFMA fraction: executed work per engine at its dense peak (ADVICE r5:
+    the MX-fp8 tower's CLS-row last block counted; VERDICT r5: the fp32 parity mode no longer
+    reports f32-equivalent flops over the f32 peak, a fraction above 1)."""
+    import bench
+    from miclip import config
+    b32, l336 = config.get_config("ViT-B/32"), config.get_config("ViT-L/14@336px")
+    w = bench.step_work(b32, "bf16", 10_000, True)
+    assert w["cls_last"] and w["image"] == b32.image_flops_executed(True, True, 16)
+    assert not bench.step_work(b32, "bf16", 200, True)["cls_last"]        # < 256 frames per chunk
+    w8 = bench.step_work(l336, "fp8", 863, False)
+    assert w8["cls_last"] and w8["image"] == l336.image_flops_executed(True)   # MX: no Q / attention skip
+    w32 = bench.step_work(b32, "fp32", 10_000, False)
+    assert w32["image"] == b32.image_flops_executed(True, True, 32)
+    t16 = bench.mfma_time_at_peak(w, "bf16", 10_000, 32, 512)
+    t32 = bench.mfma_time_at_peak(w32, "fp32", 10_000, 32, 512)
+    assert 0.03 < t16 < 0.04            # ~35 ms of bf16 MFMA work at 2.5 PF for 10k B/32 frames
+    assert 3 * t16 < t32 < 5 * t16      # 3x the products on the f16 MFMA + exact-f32 attention
 
 
 def test_pack_order_covers_state_dict():
