@@ -696,13 +696,17 @@ __global__ __launch_bounds__(NT) void rank_merge_kernel(const float* __restrict_
 
 // The split merge's second launch (rank_keys.hpp lines_publish): one workgroup per query
 // reduces the pass's nlines slab lines (one per pass workgroup: its top-k, sorted desc), thread
-// w loading line w whole.  A cut first: the k-th largest key among a wave's 64 line heads (k
-// distinct rows score at least that much, so the query's k-th does too), the largest such over
-// the waves and gtau (the largest workgroup k-th); sorting the heads' keys across the lanes is a
-// 21-step bitonic network of 32-bit shuffles.  Each line's prefix at or above the cut (ties on the
-// key kept) is appended to LDS, and thread j ranks appended entry j by counting the entries that
-// beat it (packed keys are unique: index asc breaks ties) -- the in-launch reducer's rule, so
-// results are bit-identical.  gtau alone kept ~800 of 2450 entries at 125k rows (a 117-us count).
+// w loading line w whole.  A cut first: the k-th largest PACKED entry (key, ~index) among a wave's
+// 64 line heads (k distinct rows rank at least that high, so the query's k-th does too), the
+// largest such over the waves and gtau (the largest workgroup k-th key); sorting the heads across
+// the lanes is a 21-step bitonic network of 64-bit (two 32-bit) shuffles.  Each line's prefix at
+// or above the cut is appended to LDS, and thread j ranks appended entry j by counting the entries
+// that beat it (packed entries are unique: index asc breaks ties) -- the in-launch reducer's rule,
+// so results are bit-identical.  gtau alone kept ~800 of 2450 entries at 125k rows (a 117-us
+// count).  The cut is on the packed entry, not its 32-bit key alone: under mass ties
+// (duplicate or static frames: every line's prefix ties the cut key) a key cut kept all nlines x k
+// entries and the quadratic count took milliseconds; the packed cut keeps the ~k lines whose heads
+// beat the k-th head, ~k^2 entries.
 // gate (nullable): a query block whose queries are all certified holds its results (the
 // gated exact pass skipped it), so its queries are skipped here too.
 template <int NT>
@@ -712,7 +716,7 @@ __global__ __launch_bounds__(NT) void fold_merge_kernel(const uint64_t* __restri
                                                         int64_t* __restrict__ out_i, const int32_t* __restrict__ gate) {
   extern __shared__ __attribute__((aligned(16))) char fm_lds[];   // cnt, cut, then nlines x k entries
   uint32_t& cnt = *(uint32_t*)fm_lds;
-  uint32_t& cutk = *((uint32_t*)fm_lds + 1);
+  unsigned long long& cut64 = *((unsigned long long*)fm_lds + 1);
   uint64_t* buf = (uint64_t*)(fm_lds + 16);
   const int tid = threadIdx.x, lane = tid & 63;
   const int64_t q = blockIdx.x;
@@ -722,7 +726,7 @@ __global__ __launch_bounds__(NT) void fold_merge_kernel(const uint64_t* __restri
   }
   if (tid == 0) {
     cnt = 0u;
-    cutk = gtau[q];
+    cut64 = (unsigned long long)gtau[q] << 32;   // every entry below has a key below gtau
   }
   const int nld = (k + 1) >> 1;   // 16-byte pieces of a line holding k entries
   typedef unsigned int u32x4m __attribute__((ext_vector_type(4)));
@@ -739,24 +743,28 @@ __global__ __launch_bounds__(NT) void fold_merge_kernel(const uint64_t* __restri
       e[2 * c + 1] = ((uint64_t)pc[c][3] << 32) | pc[c][2];
     }
   }
-  // the wave's line heads' keys sorted descending across the lanes (an empty head sorts as key 0;
-  // a real key 0 is a NaN-last row, which then only makes the cut 0: no cut)
-  uint32_t hk = e[0] ? (uint32_t)(e[0] >> 32) : 0u;
+  // the wave's line heads sorted descending across the lanes (an empty head -- and a missing line --
+  // sorts as 0; a real entry with key 0 is a NaN-last row, whose head then only makes the cut 0: none)
+  uint64_t hk = e[0];
 #pragma unroll
   for (int size = 2; size <= 64; size <<= 1)
 #pragma unroll
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      const uint32_t o = (uint32_t)__shfl_xor((int)hk, stride, 64);
+      const uint32_t olo = (uint32_t)__shfl_xor((int)(uint32_t)hk, stride, 64);
+      const uint32_t ohi = (uint32_t)__shfl_xor((int)(uint32_t)(hk >> 32), stride, 64);
+      const uint64_t o = ((uint64_t)ohi << 32) | olo;
       const bool lower = (lane & stride) == 0;        // this lane holds the pair's first position
       const bool desc = (lane & size) == 0 || size == 64;
-      const uint32_t mx = hk > o ? hk : o, mn = hk > o ? o : hk;
+      const uint64_t mx = hk > o ? hk : o, mn = hk > o ? o : hk;
       hk = (lower == desc) ? mx : mn;
     }
-  const uint32_t kth_head = (uint32_t)__shfl((int)hk, k - 1, 64);
-  __syncthreads();   // cnt / cutk initialised
-  if (lane == 0 && kth_head) atomicMax(&cutk, kth_head);
+  const uint32_t klo = (uint32_t)__shfl((int)(uint32_t)hk, k - 1, 64);
+  const uint32_t khi = (uint32_t)__shfl((int)(uint32_t)(hk >> 32), k - 1, 64);
+  const uint64_t kth_head = ((uint64_t)khi << 32) | klo;
+  __syncthreads();   // cnt / cut64 initialised
+  if (lane == 0 && kth_head) atomicMax(&cut64, (unsigned long long)kth_head);
   __syncthreads();
-  const uint64_t cut = (uint64_t)cutk << 32;
+  const uint64_t cut = cut64;
   int m = 0;   // the line's prefix at or above the cut (sorted desc, zeros after)
 #pragma unroll
   for (int p = 0; p < 16; ++p) m += (p < k && e[p] != 0ull && e[p] >= cut) ? 1 : 0;

@@ -2,7 +2,7 @@
 # block), then the whole GPU suite, smoke and the bench line on the counted-wait tree
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/r6a
-timeout -k 10 600 python -u -m pytest tests/test_gpu_config_scale.py -v -s --timeout 300 --timeout-method thread \
+timeout -k 10 600 python -u -m pytest tests/test_gpu_config_scale.py "tests/test_gpu_rank.py::test_split_merge_static_frames_no_cliff" -v -s --timeout 300 --timeout-method thread \
   > gpurun_out/r6a/pytest_config_scale.log 2>&1 || { grep -E "FAILED|Error|passed|failed|assert" gpurun_out/r6a/pytest_config_scale.log | tail -30; exit 1; }
 grep -E "chunk|passed|failed" gpurun_out/r6a/pytest_config_scale.log | tail -6
 timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread --ignore=tests/test_gpu_config_scale.py \

@@ -391,6 +391,41 @@ def test_in_launch_merge_mass_ties(gpu, D, k):
             np.testing.assert_array_equal(i[r], want, err_msg=f"query {r} {pol}")
 
 
+@pytest.mark.parametrize("D", [512, 768])
+def test_split_merge_static_frames_no_cliff(gpu, D):
+    """a corpus of identical rows (a static video: every frame embeds alike) ties every
+    workgroup's whole top-k on one key.  The split merge (rank.hip fold_merge_kernel) cuts on the
+    packed (key, ~index) entry, so it appends ~k^2 entries instead of all nlines x k and its
+    quadratic rank-by-counting stays small: the call is bit-exact (the k lowest indices, one score)
+    and costs no more than ranking a random corpus of the same size, beyond noise.  D = 512 takes
+    rank_reg (256 workgroups), D = 768 rank_stream (up to 512)."""
+    import torch
+    from miclip import retrieval, weights
+    N, Q, k = 200_000, 32, 10
+    row = weights.normal(61, "static", (1, D))
+    same = _t(np.repeat(row, N, axis=0), gpu)
+    rand = _t(weights.normal(62, "random", (N, D)), gpu)
+    q = _t(weights.synthetic_corpus(Q, D, seed=63), gpu)
+    s, i = retrieval.rank_topk(same, q, k)
+    torch.cuda.synchronize()
+    assert (i.cpu().numpy() == np.arange(k)[None, :]).all()
+    sc = s.cpu().numpy()
+    assert (sc == sc[:, :1]).all()
+
+    def timed(c, n=20):
+        retrieval.rank_topk(c, q, k)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(n):
+            retrieval.rank_topk(c, q, k)
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) * 1e3 / n
+    t_same, t_rand = timed(same), timed(rand)
+    print(f"D {D}: identical rows {t_same:.1f} us, random rows {t_rand:.1f} us per call")
+    assert t_same < 1.5 * t_rand + 30.0, (t_same, t_rand)
+
+
 def _ranked_both_ways(monkeypatch, c, q, k, **kw):
     """mi_rank_topk through the A/B build with the certified pass forced on for
     every eligible call (MICLIP_RANK_CERT=2) and switched off (0)."""
