@@ -44,6 +44,7 @@ SHAPES = {
     "lnfcL": (428459, 4096, 1024, 7),   # ViT-L/14 c_fc (1667 frames x 257 tokens)
     "lnqkvL": (428459, 3072, 1024, 6),   # ViT-L/14 in_proj
     "lnqkv250": (250000, 2304, 768, 6),
+    "lnqkv100": (100000, 2304, 768, 6), "lnfc100": (100000, 3072, 768, 7),
     "lnfc250": (250000, 3072, 768, 7),
     # residual add fused into out_proj / c_proj (epi 8, mi_op_gemm_residual: x16 half-slot stream
     # read + written in the epilogue, row partials, residual_finalize); variant 1 = the unfused
