@@ -86,6 +86,14 @@ constexpr int F_BEARLY = 512;
 // flag: the same choice as a runtime branch around the second y1 store made the in-loop epilogues of
 // large grids produce non-finite rows at random (measured, scripts/gpu_r5zq.sh)
 constexpr int F_ODUP = 1024;
+// F_DYN (A/B): tiles handed out in order by a per-XCD counter instead of the static stride G, so
+// the CUs that share an m-block's A rows (its n-tiles on consecutive CUs of one XCD) cannot drift
+// apart over the launch: each CU takes the XCD's next unclaimed tile when it starts one.  The
+// claim for the tile after next goes out at a tile's start (one lane's atomic, before phase 1's
+// DMAs: older than the awaited K-tile, so the phase-4 wait retires it) and reaches the other waves
+// through an LDS slot
+constexpr int F_DYN = 2048;
+__device__ unsigned g_dyn8q[8];   // F_DYN: per-XCD claim counters, zeroed before each launch
 
 __device__ __forceinline__ f32x2 quick_gelu2_8q(f32x2 v) {
   const f32x2 t = v * (f32x2){-2.45546696f, -2.45546696f};   // -1.702 * log2(e)
@@ -215,7 +223,7 @@ template <int EPI, int ABL = 0, int F = 0, bool OPF16 = false>
 __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
   using EK = EpiKind8q<EPI>;
   using VM = Vm8q<EPI, ABL, F>;
-  __shared__ __attribute__((aligned(16))) char smem[EK::LDS];
+  __shared__ __attribute__((aligned(16))) char smem[EK::LDS + ((F & F_DYN) ? 16 : 0)];
   float* sbias = (float*)(smem + 2 * BUF);
   float* srs = (float*)(smem + 2 * BUF + 2 * BN * 4);              // LN: [2][BM][2]
   float* scol = (float*)(smem + 2 * BUF + 2 * BN * 4 + 2 * BM * 8);  // LN: [2][BN]
@@ -237,9 +245,48 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
     nn = nb * BN;
   };
 
+  // F_DYN: this XCD's logical tile range [dxs, dxe) (xcd_remap's), tiles in logical order
+  constexpr bool DYN = (F & F_DYN) != 0;
+  const int dxcd = blockIdx.x & 7;
+  const int dq = ntiles >> 3, dr = ntiles & 7;
+  const int dxs = dxcd < dr ? dxcd * (dq + 1) : dr * (dq + 1) + (dxcd - dr) * dq;
+  const int dxe = dxs + dq + (dxcd < dr ? 1 : 0);
+  auto coords_l = [&](int t, int& mm, int& nn) {
+    int mb, nb;
+    tile_coords_8q(t, tiles_m, tiles_n, a.ngroup, mb, nb);
+    mm = mb * BM;
+    nn = nb * BN;
+  };
+  const uint32_t dyn_slot = (uint32_t)(uintptr_t)(const LDS_AS char*)(smem + EK::LDS);
+  // claim the XCD's next tile: lane 0's atomic, in asm with exec = lane 0 (no branch): hipcc's own
+  // waitcnt pass drained every VMEM op in flight right after a compiler-visible atomic.  The
+  // caller retires it with a counted wait (an op older than the awaited DMAs: vmcnt retires in
+  // order, and an op the compiler does not see only makes its own waits over-wait)
+  auto dyn_claim = [&]() {
+    unsigned got = 0;
+    unsigned long long sv;
+    const unsigned one = 1u;
+    unsigned* ctr = &g_dyn8q[dxcd];
+    asm volatile("s_mov_b64 %1, exec\n\ts_mov_b64 exec, 1\n\tglobal_atomic_add %0, %2, %3, off sc0\n\ts_mov_b64 exec, %1"
+                 : "+v"(got), "=&s"(sv) : "v"(ctr), "v"(one) : "memory");
+    return got;
+  };
+  auto dyn_publish = [&](unsigned got) {   // wave 0, after the wait that retired the claim
+    asm volatile("" : "+v"(got));
+    const int t = dxs + (G >> 3) + (int)__builtin_amdgcn_readlane(got, 0);
+    asm volatile("ds_write_b32 %0, %1" ::"v"(dyn_slot), "v"(t) : "memory");
+  };
+  auto dyn_read = [&]() {
+    int t;
+    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(t) : "v"(dyn_slot) : "memory");
+    return __builtin_amdgcn_readfirstlane(t);
+  };
+  int dyn_next = 0;   // F_DYN: the tile after the current one (the restage cursor's next)
+  unsigned dyn_got = 0;
   // ---- restage cursor: K-tile pair rpp of tile rv (origin rm0, rn0)
-  int rv = blockIdx.x, rpp = 0, rm0, rn0;
-  coords(rv, rm0, rn0);
+  int rv = DYN ? dxs + (int)(blockIdx.x >> 3) : (int)blockIdx.x, rpp = 0, rm0, rn0;
+  if constexpr (DYN) coords_l(rv, rm0, rn0);
+  else coords(rv, rm0, rn0);
   const int drow = lane >> 3;
   const int c0 = (lane & 7) ^ (lane >> 4), c1 = (lane & 7) ^ (4 + (lane >> 4));
   // per-lane byte offsets of this thread's two DMA rows in each half-tile
@@ -265,10 +312,18 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
   auto advance = [&]() {
     if (++rpp == npairs) {
       rpp = 0;
-      rv += G;
-      if (rv < ntiles) {   // past the end: keep re-loading the last tile's valid rows
-        coords(rv, rm0, rn0);
-        if (!(F & F_GLDS)) make_rs();
+      if constexpr (DYN) {
+        rv = dyn_next;
+        if (rv < dxe) {   // past the end: keep re-loading the last tile's valid rows
+          coords_l(rv, rm0, rn0);
+          make_rs();
+        }
+      } else {
+        rv += G;
+        if (rv < ntiles) {   // past the end: keep re-loading the last tile's valid rows
+          coords(rv, rm0, rn0);
+          if (!(F & F_GLDS)) make_rs();
+        }
       }
     }
   };
@@ -773,6 +828,10 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
     constexpr int b = P <= 4 ? 0 : 1;
     constexpr int q = (P - 1) & 3;
     const char* rbuf = smem + b * BUF;
+    if constexpr (DYN) if (P == 1 && FIRST && wave == 0 && has_next) {   // the tile after next, before phase 1's DMAs
+      dyn_got = dyn_claim();
+      __builtin_amdgcn_sched_barrier(0);
+    }
     if (P == 1 && FIRST) {
       stamp(0);   // S0: tile start
       if ((ABL == 9 || ABL == 10) && ti == 2) st[7] = __builtin_amdgcn_s_memrealtime();
@@ -841,6 +900,7 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
       // issued three barrier intervals earlier)
       if (FIRST && has_prev && !((F & F_BEARLY) && wr == 1)) vm_wait<VM::FIRST_P4>();
       else vm_wait<VM::YOUNGER>();
+      if constexpr (DYN) if (FIRST && wave == 0 && has_next) dyn_publish(dyn_got);   // (retired: older than phase 1's DMAs)
       if (FIRST) stamp(3);   // S3: first pair's phase-4 wait passed
     }
     if (P == 8 && FIRST) stamp(4);   // S4: before the first pair's phase-8 wait (the stores must be done)
@@ -918,9 +978,11 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
   // ---- prologue: tile 0's bias, the whole even K-tile and the odd A_m0 / B_n1 of pair 0
   {
     int m0, n0;
-    coords(blockIdx.x, m0, n0);
+    if constexpr (DYN) coords_l(rv, m0, n0);
+    else coords(blockIdx.x, m0, n0);
     stage_vectors(m0, n0, 0);
   }
+  if constexpr (DYN) if (wave == 0) dyn_got = dyn_claim();   // the second tile, retired by the prologue's wait
   issue(H_A0, 0);
   issue(H_B1, 0);
   issue(H_A1, 0);
@@ -928,16 +990,28 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
   issue(H_A0, 1);
   issue(H_B1, 1);
   vm_wait<VM::YOUNGER>();   // the even K-tile (and the vectors) landed
+  if constexpr (DYN) if (wave == 0) {   // (landed before the barrier: the other waves read it right after)
+    dyn_publish(dyn_got);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
   barrier();
   if (wr == 1) barrier();   // stagger the two M-groups by one barrier
 
-  for (int v = blockIdx.x; v < ntiles; v += G) {
+  int dcur = rv, dnext = DYN ? dyn_read() : 0;   // F_DYN: the current and the next tile
+  for (int v = blockIdx.x; DYN ? dcur < dxe : v < ntiles; v += G) {
     int cm0, cn0;
-    coords(v, cm0, cn0);
+    if constexpr (DYN) {
+      coords_l(dcur, cm0, cn0);
+      has_next = dnext < dxe;
+      if (has_next) coords_l(dnext, nxt_m0, nxt_n0);
+      dyn_next = dnext;
+    } else {
+      coords(v, cm0, cn0);
+      has_next = v + G < ntiles;
+      if (has_next) coords(v + G, nxt_m0, nxt_n0);
+    }
     cur_m0 = cm0;
     cur_n0 = cn0;
-    has_next = v + G < ntiles;
-    if (has_next) coords(v + G, nxt_m0, nxt_n0);
     // (npairs >= 2, gemm_8q_ok: a one-pair instance beside these made hipcc spill ~200 VGPRs)
     pair(BoolC<true>{}, BoolC<false>{});
     for (int pp = 1; pp < npairs - 1; ++pp) pair(BoolC<false>{}, BoolC<false>{});
@@ -950,6 +1024,10 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
     ppar = cpar;
     has_prev = true;
     cpar ^= 1;
+    if constexpr (DYN) {   // the claim published in this tile's first pair: the tile after next
+      dcur = dnext;
+      if (has_next) dnext = dyn_read();
+    }
   }
   // the last tile's epilogue
   if (wr == 0) barrier();   // the M-groups' barrier counts meet
@@ -1063,6 +1141,23 @@ hipError_t gemm_8q(const GemmArgs& a0, int epi, hipStream_t s, int cus, int mode
     // weight panel from L2, profiles/r05_b_fullnt_gemm_traffic_ab.json).  Both: the lagging
     // M-group's epilogue beside the leading one's (F_BEARLY): c_fc 2143-2149 vs 2230 us, qkv 1606
     // vs 1615 us, bit-identical (profiles/r05_f_lnfc.log, r05_f_lnqkv.log)
+#if MICLIP_AB   // A/B (MICLIP_8Q_DYN=1): the product flags + per-XCD claimed tile order (F_DYN)
+    if (const char* dy = std::getenv("MICLIP_8Q_DYN")) {
+      if (std::atoi(dy) == 1 && grid % 8 == 0 && nt >= grid) {
+        void* ctr = nullptr;
+        if (hipGetSymbolAddress(&ctr, HIP_SYMBOL(g_dyn8q)) != hipSuccess) return hipErrorInvalidSymbol;
+        const hipError_t e = hipMemsetAsync(ctr, 0, sizeof(unsigned) * 8, s);
+        if (e != hipSuccess) return e;
+        if (epi == EPI_LN_BF16)
+          hipLaunchKernelGGL((gemm_8q_kernel<EPI_LN_BF16, 0, F_DYN | F_BEARLY | F_FULL | F_ONT, true>), dim3(grid), dim3(512), 0, s, a);
+        else
+          hipLaunchKernelGGL(
+              (gemm_8q_kernel<EPI_LN_GELU_BF16, 0, F_DYN | F_BEARLY | F_GPK | F_ONT | F_FULL | F_GSTAGE16 | F_GSTAGE | F_VOREC, true>),
+              dim3(grid), dim3(512), 0, s, a);
+        return hipGetLastError();
+      }
+    }
+#endif
     if (epi == EPI_LN_BF16)
       hipLaunchKernelGGL((gemm_8q_kernel<EPI_LN_BF16, 0, F_BEARLY | F_FULL | F_ONT, true>), dim3(grid), dim3(512), 0, s, a);
     else

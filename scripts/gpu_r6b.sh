@@ -2,6 +2,17 @@
 # c_fc / in_proj over M (does the A re-fetch grow with the pass length? -- CU drift hypothesis)
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/r6b
+# the per-XCD claimed tile order (F_DYN, A/B) against the product c_fc / in_proj: timing + maxdiff,
+# then its FETCH / WRITE
+LN_FLAGS=1 timeout -k 10 180 python3 scripts/gemm_micro.py 20 lnfc500,lnqkv500 0,10000 > gpurun_out/r6b/dyn_micro.log 2>&1 || { tail -20 gpurun_out/r6b/dyn_micro.log; exit 1; }
+cat gpurun_out/r6b/dyn_micro.log | grep -v amdgpu.ids
+for c in FETCH_SIZE WRITE_SIZE; do
+  GEMM_MICRO_V0=1 MICLIP_8Q_DYN=1 timeout -s KILL 180 rocprofv3 --pmc $c --output-format csv -d gpurun_out/r6b/pmcdyn/$c -o run -- \
+    python3 scripts/gemm_micro.py 1 lnfc500,lnqkv500 > gpurun_out/r6b/pmcdyn_$c.log 2>&1 || exit $?
+done
+GEMM_MICRO_V0=1 MICLIP_8Q_DYN=1 timeout -s KILL 180 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES TCC_HIT_sum TCC_MISS_sum \
+  --output-format csv -d gpurun_out/r6b/pmcdyn/MFMA -o run -- python3 scripts/gemm_micro.py 1 lnfc500,lnqkv500 > gpurun_out/r6b/pmcdyn_MFMA.log 2>&1 || exit $?
+python3 scripts/pmc_traffic.py gpurun_out/r6b/pmcdyn lnfc500,lnqkv500 gpurun_out/r6b/r06_b_gemm_traffic_dyn.json
 timeout -k 10 900 python -u -m pytest tests -m gpu -q -rA --timeout 300 --timeout-method thread \
   > gpurun_out/r6b/pytest_gpu.log 2>&1 || { grep -E "FAILED|Error|passed|failed" gpurun_out/r6b/pytest_gpu.log | tail -30; exit 1; }
 tail -2 gpurun_out/r6b/pytest_gpu.log
