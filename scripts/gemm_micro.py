@@ -117,9 +117,15 @@ def main():
             if ln:   # LN_FLAGS=1: variant v = gemm_8q epilogue flags (MICLIP_8Q_F, A/B build)
                 # (+ 10000: the per-XCD claimed tile order, MICLIP_8Q_DYN=1; without LN_FLAGS the
                 # process environment's MICLIP_8Q_DYN stands, for PMC passes)
+                # (19999 / 200xx: the product kernel with tile-order group width -1 (m-major) / xx,
+                # MICLIP_8Q_NG)
                 if os.environ.get("LN_FLAGS"):
-                    os.environ["MICLIP_8Q_DYN"] = "1" if v >= 10000 else "0"
-                os.environ["MICLIP_8Q_F"] = str(v % 10000)
+                    os.environ["MICLIP_8Q_DYN"] = "1" if 10000 <= v < 19999 else "0"
+                    if v >= 19999:
+                        os.environ["MICLIP_8Q_NG"] = str(v - 20000)
+                    else:
+                        os.environ.pop("MICLIP_8Q_NG", None)
+                os.environ["MICLIP_8Q_F"] = str(v % 10000) if v < 19999 else "0"
                 N.check(L.mi_op_gemm_ln(A.data_ptr(), 2 * K, rs.data_ptr(), W.data_ptr(), colsum.data_ptr(),
                                         bias.data_ptr(), outs[v].data_ptr(), M, Nn, K, epi - 6, sp), "gemm_ln")
                 return
