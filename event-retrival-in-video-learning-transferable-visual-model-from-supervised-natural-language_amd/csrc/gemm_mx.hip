@@ -25,6 +25,8 @@
 // LDS row image: 16-byte chunk c of row r sits in slot c ^ ((r >> 1) & 5), so
 // the two 16-byte reads of every fragment (chunks 2g, 2g+1 for lane group g)
 // hit 16 distinct bank quads per ds_read_b128 lane group (exhaustive search).
+#include <cstdlib>
+
 #include "common.hpp"
 #include "internal.hpp"
 
@@ -475,6 +477,278 @@ __global__ __launch_bounds__(512) void gemm_mxpp_kernel(GemmArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Persistent MX-fp8 ping-pong (round 6; configs[4]): gemm_mxpp_kernel's
+// stage, fragment, MFMA and epilogue arithmetic (bit-identical results) with one workgroup per
+// CU walking its tiles as gemm.hip's gemm_ppp_kernel does for bf16.  At K = 1024 a non-persistent
+// tile paid a fixed ~8.6 us of its ~25 us (launch, the first LEAD stages' DMA latency exposed,
+// the ring draining over its last LEAD stages) -- the K sweep of round 5: c_proj (K = 4096) ran
+// at 0.37 of the fp8 peak, c_fc (K = 1024) at 0.27.  Here the stages of all of a workgroup's
+// tiles are one stream through the ring: the next tile's first LEAD stages (with its bias, by
+// LDS-DMA into a parity slot) are issued in this tile's last LEAD iterations, so they land under
+// this tile's MFMAs and epilogue.  Counted waits: a stage is OPS_AW row DMAs (+ the scale dword in
+// group 0); the previous tile's NSTORE epilogue stores are younger than the next tile's first
+// LEAD stages and older than every later one, so the waits add them while waiting for stages
+// < LEAD; a partial last m-tile (an unknown store count) drains with vmcnt(0) instead.
+__device__ __forceinline__ float4 mx_lds_f4(const float* p) {   // (an LDS read hipcc does not see)
+  float4 v;
+  const uint32_t addr = (uint32_t)(uintptr_t)(const LDS_AS float*)p;
+  asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(addr) : "memory");
+  return v;
+}
+
+template <int EPI>
+__global__ __launch_bounds__(512) void gemm_mxppp_kernel(GemmArgs a) {
+  typedef float f32x16 __attribute__((ext_vector_type(16)));
+  constexpr int BM = 256, BN = 256, WTM = 128, WTN = 64;
+  constexpr int SB = 64;                               // k bytes per stage
+  constexpr int RING = 4, LEAD = 3;
+  constexpr int A_BYTES = BM * SB, STAGE = (BM + BN) * SB;
+  constexpr int SC = 1024;                             // scale ring slot
+  // epilogue store instructions per wave of a full tile: GELU_MX 2 row pieces + the scale byte per
+  // 32-row block; bf16 2 (ni) x 2 (ip) per block; f32 2 (ni) x 4 per block
+  constexpr int NSTORE = EPI == EPI_GELU_MX ? 4 * (2 + 1) : EPI == EPI_F32 ? 4 * 2 * 4 : 4 * 2 * 2;
+  constexpr int DMA_ROWS = 2;
+  constexpr int OPS_AW = 2 * DMA_ROWS, OPS_SC = 1;
+  constexpr int OPS0 = OPS_AW + OPS_SC, OPS1 = OPS_AW;
+  static_assert((LEAD - 1) * OPS0 + NSTORE <= VM_MAX, "the ops in flight exceed vmcnt's 6-bit field");
+  __shared__ __attribute__((aligned(16))) char smem[RING * STAGE + RING * SC + 2 * BN * 4];
+  float* sbias = (float*)(smem + RING * STAGE + RING * SC);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int grp = __builtin_amdgcn_readfirstlane(wave >> 2), wc = wave & 3;
+  const int tiles_n = a.N / BN;
+  const int tiles_m = (a.M + BM - 1) / BM;
+  const int ntiles = tiles_m * tiles_n;
+  const int nk = a.K / SB;
+  const int m_pad = (a.M + 1) & ~1;
+  const uint8_t* A = (const uint8_t*)a.A;
+  const uint8_t* Wt = (const uint8_t*)a.W;
+  auto coords = [&](int v, int& mm, int& nn) {   // grid % 8 == 0 keeps a WG's tiles on its XCD's run
+    const int t = xcd_remap(v, ntiles);
+    mm = (t / tiles_n) * BM;
+    nn = (t % tiles_n) * BN;
+  };
+  int vb = blockIdx.x, m0, n0;
+  coords(vb, m0, n0);
+
+  const int lrow = lane >> 2;
+  const int lchunk = ((lane & 3) ^ pp_swz(lane >> 4)) * 16;
+  const int spair = (wave & 1) * 64 + lane;
+  const int64_t sstage = (wave & 2) ? (int64_t)a.N * 2 : (int64_t)m_pad * 2;
+  const uint8_t* asrc[2];
+  const uint8_t* wsrc[2];
+  const uint8_t* ssrc;
+  auto set_src = [&](int mm, int nn) {
+#pragma unroll
+    for (int j = 0; j < DMA_ROWS; ++j) {
+      asrc[j] = A + (int64_t)min(mm + (wave * 2 + j) * 16 + lrow, a.M - 1) * a.lda + lchunk;
+      wsrc[j] = Wt + (int64_t)(nn + (wave * 2 + j) * 16 + lrow) * a.ldw + lchunk;
+    }
+    ssrc = (wave & 2) ? a.w_scale + (int64_t)(nn + 2 * spair) * 2
+                      : a.a_scale + (int64_t)min(mm + 2 * spair, m_pad - 2) * 2;
+  };
+  auto issue = [&](int st, int slot) {   // stage st of the tile set_src points at -> ring slot
+    char* base = smem + slot * STAGE;
+    int n = 0;
+#pragma unroll
+    for (int j = 0; j < DMA_ROWS; ++j, ++n) glds16(asrc[j] + st * SB, base + (wave * 2 + j) * 1024);
+#pragma unroll
+    for (int j = 0; j < DMA_ROWS; ++j, ++n) glds16(wsrc[j] + st * SB, base + A_BYTES + (wave * 2 + j) * 1024);
+    if (MICLIP_VMCHECK) vm_count_check<OPS_AW>(n);
+    if (grp == 0) glds4(ssrc + (st >> 1) * sstage, smem + RING * STAGE + slot * SC + (wave & 3) * 256);   // OPS_SC
+  };
+  bool pend = false;   // the previous tile's NSTORE stores are in flight, younger than stages 0..LEAD-1
+  int rb = 0, nm0 = 0, nn0 = 0;   // rb: ring slot of this tile's stage 0
+  bool has_next = false;
+  auto wait_stage = [&](int g1) {
+    const int younger = has_next ? LEAD - 1 : min(LEAD - 1, nk - 1 - g1);
+    if (grp == 0) {
+      if (g1 < LEAD && pend) vm_wait_stages<OPS0, LEAD - 1, NSTORE>(younger);
+      else vm_wait_stages<OPS0, LEAD - 1>(younger);
+    } else {
+      if (g1 < LEAD && pend) vm_wait_stages<OPS1, LEAD - 1, NSTORE>(younger);
+      else vm_wait_stages<OPS1, LEAD - 1>(younger);
+    }
+  };
+  auto barrier = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto lgkm_barrier = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  int tpar = 0;   // tile parity: bias slot
+  auto load_bias = [&](int slot, int nn) {   // wave 0: 64 lanes x 16 B = the tile's 256 bias values
+    if (wave == 0 && a.bias) glds16(a.bias + nn + lane * 4, sbias + slot * BN);
+  };
+  load_bias(0, n0);
+  set_src(m0, n0);
+#pragma unroll
+  for (int st = 0; st < LEAD; ++st)
+    if (st < nk) issue(st, st);
+
+  const int lr = lane & 31, h = lane >> 5;
+  const int rd0 = lr * SB + (((2 * h) ^ pp_swz((lr >> 2) & 3)) * 16);
+  const int rd1 = lr * SB + (((2 * h + 1) ^ pp_swz((lr >> 2) & 3)) * 16);
+  while (true) {
+    const int nvb = vb + (int)gridDim.x;
+    has_next = nvb < ntiles;
+    if (has_next) coords(nvb, nm0, nn0);
+    wait_stage(0);
+    barrier();
+    if (grp == 1) barrier();
+    f32x16 acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
+    v8i wf[2], af[4];
+    int sw[2], sa[4];
+    for (int gs = 0; gs < nk; ++gs) {
+      const int slot = (rb + gs) % RING;
+      const char* As = smem + slot * STAGE + (grp * WTM) * SB;
+      const char* Ws = smem + slot * STAGE + A_BYTES + (wc * WTN) * SB;
+      const uint8_t* Sc = (const uint8_t*)(smem + RING * STAGE + slot * SC) + (gs & 1);
+      if (gs + LEAD < nk) {
+        issue(gs + LEAD, (rb + gs + LEAD) % RING);
+      } else if (has_next) {   // the next tile's stage gs + LEAD - nk, the same ring position in the stream
+        const int st = gs + LEAD - nk;
+        if (st == 0) {
+          load_bias(tpar ^ 1, nn0);
+          set_src(nm0, nn0);
+        }
+        issue(st, (rb + gs + LEAD) % RING);
+      }
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) {
+        wf[ni] = lds_frag32(Ws + ni * 32 * SB, rd0, rd1);
+        sw[ni] = lds_u8(Sc + 512 + (wc * WTN + ni * 32 + lr) * 2);
+      }
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) {
+        af[mi] = lds_frag32(As + mi * 32 * SB, rd0, rd1);
+        sa[mi] = lds_u8(Sc + (grp * WTM + mi * 32 + lr) * 2);
+      }
+      if (grp == 1 && gs + 1 < nk) wait_stage(gs + 1);
+      lgkm_barrier();
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(wf[ni], af[mi], acc[mi][ni], 0, 0, 0, sw[ni], 0,
+                                                                        sa[mi]);
+      if (grp == 0 && gs + 1 < nk) wait_stage(gs + 1);
+      barrier();
+    }
+    if (grp == 0) barrier();   // groups realigned; every ring read of this tile is done
+
+    // ---- epilogue of tile (cm0, cn0) (gemm_mxpp_kernel's arithmetic; bias from its LDS slot)
+    const int cm0 = m0, cn0 = n0;
+    int vm_st = 0;   // store instructions of a full tile (MICLIP_VMCHECK: checked against NSTORE)
+    float4 bias[2][4];
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        bias[ni][i] = a.bias ? mx_lds_f4(sbias + tpar * BN + wc * WTN + ni * 32 + 8 * i + 4 * h)
+                             : make_float4(0.f, 0.f, 0.f, 0.f);
+    auto val = [&](int mi, int ni, int j) -> float {
+      const float4 b = bias[ni][j >> 2];
+      const float bb = (j & 3) == 0 ? b.x : (j & 3) == 1 ? b.y : (j & 3) == 2 ? b.z : b.w;
+      const float v = acc[mi][ni][j] + bb;
+      return (EPI == EPI_GELU_BF16 || EPI == EPI_GELU_MX) ? mx_gelu(v) : v;
+    };
+    if constexpr (EPI == EPI_GELU_MX) {
+      const int blk = (cn0 + wc * WTN) >> 6;
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) {
+        const int m = cm0 + grp * WTM + mi * 32 + lr;
+        float v[2][16];
+        float amax = 0.f;
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+          for (int j = 0; j < 16; ++j) {
+            v[ni][j] = val(mi, ni, j);
+            amax = fmaxf(amax, fabsf(v[ni][j]));
+          }
+        const auto sx = __builtin_amdgcn_permlane32_swap(__float_as_uint(amax), __float_as_uint(amax), false, false);
+        amax = fmaxf(__uint_as_float(sx[0]), __uint_as_float(sx[1]));
+        const int X = mx_block_exp(amax);
+        const float inv = ldexpf(1.0f, -X);
+        uint4 q16[2];
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) {
+          uint32_t d[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) d[i] = mx_pack4(v[ni][4 * i], v[ni][4 * i + 1], v[ni][4 * i + 2], v[ni][4 * i + 3], inv);
+          __builtin_amdgcn_sched_barrier(0);
+          asm volatile("s_nop 4");   // wait states between the packs and the swaps (gemm_mx8q.hip permlane_gap)
+          __builtin_amdgcn_sched_barrier(0);
+          const auto s02 = __builtin_amdgcn_permlane32_swap(d[0], d[2], false, false);
+          const auto s13 = __builtin_amdgcn_permlane32_swap(d[1], d[3], false, false);
+          q16[ni] = make_uint4(s02[0], s02[1], s13[0], s13[1]);
+        }
+        if (MICLIP_VMCHECK) vm_st += 3;
+        if (m < a.M) {
+          uint8_t* o = (uint8_t*)a.out + (int64_t)m * a.ldo + cn0 + wc * WTN + 16 * h;
+#pragma unroll
+          for (int ni = 0; ni < 2; ++ni) *(uint4*)(o + ni * 32) = q16[ni];
+          if (h == 0) a.o_scale[mx_scale_index(m, blk, m_pad)] = (uint8_t)(X + 127);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) {
+        const int m = cm0 + grp * WTM + mi * 32 + lr;
+        if constexpr (EPI == EPI_F32) {
+          if (MICLIP_VMCHECK) vm_st += 2 * 4;
+          if (m < a.M)
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+              for (int i = 0; i < 4; ++i)
+                *(float4*)((float*)a.out + (int64_t)m * a.ldo + cn0 + wc * WTN + ni * 32 + 8 * i + 4 * h) =
+                    make_float4(val(mi, ni, 4 * i), val(mi, ni, 4 * i + 1), val(mi, ni, 4 * i + 2), val(mi, ni, 4 * i + 3));
+          continue;
+        }
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+          for (int ip = 0; ip < 2; ++ip) {
+            const int j0 = 8 * ip, j1 = 8 * ip + 4;
+            const uint32_t ax = pack_bf16x2(val(mi, ni, j0), val(mi, ni, j0 + 1));
+            const uint32_t ay = pack_bf16x2(val(mi, ni, j0 + 2), val(mi, ni, j0 + 3));
+            const uint32_t bx = pack_bf16x2(val(mi, ni, j1), val(mi, ni, j1 + 1));
+            const uint32_t by = pack_bf16x2(val(mi, ni, j1 + 2), val(mi, ni, j1 + 3));
+            const auto sx = __builtin_amdgcn_permlane32_swap(ax, bx, false, false);
+            const auto sy = __builtin_amdgcn_permlane32_swap(ay, by, false, false);
+            if (MICLIP_VMCHECK) ++vm_st;
+            if (m < a.M)
+              *(uint4*)((uint16_t*)a.out + (int64_t)m * a.ldo + cn0 + wc * WTN + ni * 32 + 16 * ip + 8 * h) =
+                  make_uint4(sx[0], sy[0], sx[1], sy[1]);
+          }
+      }
+    }
+    if (MICLIP_VMCHECK) vm_count_check<NSTORE>(vm_st);
+    if (!has_next) break;
+    vb = nvb;
+    m0 = nm0;
+    n0 = nn0;
+    rb = (rb + nk) % RING;
+    tpar ^= 1;
+    if (cm0 + BM <= a.M) {
+      pend = true;
+    } else {   // partial tile: an unknown number of stores issued
+      pend = false;
+      vm_wait_all();
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // bf16 -> MX-fp8 (OCP e4m3 + one e8m0 scale per 64 consecutive k): one lane
 // per 64-element block.  Shared exponent X = floor(log2(amax)) - 8 (e4m3's
 // largest exponent), element = RNE e4m3 of v * 2^-X, saturated to +-448;
@@ -534,6 +808,26 @@ hipError_t gemm_mx(const GemmArgs& a, int epi, hipStream_t s) {
   if (a.variant != 0) return hipErrorNotSupported;   // kernel overrides exist in the A/B build only
   const bool force_dbuf = false;
 #endif
+  // persistent ping-pong (round 6; A/B MICLIP_MX_PERSIST=0 keeps one workgroup per tile): at least
+  // one tile per CU and whole XCD runs (grid % 8 == 0)
+  const int cus = cu_count();
+  bool persist = nt >= cus && cus % 8 == 0;
+#if MICLIP_AB
+  if (const char* pe = std::getenv("MICLIP_MX_PERSIST")) persist = persist && std::atoi(pe) != 0;
+#endif
+  if (!force_dbuf && a.K / 64 >= 3 && persist) {
+    switch (epi) {
+      case EPI_BF16: hipLaunchKernelGGL(gemm_mxppp_kernel<EPI_BF16>, dim3(cus), dim3(512), 0, s, a); break;
+      case EPI_GELU_BF16: hipLaunchKernelGGL(gemm_mxppp_kernel<EPI_GELU_BF16>, dim3(cus), dim3(512), 0, s, a); break;
+      case EPI_F32: hipLaunchKernelGGL(gemm_mxppp_kernel<EPI_F32>, dim3(cus), dim3(512), 0, s, a); break;
+      case EPI_GELU_MX:
+        if (!a.o_scale) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(gemm_mxppp_kernel<EPI_GELU_MX>, dim3(cus), dim3(512), 0, s, a);
+        break;
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
   if (!force_dbuf && a.K / 64 >= 3) {
     switch (epi) {
       case EPI_BF16: hipLaunchKernelGGL(gemm_mxpp_kernel<EPI_BF16>, dim3(nt), dim3(512), 0, s, a); break;

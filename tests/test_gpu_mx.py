@@ -183,3 +183,39 @@ def test_gemm_mx_default_fp8_output_rows(gpu, M, N, K):
     ref = mx_ref.gemm(qa.cpu().numpy()[rows], sa_, qw.cpu().numpy(), sw_) + bias.double().cpu().numpy()
     ref = ref / (1 + np.exp(-1.702 * ref))
     assert np.all(np.abs(got - ref) <= 0.125 * np.abs(ref) + 0.01 * np.abs(ref).max())
+
+
+@pytest.mark.parametrize("M,N,K", [(40000, 1024, 1024), (70001, 4096, 1024), (100003, 1024, 4096)])
+@pytest.mark.parametrize("epi", [0, 1, 3, 4])
+def test_gemm_mx_persistent_bit_identical(gpu, monkeypatch, M, N, K, epi):
+    """The persistent MX ping-pong (gemm_mxppp_kernel: one workgroup per CU, the next tile's first
+    stages and bias streamed in under this tile's last stages, counted waits across the tile
+    boundary) against one workgroup per tile (gemm_mxpp_kernel, MICLIP_MX_PERSIST=0, A/B build):
+    the same MFMAs in the same k order and the same epilogue arithmetic, so bf16 / GELU / f32 /
+    MX-fp8 outputs (e4m3 bytes and their scales) are byte-identical -- several tiles per CU, odd M
+    and a partial last m-tile (its stores drain with vmcnt(0)), K = 1024 and 4096."""
+    import torch
+    N_ = _lib()
+    g = torch.Generator(device="cpu").manual_seed(M + N + K + epi)
+    a = (torch.randn(M, K, generator=g) * 2).bfloat16()
+    w = (torch.randn(N, K, generator=g) * K ** -0.5).bfloat16()
+    bias = torch.randn(N, generator=g).to(gpu)
+    qa, sa = _quant_gpu(a.to(gpu))
+    qw, sw = _quant_gpu(w.to(gpu))
+    outs = []
+    for lib, persist in ((N_.lib(), None), (N_.lib_ab(), "1"), (N_.lib_ab(), "0")):
+        if persist is not None:
+            monkeypatch.setenv("MICLIP_MX_PERSIST", persist)
+        if epi == 4:
+            mp = M + (M & 1)
+            out = torch.zeros((M * N + 255) // 256 * 256 + (N // 128) * mp * 2, dtype=torch.uint8, device=gpu)
+        else:
+            out = torch.zeros(M, N, dtype=torch.float32 if epi == 3 else torch.bfloat16, device=gpu)
+        rc = lib.mi_op_gemm_mx(qa.data_ptr(), sa.data_ptr(), qw.data_ptr(), sw.data_ptr(), bias.data_ptr(),
+                               out.data_ptr(), M, N, K, epi, _stream())
+        if rc:
+            raise N_.MiClipError(f"gemm_mx: {lib.mi_last_error()}")
+        outs.append(out)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0].view(torch.uint8), outs[1].view(torch.uint8))   # product = A/B persistent
+    assert torch.equal(outs[1].view(torch.uint8), outs[2].view(torch.uint8))   # persistent = per tile
