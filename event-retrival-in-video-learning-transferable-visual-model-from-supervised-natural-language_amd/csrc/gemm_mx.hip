@@ -809,9 +809,12 @@ hipError_t gemm_mx(const GemmArgs& a, int epi, hipStream_t s) {
   const bool force_dbuf = false;
 #endif
   // persistent ping-pong (round 6; A/B MICLIP_MX_PERSIST=0 keeps one workgroup per tile): at least
-  // one tile per CU and whole XCD runs (grid % 8 == 0)
+  // one tile per CU, whole XCD runs (grid % 8 == 0) and K <= 2048.  At the configs[4] pass shapes
+  // (M = 497951, scripts/mx_persist_micro.py, profiles/r06_d_mx_persist_micro.log; bit-identical):
+  // c_fc -> MX-fp8 2831 vs 2947 us, qkv 1966 vs 2002, out_proj 686 vs 738; c_proj (K = 4096, a
+  // 64-stage main loop) 2119 vs 2009 us, so long-K GEMMs keep one workgroup per tile
   const int cus = cu_count();
-  bool persist = nt >= cus && cus % 8 == 0;
+  bool persist = nt >= cus && cus % 8 == 0 && a.K <= 2048;
 #if MICLIP_AB
   if (const char* pe = std::getenv("MICLIP_MX_PERSIST")) persist = persist && std::atoi(pe) != 0;
 #endif

@@ -6,7 +6,11 @@ import sys
 import torch
 
 SHAPES = {"qkv": (100000, 2304, 768), "out": (100000, 768, 768), "fc": (100000, 3072, 768),
-          "proj": (100000, 768, 3072), "long": (16384, 4096, 4096)}
+          "proj": (100000, 768, 3072), "long": (16384, 4096, 4096),
+          # the bench's 500k-row pass (10k ViT-B/32 frames): the library's plain bf16 GEMM + bias at
+          # the shapes of the tower's LN-folded / fused kernels
+          "qkv500": (500000, 2304, 768), "out500": (500000, 768, 768), "fc500": (500000, 3072, 768),
+          "proj500": (500000, 768, 3072)}
 
 
 def main():
