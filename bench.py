@@ -203,6 +203,10 @@ def kernel_timing(model, cfg, chunk, reps=20):
         for name, Nn, K, epi, out in gemms:
             Aq, As = mx(A[:, :K].contiguous())
             Wq, Ws = mx(Wt[:Nn, :K].contiguous())
+            if name == "gemm_fc":   # the tower's c_fc: QuickGELU -> MX-fp8 codes + scales (EPI_GELU_MX)
+                epi = 4
+                out = torch.empty((M * Nn + 255) // 256 * 256 + (Nn // 128) * ((M + 1) & ~1) * 2,
+                                  dtype=torch.uint8, device=dev)
             timed(name, lambda Nn=Nn, K=K, epi=epi, out=out, Aq=Aq, As=As, Wq=Wq, Ws=Ws: N.check(
                 L.mi_op_gemm_mx(Aq.data_ptr(), As.data_ptr(), Wq.data_ptr(), Ws.data_ptr(), bias.data_ptr(),
                                 out.data_ptr(), M, Nn, K, epi, sp), "gemm_mx"), flops=2.0 * M * Nn * K)
@@ -782,7 +786,8 @@ def main():
             peak = FP8_PEAK_TFLOPS if fp8 else BF16_PEAK_TFLOPS
             eb = 1 if fp8 else 2   # operand element bytes (fp8 adds 1/64 B of scales per element; fp32: 3 fp16 terms)
             roof = {"bound": "mfma",
-                    "kernel": ("gemm_mx_kernel<EPI_GELU_BF16> (mlp.c_fc + QuickGELU, MX-fp8 operands)" if fp8
+                    "kernel": ("gemm_mxppp_kernel<EPI_GELU_MX> (mlp.c_fc + QuickGELU -> MX-fp8, MX-fp8 operands; "
+                               "persistent ping-pong)" if fp8
                                else "gemm_8q_kernel<EPI_F32> (split-f16 operands, K' = 3K, at mlp.c_fc's shape)" if f32
                                else "gemm_8q_kernel<EPI_LN_GELU_BF16> (8-phase interleaved persistent, 256x256x64, descriptor DMAs; "
                                "ln_2 folded into the epilogue, fp16 operands on the f16 MFMA; mlp.c_fc + QuickGELU)" if lnf
@@ -792,7 +797,7 @@ def main():
                     "traffic_source": tsrc,
                     "mfma_busy_pmc": busy,
                     "algorithmic_bytes": int(eb * (1 + fp8 / 64) * (3 if f32 else 1) * (M * cfg.vision_width + 4 * cfg.vision_width ** 2)
-                                             + (4 if f32 else 2) * M * 4 * cfg.vision_width
+                                             + ((1 + 1 / 64) if fp8 else 4 if f32 else 2) * M * 4 * cfg.vision_width
                                              + (8 * M + 8 * 4 * cfg.vision_width if lnf else 0)),
                     "flops_per_launch": fl, "launch_shape": [M, 4 * cfg.vision_width, cfg.vision_width],
                     "avg_launch_us": dom["us"],

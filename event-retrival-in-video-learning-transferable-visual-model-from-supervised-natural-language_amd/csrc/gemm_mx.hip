@@ -665,13 +665,28 @@ __global__ __launch_bounds__(512) void gemm_mxppp_kernel(GemmArgs a) {
 #pragma unroll
       for (int mi = 0; mi < 4; ++mi) {
         const int m = cm0 + grp * WTM + mi * 32 + lr;
-        float v[2][16];
+        // QuickGELU in stage order over the block's 32 values (each value's operations are
+        // mx_gelu's, so the result is bit-identical; consecutive transcendentals are independent,
+        // as gemm_8q's F_GSTAGE16)
+        float v[2][16], e[2][16];
         float amax = 0.f;
 #pragma unroll
         for (int ni = 0; ni < 2; ++ni)
 #pragma unroll
           for (int j = 0; j < 16; ++j) {
-            v[ni][j] = val(mi, ni, j);
+            const float4 b = bias[ni][j >> 2];
+            v[ni][j] = acc[mi][ni][j] + ((j & 3) == 0 ? b.x : (j & 3) == 1 ? b.y : (j & 3) == 2 ? b.z : b.w);
+            e[ni][j] = __expf(-1.702f * v[ni][j]);
+          }
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+          for (int j = 0; j < 16; ++j) e[ni][j] = __builtin_amdgcn_rcpf(1.0f + e[ni][j]);
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+          for (int j = 0; j < 16; ++j) {
+            v[ni][j] = v[ni][j] * e[ni][j];
             amax = fmaxf(amax, fabsf(v[ni][j]));
           }
         const auto sx = __builtin_amdgcn_permlane32_swap(__float_as_uint(amax), __float_as_uint(amax), false, false);
