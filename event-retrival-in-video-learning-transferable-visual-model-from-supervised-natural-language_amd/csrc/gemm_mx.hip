@@ -496,6 +496,22 @@ __device__ __forceinline__ float4 mx_lds_f4(const float* p) {   // (an LDS read 
   return v;
 }
 
+// Logical tile t -> (m-block, n-block) in groups of ng n-blocks (ng <= 0 or >= tiles_n: m-major):
+// within a group every m-block, so an XCD's contiguous run of tiles keeps its group's weight panel
+// (ng x 256 rows x K bytes of e4m3) in its 4-MB L2 (gemm_8q.hip tile_coords_8q)
+__device__ __forceinline__ void tile_coords_mx(int t, int tiles_m, int tiles_n, int ng, int& mb, int& nb) {
+  if (ng <= 0 || ng >= tiles_n) {
+    mb = t / tiles_n;
+    nb = t % tiles_n;
+    return;
+  }
+  const int per = tiles_m * ng;
+  const int gg = t / per, r = t - gg * per;
+  const int ngg = min(ng, tiles_n - gg * ng);
+  mb = r / ngg;
+  nb = gg * ng + r % ngg;
+}
+
 template <int EPI>
 __global__ __launch_bounds__(512) void gemm_mxppp_kernel(GemmArgs a) {
   typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -524,8 +540,10 @@ __global__ __launch_bounds__(512) void gemm_mxppp_kernel(GemmArgs a) {
   const uint8_t* Wt = (const uint8_t*)a.W;
   auto coords = [&](int v, int& mm, int& nn) {   // grid % 8 == 0 keeps a WG's tiles on its XCD's run
     const int t = xcd_remap(v, ntiles);
-    mm = (t / tiles_n) * BM;
-    nn = (t % tiles_n) * BN;
+    int mb, nb;
+    tile_coords_mx(t, tiles_m, tiles_n, a.ngroup, mb, nb);
+    mm = mb * BM;
+    nn = nb * BN;
   };
   int vb = blockIdx.x, m0, n0;
   coords(vb, m0, n0);
@@ -834,6 +852,23 @@ hipError_t gemm_mx(const GemmArgs& a, int epi, hipStream_t s) {
   if (const char* pe = std::getenv("MICLIP_MX_PERSIST")) persist = persist && std::atoi(pe) != 0;
 #endif
   if (!force_dbuf && a.K / 64 >= 3 && persist) {
+#if MICLIP_AB   // A/B: MICLIP_MX_NG forces the tile-order group width (-1 = m-major)
+    if (const char* ng = std::getenv("MICLIP_MX_NG")) {
+      GemmArgs g = a;
+      g.ngroup = std::atoi(ng);
+      switch (epi) {
+        case EPI_BF16: hipLaunchKernelGGL(gemm_mxppp_kernel<EPI_BF16>, dim3(cus), dim3(512), 0, s, g); break;
+        case EPI_GELU_BF16: hipLaunchKernelGGL(gemm_mxppp_kernel<EPI_GELU_BF16>, dim3(cus), dim3(512), 0, s, g); break;
+        case EPI_F32: hipLaunchKernelGGL(gemm_mxppp_kernel<EPI_F32>, dim3(cus), dim3(512), 0, s, g); break;
+        case EPI_GELU_MX:
+          if (!a.o_scale) return hipErrorInvalidValue;
+          hipLaunchKernelGGL(gemm_mxppp_kernel<EPI_GELU_MX>, dim3(cus), dim3(512), 0, s, g);
+          break;
+        default: return hipErrorInvalidValue;
+      }
+      return hipGetLastError();
+    }
+#endif
     switch (epi) {
       case EPI_BF16: hipLaunchKernelGGL(gemm_mxppp_kernel<EPI_BF16>, dim3(cus), dim3(512), 0, s, a); break;
       case EPI_GELU_BF16: hipLaunchKernelGGL(gemm_mxppp_kernel<EPI_GELU_BF16>, dim3(cus), dim3(512), 0, s, a); break;

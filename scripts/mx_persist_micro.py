@@ -2,7 +2,8 @@
 workgroup per tile (gemm_mxpp_kernel, MICLIP_MX_PERSIST=0 in the A/B build) at the configs[4]
 pass shapes (ViT-L/14@336px, 863 frames x 577 tokens = 497951 rows): random operands, HIP events,
 interleaved rounds in one process, outputs compared byte for byte.
-usage: python scripts/mx_persist_micro.py [reps] [shapes,comma]"""
+usage: python scripts/mx_persist_micro.py [reps] [shapes,comma] [group widths,comma]
+(group widths: the persistent kernel's tile order, MICLIP_MX_NG, -1 = m-major; each also compared)"""
 import os
 import sys
 
@@ -21,6 +22,7 @@ SHAPES = {"qkv": (M4, 3072, 1024, 0), "out": (M4, 1024, 1024, 0), "fc8": (M4, 40
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
     only = sys.argv[2].split(",") if len(sys.argv) > 2 else list(SHAPES)
+    ngs = [int(x) for x in sys.argv[3].split(",")] if len(sys.argv) > 3 else []
     L = N.lib_ab()
     dev = torch.device("cuda:0")
     sp = torch.cuda.current_stream().cuda_stream
@@ -43,9 +45,15 @@ def main():
         else:
             mk = lambda: torch.zeros(M, Nn, dtype=torch.bfloat16, device=dev)  # noqa: E731
         outs = {"persistent": mk(), "per_tile": mk()}
+        for ng in ngs:
+            outs[f"ng{ng}"] = mk()
 
         def run(k):
-            os.environ["MICLIP_MX_PERSIST"] = "1" if k == "persistent" else "0"
+            os.environ["MICLIP_MX_PERSIST"] = "0" if k == "per_tile" else "1"
+            if k.startswith("ng"):
+                os.environ["MICLIP_MX_NG"] = k[2:]
+            else:
+                os.environ.pop("MICLIP_MX_NG", None)
             N.check(L.mi_op_gemm_mx(qa.data_ptr(), sa.data_ptr(), qw.data_ptr(), sw.data_ptr(), bias.data_ptr(),
                                     outs[k].data_ptr(), M, Nn, K, epi, sp), "gemm_mx")
         for k in outs:
@@ -67,6 +75,11 @@ def main():
               f"{fl / best['persistent'] / 1e6:7.1f} TF ({fl / best['persistent'] / 1e6 / 5000:.3f} of fp8 peak) | "
               f"per-tile {best['per_tile']:8.1f} us {fl / best['per_tile'] / 1e6:7.1f} TF | bit-identical {same}",
               flush=True)
+        for ng in ngs:
+            k = f"ng{ng}"
+            eq = torch.equal(outs[k].view(torch.uint8), outs["per_tile"].view(torch.uint8))
+            print(f"{name:8s}   group width {ng:3d}: {best[k]:8.1f} us {fl / best[k] / 1e6:7.1f} TF "
+                  f"({fl / best[k] / 1e6 / 5000:.3f} of fp8 peak) | bit-identical {eq}", flush=True)
         del qa, qw, outs
 
 
