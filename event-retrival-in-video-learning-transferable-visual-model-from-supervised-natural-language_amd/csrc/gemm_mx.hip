@@ -869,13 +869,22 @@ hipError_t gemm_mx(const GemmArgs& a, int epi, hipStream_t s) {
       return hipGetLastError();
     }
 #endif
+    // tile order: n-tiles in groups of 6 when there are >= 12 and a group's e4m3 panel fits 2.4 MB
+    // (an XCD's 32 concurrent tiles then hold a 1.5-MB panel at K = 1024, not the m-major walk's
+    // whole 3-4 MB, which the L2 re-fetched per m-block: FETCH 9x the operand bytes on c_fc,
+    // profiles/r06_h_fp8_gemm_traffic.json).  configs[4] shapes, bit-identical
+    // (profiles/r06_i_mx_ng.log): c_fc -> MX-fp8 2756 vs 2854 us m-major (groups of 8 2801, 4 2819,
+    // 2 2864), qkv 1961 vs 1986 (4: 2049, 2: 2070); out_proj's 4 n-tiles stay m-major
+    GemmArgs g = a;
+    const int tn = a.N / 256;
+    if (g.ngroup == 0) g.ngroup = (tn >= 12 && (int64_t)6 * 256 * a.K <= 2400000) ? 6 : -1;
     switch (epi) {
-      case EPI_BF16: hipLaunchKernelGGL(gemm_mxppp_kernel<EPI_BF16>, dim3(cus), dim3(512), 0, s, a); break;
-      case EPI_GELU_BF16: hipLaunchKernelGGL(gemm_mxppp_kernel<EPI_GELU_BF16>, dim3(cus), dim3(512), 0, s, a); break;
-      case EPI_F32: hipLaunchKernelGGL(gemm_mxppp_kernel<EPI_F32>, dim3(cus), dim3(512), 0, s, a); break;
+      case EPI_BF16: hipLaunchKernelGGL(gemm_mxppp_kernel<EPI_BF16>, dim3(cus), dim3(512), 0, s, g); break;
+      case EPI_GELU_BF16: hipLaunchKernelGGL(gemm_mxppp_kernel<EPI_GELU_BF16>, dim3(cus), dim3(512), 0, s, g); break;
+      case EPI_F32: hipLaunchKernelGGL(gemm_mxppp_kernel<EPI_F32>, dim3(cus), dim3(512), 0, s, g); break;
       case EPI_GELU_MX:
         if (!a.o_scale) return hipErrorInvalidValue;
-        hipLaunchKernelGGL(gemm_mxppp_kernel<EPI_GELU_MX>, dim3(cus), dim3(512), 0, s, a);
+        hipLaunchKernelGGL(gemm_mxppp_kernel<EPI_GELU_MX>, dim3(cus), dim3(512), 0, s, g);
         break;
       default: return hipErrorInvalidValue;
     }
