@@ -265,6 +265,22 @@ __device__ __forceinline__ v8i lds_frag32(const char* p, int rd0, int rd1) {
   return v8i{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
+// Logical tile t -> (m-block, n-block) in groups of ng n-blocks (ng <= 0 or >= tiles_n: m-major):
+// within a group every m-block, so an XCD's contiguous run of tiles keeps its group's weight panel
+// (ng x 256 rows x K bytes of e4m3) in its 4-MB L2 (gemm_8q.hip tile_coords_8q)
+__device__ __forceinline__ void tile_coords_mx(int t, int tiles_m, int tiles_n, int ng, int& mb, int& nb) {
+  if (ng <= 0 || ng >= tiles_n) {
+    mb = t / tiles_n;
+    nb = t % tiles_n;
+    return;
+  }
+  const int per = tiles_m * ng;
+  const int gg = t / per, r = t - gg * per;
+  const int ngg = min(ng, tiles_n - gg * ng);
+  mb = r / ngg;
+  nb = gg * ng + r % ngg;
+}
+
 template <int EPI>
 __global__ __launch_bounds__(512) void gemm_mxpp_kernel(GemmArgs a) {
   typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -279,7 +295,9 @@ __global__ __launch_bounds__(512) void gemm_mxpp_kernel(GemmArgs a) {
   const int tiles_n = a.N / BN;
   const int tiles_m = (a.M + BM - 1) / BM;
   const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
-  const int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
+  int mb_, nb_;
+  tile_coords_mx(t, tiles_m, tiles_n, a.ngroup, mb_, nb_);
+  const int m0 = mb_ * BM, n0 = nb_ * BN;
   const int nk = a.K / SB;
   const int m_pad = (a.M + 1) & ~1;
   const uint8_t* A = (const uint8_t*)a.A;
@@ -494,22 +512,6 @@ __device__ __forceinline__ float4 mx_lds_f4(const float* p) {   // (an LDS read 
   const uint32_t addr = (uint32_t)(uintptr_t)(const LDS_AS float*)p;
   asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(addr) : "memory");
   return v;
-}
-
-// Logical tile t -> (m-block, n-block) in groups of ng n-blocks (ng <= 0 or >= tiles_n: m-major):
-// within a group every m-block, so an XCD's contiguous run of tiles keeps its group's weight panel
-// (ng x 256 rows x K bytes of e4m3) in its 4-MB L2 (gemm_8q.hip tile_coords_8q)
-__device__ __forceinline__ void tile_coords_mx(int t, int tiles_m, int tiles_n, int ng, int& mb, int& nb) {
-  if (ng <= 0 || ng >= tiles_n) {
-    mb = t / tiles_n;
-    nb = t % tiles_n;
-    return;
-  }
-  const int per = tiles_m * ng;
-  const int gg = t / per, r = t - gg * per;
-  const int ngg = min(ng, tiles_n - gg * ng);
-  mb = r / ngg;
-  nb = gg * ng + r % ngg;
 }
 
 template <int EPI>
@@ -848,8 +850,9 @@ hipError_t gemm_mx(const GemmArgs& a, int epi, hipStream_t s) {
   // 64-stage main loop) 2119 vs 2009 us, so long-K GEMMs keep one workgroup per tile
   const int cus = cu_count();
   bool persist = nt >= cus && cus % 8 == 0 && a.K <= 2048;
-#if MICLIP_AB
-  if (const char* pe = std::getenv("MICLIP_MX_PERSIST")) persist = persist && std::atoi(pe) != 0;
+#if MICLIP_AB   // (2: persistent whatever K)
+  if (const char* pe = std::getenv("MICLIP_MX_PERSIST"))
+    persist = std::atoi(pe) == 2 ? nt >= cus && cus % 8 == 0 : persist && std::atoi(pe) != 0;
 #endif
   if (!force_dbuf && a.K / 64 >= 3 && persist) {
 #if MICLIP_AB   // A/B: MICLIP_MX_NG forces the tile-order group width (-1 = m-major)
@@ -891,13 +894,17 @@ hipError_t gemm_mx(const GemmArgs& a, int epi, hipStream_t s) {
     return hipGetLastError();
   }
   if (!force_dbuf && a.K / 64 >= 3) {
+    GemmArgs g = a;   // (the per-tile kernel walks m-major unless asked: A/B MICLIP_MX_NG)
+#if MICLIP_AB
+    if (const char* ng = std::getenv("MICLIP_MX_NG")) g.ngroup = std::atoi(ng);
+#endif
     switch (epi) {
-      case EPI_BF16: hipLaunchKernelGGL(gemm_mxpp_kernel<EPI_BF16>, dim3(nt), dim3(512), 0, s, a); break;
-      case EPI_GELU_BF16: hipLaunchKernelGGL(gemm_mxpp_kernel<EPI_GELU_BF16>, dim3(nt), dim3(512), 0, s, a); break;
-      case EPI_F32: hipLaunchKernelGGL(gemm_mxpp_kernel<EPI_F32>, dim3(nt), dim3(512), 0, s, a); break;
+      case EPI_BF16: hipLaunchKernelGGL(gemm_mxpp_kernel<EPI_BF16>, dim3(nt), dim3(512), 0, s, g); break;
+      case EPI_GELU_BF16: hipLaunchKernelGGL(gemm_mxpp_kernel<EPI_GELU_BF16>, dim3(nt), dim3(512), 0, s, g); break;
+      case EPI_F32: hipLaunchKernelGGL(gemm_mxpp_kernel<EPI_F32>, dim3(nt), dim3(512), 0, s, g); break;
       case EPI_GELU_MX:
         if (!a.o_scale) return hipErrorInvalidValue;
-        hipLaunchKernelGGL(gemm_mxpp_kernel<EPI_GELU_MX>, dim3(nt), dim3(512), 0, s, a);
+        hipLaunchKernelGGL(gemm_mxpp_kernel<EPI_GELU_MX>, dim3(nt), dim3(512), 0, s, g);
         break;
       default: return hipErrorInvalidValue;
     }

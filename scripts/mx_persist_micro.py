@@ -3,7 +3,8 @@ workgroup per tile (gemm_mxpp_kernel, MICLIP_MX_PERSIST=0 in the A/B build) at t
 pass shapes (ViT-L/14@336px, 863 frames x 577 tokens = 497951 rows): random operands, HIP events,
 interleaved rounds in one process, outputs compared byte for byte.
 usage: python scripts/mx_persist_micro.py [reps] [shapes,comma] [group widths,comma]
-(group widths: the persistent kernel's tile order, MICLIP_MX_NG, -1 = m-major; each also compared)"""
+(group widths: the persistent kernel's tile order, MICLIP_MX_NG, -1 = m-major; each also compared;
+ an entry "pP:G" runs MICLIP_MX_PERSIST=P with MICLIP_MX_NG=G -- P 2 = persistent whatever K)"""
 import os
 import sys
 
@@ -22,7 +23,7 @@ SHAPES = {"qkv": (M4, 3072, 1024, 0), "out": (M4, 1024, 1024, 0), "fc8": (M4, 40
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
     only = sys.argv[2].split(",") if len(sys.argv) > 2 else list(SHAPES)
-    ngs = [int(x) for x in sys.argv[3].split(",")] if len(sys.argv) > 3 else []
+    ngs = sys.argv[3].split(",") if len(sys.argv) > 3 else []
     L = N.lib_ab()
     dev = torch.device("cuda:0")
     sp = torch.cuda.current_stream().cuda_stream
@@ -50,10 +51,13 @@ def main():
 
         def run(k):
             os.environ["MICLIP_MX_PERSIST"] = "0" if k == "per_tile" else "1"
-            if k.startswith("ng"):
+            os.environ.pop("MICLIP_MX_NG", None)
+            if k.startswith("ngp"):      # "ngpP:G"
+                pp, gg = k[3:].split(":")
+                os.environ["MICLIP_MX_PERSIST"] = pp
+                os.environ["MICLIP_MX_NG"] = gg
+            elif k.startswith("ng"):
                 os.environ["MICLIP_MX_NG"] = k[2:]
-            else:
-                os.environ.pop("MICLIP_MX_NG", None)
             N.check(L.mi_op_gemm_mx(qa.data_ptr(), sa.data_ptr(), qw.data_ptr(), sw.data_ptr(), bias.data_ptr(),
                                     outs[k].data_ptr(), M, Nn, K, epi, sp), "gemm_mx")
         for k in outs:
@@ -78,7 +82,7 @@ def main():
         for ng in ngs:
             k = f"ng{ng}"
             eq = torch.equal(outs[k].view(torch.uint8), outs["per_tile"].view(torch.uint8))
-            print(f"{name:8s}   group width {ng:3d}: {best[k]:8.1f} us {fl / best[k] / 1e6:7.1f} TF "
+            print(f"{name:8s}   group width {ng:>5s}: {best[k]:8.1f} us {fl / best[k] / 1e6:7.1f} TF "
                   f"({fl / best[k] / 1e6 / 5000:.3f} of fp8 peak) | bit-identical {eq}", flush=True)
         del qa, qw, outs
 
