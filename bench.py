@@ -72,6 +72,9 @@ def parse():
                     help="launcher rehearsal on CPU/gloo: rendezvous + all-gather, no GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                    help="the N > 1 process group: nccl (RCCL over xGMI, the measured path) or gloo (a rehearsal "
+                         "of the multi-rank step on fewer GPUs than ranks: rank r uses GPU r %% device_count)")
     return ap.parse_args()
 
 
@@ -659,8 +662,13 @@ def main():
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     os.environ.setdefault("MICLIP_SYNTHETIC_WEIGHTS", "1")     # random-init weights of the architecture (data: synthetic)
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:   # rehearsal: ranks may share a GPU (RCCL refuses two ranks on one device)
+            local = local % torch.cuda.device_count()
+            torch.cuda.set_device(local)
+            dist.init_process_group("gloo")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 

@@ -53,8 +53,16 @@ def sharded_topk(local_corpus, queries, k, index_base, group=None, nan_policy="f
     # [Q, 3k] 32-bit words (12 B per candidate), all-gathered, then unpacked
     Q = s.shape[0]
     packed = torch.cat([s.contiguous().view(torch.int32), i.contiguous().view(torch.int32)], dim=1).contiguous()
-    gp = [torch.empty_like(packed) for _ in range(world)]
-    dist.all_gather(gp, packed, group=group)
+    if packed.is_cuda and dist.get_backend(group) == "gloo":
+        # gloo all-gathers host tensors only (bench.py --dist-backend gloo: the multi-rank step
+        # rehearsed with ranks sharing a GPU); the measured path is RCCL on device tensors
+        host = packed.cpu()
+        gh = [torch.empty_like(host) for _ in range(world)]
+        dist.all_gather(gh, host, group=group)
+        gp = [g.to(packed.device) for g in gh]
+    else:
+        gp = [torch.empty_like(packed) for _ in range(world)]
+        dist.all_gather(gp, packed, group=group)
     cand_s = torch.cat([g[:, :k].contiguous().view(torch.float32) for g in gp], dim=1).contiguous()   # [Q, world*k]
     cand_i = torch.cat([g[:, k:].contiguous().view(torch.int64) for g in gp], dim=1).contiguous()
     assert cand_s.shape == (Q, world * k) and cand_i.shape == (Q, world * k)
