@@ -838,7 +838,8 @@ def main():
         else:
             workload += f"{Nf} frames/GPU x {Q} text queries, top-{k}"
         if world > 1:
-            workload += " (RCCL all-gather top-k)"
+            workload += (" (RCCL all-gather top-k)" if args.dist_backend == "nccl"
+                         else " (gloo all-gather top-k: a rehearsal, ranks sharing GPUs)")
         elif (cfg.name, Nf, Q, k) == ("ViT-B/32", 10_000, 32, 10):
             workload += " (BASELINE configs[1])"
         result = {
