@@ -42,6 +42,8 @@ SHAPES = {
     "lnfc500": (500000, 3072, 768, 7),
     "lnfc1k": (1000, 3072, 768, 7), "lnfc40k": (40003, 3072, 768, 7),   # (few / odd tile counts per CU)
     "lnfcL": (428459, 4096, 1024, 7),   # ViT-L/14 c_fc (1667 frames x 257 tokens)
+    "lnfcL2": (494468, 4096, 1024, 7),  # ViT-L/14 c_fc at configs[2]'s bench pass (1924 frames x 257)
+    "lnfc481": (480800, 3072, 768, 7),  # ViT-B/32 c_fc at configs[3]'s bench pass (9616 frames x 50)
     "lnqkvL": (428459, 3072, 1024, 6),   # ViT-L/14 in_proj
     "lnqkv250": (250000, 2304, 768, 6),
     "lnqkv100": (100000, 2304, 768, 6), "lnfc100": (100000, 3072, 768, 7),
