@@ -550,6 +550,115 @@ __global__ __launch_bounds__(256, MINB) void attn_f32_mfma_kernel(const float* _
   }
 }
 
+// The same kernel for S <= 64 (B/32's 50 tokens: the fp32 tower's attention) with every load of a
+// (sequence, head) issued before its first MFMA (round 6).  attn_f32_mfma_kernel loads K and V
+// inside its query-block loop (twice at S > 32), each key tile's K and each (dim tile, key tile)'s
+// V as a batch that the next MFMAs wait for, and at 254 VGPRs hipcc reuses the load destinations,
+// so the Q loads went out one at a time (a load, then vmcnt(0)): ~7 serialized HBM round trips per
+// wave.  Here K and V of both key tiles (64 + 64 VGPRs) and the first query block's Q are in flight
+// together, once per (sequence, head); the second block's Q goes out behind the first block's
+// scores.  The MFMAs, their order, the masks, expf and the stores are attn_f32_mfma_kernel's, so
+// the output is bit-identical (tests/test_gpu_ops.py::test_attention_f32_prefetch_bit_identical).
+template <int MINB>
+__global__ __launch_bounds__(256, MINB) void attn_f32_mfma_pre_kernel(const float* __restrict__ qkv, float* __restrict__ out,
+                                                                int nseq, int S, int W, int causal) {
+  constexpr int NKT = 2;
+  const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
+  const int H = W / 64;
+  const int item = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (item >= nseq * H) return;
+  const int qend = ((causal >> 11) & 1) ? min(S, 32) : S;   // (bit 11: the first query block only)
+  causal &= 1;
+  const int bseq = item / H, head = item % H;
+  const int ld = 3 * W;
+  auto rho = [&](int r) { return (r & 3) + 8 * (r >> 2) + 4 * h; };
+  const __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(qkv + (int64_t)bseq * S * ld), (short)0, S * ld * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rout = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(out + (int64_t)bseq * S * W), (short)0, S * W * 4, 0x00020000);
+  typedef unsigned int u32x4a __attribute__((ext_vector_type(4)));
+  auto ld4 = [&](int r, int col) {   // rows >= S are out of the descriptor's range: zeros
+    const u32x4a t = __builtin_bit_cast(u32x4a, __builtin_amdgcn_raw_buffer_load_b128(rin, (uint32_t)((r * ld + col) * 4), 0, 0));
+    return make_float4(__uint_as_float(t[0]), __uint_as_float(t[1]), __uint_as_float(t[2]), __uint_as_float(t[3]));
+  };
+  auto ld1 = [&](int r, int col) { return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rin, (uint32_t)((r * ld + col) * 4), 0, 0)); };
+  auto load_q = [&](int q0, float (&qv)[32]) {   // (rows past S: zeros)
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const float4 t = ld4(q0 + j, head * 64 + 32 * h + 4 * c);
+      qv[4 * c] = t.x * 0.125f; qv[4 * c + 1] = t.y * 0.125f; qv[4 * c + 2] = t.z * 0.125f; qv[4 * c + 3] = t.w * 0.125f;
+    }
+  };
+  // every load of the item, ahead of the first MFMA: Q of block 0, K and V of both key tiles
+  float qv[32], kv[NKT][32], vv[2][NKT][16];
+  load_q(0, qv);
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const float4 t = ld4(kt * 32 + j, W + head * 64 + 32 * h + 4 * c);
+      kv[kt][4 * c] = t.x; kv[kt][4 * c + 1] = t.y; kv[kt][4 * c + 2] = t.z; kv[kt][4 * c + 3] = t.w;
+    }
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+      for (int st = 0; st < 16; ++st) {
+        const int key = kt * 32 + (st & 3) + 8 * (st >> 2) + 4 * h;
+        vv[dt][kt][st] = ld1(key, 2 * W + head * 64 + 32 * dt + j);
+      }
+  for (int q0 = 0; q0 < qend; q0 += 32) {
+    const int qi = q0 + j;   // this lane's query in the S^T layout
+    if (q0) load_q(q0, qv);
+    f32x16 sc[NKT];
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+      sc[kt] = f32x16{};
+      if (kt * 32 >= S) continue;
+#pragma unroll
+      for (int st = 0; st < 32; ++st) sc[kt] = __builtin_amdgcn_mfma_f32_32x32x2f32(kv[kt][st], qv[st], sc[kt], 0, 0, 0);
+    }
+    float m = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kt * 32 + rho(r);
+        if (key >= S || (causal && key > qi)) sc[kt][r] = -INFINITY;
+        m = fmaxf(m, sc[kt][r]);
+      }
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    float l = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = expf(sc[kt][r] - m);   // masked keys: exp(-inf) = 0
+        sc[kt][r] = p;
+        l += p;
+      }
+    l += __shfl_xor(l, 32, 64);
+    const float inv = 1.0f / l;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+      f32x16 o = f32x16{};
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt) {
+        if (kt * 32 >= S) continue;
+#pragma unroll
+        for (int st = 0; st < 16; ++st) o = __builtin_amdgcn_mfma_f32_32x32x2f32(sc[kt][st], vv[dt][kt][st], o, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int qr = q0 + rho(r);
+        const float iv = __shfl(inv, rho(r), 64);   // 1 / l of query rho(r) (held by lane rho(r))
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(o[r] * iv), rout, (uint32_t)((qr * W + head * 64 + 32 * dt + j) * 4), 0, 0);
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------ im2col + split
 // conv1's split-f16 operand straight from the pixels (P % 4 == 0, Kp = 3 P^2; B/32, B/16): one
 // wave per patch row, its 3 P^2 values gathered as float4s (kw .. kw + 3 of one image row), then
@@ -712,7 +821,11 @@ hipError_t attention_f32(const float* qkv, float* out, int B, int S, int W, int 
     return hipGetLastError();
   }
 #endif
-  if (attn_f32_mfma_on() && S <= 64)   // (held to 256 registers: two waves per SIMD, no spills)
+  // S <= 64: every load ahead of the first MFMA (attn_f32_mfma_pre_kernel, round 6; A/B
+  // MICLIP_ATTN_F32_V=2 keeps the in-loop loads)
+  if (attn_f32_mfma_on() && S <= 64 && attn_f32_variant() != 2)
+    hipLaunchKernelGGL((attn_f32_mfma_pre_kernel<1>), grid4, dim3(256), 0, s, qkv, out, B, S, W, cq);
+  else if (attn_f32_mfma_on() && S <= 64)   // (held to 256 registers: two waves per SIMD, no spills)
     hipLaunchKernelGGL((attn_f32_mfma_kernel<2, 2>), grid4, dim3(256), 0, s, qkv, out, B, S, W, cq);
   else if (attn_f32_mfma_on() && S <= 96)
     hipLaunchKernelGGL(attn_f32_mfma_kernel<3>, grid4, dim3(256), 0, s, qkv, out, B, S, W, cq);
