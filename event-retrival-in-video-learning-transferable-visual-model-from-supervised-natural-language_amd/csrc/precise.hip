@@ -559,6 +559,10 @@ __global__ __launch_bounds__(256, MINB) void attn_f32_mfma_kernel(const float* _
 // together, once per (sequence, head); the second block's Q goes out behind the first block's
 // scores.  The MFMAs, their order, the masks, expf and the stores are attn_f32_mfma_kernel's, so
 // the output is bit-identical (tests/test_gpu_ops.py::test_attention_f32_prefetch_bit_identical).
+// Measured slower (scripts/attn_f32_micro.py, 10k B/32 frames: 2754 vs 2365 us,
+// profiles/r06_n_attn_f32_micro.log): at 350 VGPRs one wave per SIMD, and nothing overlaps a
+// wave's loads with another's MFMAs.  A/B only (MICLIP_ATTN_F32_V=3).
+#if MICLIP_AB
 template <int MINB>
 __global__ __launch_bounds__(256, MINB) void attn_f32_mfma_pre_kernel(const float* __restrict__ qkv, float* __restrict__ out,
                                                                 int nseq, int S, int W, int causal) {
@@ -658,6 +662,8 @@ __global__ __launch_bounds__(256, MINB) void attn_f32_mfma_pre_kernel(const floa
     }
   }
 }
+
+#endif  // MICLIP_AB
 
 // ------------------------------------------------------------------ im2col + split
 // conv1's split-f16 operand straight from the pixels (P % 4 == 0, Kp = 3 P^2; B/32, B/16): one
@@ -821,11 +827,13 @@ hipError_t attention_f32(const float* qkv, float* out, int B, int S, int W, int 
     return hipGetLastError();
   }
 #endif
-  // S <= 64: every load ahead of the first MFMA (attn_f32_mfma_pre_kernel, round 6; A/B
-  // MICLIP_ATTN_F32_V=2 keeps the in-loop loads)
-  if (attn_f32_mfma_on() && S <= 64 && attn_f32_variant() != 2)
+#if MICLIP_AB   // 3: every load ahead of the first MFMA (attn_f32_mfma_pre_kernel; measured slower)
+  if (attn_f32_mfma_on() && S <= 64 && attn_f32_variant() == 3) {
     hipLaunchKernelGGL((attn_f32_mfma_pre_kernel<1>), grid4, dim3(256), 0, s, qkv, out, B, S, W, cq);
-  else if (attn_f32_mfma_on() && S <= 64)   // (held to 256 registers: two waves per SIMD, no spills)
+    return hipGetLastError();
+  }
+#endif
+  if (attn_f32_mfma_on() && S <= 64)   // (held to 256 registers: two waves per SIMD, no spills)
     hipLaunchKernelGGL((attn_f32_mfma_kernel<2, 2>), grid4, dim3(256), 0, s, qkv, out, B, S, W, cq);
   else if (attn_f32_mfma_on() && S <= 96)
     hipLaunchKernelGGL(attn_f32_mfma_kernel<3>, grid4, dim3(256), 0, s, qkv, out, B, S, W, cq);

@@ -1,6 +1,6 @@
 """The fp32 tower's S <= 64 attention (mi_op_attention_f32) at the bench's pass (10k ViT-B/32
-frames, S = 50, W = 768): the product kernel (every load ahead of the first MFMA, round 6) against
-the in-loop-load kernel (A/B MICLIP_ATTN_F32_V=2), interleaved, HIP events, outputs compared.
+frames, S = 50, W = 768): the product kernel (in-loop loads) against the every-load-ahead-of-the-first-MFMA
+kernel (A/B MICLIP_ATTN_F32_V=3), interleaved, HIP events, outputs compared.
 usage: python scripts/attn_f32_micro.py [frames] [reps]"""
 import os
 import sys
@@ -25,7 +25,7 @@ def main():
     L = N.lib_ab()
 
     def run(k):
-        os.environ["MICLIP_ATTN_F32_V"] = "0" if k == "prefetch" else "2"
+        os.environ["MICLIP_ATTN_F32_V"] = "3" if k == "prefetch" else "0"
         N.check(L.mi_op_attention_f32(qkv.data_ptr(), outs[k].data_ptr(), B, S, W, 0, sp), "attn f32")
     for k in outs:
         run(k)
