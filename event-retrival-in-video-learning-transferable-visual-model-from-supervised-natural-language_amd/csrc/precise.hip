@@ -446,7 +446,7 @@ __global__ __launch_bounds__(256, MINB) void attn_f32_mfma_kernel(const float* _
                                                             int nseq, int S, int W, int causal) {
   const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
   const int H = W / 64;
-  const int item = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int item = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // (wave-uniform: SGPR descriptors)
   if (item >= nseq * H) return;
   // causal bit 11: the first 32-query block only (the last vision block: outputs read at the CLS rows)
   const int qend = ((causal >> 11) & 1) ? min(S, 32) : S;
@@ -569,7 +569,7 @@ __global__ __launch_bounds__(256, MINB) void attn_f32_mfma_pre_kernel(const floa
   constexpr int NKT = 2;
   const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
   const int H = W / 64;
-  const int item = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int item = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // (wave-uniform: SGPR descriptors)
   if (item >= nseq * H) return;
   const int qend = ((causal >> 11) & 1) ? min(S, 32) : S;   // (bit 11: the first query block only)
   causal &= 1;
