@@ -550,6 +550,114 @@ __global__ __launch_bounds__(256, MINB) void attn_f32_mfma_kernel(const float* _
   }
 }
 
+// The S <= 64 form with its loads batched (round 6; B/32's 50 tokens, the fp32 tower's attention).
+// attn_f32_mfma_kernel above lets hipcc place each load next to its first use: at two waves per
+// SIMD its scheduler keeps two of a key tile's eight K loads in flight and issues V one MFMA ahead,
+// so a wave waits for ~20 dependent L2 round trips per query block.  Here each query block issues
+// Q, both key tiles' K and the first dim tile's V (8 + 16 + 32 loads) together, then a scheduling
+// barrier; the second dim tile's V goes out after the softmax, ahead of the first dim tile's MFMAs.
+// Rows stay in the per-lane offset (rows >= S read zeros and drop their stores by the descriptor's
+// range, which the scalar offset does not enter); the head's column base is the scalar offset.
+// Same MFMAs in the same order, masks, expf and stores: bit-identical to attn_f32_mfma_kernel<2>
+// (tests/test_gpu_ops.py::test_attention_f32_batched_bit_identical).
+__global__ __launch_bounds__(256, 2) void attn_f32_mfma_b_kernel(const float* __restrict__ qkv, float* __restrict__ out,
+                                                                int nseq, int S, int W, int causal) {
+  constexpr int NKT = 2;
+  const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
+  const int H = W / 64;
+  const int item = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // (wave-uniform)
+  if (item >= nseq * H) return;
+  const int qend = ((causal >> 11) & 1) ? min(S, 32) : S;   // (bit 11: the first query block only)
+  causal &= 1;
+  const int bseq = item / H, head = item % H;
+  const int ld = 3 * W;
+  auto rho = [&](int r) { return (r & 3) + 8 * (r >> 2) + 4 * h; };
+  const __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(qkv + (int64_t)bseq * S * ld), (short)0, S * ld * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rout = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(out + (int64_t)bseq * S * W), (short)0, S * W * 4, 0x00020000);
+  typedef unsigned int u32x4a __attribute__((ext_vector_type(4)));
+  // row r's 32 columns 32 h .. 32 h + 31 of the block at column cb (Q: head * 64, K: W + head * 64)
+  auto ld_row32 = [&](int r, int cb, float* v, float mul) {
+    const uint32_t vo = (uint32_t)((r * ld + 32 * h) * 4);
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const u32x4a t = __builtin_bit_cast(u32x4a, __builtin_amdgcn_raw_buffer_load_b128(rin, vo + 16 * c, cb * 4, 0));
+      v[4 * c] = __uint_as_float(t[0]) * mul; v[4 * c + 1] = __uint_as_float(t[1]) * mul;
+      v[4 * c + 2] = __uint_as_float(t[2]) * mul; v[4 * c + 3] = __uint_as_float(t[3]) * mul;
+    }
+  };
+  // V[key rho(st, h) of key tile kt][32 dt + j], the B operand of step st
+  auto ld_v = [&](int dt, float (&vv)[NKT][16]) {
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+      for (int st = 0; st < 16; ++st) {
+        const int key = kt * 32 + (st & 3) + 8 * (st >> 2) + 4 * h;
+        vv[kt][st] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+            rin, (uint32_t)((key * ld + j) * 4), (2 * W + head * 64 + 32 * dt) * 4, 0));
+      }
+  };
+  for (int q0 = 0; q0 < qend; q0 += 32) {
+    const int qi = q0 + j;   // this lane's query in the S^T layout
+    float qv[32], kv[NKT][32], v0[NKT][16], v1[NKT][16];
+    ld_row32(qi, head * 64, qv, 0.125f);
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) ld_row32(kt * 32 + j, W + head * 64, kv[kt], 1.0f);
+    ld_v(0, v0);
+    __builtin_amdgcn_sched_barrier(0);
+    f32x16 sc[NKT];
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+      sc[kt] = f32x16{};
+      if (kt * 32 >= S) continue;
+#pragma unroll
+      for (int st = 0; st < 32; ++st) sc[kt] = __builtin_amdgcn_mfma_f32_32x32x2f32(kv[kt][st], qv[st], sc[kt], 0, 0, 0);
+    }
+    float m = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kt * 32 + rho(r);
+        if (key >= S || (causal && key > qi)) sc[kt][r] = -INFINITY;
+        m = fmaxf(m, sc[kt][r]);
+      }
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    float l = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = expf(sc[kt][r] - m);   // masked keys: exp(-inf) = 0
+        sc[kt][r] = p;
+        l += p;
+      }
+    l += __shfl_xor(l, 32, 64);
+    const float inv = 1.0f / l;
+    ld_v(1, v1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+      f32x16 o = f32x16{};
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt) {
+        if (kt * 32 >= S) continue;
+#pragma unroll
+        for (int st = 0; st < 16; ++st)
+          o = __builtin_amdgcn_mfma_f32_32x32x2f32(sc[kt][st], dt ? v1[kt][st] : v0[kt][st], o, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int qr = q0 + rho(r);
+        const float iv = __shfl(inv, rho(r), 64);   // 1 / l of query rho(r) (held by lane rho(r))
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(o[r] * iv), rout, (uint32_t)((qr * W + j) * 4),
+                                              (head * 64 + 32 * dt) * 4, 0);
+      }
+    }
+  }
+}
+
 // The same kernel for S <= 64 (B/32's 50 tokens: the fp32 tower's attention) with every load of a
 // (sequence, head) issued before its first MFMA (round 6).  attn_f32_mfma_kernel loads K and V
 // inside its query-block loop (twice at S > 32), each key tile's K and each (dim tile, key tile)'s
@@ -833,7 +941,9 @@ hipError_t attention_f32(const float* qkv, float* out, int B, int S, int W, int 
     return hipGetLastError();
   }
 #endif
-  if (attn_f32_mfma_on() && S <= 64)   // (held to 256 registers: two waves per SIMD, no spills)
+  if (attn_f32_mfma_on() && S <= 64 && attn_f32_variant() == 0)   // batched loads (round 6)
+    hipLaunchKernelGGL(attn_f32_mfma_b_kernel, grid4, dim3(256), 0, s, qkv, out, B, S, W, cq);
+  else if (attn_f32_mfma_on() && S <= 64)   // (A/B MICLIP_ATTN_F32_V=2; held to 256 registers: two waves per SIMD)
     hipLaunchKernelGGL((attn_f32_mfma_kernel<2, 2>), grid4, dim3(256), 0, s, qkv, out, B, S, W, cq);
   else if (attn_f32_mfma_on() && S <= 96)
     hipLaunchKernelGGL(attn_f32_mfma_kernel<3>, grid4, dim3(256), 0, s, qkv, out, B, S, W, cq);

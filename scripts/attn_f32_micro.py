@@ -1,6 +1,6 @@
 """The fp32 tower's S <= 64 attention (mi_op_attention_f32) at the bench's pass (10k ViT-B/32
-frames, S = 50, W = 768): the product kernel (in-loop loads) against the every-load-ahead-of-the-first-MFMA
-kernel (A/B MICLIP_ATTN_F32_V=3), interleaved, HIP events, outputs compared.
+frames, S = 50, W = 768): the product kernel (batched loads, round 6) against the round-5 kernel (loads next
+to their first use, A/B MICLIP_ATTN_F32_V=2) and the one-wave-per-SIMD prefetch kernel (=3), interleaved, HIP events, outputs compared.
 usage: python scripts/attn_f32_micro.py [frames] [reps]"""
 import os
 import sys
@@ -21,16 +21,16 @@ def main():
     sp = torch.cuda.current_stream().cuda_stream
     g = torch.Generator(device=dev).manual_seed(3)
     qkv = torch.randn(B * S, 3 * W, device=dev, generator=g) * 2
-    outs = {k: torch.empty(B * S, W, device=dev) for k in ("prefetch", "in_loop")}
+    outs = {k: torch.empty(B * S, W, device=dev) for k in ("batched", "in_loop", "prefetch")}
     L = N.lib_ab()
 
     def run(k):
-        os.environ["MICLIP_ATTN_F32_V"] = "3" if k == "prefetch" else "0"
+        os.environ["MICLIP_ATTN_F32_V"] = {"batched": "0", "in_loop": "2", "prefetch": "3"}[k]
         N.check(L.mi_op_attention_f32(qkv.data_ptr(), outs[k].data_ptr(), B, S, W, 0, sp), "attn f32")
     for k in outs:
         run(k)
     torch.cuda.synchronize()
-    same = torch.equal(outs["prefetch"].view(torch.int32), outs["in_loop"].view(torch.int32))
+    same = all(torch.equal(outs["batched"].view(torch.int32), o.view(torch.int32)) for o in outs.values())
     best = {k: 1e30 for k in outs}
     for _ in range(3):
         for k in outs:

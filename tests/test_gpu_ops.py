@@ -842,22 +842,26 @@ def test_gemm_residual_lagging_group_early_epilogue_bit_identical(gpu, monkeypat
 
 @pytest.mark.parametrize("B,S,W,causal", [(7, 50, 768, 0), (5, 33, 256, 1), (3, 64, 128, 0), (4, 17, 512, 1),
                                           (300, 50, 768, 0), (9, 1, 768, 0)])
-def test_attention_f32_prefetch_bit_identical(gpu, monkeypatch, B, S, W, causal):
-    """The fp32 tower's S <= 64 attention (the product kernel, which loads K and V inside its
-    query-block loop) against the form with every load of a (sequence, head) issued ahead of its
-    first MFMA (attn_f32_mfma_pre_kernel, A/B build, MICLIP_ATTN_F32_V=3; measured slower, kept for
-    the record): the same MFMAs in the same order, so the outputs are bit-identical -- one and two key tiles, causal, 300 sequences, S = 1
-    (the tower tests cover the CLS-row last block's first-query-block flag)."""
+def test_attention_f32_batched_bit_identical(gpu, monkeypatch, B, S, W, causal):
+    """The fp32 tower's S <= 64 attention (attn_f32_mfma_b_kernel, the product kernel since round 6:
+    each query block's loads issued together, K and V once per (sequence, head)) against the
+    kernel that loads next to each first use (A/B build, MICLIP_ATTN_F32_V=2, the round-5 default)
+    and the form with one wave per SIMD and every load ahead of the first MFMA
+    (attn_f32_mfma_pre_kernel, MICLIP_ATTN_F32_V=3): the same MFMAs in the same order, so the
+    outputs are bit-identical -- one and two key tiles, causal, 300 sequences, S = 1 (the tower
+    tests cover the CLS-row last block's first-query-block flag)."""
     import torch
     from miclip import _native
     rng = np.random.default_rng(B * 1000 + S + W + causal)
     qkv = torch.from_numpy((rng.standard_normal((B * S, 3 * W)) * 2).astype(np.float32)).to(gpu)
     outs = []
-    for lib, env in ((_native.lib(), None), (_native.lib_ab(), "3")):
+    for lib, env in ((_native.lib(), None), (_native.lib_ab(), "2"), (_native.lib_ab(), "3")):
         if env:
             monkeypatch.setenv("MICLIP_ATTN_F32_V", env)
         out = torch.full((B * S, W), float("nan"), device=gpu)
         _native.check(lib.mi_op_attention_f32(qkv.data_ptr(), out.data_ptr(), B, S, W, causal, _stream()), "attn f32")
         torch.cuda.synchronize()
         outs.append(out)
-    assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))
+    assert torch.isfinite(outs[0]).all()
+    for o in outs[1:]:
+        assert torch.equal(outs[0].view(torch.int32), o.view(torch.int32))
