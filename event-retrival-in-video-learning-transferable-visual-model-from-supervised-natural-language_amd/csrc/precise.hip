@@ -658,6 +658,192 @@ __global__ __launch_bounds__(256, 2) void attn_f32_mfma_b_kernel(const float* __
   }
 }
 
+// The fp32 tower's S <= 64 attention on the f16 MFMA over split operands (round 6; VERDICT r5 item
+// 5): the operands of both products are split as the tower GEMMs' are (split2h: x s = x1 + x2 + r,
+// |r| <= 2^-22 |x s|), and each product runs as three f16 MFMAs, a1 b1 + a1 b2 + a2 b1, with f32
+// accumulation (the dropped a2 b2 <= 2^-22 |a b|): f32-GEMM-grade scores and outputs, like every
+// other product of the tower.  Scales (powers of two, undone exactly after the MFMAs):
+//   Q  per query row (the lane's 32 dims + its partner lane's: max |q s| in [2^13, 2^14));
+//   K  one per (sequence, head) block: an element's error stays <= max(2^-22 |k|, 2^-39 max |K|),
+//      so a key row far below the block's largest loses nothing that reaches a score at f32 grade;
+//   V  per dim (the C layout of O keeps a dim in one lane);
+//   P  2^14 (softmax values are in [0, 1], the row's largest exactly 1).
+// Layout and loads as attn_f32_mfma_b_kernel: S^T = K Q^T then O = P V with v_mfma_f32_32x32x16_f16
+// (k slot e of step c in lane half h = dim 32 h + 8 c + e; P straight from the S^T registers),
+// 3 x (8 + 4) MFMAs of 32 cycles per 32-query block against 64 + 64 exact-f32 ones of 64.
+typedef _Float16 f16x8_s __attribute__((ext_vector_type(8)));
+typedef float f32x2_s __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x2_s __attribute__((ext_vector_type(2)));
+
+typedef unsigned int u32x4_s __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void split8_s(const float* v, float s, f16x8_s& hi, f16x8_s& lo) {
+  u32x4_s a4, b4;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const f32x2_s x = (f32x2_s){v[2 * e] * s, v[2 * e + 1] * s};
+    const f16x2_s a = __builtin_convertvector(x, f16x2_s);
+    const f16x2_s b = __builtin_convertvector(x - __builtin_convertvector(a, f32x2_s), f16x2_s);
+    a4[e] = __builtin_bit_cast(unsigned int, a);
+    b4[e] = __builtin_bit_cast(unsigned int, b);
+  }
+  hi = __builtin_bit_cast(f16x8_s, a4);
+  lo = __builtin_bit_cast(f16x8_s, b4);
+}
+
+__global__ __launch_bounds__(256, 2) void attn_f32s_kernel(const float* __restrict__ qkv, float* __restrict__ out,
+                                                          int nseq, int S, int W, int causal) {
+  constexpr int NKT = 2;
+  const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
+  const int H = W / 64;
+  const int item = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // (wave-uniform)
+  if (item >= nseq * H) return;
+  const int qend = ((causal >> 11) & 1) ? min(S, 32) : S;   // (bit 11: the first query block only)
+  causal &= 1;
+  const int bseq = item / H, head = item % H;
+  const int ld = 3 * W;
+  auto rho = [&](int r) { return (r & 3) + 8 * (r >> 2) + 4 * h; };
+  const __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(qkv + (int64_t)bseq * S * ld), (short)0, S * ld * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rout = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(out + (int64_t)bseq * S * W), (short)0, S * W * 4, 0x00020000);
+  typedef unsigned int u32x4a __attribute__((ext_vector_type(4)));
+  auto ld_row32 = [&](int r, int cb, float* v) {   // row r, columns cb + 32 h .. + 31 (rows >= S: zeros)
+    const uint32_t vo = (uint32_t)((r * ld + 32 * h) * 4);
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const u32x4a t = __builtin_bit_cast(u32x4a, __builtin_amdgcn_raw_buffer_load_b128(rin, vo + 16 * c, cb * 4, 0));
+      v[4 * c] = __uint_as_float(t[0]); v[4 * c + 1] = __uint_as_float(t[1]);
+      v[4 * c + 2] = __uint_as_float(t[2]); v[4 * c + 3] = __uint_as_float(t[3]);
+    }
+  };
+  // K of both key tiles and V of both dim tiles, once per (sequence, head)
+  float kf[NKT][32], vf[2][NKT][16];
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt) ld_row32(kt * 32 + j, W + head * 64, kf[kt]);
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+      for (int st = 0; st < 16; ++st) {
+        const int key = kt * 32 + (st & 3) + 8 * (st >> 2) + 4 * h;
+        vf[dt][kt][st] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+            rin, (uint32_t)((key * ld + j) * 4), (2 * W + head * 64 + 32 * dt) * 4, 0));
+      }
+  float km = 0.f;
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+    for (int i = 0; i < 32; ++i) km = fmaxf(km, fabsf(kf[kt][i]));
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) km = fmaxf(km, __shfl_xor(km, o, 64));
+  const int ek = __builtin_amdgcn_readfirstlane(split_exp(km));
+  const float sk = ldexpf(1.0f, ek), isk = ldexpf(1.0f, -ek);
+  f16x8_s k1[NKT][4], k2[NKT][4];
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) split8_s(&kf[kt][8 * c], sk, k1[kt][c], k2[kt][c]);
+  f16x8_s v1[2][NKT][2], v2[2][NKT][2];
+  float isv[2];
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt) {
+    float vm = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+      for (int st = 0; st < 16; ++st) vm = fmaxf(vm, fabsf(vf[dt][kt][st]));
+    vm = fmaxf(vm, __shfl_xor(vm, 32, 64));
+    const int ev = split_exp(vm);
+    isv[dt] = ldexpf(1.0f, -ev - 14);   // (and P's 2^14)
+    const float sv = ldexpf(1.0f, ev);
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) split8_s(&vf[dt][kt][8 * u], sv, v1[dt][kt][u], v2[dt][kt][u]);
+  }
+  for (int q0 = 0; q0 < qend; q0 += 32) {
+    const int qi = q0 + j;   // this lane's query in the S^T layout
+    float qv[32];
+    ld_row32(qi, head * 64, qv);
+    float qm = 0.f;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) qm = fmaxf(qm, fabsf(qv[i]));
+    qm = fmaxf(qm, __shfl_xor(qm, 32, 64));
+    const int eq = split_exp(qm);
+    const float sq = ldexpf(1.0f, eq), isq8 = ldexpf(0.125f, -eq);
+    f16x8_s q1[4], q2[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) split8_s(&qv[8 * c], sq, q1[c], q2[c]);
+    f32x16 sc[NKT];
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+      sc[kt] = f32x16{};
+      if (kt * 32 >= S) continue;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        sc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(k1[kt][c], q1[c], sc[kt], 0, 0, 0);
+        sc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(k1[kt][c], q2[c], sc[kt], 0, 0, 0);
+        sc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(k2[kt][c], q1[c], sc[kt], 0, 0, 0);
+      }
+    }
+    float m = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kt * 32 + rho(r);
+        sc[kt][r] = (sc[kt][r] * isk) * isq8;
+        if (key >= S || (causal && key > qi)) sc[kt][r] = -INFINITY;
+        m = fmaxf(m, sc[kt][r]);
+      }
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    float l = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = expf(sc[kt][r] - m);   // masked keys: exp(-inf) = 0
+        sc[kt][r] = p;
+        l += p;
+      }
+    l += __shfl_xor(l, 32, 64);
+    const float inv = 1.0f / l;
+    f16x8_s p1[NKT][2], p2[NKT][2];
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        float pv[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) pv[t] = sc[kt][8 * u + t];
+        split8_s(pv, 16384.0f, p1[kt][u], p2[kt][u]);
+      }
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+      f32x16 o = f32x16{};
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt) {
+        if (kt * 32 >= S) continue;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          o = __builtin_amdgcn_mfma_f32_32x32x16_f16(p1[kt][u], v1[dt][kt][u], o, 0, 0, 0);
+          o = __builtin_amdgcn_mfma_f32_32x32x16_f16(p1[kt][u], v2[dt][kt][u], o, 0, 0, 0);
+          o = __builtin_amdgcn_mfma_f32_32x32x16_f16(p2[kt][u], v1[dt][kt][u], o, 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int qr = q0 + rho(r);
+        const float iv = __shfl(inv, rho(r), 64);   // 1 / l of query rho(r) (held by lane rho(r))
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint((o[r] * isv[dt]) * iv), rout, (uint32_t)((qr * W + j) * 4),
+                                              (head * 64 + 32 * dt) * 4, 0);
+      }
+    }
+  }
+}
+
 // The same kernel for S <= 64 (B/32's 50 tokens: the fp32 tower's attention) with every load of a
 // (sequence, head) issued before its first MFMA (round 6).  attn_f32_mfma_kernel loads K and V
 // inside its query-block loop (twice at S > 32), each key tile's K and each (dim tile, key tile)'s
@@ -941,7 +1127,9 @@ hipError_t attention_f32(const float* qkv, float* out, int B, int S, int W, int 
     return hipGetLastError();
   }
 #endif
-  if (attn_f32_mfma_on() && S <= 64 && attn_f32_variant() == 0)   // batched loads (round 6)
+  if (attn_f32_mfma_on() && S <= 64 && attn_f32_variant() == 0)   // split-f16 operands (round 6)
+    hipLaunchKernelGGL(attn_f32s_kernel, grid4, dim3(256), 0, s, qkv, out, B, S, W, cq);
+  else if (attn_f32_mfma_on() && S <= 64 && attn_f32_variant() == 4)   // exact f32, batched loads (A/B)
     hipLaunchKernelGGL(attn_f32_mfma_b_kernel, grid4, dim3(256), 0, s, qkv, out, B, S, W, cq);
   else if (attn_f32_mfma_on() && S <= 64)   // (A/B MICLIP_ATTN_F32_V=2; held to 256 registers: two waves per SIMD)
     hipLaunchKernelGGL((attn_f32_mfma_kernel<2, 2>), grid4, dim3(256), 0, s, qkv, out, B, S, W, cq);

@@ -843,21 +843,21 @@ def test_gemm_residual_lagging_group_early_epilogue_bit_identical(gpu, monkeypat
 @pytest.mark.parametrize("B,S,W,causal", [(7, 50, 768, 0), (5, 33, 256, 1), (3, 64, 128, 0), (4, 17, 512, 1),
                                           (300, 50, 768, 0), (9, 1, 768, 0)])
 def test_attention_f32_batched_bit_identical(gpu, monkeypatch, B, S, W, causal):
-    """The fp32 tower's S <= 64 attention (attn_f32_mfma_b_kernel, the product kernel since round 6:
-    each query block's loads issued together, K and V once per (sequence, head)) against the
-    kernel that loads next to each first use (A/B build, MICLIP_ATTN_F32_V=2, the round-5 default)
-    and the form with one wave per SIMD and every load ahead of the first MFMA
-    (attn_f32_mfma_pre_kernel, MICLIP_ATTN_F32_V=3): the same MFMAs in the same order, so the
-    outputs are bit-identical -- one and two key tiles, causal, 300 sequences, S = 1 (the tower
-    tests cover the CLS-row last block's first-query-block flag)."""
+    """The exact-f32 MFMA forms of the fp32 tower's S <= 64 attention (A/B build): the batched-load
+    kernel (attn_f32_mfma_b_kernel, MICLIP_ATTN_F32_V=4: each query block's loads issued together,
+    K and V once per (sequence, head)), the kernel that loads next to each first use (=2, the
+    round-5 default) and the one-wave-per-SIMD form with every load ahead of the first MFMA
+    (attn_f32_mfma_pre_kernel, =3): the same MFMAs in the same order, so the outputs are
+    bit-identical -- one and two key tiles, causal, 300 sequences, S = 1.  The product kernel
+    (split-f16 operands) is checked against float64 by test_attention_f32_vs_float64 and against
+    these by test_attention_f32_split_vs_exact."""
     import torch
     from miclip import _native
     rng = np.random.default_rng(B * 1000 + S + W + causal)
     qkv = torch.from_numpy((rng.standard_normal((B * S, 3 * W)) * 2).astype(np.float32)).to(gpu)
     outs = []
-    for lib, env in ((_native.lib(), None), (_native.lib_ab(), "2"), (_native.lib_ab(), "3")):
-        if env:
-            monkeypatch.setenv("MICLIP_ATTN_F32_V", env)
+    for lib, env in ((_native.lib_ab(), "4"), (_native.lib_ab(), "2"), (_native.lib_ab(), "3")):
+        monkeypatch.setenv("MICLIP_ATTN_F32_V", env)
         out = torch.full((B * S, W), float("nan"), device=gpu)
         _native.check(lib.mi_op_attention_f32(qkv.data_ptr(), out.data_ptr(), B, S, W, causal, _stream()), "attn f32")
         torch.cuda.synchronize()
@@ -865,3 +865,39 @@ def test_attention_f32_batched_bit_identical(gpu, monkeypatch, B, S, W, causal):
     assert torch.isfinite(outs[0]).all()
     for o in outs[1:]:
         assert torch.equal(outs[0].view(torch.int32), o.view(torch.int32))
+
+
+@pytest.mark.parametrize("B,S,W,causal,scale", [(7, 50, 768, 0, 2.0), (5, 33, 256, 1, 2.0), (3, 64, 128, 0, 2.0),
+                                                (300, 50, 768, 0, 2.0), (9, 1, 768, 0, 2.0), (6, 50, 512, 0, 30.0),
+                                                (6, 50, 512, 0, 1e-3)])
+def test_attention_f32_split_vs_exact(gpu, monkeypatch, B, S, W, causal, scale):
+    """The product S <= 64 attention of the fp32 tower (attn_f32s_kernel: split-f16 operands on the
+    f16 MFMA, the tower GEMMs' arithmetic) against the exact-f32 MFMA kernel (A/B build,
+    MICLIP_ATTN_F32_V=4) and float64: within f32-GEMM grade of float64 (the same 2e-6 of the
+    output scale as the exact kernel's test), and per-row (sequence, head) ranges that differ by
+    orders of magnitude (rows scaled by 10^[-3, 3]) keep that grade row by row."""
+    import torch
+    from miclip import _native
+    rng = np.random.default_rng(B * 1000 + S + W + causal + int(scale * 7))
+    qkv = (rng.standard_normal((B * S, 3 * W)) * scale).astype(np.float32)
+    qkv *= (10.0 ** rng.uniform(-3, 3, size=(B * S, 1))).astype(np.float32)   # rows of any magnitude
+    d = torch.from_numpy(qkv).to(gpu)
+    outs = []
+    for lib, env in ((_native.lib(), None), (_native.lib_ab(), "4")):
+        if env:
+            monkeypatch.setenv("MICLIP_ATTN_F32_V", env)
+        out = torch.full((B * S, W), float("nan"), device=gpu)
+        _native.check(lib.mi_op_attention_f32(d.data_ptr(), out.data_ptr(), B, S, W, causal, _stream()), "attn f32")
+        torch.cuda.synchronize()
+        outs.append(out.cpu().numpy().astype(np.float64))
+    ref = _attn_ref(qkv, B, S, W, causal)
+    got, exact = outs
+    assert np.isfinite(got).all()
+    H = W // 64
+    # per (row, head): error against the head's output scale (max |V| of the sequence's head)
+    vmax = np.abs(qkv[:, 2 * W:].astype(np.float64)).reshape(B, S, H, 64).max(axis=(1, 3))   # [B, H]
+    scl = np.repeat(vmax, S, axis=0)[:, :, None]                                                 # [B S, H, 1]
+    e_split = (np.abs(got - ref).reshape(B * S, H, 64) / scl).max()
+    e_exact = (np.abs(exact - ref).reshape(B * S, H, 64) / scl).max()
+    print(f"split-f16 {e_split:.3e}  exact-f32 {e_exact:.3e}  (relative to the head's max |V|)")
+    assert e_split < 2e-6, (e_split, e_exact)
