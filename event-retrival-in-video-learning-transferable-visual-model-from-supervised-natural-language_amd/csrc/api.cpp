@@ -75,6 +75,9 @@ struct Layer {
   const float *c3_qkv = nullptr, *c3_out = nullptr, *c3_fc = nullptr, *c3_proj = nullptr;
   // c_fc's output bound for the fused split (EPI_SPLIT_GELU): max_n sum_k |W_fc| and max |b_fc|
   float fc_bw = 0.f, fc_bb = 0.f;
+  // the same for attention's output split (attention_f32_split): max over V's rows of sum_k |W_v|
+  // and max |b_v| (rows 2W .. 3W of in_proj)
+  float v_bw = 0.f, v_bb = 0.f;
   // MX-fp8 copies (weight_dtype MI_FP8, vision tower): e4m3 codes + stage-major e8m0 scales
   const uint8_t *q_qkv = nullptr, *s_qkv = nullptr, *q_out = nullptr, *s_out = nullptr;
   const uint8_t *q_fc = nullptr, *s_fc = nullptr, *q_proj = nullptr, *s_proj = nullptr;
@@ -458,6 +461,17 @@ int mi_clip_create(const mi_clip_arch* arch, const float* weights, int64_t numel
           }
           L[i].fc_bw = (float)(bw * (1.0 + 1e-6));
           L[i].fc_bb = (float)(bb * (1.0 + 1e-6));
+          const float* wq = b.src + o.p_w_qkv;
+          const float* bq = b.src + o.p_b_qkv;
+          bw = bb = 0;
+          for (int64_t n = 2 * Wd; n < 3 * Wd; ++n) {
+            double r = 0;
+            for (int64_t k = 0; k < Wd; ++k) r += std::fabs((double)wq[n * Wd + k]);
+            bw = r > bw ? r : bw;
+            bb = std::fabs((double)bq[n]) > bb ? std::fabs((double)bq[n]) : bb;
+          }
+          L[i].v_bw = (float)(bw * (1.0 + 1e-6));
+          L[i].v_bb = (float)(bb * (1.0 + 1e-6));
         }
       } else {
         L[i] = Layer{F(o.ln1_g), F(o.ln1_b), F(o.b_qkv), F(o.b_out), F(o.ln2_g), F(o.ln2_b), F(o.b_fc), F(o.b_proj),
@@ -1060,6 +1074,9 @@ static int run_tower_f32(mi_clip* c, const std::vector<Layer>& layers, int B, in
     const char* de = ab_getenv("MICLIP_F32_DUP");
     const char* e8 = ab_getenv("MICLIP_F32_8Q");
     const int dmask = de ? atoi(de) : 15;
+    // MICLIP_F32_ATTN_FUSED=0 (A/B): attention's f32 output and the split pass (round 5)
+    const char* ae = ab_getenv("MICLIP_F32_ATTN_FUSED");
+    const bool att_fused = !ae || atoi(ae) != 0;
     const bool dup_on = dmask != 0 && (!e8 || atoi(e8) != 0);
     auto sargs = [&](const uint16_t* A, int64_t lda_rows, bool dup, const uint16_t* w3, const float* c3, const float* b,
                      float* out, int64_t ldo, int rows, int N, int K) {   // lda_rows: row stride in rows of the operand
@@ -1087,7 +1104,10 @@ static int run_tower_f32(mi_clip* c, const std::vector<Layer>& layers, int B, in
       // ln_1's operand feeds in_proj (every row; in the CLS-row last block K / V for every row and Q
       // for the CLS rows, read with a row stride of S)
       const bool d1 = (dmask & 1) && (cls ? dup_ok(M, 2 * W, W) && dup_ok(B, W, W, S) : dup_ok(M, 3 * W, W));
-      HIP_TRY(layernorm_split2h(c->x, W, L.ln1_g, L.ln1_b, M, W, a3, rsc, s, nullptr, d1));
+      // S <= 64: attention writes out_proj's split operand itself (attention_f32_split, its scale
+      // bounded through ln_1's row max; round 6), in place of its f32 output and a split pass
+      const bool fuse_att = S <= 64 && att_fused;
+      HIP_TRY(layernorm_split2h(c->x, W, L.ln1_g, L.ln1_b, M, W, a3, rsc, s, fuse_att ? rmax : nullptr, d1));
       if (cls) {   // K and V for every row, Q for the CLS rows only (as run_tower_fold's last block)
         GemmArgs kv = sargs(a3, 1, d1, L.h3_qkv + (size_t)W * 3 * W, L.c3_qkv + W, L.b_qkv + W, qkv + W, 3 * W, M, 2 * W, W);
         HIP_TRY(gemm_bf16(kv, EPI_F32, s));
@@ -1099,8 +1119,30 @@ static int run_tower_f32(mi_clip* c, const std::vector<Layer>& layers, int B, in
       } else {
         MI_TRY(gemm3(W, L.h3_qkv, L.c3_qkv, L.b_qkv, qkv, 3 * W, EPI_F32, d1));
       }
-      HIP_TRY(attention_f32(qkv, att, B, S, W, causal | (cls ? 0x800 : 0), s));   // (cls: the CLS queries' block)
       float* xr = c->x;
+      if (fuse_att) {
+        // out_proj reads the operand in place: the CLS rows with a row stride of S in the CLS-row
+        // last block (their scales gathered, as the CLS Q GEMM's above)
+        const bool da = (dmask & 2) && (cls ? dup_ok(B, W, W, S) : dup_ok(M, W, W));
+        HIP_TRY(attention_f32_split(qkv, rmax, L.v_bw, L.v_bb, a3, da ? 2 : 0, rsc, B, S, W,
+                                    causal | (cls ? 0x800 : 0), s));
+        if (cls) {
+          float* x_c = qkv + (((size_t)B * W + 63) & ~(size_t)63);
+          float* rsc_c = (float*)c->h;
+          HIP_TRY(hipMemcpy2DAsync(x_c, (size_t)W * 4, c->x, (size_t)S * W * 4, (size_t)W * 4, B, hipMemcpyDeviceToDevice, s));
+          HIP_TRY(hipMemcpy2DAsync(rsc_c, 4, rsc, (size_t)S * 4, 4, B, hipMemcpyDeviceToDevice, s));
+          Mr = B;
+          xr = x_c;
+          *xpost = x_c;
+          *post_stride = 1;
+          GemmArgs g = sargs(a3, S, da, L.h3_out, L.c3_out, L.b_out, xr, W, B, W, W);
+          g.rsc = rsc_c;
+          HIP_TRY(gemm_bf16(g, EPI_RESID_F32, s));
+        } else {
+          MI_TRY(gemm3(W, L.h3_out, L.c3_out, L.b_out, xr, W, EPI_RESID_F32, da));
+        }
+      } else {
+      HIP_TRY(attention_f32(qkv, att, B, S, W, causal | (cls ? 0x800 : 0), s));   // (cls: the CLS queries' block)
       const float* ar = att;
       if (cls) {
         // the last block after attention on the CLS rows only (see last_block_cls), gathered into
@@ -1116,10 +1158,11 @@ static int run_tower_f32(mi_clip* c, const std::vector<Layer>& layers, int B, in
         *post_stride = 1;
       }
       const bool da = (dmask & 2) && dup_ok(Mr, W, W);          // attention's split -> out_proj
-      const bool df = (dmask & 4) && dup_ok(Mr, 4 * W, W);      // ln_2's split -> c_fc
-      const bool dp = (dmask & 8) && dup_ok(Mr, W, 4 * W);      // c_fc's output split -> c_proj
       HIP_TRY(split2h_rows(ar, W, Mr, W, da ? 2 : 0, 0, a3, rsc, s));
       MI_TRY(gemm3(W, L.h3_out, L.c3_out, L.b_out, xr, W, EPI_RESID_F32, da));
+      }
+      const bool df = (dmask & 4) && dup_ok(Mr, 4 * W, W);      // ln_2's split -> c_fc
+      const bool dp = (dmask & 8) && dup_ok(Mr, W, 4 * W);      // c_fc's output split -> c_proj
       if (fuse_split) {   // c_fc's epilogue writes c_proj's split operand (EPI_SPLIT_GELU)
         HIP_TRY(layernorm_split2h(xr, W, L.ln2_g, L.ln2_b, Mr, W, a3, rsc, s, rmax, df));
         GemmArgs g = sargs(a3, 1, df, L.h3_fc, L.c3_fc, L.b_fc, nullptr, 0, Mr, 4 * W, W);
@@ -1568,6 +1611,15 @@ int mi_op_gemm_split2h(const void* A3, const void* W3, const float* a_scale, con
   if (dup && (K3 % 3 || !bias || !gemm_8q_ok(g)))
     return fail(MI_ERR_UNSUPPORTED, "mi_op_gemm_split2h: the [x1 x2] layout needs M >= 256, N %% 256 == 0, K %% 64 == 0");
   HIP_TRY(gemm_bf16(g, epi, (hipStream_t)stream));
+  return MI_OK;
+}
+
+int mi_op_attention_f32_split(const float* qkv, const float* rmax, float bw, float bb, void* out, int32_t role,
+                              float* scale, int32_t B, int32_t S, int32_t W, int32_t causal, void* stream) {
+  if (!qkv || !rmax || !out || !scale || B < 0 || S < 1 || W < 64 || (causal & ~1) || (role != 0 && role != 2))
+    return fail(MI_ERR_ARG, "mi_op_attention_f32_split: bad arguments");
+  if (W % 64 || S > 64) return fail(MI_ERR_UNSUPPORTED, "mi_op_attention_f32_split: W %% 64 == 0 and S <= 64");
+  HIP_TRY(attention_f32_split(qkv, rmax, bw, bb, (uint16_t*)out, role, scale, B, S, W, causal, (hipStream_t)stream));
   return MI_OK;
 }
 

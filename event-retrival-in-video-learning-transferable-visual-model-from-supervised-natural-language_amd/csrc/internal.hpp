@@ -200,6 +200,11 @@ hipError_t layernorm_f32(const float* x, int64_t in_stride, const float* g, cons
                          int S = 0);
 // MHA core over qkv f32 [B*S, 3W] -> out f32 [B*S, W], head dim 64
 hipError_t attention_f32(const float* qkv, float* out, int B, int S, int W, int causal, hipStream_t s);
+// S <= 64: the attention output as out_proj's split operand (role 0 [x1 x1 x2] / role 2 [x1 x2],
+// a3 row stride 3W / 2W fp16) and rsc[row] = 1 / s, s from the bound rmax[row] * bw + bb over the
+// sequence's rows (precise.hip attn_f32s_kernel)
+hipError_t attention_f32_split(const float* qkv, const float* rmax, float bw, float bb, uint16_t* a3, int role,
+                               float* rsc, int B, int S, int W, int causal, hipStream_t s);
 // pixels [B,3,R,R] (f32 / bf16) -> patches f32 [B*G*G, Kp]
 hipError_t im2col_f32(const void* pixels, int in_bf16, float* out, int B, int R, int P, int Kp, hipStream_t s);
 // im2col_f32 + split2h_rows (role 0) in one pass: conv1's split operand [B G^2][3 Kp] fp16 and its

@@ -691,8 +691,20 @@ __device__ __forceinline__ void split8_s(const float* v, float s, f16x8_s& hi, f
   lo = __builtin_bit_cast(f16x8_s, b4);
 }
 
+// OUT 0: f32 out [rows][W].  OUT 1 / 2: out_proj's split operand straight from the registers
+// (the split pass over the f32 output, split2h_rows role 0 / 2, folded in): o s = x1 + x2 stored as
+// [x1 | x1 | x2] / [x1 | x2] fp16 rows (a3, row stride 3W / 2W) and rsc[row] = 1 / s.  A row's scale
+// has to be one for all its heads (out_proj sums over them), so it comes from a bound instead of
+// the row's max: |o[r][d]| <= max_k |V[k][d]| (softmax weights are a convex combination) and
+// |V[k][d]| <= rmax[k] max_d sum_k' |W_v[d][k']| + max |b_v| (rmax: ln_1's row max |h|, bw / bb:
+// the weight constants api.cpp computes at load), maximised over the sequence's rows and padded by
+// 2^-8 for the rounding of the computed values; every head's wave derives the same power of two.
+// A loose bound only lowers the split's subnormal floor (|o s| < 2^14 always), as EPI_SPLIT_GELU's.
+template <int OUT>
 __global__ __launch_bounds__(256, 2) void attn_f32s_kernel(const float* __restrict__ qkv, float* __restrict__ out,
-                                                          int nseq, int S, int W, int causal) {
+                                                          int nseq, int S, int W, int causal,
+                                                          const float* __restrict__ rmax, float bw, float bb,
+                                                          uint16_t* __restrict__ a3, float* __restrict__ rsc) {
   constexpr int NKT = 2;
   const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
   const int H = W / 64;
@@ -706,7 +718,21 @@ __global__ __launch_bounds__(256, 2) void attn_f32s_kernel(const float* __restri
   const __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(qkv + (int64_t)bseq * S * ld), (short)0, S * ld * 4, 0x00020000);
   const __amdgpu_buffer_rsrc_t rout = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(out + (int64_t)bseq * S * W), (short)0, S * W * 4, 0x00020000);
+      (void*)(out + (int64_t)bseq * S * W), (short)0, OUT == 0 ? S * W * 4 : 0, 0x00020000);
+  // OUT 1 / 2: the sequence's rows of the split operand, and their scale (see above)
+  const __amdgpu_buffer_rsrc_t rsp = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a3 + (OUT == 0 ? 0 : (int64_t)bseq * S * (OUT == 2 ? 2 : 3) * W)), (short)0,
+      OUT == 0 ? 0 : S * (OUT == 2 ? 2 : 3) * W * 2, 0x00020000);
+  float so = 1.0f;
+  if constexpr (OUT != 0) {
+    float rm = lane < S ? rmax[(int64_t)bseq * S + lane] : 0.f;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) rm = fmaxf(rm, __shfl_xor(rm, o, 64));
+    const float bound = (rm * bw + bb) * (1.0f + 1.0f / 256.0f);
+    const int eo = __builtin_amdgcn_readfirstlane(split_exp(bound));
+    so = ldexpf(1.0f, eo);
+    if (head == 0 && lane < S) rsc[(int64_t)bseq * S + lane] = ldexpf(1.0f, -eo);
+  }
   typedef unsigned int u32x4a __attribute__((ext_vector_type(4)));
   auto ld_row32 = [&](int r, int cb, float* v) {   // row r, columns cb + 32 h .. + 31 (rows >= S: zeros)
     const uint32_t vo = (uint32_t)((r * ld + 32 * h) * 4);
@@ -837,8 +863,28 @@ __global__ __launch_bounds__(256, 2) void attn_f32s_kernel(const float* __restri
       for (int r = 0; r < 16; ++r) {
         const int qr = q0 + rho(r);
         const float iv = __shfl(inv, rho(r), 64);   // 1 / l of query rho(r) (held by lane rho(r))
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint((o[r] * isv[dt]) * iv), rout, (uint32_t)((qr * W + j) * 4),
-                                              (head * 64 + 32 * dt) * 4, 0);
+        const float y = (o[r] * isv[dt]) * iv;
+        if constexpr (OUT == 0) {
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(y), rout, (uint32_t)((qr * W + j) * 4),
+                                                (head * 64 + 32 * dt) * 4, 0);
+        } else {
+          // split2h's arithmetic; lanes j, j ^ 1 (dims d, d ^ 1 of row qr) pair their halves into
+          // dwords: the even lane stores x1 of both, the odd lane x2 of both
+          _Float16 x1, x2;
+          split2h(y * so, x1, x2);
+          const uint32_t b1 = __builtin_bit_cast(uint16_t, x1), b2 = __builtin_bit_cast(uint16_t, x2);
+          const uint32_t mine = (j & 1) ? b1 : b2;   // what the partner lane needs
+          const uint32_t got = (uint32_t)__builtin_amdgcn_mov_dpp((int)mine, 0xb1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
+          const uint32_t pk = (j & 1) ? (got | (b2 << 16)) : (b1 | (got << 16));
+          // (no branch: the odd lane's offset selects the x2 block; OUT 1's second x1 copy is
+          // stored by the even lanes, the odd lanes' copy goes out of the descriptor's range)
+          const uint32_t ro = (uint32_t)((qr * (OUT == 2 ? 2 : 3) * W + (j & ~1)) * 2);
+          const uint32_t xo = (j & 1) ? (uint32_t)((OUT == 2 ? 1 : 2) * W * 2) : 0u;
+          __builtin_amdgcn_raw_buffer_store_b32(pk, rsp, ro + xo, (head * 64 + 32 * dt) * 2, 0);
+          if (OUT == 1)
+            __builtin_amdgcn_raw_buffer_store_b32(pk, rsp, (j & 1) ? 0x80000000u : ro + (uint32_t)(W * 2),
+                                                  (head * 64 + 32 * dt) * 2, 0);
+        }
       }
     }
   }
@@ -1128,7 +1174,8 @@ hipError_t attention_f32(const float* qkv, float* out, int B, int S, int W, int 
   }
 #endif
   if (attn_f32_mfma_on() && S <= 64 && attn_f32_variant() == 0)   // split-f16 operands (round 6)
-    hipLaunchKernelGGL(attn_f32s_kernel, grid4, dim3(256), 0, s, qkv, out, B, S, W, cq);
+    hipLaunchKernelGGL(attn_f32s_kernel<0>, grid4, dim3(256), 0, s, qkv, out, B, S, W, cq, nullptr, 0.f, 0.f,
+                       nullptr, nullptr);
   else if (attn_f32_mfma_on() && S <= 64 && attn_f32_variant() == 4)   // exact f32, batched loads (A/B)
     hipLaunchKernelGGL(attn_f32_mfma_b_kernel, grid4, dim3(256), 0, s, qkv, out, B, S, W, cq);
   else if (attn_f32_mfma_on() && S <= 64)   // (A/B MICLIP_ATTN_F32_V=2; held to 256 registers: two waves per SIMD)
@@ -1141,6 +1188,18 @@ hipError_t attention_f32(const float* qkv, float* out, int B, int S, int W, int 
     hipLaunchKernelGGL(attn_f32_kernel<64>, grid, dim3(64), 0, s, qkv, out, S, W, causal);
   else
     hipLaunchKernelGGL(attn_f32_kernel<256>, grid, dim3(256), 0, s, qkv, out, S, W, causal);
+  return hipGetLastError();
+}
+
+hipError_t attention_f32_split(const float* qkv, const float* rmax, float bw, float bb, uint16_t* a3, int role,
+                               float* rsc, int B, int S, int W, int causal, hipStream_t s) {
+  if (B <= 0) return hipSuccess;
+  if (W % 64 || S < 1 || S > 64 || (role != 0 && role != 2)) return hipErrorInvalidValue;
+  const dim3 grid4((unsigned)(((int64_t)B * (W / 64) + 3) / 4));
+  if (role == 2)
+    hipLaunchKernelGGL(attn_f32s_kernel<2>, grid4, dim3(256), 0, s, qkv, nullptr, B, S, W, causal, rmax, bw, bb, a3, rsc);
+  else
+    hipLaunchKernelGGL(attn_f32s_kernel<1>, grid4, dim3(256), 0, s, qkv, nullptr, B, S, W, causal, rmax, bw, bb, a3, rsc);
   return hipGetLastError();
 }
 

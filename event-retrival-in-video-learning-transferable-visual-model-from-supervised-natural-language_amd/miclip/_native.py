@@ -41,6 +41,7 @@ EXPORTS = (
     "mi_op_quantize_mx", "mi_op_gemm_mx",
     "mi_mirror_build", "mi_rank_mirror_workspace_bytes", "mi_rank_mirror", "mi_normalize_rows_f16",
     "mi_jpeg_decode_transform", "mi_op_split2h", "mi_op_gemm_split2h", "mi_op_attention_f32",
+    "mi_op_attention_f32_split",
     "mi_clip_kernel_events", "mi_clip_kernel_times",
 )
 
@@ -136,6 +137,8 @@ def _bind(path):
         "mi_op_split2h": (ctypes.c_int, [P, I64, I64, I32, I32, I32, P, P, P]),
         "mi_op_gemm_split2h": (ctypes.c_int, [P, P, P, P, P, P, I32, I32, I32, I32, P]),
         "mi_op_attention_f32": (ctypes.c_int, [P, P, I32, I32, I32, I32, P]),
+        "mi_op_attention_f32_split": (ctypes.c_int, [P, P, ctypes.c_float, ctypes.c_float, P, I32, P, I32, I32, I32, I32,
+                                                     P]),
         "mi_clip_kernel_events": (ctypes.c_int, [P, I32, I32]),
         "mi_clip_kernel_times": (ctypes.c_int, [P, P, I32]),
         "mi_op_quantize_mx": (ctypes.c_int, [P, P, P, I32, I32, P]),
@@ -153,7 +156,7 @@ def _bind(path):
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
-    if L.mi_abi_version() != 6:
+    if L.mi_abi_version() != 7:
         raise MiClipError("libmiclip ABI version mismatch")
     _check_sources(L, path)
     return L

@@ -35,11 +35,12 @@
 extern "C" {
 #endif
 
-#define MICLIP_ABI_VERSION 6   /* 2: mi_jpeg_workspace_bytes / mi_jpeg_decode take the data size;
+#define MICLIP_ABI_VERSION 7   /* 2: mi_jpeg_workspace_bytes / mi_jpeg_decode take the data size;
                                   3: mi_normalize_rows_f16, mi_jpeg_decode_transform;
                                   4: mi_op_split2h, mi_op_gemm_split2h, mi_op_attention_f32;
                                   5: mi_clip_kernel_events, mi_clip_kernel_times;
-                                  6: mi_build_id, mi_build_sources */
+                                  6: mi_build_id, mi_build_sources;
+                                  7: mi_op_attention_f32_split */
 
 enum mi_dtype { MI_F32 = 0, MI_BF16 = 1, MI_F16 = 2, MI_FP8 = 3 /* weights only: MX-fp8 vision GEMMs */ };
 enum mi_status { MI_OK = 0, MI_ERR_ARG = -1, MI_ERR_HIP = -2, MI_ERR_UNSUPPORTED = -3, MI_ERR_STATE = -4 };
@@ -354,8 +355,15 @@ int mi_op_split6(const float* x, int64_t ldx, int64_t rows, int32_t K, int32_t r
  *   [M][2K] (the 8-phase kernel reads it as [x1 x1 x2]; needs a bias, M >= 256,
  *   N % 256 == 0, K % 64 == 0).
  * mi_op_attention_f32: f32 MHA core of the fp32 tower: qkv f32 [B*S, 3W] (q | k | v, head dim
- *   64) -> out f32 [B*S, W], softmax(q k^T / 8 (+ causal mask)) v per (sequence, head); S <= 128
- *   on the exact-f32 MFMA, longer sequences on a per-row f32 kernel. */
+ *   64) -> out f32 [B*S, W], softmax(q k^T / 8 (+ causal mask)) v per (sequence, head); S <= 64
+ *   on split-f16 operands on the f16 MFMA (f32-GEMM grade, as mi_op_gemm_split2h), S <= 128 on the
+ *   exact-f32 MFMA, longer sequences on a per-row f32 kernel.
+ * mi_op_attention_f32_split (S <= 64): the same output as out_proj's split operand (role 0
+ *   [x1 x1 x2] / role 2 [x1 x2] fp16 rows, as mi_op_split2h) with ONE scale per sequence,
+ *   scale[row] = 1 / s: s is the power of two with B_seq s in [2^13, 2^14) for the bound
+ *   B_seq = (max over the sequence's rows of rmax[row] * bw + bb) * (1 + 2^-8) -- rmax the row max
+ *   |h| of the LayerNorm output that produced V = h W_v^T + b_v, bw = max_d sum_k |W_v[d][k]|,
+ *   bb = max |b_v| -- so every head of a row shares it; x1 = f16(o s), x2 = f16(o s - x1). */
 int mi_op_split2h(const float* x, int64_t ldx, int64_t rows, int32_t K, int32_t role, int32_t gelu, void* out,
                   float* scale, void* stream);
 /* Kernel timing of the product path (measurement only; bench.py's roofline): after
@@ -370,6 +378,8 @@ int mi_clip_kernel_times(mi_clip* ctx, float* us, int32_t n);
 int mi_op_gemm_split2h(const void* A3, const void* W3, const float* a_scale, const float* w_scale, const float* bias,
                        float* out, int32_t M, int32_t N, int32_t K3, int32_t epi, void* stream);
 int mi_op_attention_f32(const float* qkv, float* out, int32_t B, int32_t S, int32_t W, int32_t causal, void* stream);
+int mi_op_attention_f32_split(const float* qkv, const float* rmax, float bw, float bb, void* out, int32_t role,
+                              float* scale, int32_t B, int32_t S, int32_t W, int32_t causal, void* stream);
 int mi_op_gemm_ln(const void* x16, int64_t lda, const float* rs, const void* Wf, const float* colsum,
                   const float* colc, void* out, int32_t M, int32_t N, int32_t K, int32_t gelu, void* stream);
 /* mi_op_gemm_residual: attn.out_proj / mlp.c_proj with the residual add fused (replaces

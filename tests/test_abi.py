@@ -28,7 +28,7 @@ def test_library_exports_every_symbol():
     out = os.popen(f"nm -D --defined-only {_native.LIB_PATH}").read()
     for name in _declared():
         assert re.search(rf"\bT {name}$", out, re.M), f"{name} not exported"
-    assert L.mi_abi_version() == 6
+    assert L.mi_abi_version() == 7
 
 
 def test_library_fingerprint_matches_its_sources(tmp_path):
