@@ -166,8 +166,10 @@ def kernel_timing(model, cfg, chunk, reps=20):
         # row scale, 2 fp16 terms per f32 value; the weights' copies built at load) and one f16 GEMM
         # over K' = 3K with the row / column scales in its f32 epilogue (api.cpp run_tower_f32);
         # "tflops" counts the f32 GEMM's useful flops, "f16_tflops" the MFMA work executed (3x);
-        # "<gemm>_split" times the split of that GEMM's input (attention / c_fc outputs; ln_1 / ln_2
-        # write theirs directly), "attention" the exact-f32 MFMA attention
+        # "<gemm>_split" times a split pass over that GEMM's input (in the tower none runs: ln_1 / ln_2
+        # write their splits directly, c_fc's epilogue writes c_proj's and, since round 6, attention
+        # writes out_proj's), "attention" the S <= 64 attention on split-f16 operands with f32
+        # output, "attention_split" the same writing out_proj's split operand (the tower's launch)
         del A, outb
         Af = torch.randn(M, 4 * W, device=dev, generator=g) * 0.5
         Wf = torch.randn(4 * W, 4 * W, device=dev, generator=g) * 0.02
@@ -193,6 +195,14 @@ def kernel_timing(model, cfg, chunk, reps=20):
         att32 = outF[:, :W].contiguous()
         timed("attention", lambda: N.check(L.mi_op_attention_f32(qkv32.data_ptr(), att32.data_ptr(), chunk, S, W, 0, sp),
                                            "attn f32"), flops=4.0 * chunk * S * S * W, nbytes=M * 4 * W * 4)
+        if S <= 64:
+            rmax = qkv32[:, 2 * W:].abs().amax(dim=1).contiguous()   # a valid bound: bw = 1, bb = 0
+            a3o = torch.empty(M, 2 * W, dtype=torch.int16, device=dev)
+            rso = torch.empty(M, device=dev)
+            timed("attention_split", lambda: N.check(L.mi_op_attention_f32_split(
+                qkv32.data_ptr(), rmax.data_ptr(), 1.0, 0.0, a3o.data_ptr(), 2, rso.data_ptr(), chunk, S, W, 0, sp),
+                "attn f32 split"), flops=4.0 * chunk * S * S * W, nbytes=M * 4 * W * 4)
+            del rmax, a3o, rso
         del outF, qkv32, att32
         return res
     if getattr(model, "weights", "bf16") == "fp8":
