@@ -164,7 +164,9 @@ __global__ __launch_bounds__(64) void attention_kernel(const uint16_t* __restric
 // PIPE (S <= 64: NT = 1, SLOTS = 1, HP = 1): persistent workgroups walk items blockIdx.x,
 // + gridDim.x, ... and load the next item's Q fragments and K / V pieces into registers before
 // computing the current one, so a workgroup always has an item's qkv reads in flight.
-template <int NT, int PP, int SLOTS, int HP = 1, bool PIPE = false>
+// VB (S <= 64 instance): the V^T fragments' eight LDS reads issued together and waited for once
+// before the P V MFMAs (hipcc otherwise waits for each read right before its MFMA)
+template <int NT, int PP, int SLOTS, int HP = 1, bool PIPE = false, bool VB = false>
 __device__ __forceinline__ void attention_flash_body(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ out,
                                                      int S, int W, int H, int causal, uint8_t* __restrict__ q8,
                                                      uint8_t* __restrict__ qs, int64_t rows_pad, int items = 0) {
@@ -339,6 +341,7 @@ __device__ __forceinline__ void attention_flash_body(const uint16_t* __restrict_
       if (SLOTS == 1) {
         __builtin_amdgcn_sched_barrier(0);
         read_vf();
+        if (VB) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       }
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
@@ -433,6 +436,12 @@ __global__ __launch_bounds__(256) void attention_pipe_kernel(const uint16_t* __r
                                                              int S, int W, int H, int causal, uint8_t* __restrict__ q8,
                                                              uint8_t* __restrict__ qs, int64_t rows_pad, int items) {
   attention_flash_body<1, 2, 1, 1, true>(qkv, out, S, W, H, causal, q8, qs, rows_pad, items);
+}
+
+__global__ __launch_bounds__(256) void attention_vb_kernel(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ out,
+                                                           int S, int W, int H, int causal, uint8_t* __restrict__ q8,
+                                                           uint8_t* __restrict__ qs, int64_t rows_pad) {
+  attention_flash_body<1, 2, 1, 1, false, true>(qkv, out, S, W, H, causal, q8, qs, rows_pad);
 }
 
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6))) void attention_short2_kernel(
@@ -1166,6 +1175,12 @@ hipError_t attention(const uint16_t* qkv, uint16_t* out, int B, int S, int W, in
     const int gp = std::min(items, cu_count() * (per > 0 ? per : 5));
     hipLaunchKernelGGL(attention_pipe_kernel, dim3(gp), dim3(256), 0, s, qkv, out, S, W, H, causal, q8, qs,
                        ((int64_t)B * S + 1) & ~1, items);
+    return hipGetLastError();
+  }
+  // 6: the V^T fragment reads batched (attention_vb_kernel)
+  if (se && se[0] == '6' && !one_wave && !old_flash && S <= 64) {
+    hipLaunchKernelGGL(attention_vb_kernel, grid, dim3(256), 0, s, qkv, out, S, W, H, causal | (q0only << 11), q8, qs,
+                       ((int64_t)B * S + 1) & ~1);
     return hipGetLastError();
   }
   // 2: two heads per workgroup; 3: the occupancy-targeted single-head kernel

@@ -29,7 +29,8 @@ def main():
             continue
         qkv = (torch.randn(B * S, 3 * W, device=dev) * 1.5).bfloat16()
         outs = {}
-        modes = ([0, 0x100, "short", "short2", "short3", "pipe4", "pipe8"] if S <= 64 else [0, 0x100] if S <= 96
+        modes = ([0, "vb"] if S <= 64 and os.environ.get("ATTN_SHORT_MODES") == "vb" else
+                 [0, 0x100, "short", "short2", "short3", "pipe4", "pipe8", "vb"] if S <= 64 else [0, 0x100] if S <= 96
                  else [0] + [f"v{i}" for i in os.environ.get("ATTN_VARS", "4,5,6,7,8,9,10").split(",")])
         # resident-K/V kernel variants (attention.hip): v1 8 waves one tile at a time, v2 8 waves
         # two tiles at a time, v3 16 waves one tile at a time.  Every mode is timed in 3
@@ -39,8 +40,9 @@ def main():
 
         def run(mode):
             os.environ.pop("MICLIP_ATTN_SHORT", None)
-            if mode in ("short", "short2", "short3", "pipe4", "pipe8"):
-                os.environ["MICLIP_ATTN_SHORT"] = {"short": "1", "short2": "2", "short3": "3", "pipe4": "54", "pipe8": "58"}[mode]
+            if mode in ("short", "short2", "short3", "pipe4", "pipe8", "vb"):
+                os.environ["MICLIP_ATTN_SHORT"] = {"short": "1", "short2": "2", "short3": "3", "pipe4": "54", "pipe8": "58",
+                                                   "vb": "6"}[mode]
                 os.environ.pop("MICLIP_ATTN_VAR", None)
             elif isinstance(mode, str):
                 os.environ["MICLIP_ATTN_VAR"] = mode[1:]
@@ -66,7 +68,7 @@ def main():
             fl = 4.0 * B * S * S * W * (0.5 if causal else 1.0)
             by = B * S * 4 * W * 2
             d = (outs[mode].float() - outs[0].float()).abs().max().item()
-            kind = {0: "default", "v1": "res 8w x1", "v11": "res 8w x1 unsplit", "v12": "res 8w x1 split", "v13": "res 8w split first", "v14": "res 8w Q ahead", "v2": "res 8w x2", "v3": "res 16w x1", "v4": "r32 8w x2", "v5": "r32 12w", "v6": "r32 12w stag1", "v7": "r32 12w stag2", "v8": "r32 12w noload", "v9": "r32 12w noexp", "v10": "r32 12w 2-phase", "short": "res 4w (S<=64)", "short2": "flash 2 heads/wg", "short3": "flash 1h occ-6", "pipe4": "pipe 4/CU", "pipe8": "pipe 8/CU", 0x100: "one-wave", 0x200: "flash(chunked)"}[mode]
+            kind = {0: "default", "v1": "res 8w x1", "v11": "res 8w x1 unsplit", "v12": "res 8w x1 split", "v13": "res 8w split first", "v14": "res 8w Q ahead", "v2": "res 8w x2", "v3": "res 16w x1", "v4": "r32 8w x2", "v5": "r32 12w", "v6": "r32 12w stag1", "v7": "r32 12w stag2", "v8": "r32 12w noload", "v9": "r32 12w noexp", "v10": "r32 12w 2-phase", "short": "res 4w (S<=64)", "short2": "flash 2 heads/wg", "short3": "flash 1h occ-6", "pipe4": "pipe 4/CU", "pipe8": "pipe 8/CU", "vb": "flash V reads batched", 0x100: "one-wave", 0x200: "flash(chunked)"}[mode]
             print(f"{name:9s} {kind:16s} B={B} S={S} W={W}: {us:8.1f} us "
                   f"{fl / us / 1e6:6.1f} TFLOP/s {by / us / 1e3:7.1f} GB/s  maxdiff {d:.3g}", flush=True)
 
