@@ -1162,8 +1162,19 @@ hipError_t launch(const GemmArgs& a, hipStream_t s) {
 #if MICLIP_AB
   if (const char* sm = std::getenv("MICLIP_SMALLM")) small_t = std::atoi(sm);
 #endif
+  // (A/B MICLIP_SMALL64=u: 64 x 64 tiles when there are fewer than u tiles of 128 x 128)
+  int small64 = 0;
+#if MICLIP_AB
+  if (const char* sm = std::getenv("MICLIP_SMALL64")) small64 = std::atoi(sm);
+#endif
   if (EPI == EPI_BF16 && ((a.M + 255) / 256) * (a.N / 256) < small_t && a.N % 128 == 0 && !a.group) {
     const int nt2 = ((a.M + 127) / 128) * (a.N / 128);
+    if (nt2 < small64) {
+      const int nt3 = ((a.M + 63) / 64) * (a.N / 64);
+      const int g = nt3 < 4 * cu_count() ? nt3 : 4 * cu_count();
+      hipLaunchKernelGGL((gemm_kernel<EPI, 64, 64, 2, 2>), dim3(g), dim3(256), 0, s, a);
+      return hipGetLastError();
+    }
     const int g = nt2 < 2 * cu_count() ? nt2 : 2 * cu_count();
     hipLaunchKernelGGL((gemm_kernel<EPI, 128, 128, 2, 2>), dim3(g), dim3(256), 0, s, a);
     return hipGetLastError();

@@ -1,6 +1,6 @@
 """encode_text timing (32 queries, B/32 text tower; the bench's step) with the product library
 against A/B variants of the small-M GEMM dispatch (MICLIP_SMALLM=t: 128 x 128 tiles below t
-256-tiles), interleaved in one process, HIP events.
+256-tiles; MICLIP_SMALL64=u: 64 x 64 tiles below u 128-tiles), interleaved in one process, HIP events.
 
   python scripts/text_micro.py [queries] [rounds]
 """
@@ -22,14 +22,18 @@ def main():
     dev = torch.device("cuda:0")
     cfg = config.get_config("ViT-B/32")
     tk = torch.from_numpy(weights.synthetic_tokens(Q, cfg.context_length, cfg.vocab_size)).to(dev)
-    table = {"prod": (_native.lib, None), "sm64": (_native.lib_ab, "64"), "sm128": (_native.lib_ab, "128")}
+    table = {"prod": (_native.lib, None), "sm64": (_native.lib_ab, "64"), "t64_256": (_native.lib_ab, "64", "256"),
+             "t64_1024": (_native.lib_ab, "64", "1024")}
     models = {}
 
     def use(k):
         _native.lib = table[k][0]
         os.environ.pop("MICLIP_SMALLM", None)
+        os.environ.pop("MICLIP_SMALL64", None)
         if table[k][1]:
             os.environ["MICLIP_SMALLM"] = table[k][1]
+        if len(table[k]) > 2:
+            os.environ["MICLIP_SMALL64"] = table[k][2]   # 64 x 64 tiles below that many 128 x 128 tiles
 
     for k in table:
         use(k)
