@@ -1162,8 +1162,11 @@ hipError_t launch(const GemmArgs& a, hipStream_t s) {
 #if MICLIP_AB
   if (const char* sm = std::getenv("MICLIP_SMALLM")) small_t = std::atoi(sm);
 #endif
-  // (A/B MICLIP_SMALL64=u: 64 x 64 tiles when there are fewer than u tiles of 128 x 128)
-  int small64 = 0;
+  // Fewer 128 x 128 tiles than CUs (the text tower's in_proj / out_proj / c_proj at 32 queries):
+  // 64 x 64 tiles, bit-identical again (round 6: encode_text of 32 queries 1131 -> 1006 us,
+  // scripts/text_micro.py, profiles/r06_v_text_micro.log).  A/B MICLIP_SMALL64=u moves the
+  // threshold to u tiles of 128 x 128 (0: off).
+  int small64 = cu_count();
 #if MICLIP_AB
   if (const char* sm = std::getenv("MICLIP_SMALL64")) small64 = std::atoi(sm);
 #endif

@@ -943,3 +943,33 @@ def test_attention_f32_split_output_bit_exact(gpu, B, S, W, causal):
         want = np.concatenate(blocks, axis=1)
         got = a3.cpu().numpy()
         assert np.array_equal(got.view(np.uint16), want.view(np.uint16)), np.argwhere(got.view(np.uint16) != want.view(np.uint16))[:5]
+
+
+@pytest.mark.parametrize("M,N,K", [(2464, 1536, 512), (2464, 512, 512), (2464, 512, 2048), (400, 2304, 768),
+                                   (65, 128, 64), (1000, 768, 3072)])
+def test_gemm_small_tiles_bit_identical(gpu, monkeypatch, M, N, K):
+    """The smallest bf16 GEMMs (fewer 128 x 128 tiles than CUs: the text tower at 32 queries, small
+    image batches) on 64 x 64 tiles (round 6) against 128 x 128 tiles (A/B MICLIP_SMALL64=0) and the
+    256 x 256 path (MICLIP_SMALLM=0): the same k order per output, bit for bit; ragged M."""
+    import torch
+    from miclip import _native
+    g = torch.Generator(device="cpu").manual_seed(M + 3 * N + K)
+    A = (torch.randn(M, K, generator=g) * 0.5).bfloat16().to(gpu)
+    W = (torch.randn(N, K, generator=g) * K ** -0.5).bfloat16().to(gpu)
+    bias = torch.randn(N, generator=g).float().to(gpu)
+    outs = []
+    for lib, env in ((_native.lib(), {}), (_native.lib_ab(), {"MICLIP_SMALL64": "0"}),
+                     (_native.lib_ab(), {"MICLIP_SMALLM": "0"})):
+        for k in ("MICLIP_SMALL64", "MICLIP_SMALLM"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        out = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=gpu)
+        _native.check(lib.mi_op_gemm(A.data_ptr(), W.data_ptr(), bias.data_ptr(), out.data_ptr(), M, N, K, 0,
+                                     _stream()), "gemm")
+        torch.cuda.synchronize()
+        outs.append(out)
+    ref = A.float() @ W.float().t() + bias
+    assert (outs[0].float() - ref).abs().max().item() < 2e-2 * max(1.0, ref.abs().max().item())
+    for o in outs[1:]:
+        assert torch.equal(outs[0].view(torch.int16), o.view(torch.int16))
