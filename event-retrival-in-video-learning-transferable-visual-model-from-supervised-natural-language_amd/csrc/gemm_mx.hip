@@ -26,6 +26,7 @@
 // the two 16-byte reads of every fragment (chunks 2g, 2g+1 for lane group g)
 // hit 16 distinct bank quads per ds_read_b128 lane group (exhaustive search).
 #include <cstdlib>
+#include <type_traits>
 
 #include "common.hpp"
 #include "internal.hpp"
@@ -263,6 +264,23 @@ __device__ __forceinline__ v8i lds_frag32(const char* p, int rd0, int rd1) {
   asm volatile("ds_read_b128 %0, %1" : "=v"(lo) : "v"(a0));
   asm volatile("ds_read_b128 %0, %1" : "=v"(hi) : "v"(a1));
   return v8i{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+// The same reads with the LDS address split into a VGPR base and an immediate offset (the
+// persistent kernel's lean stage body: one base add per operand per stage instead of one per read)
+template <int OFF>
+__device__ __forceinline__ v8i lds_frag32_o(uint32_t a0, uint32_t a1) {
+  typedef int v4i __attribute__((ext_vector_type(4)));
+  v4i lo, hi;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(lo) : "v"(a0), "i"(OFF));
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(hi) : "v"(a1), "i"(OFF));
+  return v8i{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+template <int OFF>
+__device__ __forceinline__ int lds_u8_o(uint32_t a) {
+  int v;
+  asm volatile("ds_read_u8 %0, %1 offset:%2" : "=v"(v) : "v"(a), "i"(OFF));
+  return v;
 }
 
 // Logical tile t -> (m-block, n-block) in groups of ng n-blocks (ng <= 0 or >= tiles_n: m-major):
@@ -514,7 +532,15 @@ __device__ __forceinline__ float4 mx_lds_f4(const float* p) {   // (an LDS read 
   return v;
 }
 
-template <int EPI>
+// LEAN (round 6, the default; A/B MICLIP_MX_PERSIST=3 keeps the first form): the stage loop split
+// into its head (the waits that may include the previous tile's stores), a steady part and its
+// tail, each with its wait immediate known at compile time, and instantiated per M-group, so a
+// steady stage carries no runtime wait chain and no group branch (the PMC pass of the first form,
+// profiles/r06_w_mx_fc_pmc.txt: per wave and tile 903 SALU, 200 branches and 2444 VALU beside 128
+// MFMAs, MFMA busy 0.32 -- the ping-pong's load-and-read section, not the MFMAs, set each stage's
+// length); the fragment reads address LDS as one base per operand plus immediate offsets.  Same
+// DMAs, reads, MFMAs and epilogue: bit-identical.
+template <int EPI, bool LEAN = true>
 __global__ __launch_bounds__(512) void gemm_mxppp_kernel(GemmArgs a) {
   typedef float f32x16 __attribute__((ext_vector_type(16)));
   constexpr int BM = 256, BN = 256, WTM = 128, WTN = 64;
@@ -612,6 +638,7 @@ __global__ __launch_bounds__(512) void gemm_mxppp_kernel(GemmArgs a) {
   const int lr = lane & 31, h = lane >> 5;
   const int rd0 = lr * SB + (((2 * h) ^ pp_swz((lr >> 2) & 3)) * 16);
   const int rd1 = lr * SB + (((2 * h + 1) ^ pp_swz((lr >> 2) & 3)) * 16);
+  static_assert(RING == 4 && 96 * SB < 65536, "LEAN: ring slot by mask, read offsets in the 16-bit field");
   while (true) {
     const int nvb = vb + (int)gridDim.x;
     has_next = nvb < ntiles;
@@ -626,6 +653,7 @@ __global__ __launch_bounds__(512) void gemm_mxppp_kernel(GemmArgs a) {
       for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
     v8i wf[2], af[4];
     int sw[2], sa[4];
+    if constexpr (!LEAN) {
     for (int gs = 0; gs < nk; ++gs) {
       const int slot = (rb + gs) % RING;
       const char* As = smem + slot * STAGE + (grp * WTM) * SB;
@@ -662,6 +690,76 @@ __global__ __launch_bounds__(512) void gemm_mxppp_kernel(GemmArgs a) {
       if (grp == 0 && gs + 1 < nk) wait_stage(gs + 1);
       barrier();
     }
+    } else {
+    // the per-wave LDS bases of the fragment and scale reads (a stage adds its ring slot), derived
+    // per tile from an opaque lane id so that they are not held across the epilogue
+    int ln;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+    const int lr_ = ln & 31, h_ = ln >> 5;
+    const int sw_ = pp_swz((lr_ >> 2) & 3);
+    // (three VGPRs: A's chunk-0 address, the lane's chunk-1 distance and the A-scale address; the W
+    // addresses differ from the A ones by wave-uniform amounts)
+    const int wcu = __builtin_amdgcn_readfirstlane(wc);
+    const uint32_t lds0 = (uint32_t)(uintptr_t)(const LDS_AS char*)smem;
+    const uint32_t vA0 = lds0 + (uint32_t)(lr_ * SB + (((2 * h_) ^ sw_) * 16) + grp * WTM * SB);
+    const uint32_t vD = (uint32_t)((((2 * h_ + 1) ^ sw_) - ((2 * h_) ^ sw_)) * 16);
+    const uint32_t vSA = lds0 + (uint32_t)(RING * STAGE + (grp * WTM + lr_) * 2);
+    const uint32_t dW = (uint32_t)(A_BYTES + wcu * WTN * SB - grp * WTM * SB);
+    const uint32_t dSW = (uint32_t)(512 + wcu * WTN * 2 - grp * WTM * 2);
+    // one stage; G the M-group, ST a steady stage: gs in [LEAD - 1, nk - LEAD), where this stage's
+    // DMA issue is the current tile's and the wait for stage gs + 1 has LEAD - 1 younger stages and
+    // no stores behind it (wait_stage's general case)
+    auto body = [&](auto g_c, const bool ST, int gs) __attribute__((always_inline)) {
+      constexpr int G = decltype(g_c)::value;
+      const int slot = (rb + gs) & (RING - 1);
+      if (ST || gs + LEAD < nk) {
+        issue(gs + LEAD, (rb + gs + LEAD) & (RING - 1));
+      } else if (has_next) {
+        const int st = gs + LEAD - nk;
+        if (st == 0) {
+          load_bias(tpar ^ 1, nn0);
+          set_src(nm0, nn0);
+        }
+        issue(st, (rb + gs + LEAD) & (RING - 1));
+      }
+      const uint32_t so = (uint32_t)(slot * STAGE), sso = (uint32_t)(slot * SC + (gs & 1));
+      const uint32_t a0 = vA0 + so, a1 = a0 + vD, w0 = a0 + dW, w1 = a1 + dW;
+      const uint32_t ssa = vSA + sso, ssw = ssa + dSW;
+      wf[0] = lds_frag32_o<0>(w0, w1);
+      wf[1] = lds_frag32_o<32 * SB>(w0, w1);
+      sw[0] = lds_u8_o<0>(ssw);
+      sw[1] = lds_u8_o<64>(ssw);
+      af[0] = lds_frag32_o<0>(a0, a1);
+      af[1] = lds_frag32_o<32 * SB>(a0, a1);
+      af[2] = lds_frag32_o<64 * SB>(a0, a1);
+      af[3] = lds_frag32_o<96 * SB>(a0, a1);
+      sa[0] = lds_u8_o<0>(ssa);
+      sa[1] = lds_u8_o<64>(ssa);
+      sa[2] = lds_u8_o<128>(ssa);
+      sa[3] = lds_u8_o<192>(ssa);
+      if (G == 1 && (ST || gs + 1 < nk)) {
+        if (ST) vm_wait<(LEAD - 1) * OPS1>();
+        else wait_stage(gs + 1);
+      }
+      lgkm_barrier();
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(wf[ni], af[mi], acc[mi][ni], 0, 0, 0, sw[ni], 0,
+                                                                        sa[mi]);
+      if (G == 0 && (ST || gs + 1 < nk)) {
+        if (ST) vm_wait<(LEAD - 1) * OPS0>();
+        else wait_stage(gs + 1);
+      }
+      barrier();
+    };
+    auto run = [&](auto g_c) __attribute__((always_inline)) {
+      for (int gs = 0; gs < nk; ++gs) body(g_c, gs >= LEAD - 1 && gs < nk - LEAD, gs);
+    };
+    if (grp == 0) run(std::integral_constant<int, 0>{});
+    else run(std::integral_constant<int, 1>{});
+    }
     if (grp == 0) barrier();   // groups realigned; every ring read of this tile is done
 
     // ---- epilogue of tile (cm0, cn0) (gemm_mxpp_kernel's arithmetic; bias from its LDS slot)
@@ -688,8 +786,28 @@ __global__ __launch_bounds__(512) void gemm_mxppp_kernel(GemmArgs a) {
         // QuickGELU in stage order over the block's 32 values (each value's operations are
         // mx_gelu's, so the result is bit-identical; consecutive transcendentals are independent,
         // as gemm_8q's F_GSTAGE16)
-        float v[2][16], e[2][16];
+        float v[2][16];
         float amax = 0.f;
+        if constexpr (LEAN) {   // (one 16-value stage order per ni: 16 fewer live registers, same values)
+#pragma unroll
+          for (int ni = 0; ni < 2; ++ni) {
+            float e[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+              const float4 b = bias[ni][j >> 2];
+              v[ni][j] = acc[mi][ni][j] + ((j & 3) == 0 ? b.x : (j & 3) == 1 ? b.y : (j & 3) == 2 ? b.z : b.w);
+              e[j] = __expf(-1.702f * v[ni][j]);
+            }
+#pragma unroll
+            for (int j = 0; j < 16; ++j) e[j] = __builtin_amdgcn_rcpf(1.0f + e[j]);
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+              v[ni][j] = v[ni][j] * e[j];
+              amax = fmaxf(amax, fabsf(v[ni][j]));
+            }
+          }
+        } else {
+        float e[2][16];
 #pragma unroll
         for (int ni = 0; ni < 2; ++ni)
 #pragma unroll
@@ -709,6 +827,7 @@ __global__ __launch_bounds__(512) void gemm_mxppp_kernel(GemmArgs a) {
             v[ni][j] = v[ni][j] * e[ni][j];
             amax = fmaxf(amax, fabsf(v[ni][j]));
           }
+        }
         const auto sx = __builtin_amdgcn_permlane32_swap(__float_as_uint(amax), __float_as_uint(amax), false, false);
         amax = fmaxf(__uint_as_float(sx[0]), __uint_as_float(sx[1]));
         const int X = mx_block_exp(amax);
@@ -852,26 +971,9 @@ hipError_t gemm_mx(const GemmArgs& a, int epi, hipStream_t s) {
   bool persist = nt >= cus && cus % 8 == 0 && a.K <= 2048;
 #if MICLIP_AB   // (2: persistent whatever K)
   if (const char* pe = std::getenv("MICLIP_MX_PERSIST"))
-    persist = std::atoi(pe) == 2 ? nt >= cus && cus % 8 == 0 : persist && std::atoi(pe) != 0;
+    persist = std::atoi(pe) == 2 ? nt >= cus && cus % 8 == 0 : persist && std::atoi(pe) != 0;   // (3: see below)
 #endif
   if (!force_dbuf && a.K / 64 >= 3 && persist) {
-#if MICLIP_AB   // A/B: MICLIP_MX_NG forces the tile-order group width (-1 = m-major)
-    if (const char* ng = std::getenv("MICLIP_MX_NG")) {
-      GemmArgs g = a;
-      g.ngroup = std::atoi(ng);
-      switch (epi) {
-        case EPI_BF16: hipLaunchKernelGGL(gemm_mxppp_kernel<EPI_BF16>, dim3(cus), dim3(512), 0, s, g); break;
-        case EPI_GELU_BF16: hipLaunchKernelGGL(gemm_mxppp_kernel<EPI_GELU_BF16>, dim3(cus), dim3(512), 0, s, g); break;
-        case EPI_F32: hipLaunchKernelGGL(gemm_mxppp_kernel<EPI_F32>, dim3(cus), dim3(512), 0, s, g); break;
-        case EPI_GELU_MX:
-          if (!a.o_scale) return hipErrorInvalidValue;
-          hipLaunchKernelGGL(gemm_mxppp_kernel<EPI_GELU_MX>, dim3(cus), dim3(512), 0, s, g);
-          break;
-        default: return hipErrorInvalidValue;
-      }
-      return hipGetLastError();
-    }
-#endif
     // tile order: n-tiles in groups of 6 when there are >= 12 and a group's e4m3 panel fits 2.4 MB
     // (an XCD's 32 concurrent tiles then hold a 1.5-MB panel at K = 1024, not the m-major walk's
     // whole 3-4 MB, which the L2 re-fetched per m-block: FETCH 9x the operand bytes on c_fc,
@@ -881,16 +983,28 @@ hipError_t gemm_mx(const GemmArgs& a, int epi, hipStream_t s) {
     GemmArgs g = a;
     const int tn = a.N / 256;
     if (g.ngroup == 0) g.ngroup = (tn >= 12 && (int64_t)6 * 256 * a.K <= 2400000) ? 6 : -1;
+    bool lean = true;
+#if MICLIP_AB   // MICLIP_MX_NG forces the tile-order group width (-1 = m-major); MICLIP_MX_PERSIST=3
+                // runs the persistent kernel's first form (runtime wait chains in every stage)
+    if (const char* ng = std::getenv("MICLIP_MX_NG")) g.ngroup = std::atoi(ng);
+    if (const char* pe = std::getenv("MICLIP_MX_PERSIST")) lean = std::atoi(pe) != 3;
+#endif
+#define MX_PPP(E)                                                                    \
+  do {                                                                               \
+    if (lean) hipLaunchKernelGGL((gemm_mxppp_kernel<E, true>), dim3(cus), dim3(512), 0, s, g);   \
+    else hipLaunchKernelGGL((gemm_mxppp_kernel<E, false>), dim3(cus), dim3(512), 0, s, g);       \
+  } while (0)
     switch (epi) {
-      case EPI_BF16: hipLaunchKernelGGL(gemm_mxppp_kernel<EPI_BF16>, dim3(cus), dim3(512), 0, s, g); break;
-      case EPI_GELU_BF16: hipLaunchKernelGGL(gemm_mxppp_kernel<EPI_GELU_BF16>, dim3(cus), dim3(512), 0, s, g); break;
-      case EPI_F32: hipLaunchKernelGGL(gemm_mxppp_kernel<EPI_F32>, dim3(cus), dim3(512), 0, s, g); break;
+      case EPI_BF16: MX_PPP(EPI_BF16); break;
+      case EPI_GELU_BF16: MX_PPP(EPI_GELU_BF16); break;
+      case EPI_F32: MX_PPP(EPI_F32); break;
       case EPI_GELU_MX:
         if (!a.o_scale) return hipErrorInvalidValue;
-        hipLaunchKernelGGL(gemm_mxppp_kernel<EPI_GELU_MX>, dim3(cus), dim3(512), 0, s, g);
+        MX_PPP(EPI_GELU_MX);
         break;
       default: return hipErrorInvalidValue;
     }
+#undef MX_PPP
     return hipGetLastError();
   }
   if (!force_dbuf && a.K / 64 >= 3) {
