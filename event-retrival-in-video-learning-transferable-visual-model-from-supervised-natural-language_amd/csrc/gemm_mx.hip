@@ -532,15 +532,18 @@ __device__ __forceinline__ float4 mx_lds_f4(const float* p) {   // (an LDS read 
   return v;
 }
 
-// LEAN (round 6, the default; A/B MICLIP_MX_PERSIST=3 keeps the first form): the stage loop split
+// LEAN (round 6, A/B MICLIP_MX_PERSIST=4; measured no faster, see below): the stage loop split
 // into its head (the waits that may include the previous tile's stores), a steady part and its
 // tail, each with its wait immediate known at compile time, and instantiated per M-group, so a
 // steady stage carries no runtime wait chain and no group branch (the PMC pass of the first form,
 // profiles/r06_w_mx_fc_pmc.txt: per wave and tile 903 SALU, 200 branches and 2444 VALU beside 128
 // MFMAs, MFMA busy 0.32 -- the ping-pong's load-and-read section, not the MFMAs, set each stage's
 // length); the fragment reads address LDS as one base per operand plus immediate offsets.  Same
-// DMAs, reads, MFMAs and epilogue: bit-identical.
-template <int EPI, bool LEAN = true>
+// DMAs, reads, MFMAs and epilogue: bit-identical.  At the configs[4] shapes (scripts/mx_persist_micro.py,
+// profiles/r06_x_mx_lean.log) c_fc -> MX-fp8 2806 vs 2777 us, qkv 1944 vs 1976, out_proj 698 vs 709:
+// within noise, so the scalar work was not what bounds the stage (and the GELU -> MX-fp8 instance
+// spills 4 registers); the first form stays the default.
+template <int EPI, bool LEAN = false>
 __global__ __launch_bounds__(512) void gemm_mxppp_kernel(GemmArgs a) {
   typedef float f32x16 __attribute__((ext_vector_type(16)));
   constexpr int BM = 256, BN = 256, WTM = 128, WTN = 64;
@@ -971,7 +974,7 @@ hipError_t gemm_mx(const GemmArgs& a, int epi, hipStream_t s) {
   bool persist = nt >= cus && cus % 8 == 0 && a.K <= 2048;
 #if MICLIP_AB   // (2: persistent whatever K)
   if (const char* pe = std::getenv("MICLIP_MX_PERSIST"))
-    persist = std::atoi(pe) == 2 ? nt >= cus && cus % 8 == 0 : persist && std::atoi(pe) != 0;   // (3: see below)
+    persist = std::atoi(pe) == 2 ? nt >= cus && cus % 8 == 0 : persist && std::atoi(pe) != 0;   // (4: see below)
 #endif
   if (!force_dbuf && a.K / 64 >= 3 && persist) {
     // tile order: n-tiles in groups of 6 when there are >= 12 and a group's e4m3 panel fits 2.4 MB
@@ -983,11 +986,11 @@ hipError_t gemm_mx(const GemmArgs& a, int epi, hipStream_t s) {
     GemmArgs g = a;
     const int tn = a.N / 256;
     if (g.ngroup == 0) g.ngroup = (tn >= 12 && (int64_t)6 * 256 * a.K <= 2400000) ? 6 : -1;
-    bool lean = true;
-#if MICLIP_AB   // MICLIP_MX_NG forces the tile-order group width (-1 = m-major); MICLIP_MX_PERSIST=3
-                // runs the persistent kernel's first form (runtime wait chains in every stage)
+    bool lean = false;
+#if MICLIP_AB   // MICLIP_MX_NG forces the tile-order group width (-1 = m-major); MICLIP_MX_PERSIST=4
+                // runs the lean stage loop
     if (const char* ng = std::getenv("MICLIP_MX_NG")) g.ngroup = std::atoi(ng);
-    if (const char* pe = std::getenv("MICLIP_MX_PERSIST")) lean = std::atoi(pe) != 3;
+    if (const char* pe = std::getenv("MICLIP_MX_PERSIST")) lean = std::atoi(pe) == 4;
 #endif
 #define MX_PPP(E)                                                                    \
   do {                                                                               \

@@ -190,7 +190,7 @@ def test_gemm_mx_default_fp8_output_rows(gpu, M, N, K):
 def test_gemm_mx_persistent_bit_identical(gpu, monkeypatch, M, N, K, epi):
     """The persistent MX ping-pong (gemm_mxppp_kernel: one workgroup per CU, the next tile's first
     stages and bias streamed in under this tile's last stages, counted waits across the tile
-    boundary; since round 6 its lean stage loop, against the first form, MICLIP_MX_PERSIST=3) against
+    boundary; and its lean stage loop, MICLIP_MX_PERSIST=4) against
     one workgroup per tile (gemm_mxpp_kernel, MICLIP_MX_PERSIST=0, A/B build):
     the same MFMAs in the same k order and the same epilogue arithmetic, so bf16 / GELU / f32 /
     MX-fp8 outputs (e4m3 bytes and their scales) are byte-identical -- several tiles per CU, odd M
@@ -204,7 +204,7 @@ def test_gemm_mx_persistent_bit_identical(gpu, monkeypatch, M, N, K, epi):
     qa, sa = _quant_gpu(a.to(gpu))
     qw, sw = _quant_gpu(w.to(gpu))
     outs = []
-    for lib, persist in ((N_.lib(), None), (N_.lib_ab(), "1"), (N_.lib_ab(), "0"), (N_.lib_ab(), "3")):
+    for lib, persist in ((N_.lib(), None), (N_.lib_ab(), "1"), (N_.lib_ab(), "0"), (N_.lib_ab(), "4")):
         if persist is not None:
             monkeypatch.setenv("MICLIP_MX_PERSIST", persist)
         if epi == 4:
@@ -220,4 +220,4 @@ def test_gemm_mx_persistent_bit_identical(gpu, monkeypatch, M, N, K, epi):
     torch.cuda.synchronize()
     assert torch.equal(outs[0].view(torch.uint8), outs[1].view(torch.uint8))   # product = A/B persistent
     assert torch.equal(outs[1].view(torch.uint8), outs[2].view(torch.uint8))   # persistent = per tile
-    assert torch.equal(outs[1].view(torch.uint8), outs[3].view(torch.uint8))   # lean stage loop = first form
+    assert torch.equal(outs[1].view(torch.uint8), outs[3].view(torch.uint8))   # the lean stage loop (A/B)
