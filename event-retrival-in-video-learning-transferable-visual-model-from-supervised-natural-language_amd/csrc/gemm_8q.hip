@@ -93,6 +93,13 @@ constexpr int F_ODUP = 1024;
 // DMAs: older than the awaited K-tile, so the phase-4 wait retires it) and reaches the other waves
 // through an LDS slot
 constexpr int F_DYN = 2048;
+// F_WARM (EPI_RES16, A/B): after the last pair's phase-4 wait each wave issues two 4-byte LDS-DMAs
+// per lane into a throw-away LDS slot, one per 128-byte line of the tile's x16 rows (1024 lines
+// over the 8 waves), so the epilogue's x16 loads five phases later find their lines in L2 (the
+// probes put the x16 loads' exposed latency at ~100 us of resout500's ~710).  The two extra VMEM
+// ops are older than every later wait's awaited DMAs, so those waits also retire them (vmcnt
+// completes in order): correct, and four phases after their issue
+constexpr int F_WARM = 4096;
 __device__ unsigned g_dyn8q[8];   // F_DYN: per-XCD claim counters, zeroed before each launch
 
 __device__ __forceinline__ f32x2 quick_gelu2_8q(f32x2 v) {
@@ -223,7 +230,7 @@ template <int EPI, int ABL = 0, int F = 0, bool OPF16 = false>
 __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
   using EK = EpiKind8q<EPI>;
   using VM = Vm8q<EPI, ABL, F>;
-  __shared__ __attribute__((aligned(16))) char smem[EK::LDS + ((F & F_DYN) ? 16 : 0)];
+  __shared__ __attribute__((aligned(16))) char smem[EK::LDS + ((F & F_DYN) ? 16 : 0) + ((F & F_WARM) ? 256 : 0)];
   float* sbias = (float*)(smem + 2 * BUF);
   float* srs = (float*)(smem + 2 * BUF + 2 * BN * 4);              // LN: [2][BM][2]
   float* scol = (float*)(smem + 2 * BUF + 2 * BN * 4 + 2 * BM * 8);  // LN: [2][BN]
@@ -471,6 +478,16 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
     // (ABL 13: non-temporal x16 loads and stores, probe of L2 pollution)
     xin[mi][0] = __builtin_bit_cast(u32x4_8q, __builtin_amdgcn_raw_buffer_load_b128(r, vo + mi * blkO, 0, ABL == 13 ? 2 : 0));
     xin[mi][1] = __builtin_bit_cast(u32x4_8q, __builtin_amdgcn_raw_buffer_load_b128(r, vo + mi * blkO + 64, 0, ABL == 13 ? 2 : 0));
+  };
+  auto res_warm = [&](int m0, int n0) {   // F_WARM (see above)
+    const __amdgpu_buffer_rsrc_t r = out_rsrc_at(m0, n0);
+    const int l = lane_id();
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int L = wave * 64 + l + i * 512;   // line L of the 256 rows x 512 bytes
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (LDS_AS void*)(smem + EK::LDS + ((F & F_DYN) ? 16 : 0)), 4,
+                                               (uint32_t)((L >> 2) * a.ldo * 2 + (L & 3) * 128), 0, 0, 0);
+    }
   };
   auto res_prefetch = [&](int mlo, int mhi, int m0, int n0) {
     if (!EK::RES || ABL == 12) return;
@@ -900,6 +917,7 @@ __global__ __launch_bounds__(512) void gemm_8q_kernel(GemmArgs a) {
       // issued three barrier intervals earlier)
       if (FIRST && has_prev && !((F & F_BEARLY) && wr == 1)) vm_wait<VM::FIRST_P4>();
       else vm_wait<VM::YOUNGER>();
+      if constexpr ((F & F_WARM) && EK::RES) if (LAST) res_warm(cur_m0, cur_n0);
       if constexpr (DYN) if (FIRST && wave == 0 && has_next) dyn_publish(dyn_got);   // (retired: older than phase 1's DMAs)
       if (FIRST) stamp(3);   // S3: first pair's phase-4 wait passed
     }
@@ -1209,6 +1227,7 @@ hipError_t gemm_8q(const GemmArgs& a0, int epi, hipStream_t s, int cus, int mode
     else if (abl == 12) hipLaunchKernelGGL((gemm_8q_kernel<EPI_RES16_BF16, 12, 0>), dim3(grid), dim3(512), 0, s, a);
     else if (abl == 13) hipLaunchKernelGGL((gemm_8q_kernel<EPI_RES16_BF16, 13, 0>), dim3(grid), dim3(512), 0, s, a);
     else if (abl == 14) hipLaunchKernelGGL((gemm_8q_kernel<EPI_RES16_BF16, 0, F_BEARLY>), dim3(grid), dim3(512), 0, s, a);
+    else if (abl == 15) hipLaunchKernelGGL((gemm_8q_kernel<EPI_RES16_BF16, 0, F_WARM>), dim3(grid), dim3(512), 0, s, a);
     else
 #endif
     hipLaunchKernelGGL((gemm_8q_kernel<EPI_RES16_BF16, 0, 0>), dim3(grid), dim3(512), 0, s, a);

@@ -103,7 +103,7 @@ def main():
             if res:   # (x16 grows by the GEMM output each call: timing only, outputs not compared)
                 # v2 / v3: timing probes of the fused kernel without statistics / without x16 loads
                 # v5: non-temporal x16 loads / stores; v9: the lagging group's epilogue early (F_BEARLY)
-                os.environ["MICLIP_RES_ABL"] = {2: "11", 3: "12", 5: "13", 9: "14"}.get(v, "0")
+                os.environ["MICLIP_RES_ABL"] = {2: "11", 3: "12", 5: "13", 9: "14", 6: "15"}.get(v, "0")
                 # v6-v8: start stagger of half / a quarter of the workgroups (phases:ticks at 100 MHz)
                 os.environ["MICLIP_RES_STAGGER"] = {6: "2:1500", 7: "2:750", 8: "4:750"}.get(v, "")
                 if v != 1:
