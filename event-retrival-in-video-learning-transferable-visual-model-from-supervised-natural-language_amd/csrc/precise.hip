@@ -723,7 +723,18 @@ __global__ __launch_bounds__(256, 2) void attn_f32s_kernel(const float* __restri
   const __amdgpu_buffer_rsrc_t rsp = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(a3 + (OUT == 0 ? 0 : (int64_t)bseq * S * (OUT == 2 ? 2 : 3) * W)), (short)0,
       OUT == 0 ? 0 : S * (OUT == 2 ? 2 : 3) * W * 2, 0x00020000);
+  // (the bound first: placed after the K / V loads it measured slower, 1737 vs 1578 us at 10k
+  // frames, profiles/r06_za_bench.json)
   float so = 1.0f;
+  if constexpr (OUT != 0) {
+    float rm = lane < S ? rmax[(int64_t)bseq * S + lane] : 0.f;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) rm = fmaxf(rm, __shfl_xor(rm, o, 64));
+    const float bound = (rm * bw + bb) * (1.0f + 1.0f / 256.0f);
+    const int eo = __builtin_amdgcn_readfirstlane(split_exp(bound));
+    so = ldexpf(1.0f, eo);
+    if (head == 0 && lane < S) rsc[(int64_t)bseq * S + lane] = ldexpf(1.0f, -eo);
+  }
   typedef unsigned int u32x4a __attribute__((ext_vector_type(4)));
   auto ld_row32 = [&](int r, int cb, float* v) {   // row r, columns cb + 32 h .. + 31 (rows >= S: zeros)
     const uint32_t vo = (uint32_t)((r * ld + 32 * h) * 4);
@@ -779,15 +790,6 @@ __global__ __launch_bounds__(256, 2) void attn_f32s_kernel(const float* __restri
     for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
       for (int u = 0; u < 2; ++u) split8_s(&vf[dt][kt][8 * u], sv, v1[dt][kt][u], v2[dt][kt][u]);
-  }
-  if constexpr (OUT != 0) {   // (after the K / V loads: its latency and shuffles behind theirs)
-    float rm = lane < S ? rmax[(int64_t)bseq * S + lane] : 0.f;
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) rm = fmaxf(rm, __shfl_xor(rm, o, 64));
-    const float bound = (rm * bw + bb) * (1.0f + 1.0f / 256.0f);
-    const int eo = __builtin_amdgcn_readfirstlane(split_exp(bound));
-    so = ldexpf(1.0f, eo);
-    if (head == 0 && lane < S) rsc[(int64_t)bseq * S + lane] = ldexpf(1.0f, -eo);
   }
   for (int q0 = 0; q0 < qend; q0 += 32) {
     const int qi = q0 + j;   // this lane's query in the S^T layout
