@@ -723,20 +723,18 @@ __global__ __launch_bounds__(256, 2) void attn_f32s_kernel(const float* __restri
   const __amdgpu_buffer_rsrc_t rsp = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(a3 + (OUT == 0 ? 0 : (int64_t)bseq * S * (OUT == 2 ? 2 : 3) * W)), (short)0,
       OUT == 0 ? 0 : S * (OUT == 2 ? 2 : 3) * W * 2, 0x00020000);
-  // (the bound's row-max load goes out first and is reduced where the first block's outputs are
-  // split, so neither its latency nor its shuffles sit ahead of the K / V loads: reduced at the
-  // top the kernel took 1578 us at 10k frames, after the K / V loads 1737 us, against 1280 us for
-  // the f32 output -- profiles/r06_z_bench.json, r06_za_bench.json)
-  float so = 1.0f, rm = 0.f;
-  if constexpr (OUT != 0) rm = lane < S ? rmax[(int64_t)bseq * S + lane] : 0.f;
-  auto bound_scale = [&]() {
+  // (the bound first: placed after the K / V loads it measured slower, 1737 vs 1578 us at 10k
+  // frames, profiles/r06_za_bench.json)
+  float so = 1.0f;
+  if constexpr (OUT != 0) {
+    float rm = lane < S ? rmax[(int64_t)bseq * S + lane] : 0.f;
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) rm = fmaxf(rm, __shfl_xor(rm, o, 64));
     const float bound = (rm * bw + bb) * (1.0f + 1.0f / 256.0f);
     const int eo = __builtin_amdgcn_readfirstlane(split_exp(bound));
     so = ldexpf(1.0f, eo);
     if (head == 0 && lane < S) rsc[(int64_t)bseq * S + lane] = ldexpf(1.0f, -eo);
-  };
+  }
   typedef unsigned int u32x4a __attribute__((ext_vector_type(4)));
   auto ld_row32 = [&](int r, int cb, float* v) {   // row r, columns cb + 32 h .. + 31 (rows >= S: zeros)
     const uint32_t vo = (uint32_t)((r * ld + 32 * h) * 4);
@@ -850,7 +848,6 @@ __global__ __launch_bounds__(256, 2) void attn_f32s_kernel(const float* __restri
         for (int t = 0; t < 8; ++t) pv[t] = sc[kt][8 * u + t];
         split8_s(pv, 16384.0f, p1[kt][u], p2[kt][u]);
       }
-    if constexpr (OUT != 0) if (q0 == 0) bound_scale();
 #pragma unroll
     for (int dt = 0; dt < 2; ++dt) {
       f32x16 o = f32x16{};
