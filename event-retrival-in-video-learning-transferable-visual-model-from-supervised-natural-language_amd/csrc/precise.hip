@@ -700,7 +700,7 @@ __device__ __forceinline__ void split8_s(const float* v, float s, f16x8_s& hi, f
 // the weight constants api.cpp computes at load), maximised over the sequence's rows and padded by
 // 2^-8 for the rounding of the computed values; every head's wave derives the same power of two.
 // A loose bound only lowers the split's subnormal floor (|o s| < 2^14 always), as EPI_SPLIT_GELU's.
-template <int OUT>
+template <int OUT, bool LATE = false>
 __global__ __launch_bounds__(256, 2) void attn_f32s_kernel(const float* __restrict__ qkv, float* __restrict__ out,
                                                           int nseq, int S, int W, int causal,
                                                           const float* __restrict__ rmax, float bw, float bb,
@@ -725,15 +725,20 @@ __global__ __launch_bounds__(256, 2) void attn_f32s_kernel(const float* __restri
       OUT == 0 ? 0 : S * (OUT == 2 ? 2 : 3) * W * 2, 0x00020000);
   // (the bound first: placed after the K / V loads it measured slower, 1737 vs 1578 us at 10k
   // frames, profiles/r06_za_bench.json)
-  float so = 1.0f;
-  if constexpr (OUT != 0) {
-    float rm = lane < S ? rmax[(int64_t)bseq * S + lane] : 0.f;
+  // (LATE, A/B MICLIP_F32_ATTN_LATE=1: the row-max load issued first and reduced where the first
+  // query block's outputs are split, off the path to the K / V loads)
+  float so = 1.0f, rm = 0.f;
+  auto bound_scale = [&]() {
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) rm = fmaxf(rm, __shfl_xor(rm, o, 64));
     const float bound = (rm * bw + bb) * (1.0f + 1.0f / 256.0f);
     const int eo = __builtin_amdgcn_readfirstlane(split_exp(bound));
     so = ldexpf(1.0f, eo);
     if (head == 0 && lane < S) rsc[(int64_t)bseq * S + lane] = ldexpf(1.0f, -eo);
+  };
+  if constexpr (OUT != 0) {
+    rm = lane < S ? rmax[(int64_t)bseq * S + lane] : 0.f;
+    if constexpr (!LATE) bound_scale();
   }
   typedef unsigned int u32x4a __attribute__((ext_vector_type(4)));
   auto ld_row32 = [&](int r, int cb, float* v) {   // row r, columns cb + 32 h .. + 31 (rows >= S: zeros)
@@ -848,6 +853,7 @@ __global__ __launch_bounds__(256, 2) void attn_f32s_kernel(const float* __restri
         for (int t = 0; t < 8; ++t) pv[t] = sc[kt][8 * u + t];
         split8_s(pv, 16384.0f, p1[kt][u], p2[kt][u]);
       }
+    if constexpr (OUT != 0 && LATE) if (q0 == 0) bound_scale();
 #pragma unroll
     for (int dt = 0; dt < 2; ++dt) {
       f32x16 o = f32x16{};
@@ -1198,6 +1204,13 @@ hipError_t attention_f32_split(const float* qkv, const float* rmax, float bw, fl
   if (B <= 0) return hipSuccess;
   if (W % 64 || S < 1 || S > 64 || (role != 0 && role != 2)) return hipErrorInvalidValue;
   const dim3 grid4((unsigned)(((int64_t)B * (W / 64) + 3) / 4));
+#if MICLIP_AB
+  if (const char* le = std::getenv("MICLIP_F32_ATTN_LATE"); le && std::atoi(le) && role == 2) {
+    hipLaunchKernelGGL((attn_f32s_kernel<2, true>), grid4, dim3(256), 0, s, qkv, nullptr, B, S, W, causal, rmax, bw, bb,
+                       a3, rsc);
+    return hipGetLastError();
+  }
+#endif
   if (role == 2)
     hipLaunchKernelGGL(attn_f32s_kernel<2>, grid4, dim3(256), 0, s, qkv, nullptr, B, S, W, causal, rmax, bw, bb, a3, rsc);
   else
