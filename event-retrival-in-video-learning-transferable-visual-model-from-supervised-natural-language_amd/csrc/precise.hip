@@ -726,7 +726,8 @@ __global__ __launch_bounds__(256, 2) void attn_f32s_kernel(const float* __restri
   // (the bound first: placed after the K / V loads it measured slower, 1737 vs 1578 us at 10k
   // frames, profiles/r06_za_bench.json)
   // (LATE, A/B MICLIP_F32_ATTN_LATE=1: the row-max load issued first and reduced where the first
-  // query block's outputs are split, off the path to the K / V loads)
+  // query block's outputs are split, off the path to the K / V loads -- measured slower, 1537 vs
+  // 1427 us at 10k frames, profiles/r06_ze_attn_split_micro.log: it holds 7 more registers)
   float so = 1.0f, rm = 0.f;
   auto bound_scale = [&]() {
 #pragma unroll
